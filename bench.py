@@ -1,0 +1,193 @@
+"""bench.py -- restic CDC + SHA-256 blob IDs on MI355X (BASELINE.json metric).
+
+python bench.py --gpus N --steps K --warmup W
+  N=1: config C2 -- one 64 GiB synthetic volume image (seed 2), device-resident,
+       restic chunker (testPol, 512 KiB / 8 MiB, 20 bits) + SHA-256 blob IDs.
+  N>1: launched by torch.distributed.run, one rank per GPU: one volume of
+       N x per-GPU bytes byte-range sharded across the ranks (C3 shape; weak
+       scaling, per-GPU work fixed); the only exchange is an RCCL all-gather of
+       one u64 per rank per stitch round (volsync_amd/shard.py).
+A step = one full pass of the hot path over the volume: fingerprint, cut
+selection, Cut values, SHA-256 of every chunk.  Inputs are generated in HBM
+before the timed region.  Prints one JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_PEAK_TOPS = 78.6        # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 ops/s
+SHA_OPS_PER_BYTE = 1384 / 64  # DESIGN.md 3.3 (per 64-byte block)
+FP_OPS_PER_BYTE = 8.5
+
+
+def cpu_baseline(sample_bytes: int, threads: int):
+    """Oracle port (oracle/cdc_ref.c) timed restic-style on the host: one chunker
+    thread + (threads-1) SHA-256 threads (OpenSSL, SHA-NI when present)."""
+    from tests import oracle_lib as O
+    data = O.synth(2, 0, sample_bytes)
+    t0 = time.perf_counter()
+    ch = O.cdc_hash(data, 0x3DA3358B4DC173, 512 << 10, 8 << 20, 20, n_hash=threads - 1)
+    dt = time.perf_counter() - t0
+    # chunker alone on one core (what restic does per file)
+    t1 = time.perf_counter()
+    O.chunk_all(data, 0x3DA3358B4DC173, 512 << 10, 8 << 20, 20)
+    dt_chunk = time.perf_counter() - t1
+    return {
+        "value": round(sample_bytes / dt / 1e9, 3),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{sample_bytes >> 30} GiB of the C2 stream (seed 2), {len(ch)} chunks; "
+                  f"1 chunker thread + {threads - 1} SHA-256 threads (OpenSSL="
+                  f"{bool(O.lib().ref_have_openssl())}); chunker alone 1 core "
+                  f"{sample_bytes / dt_chunk / 1e9:.3f} GB/s",
+        "cpu": _cpu_model(),
+    }
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--per-gpu-gib", type=float, default=64.0)
+    ap.add_argument("--cpu-sample-gib", type=int, default=4)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from volsync_amd import DeviceChunker, MaxSize, MinSize, TestPol, synth_fill_device
+    from volsync_amd.shard import ShardSpec, run_shard, torch_collectives
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    per = int(args.per_gpu_gib * (1 << 30))
+    total = per * world
+    spec = ShardSpec.for_rank(total, world, rank, MaxSize)
+    dlen = spec.data_hi - spec.data_lo
+    buf = torch.empty(dlen, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    synth_fill_device(buf.data_ptr(), 2, spec.data_lo, dlen, device=local, stream=stream)
+    torch.cuda.synchronize(dev)
+
+    dc = DeviceChunker(TestPol, MinSize, MaxSize, 20, device=local)
+    dc.set_stream(stream)
+    coll = torch_collectives(dev) if world > 1 else None
+
+    def step():
+        if world == 1:
+            n, _ = dc.process(buf.data_ptr(), dlen, 0, True)
+        else:
+            n = run_shard(dc, spec, buf.data_ptr(), *coll)
+        return n
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dc.timing(True)
+    t0 = time.perf_counter()
+    nch = 0
+    for _ in range(args.steps):
+        nch = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ms, launches = dc.timing(False)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        c = torch.tensor([nch], dtype=torch.int64, device=dev)
+        dist.all_reduce(c)
+        nch = int(c.item())
+
+    own_bytes = spec.own_hi - spec.own_lo
+    stages = ["fingerprint", "select", "sha256", "other"]
+    per_step = {s: ms[i] / args.steps for i, s in enumerate(stages)}
+    dom = max(range(4), key=lambda i: ms[i])
+    fp_ms = ms[0] / max(1, launches[0]) if launches[0] else 0.0
+    sha_ms = ms[2] / max(1, launches[2]) if launches[2] else 0.0
+    # algorithmic bytes per launch: the fingerprint pass reads each scanned byte
+    # once (plus a 64-byte warm-up per 12 KiB strip, not counted); SHA-256
+    # reads each chunk byte once.  One SHA launch per step; the fingerprint
+    # stage is one interior launch (+2 tiny guarded ones) per step.
+    fp_launch_bytes = own_bytes
+    sha_launch_bytes = own_bytes
+    fp_gbs = fp_launch_bytes / (ms[0] / args.steps) / 1e6 if ms[0] else 0.0
+    sha_gbs = sha_launch_bytes / sha_ms / 1e6 if sha_ms else 0.0
+    roof = {
+        "fingerprint": {"bound": "hbm", "achieved": round(fp_gbs, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(fp_gbs / HBM_PEAK_GBS, 4),
+                        "traffic": None,
+                        "valu_frac": round(fp_gbs * FP_OPS_PER_BYTE / 1e3 / VALU_PEAK_TOPS, 4)},
+        "sha256": {"bound": "hbm", "achieved": round(sha_gbs, 1), "peak": HBM_PEAK_GBS,
+                   "unit": "GB/s", "frac": round(sha_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                   "valu_frac": round(sha_gbs * SHA_OPS_PER_BYTE / 1e3 / VALU_PEAK_TOPS, 4)},
+    }
+    dom_name = "sha256" if per_step["sha256"] >= per_step["fingerprint"] else "fingerprint"
+    roofline = dict(roof[dom_name])
+    roofline["kernel"] = dom_name
+
+    value = total * args.steps / dt / 1e9
+    if rank == 0:
+        out = {
+            "metric": "GB/s chunked+SHA-256 (restic CDC)",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 volume image, device-resident)",
+            "config": {"workload": "C2: 64 GiB volume, restic CDC + SHA-256, 1 GPU" if world == 1
+                       else f"C3-shape: {total >> 30} GiB volume byte-range sharded over {world} GPUs",
+                       "volume_bytes": total, "per_gpu_bytes": per, "chunks": nch,
+                       "pol": "0x3DA3358B4DC173", "min": MinSize, "max": MaxSize, "avg_bits": 20,
+                       "parallelism": f"byte-range shards x{world}"},
+            "roofline": roofline,
+            "stages_ms_per_step": {k: round(v, 3) for k, v in per_step.items()},
+            "kernels": roof,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_sample_gib << 30, args.cpu_threads)
+        print(json.dumps(out), flush=True)
+    dc.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,138 @@
+/*
+ * vsgpu.h -- C ABI of the MI355X data-movement hot path behind VolSync's
+ * restic mover: content-defined chunking (restic chunker, Rabin fingerprint
+ * over a 64-byte window) plus SHA-256 blob IDs, as hand-written gfx950 HIP
+ * kernels.
+ *
+ * The reference binds this path in Go.  The restic mover image
+ * (/root/reference/mover-restic/Dockerfile:8-27) builds restic v0.13.1, whose
+ * archiver calls github.com/restic/chunker@v0.4.0 and crypto/sha256 (patched
+ * in by mover-restic/patch-sources.sh:16-27); restic runs from
+ * mover-restic/entry.sh:60-65 ("restic backup").  Each entry point below names
+ * the upstream interface it replaces; INTEGRATION.md shows the cgo binding.
+ *
+ * Conventions:
+ *  - return 0 on success, a negative VS_ERR_* on failure, VS_EOF (1) when a
+ *    chunk stream is exhausted; vs_last_error() gives a thread-local message;
+ *  - the caller owns every buffer it passes; host buffers are copied before
+ *    the call returns and never retained (cgo pointer rules);
+ *  - a handle is single-threaded; different handles may run concurrently;
+ *    each call makes the handle's device current (cgo calls hop OS threads);
+ *  - there is no CPU fallback: without a usable gfx950 device every compute
+ *    entry point fails with VS_ERR_NO_DEVICE.
+ */
+#ifndef VSGPU_H
+#define VSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VS_OK 0
+#define VS_EOF 1
+#define VS_ERR_ARG (-1)       /* bad argument */
+#define VS_ERR_POLY (-2)      /* polynomial 0 ("tables ... not initialized") or degree > 53 */
+#define VS_ERR_NO_DEVICE (-3) /* no HIP device / HIP runtime error */
+#define VS_ERR_NOMEM (-4)     /* device or host allocation failed */
+#define VS_ERR_STATE (-5)     /* call out of sequence */
+#define VS_ERR_HIP (-6)       /* a HIP call or kernel launch failed */
+
+#define VS_DEFAULT_POL 0x3DA3358B4DC173ull /* chunker_test.go testPol */
+#define VS_MIN_SIZE (512u * 1024u)         /* chunker.go MinSize */
+#define VS_MAX_SIZE (8u * 1024u * 1024u)   /* chunker.go MaxSize */
+#define VS_AVG_BITS 20u                    /* splitmask = 2^20 - 1 */
+
+/* One chunk: chunker.go `type Chunk struct { Start, Length uint; Cut uint64; Data []byte }`
+ * plus restic's blob ID (internal/restic/id.go Hash = sha256.Sum256(Data)).
+ * Data is not carried: it is data[start : start+length] of the caller's stream. */
+typedef struct vs_chunk {
+    uint64_t start;
+    uint64_t length;
+    uint64_t cut;
+    uint8_t id[32];
+} vs_chunk;
+
+typedef struct vs_cdc vs_cdc;
+
+/* ---- library / device ------------------------------------------------ */
+const char *vs_last_error(void);
+const char *vs_version(void);
+/* number of usable gfx9xx devices (0 when none; never initialises a context) */
+int vs_device_count(void);
+
+/* ---- polynomial helpers (chunker polynomials.go) ---------------------- */
+/* Pol.Deg */
+int vs_pol_deg(uint64_t pol);
+/* Pol.Irreducible (Ben-Or), 1 = irreducible */
+int vs_pol_irreducible(uint64_t pol);
+/* fillTables: out[b] = Hash(b || 63 zero bytes), mod[b] = (b x^k mod P) | (b << k) */
+int vs_pol_tables(uint64_t pol, uint64_t out_tab[256], uint64_t mod_tab[256]);
+
+/* ---- restic chunker stream (replaces chunker.New / NewWithBoundaries /
+ *      Reset / SetAverageBits / Next + restic.Hash in FileSaver.saveFile) -- */
+/* chunker.NewWithBoundaries(rd, pol, min, max) + SetAverageBits(avg_bits) */
+int vs_cdc_open(int device, uint64_t pol, uint32_t min_size, uint32_t max_size,
+                uint32_t avg_bits, vs_cdc **h);
+/* Chunker.Reset / ResetWithBoundaries: new stream, same device buffers */
+int vs_cdc_reset(vs_cdc *h, uint64_t pol, uint32_t min_size, uint32_t max_size,
+                 uint32_t avg_bits);
+/* Append n host bytes of the stream (the io.Reader's output); final = 1 at EOF.
+ * Work is batched: chunks become available once their cut is determined. */
+int vs_cdc_feed(vs_cdc *h, const void *buf, size_t n, int final);
+/* Chunker.Next: copy up to cap ready chunks (with blob IDs) into out.
+ * Returns VS_OK with *n_out > 0, VS_OK with *n_out == 0 when more input is
+ * needed, or VS_EOF once the final chunk has been returned (io.EOF). */
+int vs_cdc_next(vs_cdc *h, vs_chunk *out, size_t cap, size_t *n_out);
+void vs_cdc_close(vs_cdc *h);
+/* Bytes staged on the device per pipeline batch (default 256 MiB). */
+int vs_cdc_set_batch_bytes(vs_cdc *h, uint64_t bytes);
+
+/* ---- device-resident batch API (data already in HBM) ------------------
+ * Chunks a device byte range that begins at a chunk boundary.  dev_data
+ * points at stream offset `origin`; own_lo/own_hi are stream offsets (the
+ * byte range this call owns); data must cover [own_lo - 63, own_hi + max - 1)
+ * clipped to the stream, and final = 1 when origin + len is the stream end.
+ * Multi-GPU: each rank scans its own byte range, exchanges the exit offset of
+ * its last chunk (vs_cdc_stitch) and finishes; see DESIGN.md section 6. */
+int vs_cdc_set_stream(vs_cdc *h, void *hip_stream); /* NULL = handle's own stream */
+int vs_cdc_scan(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t origin,
+                uint64_t own_lo, uint64_t own_hi, int final);
+/* Selects cuts given the true start of the first chunk (entry).  *exit_pos =
+ * start of the first chunk at or beyond own_hi (or the stream end);
+ * *complete = 0 when a chunk's cut depends on bytes not yet supplied. */
+int vs_cdc_stitch(vs_cdc *h, uint64_t entry, uint64_t *exit_pos, int *complete);
+/* Emits the chunk list, computes Cut values and SHA-256 blob IDs on device. */
+int vs_cdc_finish(vs_cdc *h, uint64_t *n_chunks);
+/* scan + stitch(own_lo) + finish for a single device (own range = whole buffer). */
+int vs_cdc_process(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t origin, int final,
+                   uint64_t *n_chunks, uint64_t *consumed);
+/* Copy chunks [first, first+n) of the last finish() to host. */
+int vs_cdc_get_chunks(vs_cdc *h, uint64_t first, uint64_t n, vs_chunk *out);
+/* Accumulated device time (ms) per pipeline stage since the last reset of the
+ * timers, measured with HIP events on the handle's stream when enabled.
+ * stage: 0 fingerprint, 1 select, 2 sha256, 3 other. */
+int vs_cdc_timing(vs_cdc *h, int enable, double ms_out[4], uint64_t launches_out[4]);
+
+/* ---- batched SHA-256 (restic.Hash over many blobs; C5 small files) ----
+ * dev_buf: device bytes; off/len: device arrays of n entries; out: device
+ * array of n*32 bytes.  Blob i = dev_buf[off[i] : off[i]+len[i]]. */
+int vs_sha256_batch_device(int device, const void *dev_buf, const uint64_t *dev_off,
+                           const uint32_t *dev_len, size_t n, uint8_t *dev_out,
+                           void *hip_stream);
+/* Host-memory convenience form (copies in and out). */
+int vs_sha256_batch(int device, const void *buf, size_t buf_len, const uint64_t *off,
+                    const uint32_t *len, size_t n, uint8_t (*out)[32]);
+
+/* ---- device utilities for benches and tests --------------------------- */
+/* Fill dev_out[0:n] with bytes [off, off+n) of the synthetic splitmix64
+ * volume stream. */
+int vs_synth_fill_device(int device, uint64_t seed, uint64_t off, uint64_t n, void *dev_out,
+                         void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VSGPU_H */

@@ -1,0 +1,83 @@
+"""ctypes loader for the C oracle (oracle/build/liboracle.so) -- test infrastructure only."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
+        L = ctypes.CDLL(ORACLE_SO)
+        u64, vp, ci = ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int
+        L.ref_chunk_all.restype = ctypes.c_int64
+        L.ref_chunk_all.argtypes = [vp, u64, u64, u64, u64, ci, vp, vp, vp, u64]
+        L.ref_cdc_hash.restype = ctypes.c_int64
+        L.ref_cdc_hash.argtypes = [vp, u64, u64, u64, u64, ci, ci, vp, vp, vp, vp, u64]
+        L.ref_synth_fill.argtypes = [u64, u64, u64, vp]
+        L.ref_sha256.argtypes = [vp, u64, vp]
+        L.ref_sha256_fast.argtypes = [vp, u64, vp]
+        L.ref_have_openssl.restype = ci
+        L.ref_pol_deg.argtypes = [u64]
+        L.ref_pol_mod.restype = u64
+        L.ref_pol_mod.argtypes = [u64, u64]
+        L.ref_tables.argtypes = [u64, vp, vp]
+        L.ref_window_fp.restype = u64
+        L.ref_window_fp.argtypes = [vp, u64, u64]
+        L.ref_rsync_checksum1.restype = ctypes.c_uint32
+        L.ref_rsync_checksum1.argtypes = [vp, ctypes.c_int32]
+        L.ref_rsync_sum_sizes.argtypes = [ctypes.c_int64, ctypes.c_int32] + [ctypes.POINTER(ctypes.c_int32)] * 4
+        _lib = L
+    return _lib
+
+
+def chunk_all(data: np.ndarray, pol: int, mn: int, mx: int, avg_bits: int):
+    d = np.ascontiguousarray(data, dtype=np.uint8)
+    cap = len(d) // max(1, mn) + 8
+    s = np.zeros(cap, np.uint64)
+    ln = np.zeros(cap, np.uint64)
+    c = np.zeros(cap, np.uint64)
+    n = lib().ref_chunk_all(d.ctypes.data if len(d) else None, len(d), pol, mn, mx, avg_bits,
+                            s.ctypes.data, ln.ctypes.data, c.ctypes.data, cap)
+    if n < 0:
+        raise ValueError("oracle rejected the chunker parameters")
+    return [(int(s[i]), int(ln[i]), int(c[i])) for i in range(n)]
+
+
+def cdc_hash(data: np.ndarray, pol: int, mn: int, mx: int, avg_bits: int, n_hash: int = 0):
+    d = np.ascontiguousarray(data, dtype=np.uint8)
+    cap = len(d) // max(1, mn) + 8
+    s = np.zeros(cap, np.uint64)
+    ln = np.zeros(cap, np.uint64)
+    c = np.zeros(cap, np.uint64)
+    ids = np.zeros((cap, 32), np.uint8)
+    n = lib().ref_cdc_hash(d.ctypes.data if len(d) else None, len(d), pol, mn, mx, avg_bits,
+                           n_hash, s.ctypes.data, ln.ctypes.data, c.ctypes.data, ids.ctypes.data,
+                           cap)
+    if n < 0:
+        raise ValueError("oracle failed")
+    return [(int(s[i]), int(ln[i]), int(c[i]), bytes(ids[i]).hex()) for i in range(n)]
+
+
+def synth(seed: int, off: int, n: int) -> np.ndarray:
+    out = np.zeros(max(n, 1), np.uint8)
+    lib().ref_synth_fill(seed, off, n, out.ctypes.data)
+    return out[:n]
+
+
+def sha256(data) -> bytes:
+    d = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
+    out = np.zeros(32, np.uint8)
+    lib().ref_sha256(d.ctypes.data if len(d) else None, len(d), out.ctypes.data)
+    return bytes(out)

@@ -1,0 +1,85 @@
+"""CPU tests of the product library's C ABI surface (no compute without a GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import cdc_ref as P
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "vsgpu.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vs_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_loads_and_exports_header_symbols():
+    from volsync_amd import _lib
+    so = _lib.LIB_PATH
+    assert os.path.exists(so)
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (vs_[a-z0-9_]+)", out))
+    want = set(header_functions())
+    assert want, "no declarations parsed"
+    assert want <= exported, f"missing: {sorted(want - exported)}"
+    # nothing product-facing is exported that the header does not declare
+    assert exported <= want, f"undeclared exports: {sorted(exported - want)}"
+
+
+def test_library_links_no_oracle():
+    from volsync_amd import _lib
+    out = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in out
+    strings = open(_lib.LIB_PATH, "rb").read()
+    assert b"liboracle" not in strings and b"ref_chunk_all" not in strings
+
+
+def test_pol_helpers_match_oracle():
+    from volsync_amd import Pol
+    p = Pol(P.TEST_POL)
+    assert p.Deg() == 53
+    assert p.Irreducible()
+    assert not Pol(P.TEST_POL ^ 2).Irreducible()
+    out, mod = p.tables()
+    from tests import oracle_lib as O
+    ro = np.zeros(256, np.uint64)
+    rm = np.zeros(256, np.uint64)
+    O.lib().ref_tables(P.TEST_POL, ro.ctypes.data, rm.ctypes.data)
+    assert out == [int(x) for x in ro] and mod == [int(x) for x in rm]
+
+
+def test_random_polynomials_irreducibility_agrees():
+    from volsync_amd import Pol
+    rng = np.random.default_rng(7)
+    for _ in range(40):
+        p = int(rng.integers(0, 1 << 53, dtype=np.uint64)) | (1 << 53) | 1
+        assert Pol(p).Irreducible() == P.pol_irreducible(p)
+
+
+def test_pol_zero_is_rejected_like_upstream():
+    from volsync_amd import _lib
+    out = (ctypes.c_uint64 * 256)()
+    mod = (ctypes.c_uint64 * 256)()
+    rc = _lib.lib.vs_pol_tables(0, out, mod)
+    assert rc == _lib.VS_ERR_POLY
+    assert "not initialized" in _lib.last_error()
+
+
+def test_no_cpu_fallback_without_device():
+    from volsync_amd import _lib
+    if _lib.device_count() > 0:
+        pytest.skip("a GPU is present")
+    h = ctypes.c_void_p()
+    rc = _lib.lib.vs_cdc_open(0, P.TEST_POL, P.MIN_SIZE, P.MAX_SIZE, 20, ctypes.byref(h))
+    assert rc == _lib.VS_ERR_NO_DEVICE
+    assert not h.value
+    import volsync_amd
+    with pytest.raises(volsync_amd.VsError):
+        list(volsync_amd.New(__import__("io").BytesIO(b"x" * 100), P.TEST_POL))

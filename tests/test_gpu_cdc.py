@@ -1,0 +1,213 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and fixtures.
+
+Bar: bit-exact chunk boundaries (Start, Length), Cut values and SHA-256 blob IDs.
+"""
+import hashlib
+import io
+import os
+
+import numpy as np
+import pytest
+
+from oracle import cdc_ref as P
+from tests import golden_util as G
+from tests import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+MIN, MAX = P.MIN_SIZE, P.MAX_SIZE
+
+
+def to_dev(arr: np.ndarray):
+    import torch
+    t = torch.empty(max(len(arr), 16), dtype=torch.uint8, device="cuda")
+    if len(arr):
+        t[: len(arr)].copy_(torch.from_numpy(np.ascontiguousarray(arr)))
+    torch.cuda.synchronize()
+    return t
+
+
+def dev_chunks(data: np.ndarray, pol, mn, mx, ab, dc=None):
+    from volsync_amd import DeviceChunker
+    own = dc is None
+    dc = dc or DeviceChunker(pol, mn, mx, ab)
+    t = to_dev(data)
+    n, consumed = dc.process(t.data_ptr(), len(data), 0, True)
+    assert consumed == len(data)
+    ch = dc.chunks(0, n)
+    if own:
+        dc.close()
+    return [(c.Start, c.Length, c.Cut, c.ID.hex()) for c in ch]
+
+
+@pytest.mark.parametrize("path", G.fixtures(), ids=lambda p: os.path.basename(p))
+def test_device_vs_golden(gpu, path):
+    doc = G.load(path)
+    data = G.make_input(doc["input"]) if "1g" not in path else O.synth(1, 0, 1 << 30)
+    pol, mn, mx, ab = G.params(doc)
+    assert dev_chunks(data, pol, mn, mx, ab) == G.expected(doc)
+
+
+@pytest.mark.parametrize("path", [p for p in G.fixtures() if "1g" not in p and "eof_" not in p],
+                         ids=lambda p: os.path.basename(p))
+def test_stream_chunker_vs_golden(gpu, path):
+    """The Chunker mirror (New/Next) with small reads and batches: multi-batch carry-over."""
+    from volsync_amd import EOF, NewWithBoundaries
+    doc = G.load(path)
+    data = G.make_input(doc["input"])
+    pol, mn, mx, ab = G.params(doc)
+    ck = NewWithBoundaries(io.BytesIO(data.tobytes()), pol, mn, mx, read_size=3 << 20,
+                           batch_bytes=5 << 20)
+    ck.SetAverageBits(ab)
+    got = []
+    buf = bytearray()
+    while True:
+        try:
+            c = ck.Next(buf)
+        except EOF:
+            break
+        assert bytes(c.Data) == data[c.Start:c.Start + c.Length].tobytes()
+        assert hashlib.sha256(c.Data).digest() == c.ID
+        got.append((c.Start, c.Length, c.Cut, c.ID.hex()))
+    ck.close()
+    assert got == G.expected(doc)
+
+
+def test_stream_pol_zero_error(gpu):
+    import volsync_amd
+    ck = volsync_amd.New(io.BytesIO(b"abc"), 0)
+    with pytest.raises(volsync_amd.VsError, match="not initialized"):
+        ck.Next()
+
+
+def test_reader_error_propagates(gpu):
+    import volsync_amd
+
+    class Bad(io.RawIOBase):
+        def read(self, n=-1):
+            raise IOError("disk on fire")
+
+    ck = volsync_amd.New(Bad(), P.TEST_POL)
+    with pytest.raises(IOError, match="disk on fire"):
+        ck.Next()
+
+
+@pytest.mark.parametrize("seed,n,mn,mx,ab", [
+    (31, 3 << 20, 1024, 4096, 10),
+    (32, (7 << 20) + 13, 4096, 16384, 12),
+    (33, 20 << 20, 64, 64, 5),              # min == max == window: every chunk forced
+    (34, 5 << 20, 2048, 1 << 20, 16),
+    (35, 33 << 20, 65536, 1 << 20, 14),     # many segments
+    (36, 9 << 20, 1024, 2048, 30),          # rare candidates -> all forced
+    (37, 6 << 20, 4096, 8192, 33),          # 64-bit splitmask path
+])
+def test_device_vs_oracle_random(gpu, seed, n, mn, mx, ab):
+    data = O.synth(seed, 0, n)
+    assert dev_chunks(data, P.TEST_POL, mn, mx, ab) == O.cdc_hash(data, P.TEST_POL, mn, mx, ab)
+
+
+def test_dense_zero_volume_overflows_pool(gpu):
+    """An all-zero 96 MiB volume: every position is a candidate; exercises the
+    dense-strip bitmask pool and its regrow path."""
+    data = np.zeros(96 << 20, np.uint8)
+    data[50 << 20:(50 << 20) + 1000] = 7
+    assert dev_chunks(data, P.TEST_POL, MIN, MAX, 20) == O.cdc_hash(data, P.TEST_POL, MIN, MAX, 20)
+
+
+def test_periodic_data_small_min(gpu):
+    base = O.synth(40, 0, 777)
+    data = np.tile(base, (4 << 20) // 777 + 1)[: 4 << 20].copy()
+    assert dev_chunks(data, P.TEST_POL, 1024, 8192, 6) == O.cdc_hash(data, P.TEST_POL, 1024, 8192, 6)
+
+
+def test_handle_reuse_across_sizes(gpu):
+    from volsync_amd import DeviceChunker
+    dc = DeviceChunker(P.TEST_POL, 4096, 16384, 12)
+    for seed, n in [(50, 8 << 20), (51, 100), (52, 1 << 20), (53, 0), (54, 12 << 20)]:
+        data = O.synth(seed, 0, n)
+        assert dev_chunks(data, P.TEST_POL, 4096, 16384, 12, dc=dc) == \
+            O.cdc_hash(data, P.TEST_POL, 4096, 16384, 12)
+    dc.close()
+
+
+def test_sharded_equals_single(gpu):
+    """Byte-range shards with halos + exit exchange == one-device result (the
+    multi-GPU protocol of volsync_amd.shard, run in one process)."""
+    from volsync_amd import DeviceChunker
+    from volsync_amd.shard import ShardSpec, run_shards_local
+    n = 40 << 20
+    mn, mx, ab = 16384, 1 << 20, 14
+    data = O.synth(60, 0, n)
+    want = O.cdc_hash(data, P.TEST_POL, mn, mx, ab)
+    for world in (2, 3, 5):
+        specs = ShardSpec.split(n, world, mx)
+        handles = [DeviceChunker(P.TEST_POL, mn, mx, ab) for _ in range(world)]
+        bufs = [to_dev(data[s.data_lo:s.data_hi]) for s in specs]
+        got = run_shards_local(handles, specs, [b.data_ptr() for b in bufs])
+        for h in handles:
+            h.close()
+        assert [(c.Start, c.Length, c.Cut, c.ID.hex()) for c in got] == want
+
+
+def test_sha256_batch_vs_hashlib(gpu):
+    from volsync_amd import sha256_batch
+    rng = np.random.default_rng(3)
+    buf = O.synth(70, 0, 3 << 20).tobytes()
+    offs, lens = [], []
+    for n in list(range(0, 130)) + [4096, 65536, 65537, 100000, 1 << 20]:
+        o = int(rng.integers(0, len(buf) - n))
+        offs.append(o)
+        lens.append(n)
+    got = sha256_batch(buf, offs, lens)
+    for o, n, g in zip(offs, lens, got):
+        assert g == hashlib.sha256(buf[o:o + n]).digest()
+
+
+def test_synth_device_matches_oracle(gpu):
+    import torch
+    from volsync_amd import synth_fill_device
+    for seed, off, n in [(1, 0, 1 << 20), (9, 13, 100001), (2, (1 << 36) - 5, 4099)]:
+        t = torch.empty(n, dtype=torch.uint8, device="cuda")
+        synth_fill_device(t.data_ptr(), seed, off, n)
+        torch.cuda.synchronize()
+        assert (t.cpu().numpy() == O.synth(seed, off, n)).all()
+
+
+def test_full_size_c2_properties(gpu):
+    """Config C2 size (64 GiB, seed 2, default parameters) through properties:
+    chunks tile the volume, lengths obey min/max, Cut & mask == 0 unless forced,
+    and sampled chunks match the oracle (cut rule from the chunk start) and
+    hashlib (blob ID)."""
+    import torch
+    from volsync_amd import DeviceChunker, synth_fill_device
+    n = 64 << 30
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    synth_fill_device(t.data_ptr(), 2, 0, n)
+    dc = DeviceChunker(P.TEST_POL, MIN, MAX, 20)
+    nch, consumed = dc.process(t.data_ptr(), n, 0, True)
+    assert consumed == n
+    ch = dc.chunks(0, nch)
+    dc.close()
+    assert 40000 < nch < 48000
+    pos = 0
+    for i, c in enumerate(ch):
+        assert c.Start == pos
+        pos += c.Length
+        if i < nch - 1:
+            assert MIN <= c.Length <= MAX
+            if c.Length < MAX:
+                assert c.Cut & ((1 << 20) - 1) == 0
+    assert pos == n
+    rng = np.random.default_rng(0)
+    picks = sorted(set([0, nch - 1] + [int(x) for x in rng.integers(0, nch, 12)]))
+    for i in picks:
+        c = ch[i]
+        hi = min(n, c.Start + MAX + 64)
+        host = t[c.Start:hi].cpu().numpy()
+        final = hi == n
+        ref = O.cdc_hash(host, P.TEST_POL, MIN, MAX, 20)[0]
+        if not final and ref[1] >= len(host):
+            continue
+        assert (c.Start + ref[0], ref[1], ref[2], ref[3]) == (c.Start, c.Length, c.Cut, c.ID.hex())
+    del t
+    torch.cuda.empty_cache()

@@ -1,0 +1,108 @@
+"""ctypes binding of the product library volsync_amd/lib/libvsgpu.so (C ABI: include/vsgpu.h).
+
+There is no CPU fallback: importing works without a GPU (so the ABI can be
+inspected), but every compute call fails with VsError(VS_ERR_NO_DEVICE) unless
+a gfx950 device is present, and a missing library raises ImportError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libvsgpu.so")
+
+VS_OK = 0
+VS_EOF = 1
+VS_ERR_ARG = -1
+VS_ERR_POLY = -2
+VS_ERR_NO_DEVICE = -3
+VS_ERR_NOMEM = -4
+VS_ERR_STATE = -5
+VS_ERR_HIP = -6
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+vp = ctypes.c_void_p
+c_u64 = ctypes.c_uint64
+c_u32 = ctypes.c_uint32
+c_int = ctypes.c_int
+c_size = ctypes.c_size_t
+
+
+class VsChunk(ctypes.Structure):
+    _fields_ = [("start", c_u64), ("length", c_u64), ("cut", c_u64), ("id", ctypes.c_uint8 * 32)]
+
+
+class VsError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"vsgpu error {code}: {msg}")
+        self.code = code
+
+
+def _one_hip_runtime() -> None:
+    """PyTorch-ROCm bundles its own libamdhip64 (SONAME libamdhip64.so.7) and
+    loads it by file name.  If libvsgpu.so pulled /opt/rocm's copy in first, the
+    process would hold two HIP runtimes and torch's would find no GPU.  Loading
+    torch first makes libvsgpu.so bind to the already-loaded runtime (same
+    SONAME), so device pointers, streams and events are shared."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
+def _load() -> ctypes.CDLL:
+    _one_hip_runtime()
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the HIP extension is the only implementation; there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "vs_last_error": (ctypes.c_char_p, []),
+        "vs_version": (ctypes.c_char_p, []),
+        "vs_device_count": (c_int, []),
+        "vs_pol_deg": (c_int, [c_u64]),
+        "vs_pol_irreducible": (c_int, [c_u64]),
+        "vs_pol_tables": (c_int, [c_u64, u64p, u64p]),
+        "vs_cdc_open": (c_int, [c_int, c_u64, c_u32, c_u32, c_u32, ctypes.POINTER(vp)]),
+        "vs_cdc_reset": (c_int, [vp, c_u64, c_u32, c_u32, c_u32]),
+        "vs_cdc_feed": (c_int, [vp, vp, c_size, c_int]),
+        "vs_cdc_next": (c_int, [vp, ctypes.POINTER(VsChunk), c_size, ctypes.POINTER(c_size)]),
+        "vs_cdc_close": (None, [vp]),
+        "vs_cdc_set_batch_bytes": (c_int, [vp, c_u64]),
+        "vs_cdc_set_stream": (c_int, [vp, vp]),
+        "vs_cdc_scan": (c_int, [vp, vp, c_u64, c_u64, c_u64, c_u64, c_int]),
+        "vs_cdc_stitch": (c_int, [vp, c_u64, u64p, ctypes.POINTER(c_int)]),
+        "vs_cdc_finish": (c_int, [vp, u64p]),
+        "vs_cdc_process": (c_int, [vp, vp, c_u64, c_u64, c_int, u64p, u64p]),
+        "vs_cdc_get_chunks": (c_int, [vp, c_u64, c_u64, ctypes.POINTER(VsChunk)]),
+        "vs_cdc_timing": (c_int, [vp, c_int, ctypes.POINTER(ctypes.c_double), u64p]),
+        "vs_sha256_batch_device": (c_int, [c_int, vp, vp, vp, c_size, vp, vp]),
+        "vs_sha256_batch": (c_int, [c_int, vp, c_size, vp, vp, c_size, vp]),
+        "vs_synth_fill_device": (c_int, [c_int, c_u64, c_u64, c_u64, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def last_error() -> str:
+    return lib.vs_last_error().decode(errors="replace")
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise VsError(rc, last_error())
+    return rc
+
+
+def device_count() -> int:
+    return int(lib.vs_device_count())

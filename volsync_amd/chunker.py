@@ -1,0 +1,267 @@
+"""Host-side mirror of restic's chunker API over the gfx950 C ABI.
+
+Mirrors github.com/restic/chunker@v0.4.0 (the module restic v0.13.1 uses;
+fetched by /root/reference/mover-restic/Dockerfile:8-11, not vendored):
+
+    New(rd, pol) / NewWithBoundaries(rd, pol, min, max)
+    (*Chunker).Reset / ResetWithBoundaries / SetAverageBits
+    (*Chunker).Next(data []byte) (Chunk, error)     -> io.EOF at the end
+    type Chunk struct{ Start, Length uint; Cut uint64; Data []byte }
+
+plus the blob ID restic computes for every chunk (internal/restic/id.go Hash =
+sha256.Sum256), returned as Chunk.ID so FileSaver.saveFile can hand it to
+Repository.SaveBlob(..., id, ...) pre-computed.
+
+Names, argument meaning and error behaviour follow the Go package:
+pol == 0 is accepted by New and fails in Next() with "tables for polynomial
+computation not initialized"; reader errors propagate; Next() signals the end
+with EOF (an EOFError, the io.EOF analogue).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Iterator, List, Optional
+
+from . import _lib
+from ._lib import VsChunk, VsError, check, lib
+
+KiB = 1024
+MiB = 1024 * KiB
+MinSize = 512 * KiB
+MaxSize = 8 * MiB
+AverageBits = 20
+TestPol = 0x3DA3358B4DC173  # chunker_test.go testPol
+
+__all__ = ["Chunk", "Chunker", "EOF", "New", "NewWithBoundaries", "Pol", "DeviceChunker",
+           "MinSize", "MaxSize", "KiB", "MiB"]
+
+
+class EOF(EOFError):
+    """io.EOF: the stream is exhausted."""
+
+
+class Pol(int):
+    """chunker polynomials.go `type Pol uint64` (host-side helpers)."""
+
+    def Deg(self) -> int:
+        return int(lib.vs_pol_deg(ctypes.c_uint64(int(self))))
+
+    def Irreducible(self) -> bool:
+        return bool(lib.vs_pol_irreducible(ctypes.c_uint64(int(self))))
+
+    def tables(self):
+        out = (ctypes.c_uint64 * 256)()
+        mod = (ctypes.c_uint64 * 256)()
+        check(lib.vs_pol_tables(int(self), out, mod))
+        return list(out), list(mod)
+
+
+@dataclass
+class Chunk:
+    Start: int
+    Length: int
+    Cut: int
+    Data: Optional[bytes] = None
+    ID: bytes = b""  # restic blob ID (SHA-256 of Data)
+
+
+def _chunk_from(c: VsChunk, data=None) -> Chunk:
+    return Chunk(int(c.start), int(c.length), int(c.cut), data, bytes(c.id))
+
+
+class Chunker:
+    """A restic chunker whose fingerprinting, cut selection and blob hashing run
+    on the GPU.  Not goroutine-/thread-safe (same contract as the Go type)."""
+
+    def __init__(self, rd, pol: int, min_size: int = MinSize, max_size: int = MaxSize,
+                 device: int = 0, read_size: int = 64 * MiB, batch_bytes: int = 256 * MiB):
+        self._h = ctypes.c_void_p()
+        self._device = device
+        self._read_size = read_size
+        self._batch_bytes = batch_bytes
+        self._avg_bits = AverageBits
+        self.ResetWithBoundaries(rd, pol, min_size, max_size)
+
+    # ---- chunker.go API ---------------------------------------------------
+    def Reset(self, rd, pol: int) -> None:
+        self.ResetWithBoundaries(rd, pol, MinSize, MaxSize)
+
+    def ResetWithBoundaries(self, rd, pol: int, min_size: int, max_size: int) -> None:
+        self._rd = rd
+        self.pol = Pol(pol)
+        self.MinSize = int(min_size)
+        self.MaxSize = int(max_size)
+        self._avg_bits = AverageBits
+        self._buf = bytearray()   # host copy of bytes not yet returned (for Chunk.Data)
+        self._borigin = 0          # stream offset of _buf[0]
+        self._eof_fed = False
+        self._configured = False
+
+    def SetAverageBits(self, average_bits: int) -> None:
+        self._avg_bits = int(average_bits)
+        self._configured = False
+
+    def Next(self, data: Optional[bytearray] = None) -> Chunk:
+        if self.pol == 0:
+            raise VsError(_lib.VS_ERR_POLY, "tables for polynomial computation not initialized")
+        self._configure()
+        one = (VsChunk * 1)()
+        n = ctypes.c_size_t(0)
+        while True:
+            rc = lib.vs_cdc_next(self._h, one, 1, ctypes.byref(n))
+            if rc == _lib.VS_EOF:
+                raise EOF()
+            check(rc)
+            if n.value:
+                break
+            self._pump()
+        c = one[0]
+        lo = int(c.start) - self._borigin
+        payload = bytes(self._buf[lo:lo + int(c.length)])
+        del self._buf[:lo + int(c.length)]
+        self._borigin = int(c.start) + int(c.length)
+        if data is not None:          # Go: Data = append(data[:0], ...)
+            data[:] = payload
+            payload = data
+        return _chunk_from(c, payload)
+
+    def __iter__(self) -> Iterator[Chunk]:
+        while True:
+            try:
+                yield self.Next()
+            except EOF:
+                return
+
+    def close(self) -> None:
+        if self._h:
+            lib.vs_cdc_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- internals ------------------------------------------------------------
+    def _configure(self) -> None:
+        if self._configured:
+            return
+        if not self._h:
+            check(lib.vs_cdc_open(self._device, int(self.pol), self.MinSize, self.MaxSize,
+                                  self._avg_bits, ctypes.byref(self._h)))
+        else:
+            check(lib.vs_cdc_reset(self._h, int(self.pol), self.MinSize, self.MaxSize,
+                                   self._avg_bits))
+        check(lib.vs_cdc_set_batch_bytes(self._h, self._batch_bytes))
+        self._configured = True
+
+    def _pump(self) -> None:
+        if self._eof_fed:
+            raise VsError(_lib.VS_ERR_STATE, "chunk stream stalled after EOF")
+        block = self._rd.read(self._read_size)   # reader errors propagate
+        if not block:
+            check(lib.vs_cdc_feed(self._h, None, 0, 1))
+            self._eof_fed = True
+            return
+        block = bytes(block)
+        self._buf += block
+        buf = ctypes.create_string_buffer(block, len(block))
+        check(lib.vs_cdc_feed(self._h, buf, len(block), 0))
+
+
+def New(rd, pol: int, **kw) -> Chunker:
+    return Chunker(rd, pol, MinSize, MaxSize, **kw)
+
+
+def NewWithBoundaries(rd, pol: int, min_size: int, max_size: int, **kw) -> Chunker:
+    return Chunker(rd, pol, min_size, max_size, **kw)
+
+
+class DeviceChunker:
+    """Chunks device-resident byte ranges (data already in HBM): the batch API
+    used by bench.py and the multi-GPU path."""
+
+    def __init__(self, pol: int = TestPol, min_size: int = MinSize, max_size: int = MaxSize,
+                 avg_bits: int = AverageBits, device: int = 0):
+        self.device = device
+        self._h = ctypes.c_void_p()
+        check(lib.vs_cdc_open(device, int(pol), int(min_size), int(max_size), int(avg_bits),
+                              ctypes.byref(self._h)))
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, hip_stream: int) -> None:
+        check(lib.vs_cdc_set_stream(self._h, ctypes.c_void_p(hip_stream or None)))
+
+    def process(self, dev_ptr: int, length: int, origin: int = 0, final: bool = True):
+        n = ctypes.c_uint64(0)
+        consumed = ctypes.c_uint64(0)
+        check(lib.vs_cdc_process(self._h, ctypes.c_void_p(dev_ptr), length, origin,
+                                 1 if final else 0, ctypes.byref(n), ctypes.byref(consumed)))
+        return int(n.value), int(consumed.value)
+
+    def scan(self, dev_ptr: int, length: int, origin: int, own_lo: int, own_hi: int,
+             final: bool) -> None:
+        check(lib.vs_cdc_scan(self._h, ctypes.c_void_p(dev_ptr), length, origin, own_lo, own_hi,
+                              1 if final else 0))
+
+    def stitch(self, entry: int):
+        ex = ctypes.c_uint64(0)
+        complete = ctypes.c_int(0)
+        check(lib.vs_cdc_stitch(self._h, entry, ctypes.byref(ex), ctypes.byref(complete)))
+        return int(ex.value), bool(complete.value)
+
+    def finish(self) -> int:
+        n = ctypes.c_uint64(0)
+        check(lib.vs_cdc_finish(self._h, ctypes.byref(n)))
+        return int(n.value)
+
+    def chunks(self, first: int = 0, n: Optional[int] = None, total: Optional[int] = None
+               ) -> List[Chunk]:
+        if n is None:
+            n = (total or 0) - first
+        if n <= 0:
+            return []
+        arr = (VsChunk * n)()
+        check(lib.vs_cdc_get_chunks(self._h, first, n, arr))
+        return [_chunk_from(c) for c in arr]
+
+    def timing(self, enable: bool = True):
+        ms = (ctypes.c_double * 4)()
+        cnt = (ctypes.c_uint64 * 4)()
+        check(lib.vs_cdc_timing(self._h, 1 if enable else 0, ms, cnt))
+        return list(ms), list(cnt)
+
+    def close(self) -> None:
+        if self._h:
+            lib.vs_cdc_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def sha256_batch(buf: bytes, offs, lens, device: int = 0) -> List[bytes]:
+    """restic.Hash over many blobs of one host buffer, on the GPU."""
+    import numpy as np
+    n = len(offs)
+    o = np.ascontiguousarray(offs, dtype=np.uint64)
+    ln = np.ascontiguousarray(lens, dtype=np.uint32)
+    out = np.zeros((max(n, 1), 32), dtype=np.uint8)
+    b = np.frombuffer(bytes(buf), dtype=np.uint8) if len(buf) else np.zeros(1, np.uint8)
+    check(lib.vs_sha256_batch(device, b.ctypes.data, len(buf), o.ctypes.data, ln.ctypes.data, n,
+                              out.ctypes.data))
+    return [bytes(out[i]) for i in range(n)]
+
+
+def synth_fill_device(dev_ptr: int, seed: int, off: int, n: int, device: int = 0,
+                      stream: Optional[int] = None) -> None:
+    check(lib.vs_synth_fill_device(device, seed, off, n, ctypes.c_void_p(dev_ptr),
+                                   ctypes.c_void_p(stream or None)))

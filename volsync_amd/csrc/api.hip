@@ -1,0 +1,779 @@
+// api.hip -- the C ABI (include/vsgpu.h): handle, device buffers, pipeline
+// orchestration and the streaming Chunker surface.
+//
+// Pipeline per batch:
+//   fingerprint (fingerprint.hip) -> candidate compaction + speculative
+//   segment walks + boundary stitch + emit (select.hip) -> Cut values ->
+//   longest-first order -> SHA-256 blob IDs (sha256.hip).
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "internal.hpp"
+
+#define VS_API extern "C" __attribute__((visibility("default")))
+
+namespace vsgpu {
+
+static thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 256);
+        if (hipMalloc(&p, want) != hipSuccess) {
+            p = nullptr;
+            (void)hipGetLastError();
+            return fail(VS_ERR_NOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
+        }
+        cap = want;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T *as() const {
+        return (T *)p;
+    }
+};
+
+// strip = 64 * G with G % 3 == 0 (fingerprint.hip rotates three group buffers)
+constexpr uint32_t kStrip = 12288;
+
+enum Stage { kStFp = 0, kStSel = 1, kStSha = 2, kStOther = 3 };
+
+}  // namespace vsgpu
+
+using namespace vsgpu;
+
+struct vs_cdc {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own = nullptr;
+    // parameters
+    uint64_t pol = 0;
+    uint32_t min_size = 0, max_size = 0, avg_bits = 0;
+    uint32_t idx_shift = 0;
+    uint64_t out_h[256], mod_h[256], out8_h[256];
+    DevBuf tabs;  // [mod 256][out8 256]
+    // fingerprint / candidate index
+    DevBuf counts, offs, dslot, pool, flags, cstart, partials, compact;
+    uint32_t pool_cap = 0;
+    uint64_t nstrips = 0, base = 0, scan_end = 0;
+    const uint8_t *data = nullptr;
+    uint64_t dlen = 0, origin = 0, own_lo = 0, own_hi = 0;  // data offsets for own_*
+    bool final_ = false, final_eof = false;
+    // segments
+    uint32_t nseg = 0, maxc = 0;
+    uint64_t seg_len = 0;
+    DevBuf spec_cut, spec_n, spec_exit, st_cut, st_n, st_merge, st_total, exit_a, exit_b,
+        seg_off;
+    uint64_t *exit_old = nullptr, *exit_new = nullptr;
+    uint64_t entry = 0;  // data offset
+    // chunks
+    DevBuf ch_start, ch_end, ch_cut, ch_id, order, hist, n_out;
+    uint64_t n_chunks = 0;
+    int state = 0;  // 0 idle, 1 scanned, 2 stitched, 3 finished
+    // host staging
+    uint64_t *pinned = nullptr;  // 8 u64 of pinned host memory
+    // streaming
+    DevBuf sbuf[2];
+    int scur = 0;
+    uint64_t sfill = 0, sorigin = 0, batch_bytes = 256ull << 20;
+    std::deque<vs_chunk> ready;
+    bool final_fed = false;
+    // timing
+    bool timing = false;
+    struct Pend {
+        int stage;
+        hipEvent_t a, b;
+    };
+    std::vector<Pend> pend;
+    std::vector<hipEvent_t> ev_pool;
+    double ms[4] = {0, 0, 0, 0};
+    uint64_t launches[4] = {0, 0, 0, 0};
+};
+
+namespace vsgpu {
+
+static int set_dev(vs_cdc *h) {
+    if (hipSetDevice(h->device) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(VS_ERR_NO_DEVICE, "hipSetDevice(" + std::to_string(h->device) + ") failed");
+    }
+    return 0;
+}
+
+static hipEvent_t get_event(vs_cdc *h) {
+    if (!h->ev_pool.empty()) {
+        hipEvent_t e = h->ev_pool.back();
+        h->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+struct StageTimer {
+    vs_cdc *h;
+    int st;
+    hipEvent_t a = nullptr;
+    StageTimer(vs_cdc *h_, int st_) : h(h_), st(st_) {
+        if (h->timing) {
+            a = get_event(h);
+            if (a) (void)hipEventRecord(a, h->stream);
+        }
+    }
+    ~StageTimer() {
+        if (a) {
+            hipEvent_t b = get_event(h);
+            if (b) {
+                (void)hipEventRecord(b, h->stream);
+                h->pend.push_back({st, a, b});
+            } else {
+                h->ev_pool.push_back(a);
+            }
+        }
+    }
+};
+
+// call after a stream sync: fold completed event pairs into the totals
+static void drain_timers(vs_cdc *h) {
+    for (auto &p : h->pend) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            h->ms[p.stage] += ms;
+            h->launches[p.stage] += 1;
+        }
+        h->ev_pool.push_back(p.a);
+        h->ev_pool.push_back(p.b);
+    }
+    h->pend.clear();
+}
+
+static int sync_stream(vs_cdc *h) {
+    VS_HIP(hipStreamSynchronize(h->stream));
+    drain_timers(h);
+    return 0;
+}
+
+static int set_params(vs_cdc *h, uint64_t pol, uint32_t min_size, uint32_t max_size,
+                      uint32_t avg_bits) {
+    if (pol == 0) return fail(VS_ERR_POLY, "tables for polynomial computation not initialized");
+    const int deg = pol_deg(pol);
+    if (deg < 40 || deg > 53)
+        return fail(VS_ERR_POLY, "polynomial degree " + std::to_string(deg) +
+                                     " outside [40, 53] (restic draws degree 53)");
+    if (min_size < 64 || max_size < min_size)
+        return fail(VS_ERR_ARG, "need 64 <= min_size <= max_size");
+    if (avg_bits < 1 || avg_bits > 53) return fail(VS_ERR_ARG, "avg_bits must be in [1, 53]");
+    h->pol = pol;
+    h->min_size = min_size;
+    h->max_size = max_size;
+    h->avg_bits = avg_bits;
+    h->idx_shift = (uint32_t)(deg - 40);
+    pol_tables(pol, h->out_h, h->mod_h);
+    pol_out8(pol, h->out_h, h->out8_h);
+    VS_TRY(h->tabs.ensure(512 * sizeof(uint64_t)));
+    VS_HIP(hipMemcpyAsync(h->tabs.as<uint64_t>(), h->mod_h, 256 * 8, hipMemcpyHostToDevice,
+                          h->stream));
+    VS_HIP(hipMemcpyAsync(h->tabs.as<uint64_t>() + 256, h->out8_h, 256 * 8,
+                          hipMemcpyHostToDevice, h->stream));
+    VS_TRY(sync_stream(h));
+    return 0;
+}
+
+static FpArgs fp_args(vs_cdc *h) {
+    FpArgs a{};
+    a.data = h->data;
+    a.dlen = h->dlen;
+    a.base = h->base;
+    a.scan_end = h->scan_end;
+    a.strip = kStrip;
+    a.idx_shift = h->idx_shift;
+    const uint64_t mask = (h->avg_bits >= 64) ? ~0ull : ((1ull << h->avg_bits) - 1);
+    a.mask_lo = (uint32_t)mask;
+    a.mask_hi = (uint32_t)(mask >> 32);
+    a.counts = h->counts.as<uint32_t>();
+    a.offs = h->offs.as<uint32_t>();
+    a.dense_slot = h->dslot.as<uint32_t>();
+    a.pool = h->pool.as<uint32_t>();
+    a.pool_cap = h->pool_cap;
+    a.flags = h->flags.as<uint32_t>();
+    a.pool_next = h->flags.as<uint32_t>() + 1;
+    a.mod_tab = h->tabs.as<uint64_t>();
+    a.out8_tab = h->tabs.as<uint64_t>() + 256;
+    return a;
+}
+
+static SelArgs sel_args(vs_cdc *h) {
+    SelArgs a{};
+    a.base = h->base;
+    a.strip = kStrip;
+    a.nstrips = h->nstrips;
+    a.counts = h->counts.as<uint32_t>();
+    a.offs = h->offs.as<uint32_t>();
+    a.dense_slot = h->dslot.as<uint32_t>();
+    a.pool = h->pool.as<uint32_t>();
+    a.cstart = h->cstart.as<uint32_t>();
+    a.compact = h->compact.as<uint64_t>();
+    a.flags = h->flags.as<uint32_t>();
+    a.min_size = h->min_size;
+    a.max_size = h->max_size;
+    a.scan_end = h->scan_end;
+    a.dlen = h->dlen;
+    a.final_eof = h->final_eof ? 1 : 0;
+    a.own_lo = h->own_lo;
+    a.own_hi = h->own_hi;
+    a.seg_len = h->seg_len;
+    a.nseg = h->nseg;
+    a.maxc = h->maxc;
+    a.spec_cut = h->spec_cut.as<uint64_t>();
+    a.spec_n = h->spec_n.as<uint32_t>();
+    a.spec_exit = h->spec_exit.as<uint64_t>();
+    a.st_cut = h->st_cut.as<uint64_t>();
+    a.st_n = h->st_n.as<uint32_t>();
+    a.st_merge = h->st_merge.as<uint32_t>();
+    a.st_total = h->st_total.as<uint32_t>();
+    a.exit_old = h->exit_old;
+    a.exit_new = h->exit_new;
+    a.entry = h->entry;
+    return a;
+}
+
+// fingerprint pass + candidate index + speculative walks
+static int run_scan_kernels(vs_cdc *h) {
+    const size_t words = kStrip / 32;
+    VS_TRY(h->pool.ensure((size_t)h->pool_cap * words * 4));
+    VS_HIP(hipMemsetAsync(h->flags.p, 0, 4 * sizeof(uint32_t), h->stream));
+    {
+        StageTimer t(h, kStFp);
+        FpArgs a = fp_args(h);
+        const bool wide = h->avg_bits > 32;
+        // strips whose reads stay inside [0, dlen) need no bounds checks
+        uint64_t k_lo = (h->base >= 64) ? 0 : 1;
+        uint64_t k_hi = (h->dlen >= h->base) ? (h->dlen - h->base) / kStrip : 0;
+        k_hi = std::min(k_hi, h->nstrips);
+        k_lo = std::min(k_lo, h->nstrips);
+        if (k_hi < k_lo) k_hi = k_lo;
+        if (k_hi > k_lo) {
+            a.k_first = k_lo;
+            a.k_count = k_hi - k_lo;
+            VS_HIP(launch_fingerprint(a, false, wide, h->stream));
+        }
+        if (k_lo > 0) {
+            a.k_first = 0;
+            a.k_count = k_lo;
+            VS_HIP(launch_fingerprint(a, true, wide, h->stream));
+        }
+        if (h->nstrips > k_hi) {
+            a.k_first = k_hi;
+            a.k_count = h->nstrips - k_hi;
+            VS_HIP(launch_fingerprint(a, true, wide, h->stream));
+        }
+    }
+    {
+        StageTimer t(h, kStSel);
+        SelArgs s = sel_args(h);
+        VS_HIP(launch_compact(s, h->partials.as<uint32_t>(), h->compact.as<uint64_t>(),
+                              h->cstart.as<uint32_t>(), h->stream));
+        VS_HIP(launch_spec_walk(s, h->stream));
+    }
+    return 0;
+}
+
+static int cdc_scan(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t origin,
+                    uint64_t own_lo, uint64_t own_hi, int final) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    if (!dev_data && len) return fail(VS_ERR_ARG, "null device data");
+    if (((uintptr_t)dev_data & 15) != 0) return fail(VS_ERR_ARG, "device data must be 16-byte aligned");
+    if (own_lo < origin || own_hi < own_lo || own_hi > origin + len)
+        return fail(VS_ERR_ARG, "own range must lie inside [origin, origin + len)");
+    VS_TRY(set_dev(h));
+    h->data = (const uint8_t *)dev_data;
+    h->dlen = len;
+    h->origin = origin;
+    h->own_lo = own_lo - origin;
+    h->own_hi = own_hi - origin;
+    h->final_ = final != 0;
+    h->scan_end = std::min<uint64_t>(h->own_hi + h->max_size - 1, len);
+    h->final_eof = h->final_ && h->scan_end == len;
+    h->base = h->own_lo & ~63ull;
+    h->nstrips = (h->scan_end > h->base) ? (h->scan_end - h->base + kStrip - 1) / kStrip : 0;
+    const uint64_t ns = std::max<uint64_t>(h->nstrips, 1);
+    VS_TRY(h->counts.ensure(ns * 4));
+    VS_TRY(h->offs.ensure(ns * kSlots * 4));
+    VS_TRY(h->dslot.ensure(ns * 4));
+    VS_TRY(h->flags.ensure(16));
+    VS_TRY(h->cstart.ensure((ns + 1) * 4));
+    VS_TRY(h->partials.ensure((ns / 4096 + 2) * 4));
+    VS_TRY(h->compact.ensure(ns * kSlots * 8));
+    h->pool_cap = (uint32_t)std::max<uint64_t>({(uint64_t)h->pool_cap, 16, h->nstrips / 256});
+    // segments
+    const uint64_t own = h->own_hi - h->own_lo;
+    h->seg_len = std::min<uint64_t>(std::max<uint64_t>((uint64_t)h->min_size * 64, 1ull << 20),
+                                    64ull << 20);
+    h->nseg = (uint32_t)((own + h->seg_len - 1) / h->seg_len);
+    h->maxc = (uint32_t)(h->seg_len / h->min_size + 3);
+    const uint64_t sg = std::max<uint32_t>(h->nseg, 1);
+    VS_TRY(h->spec_cut.ensure(sg * h->maxc * 8));
+    VS_TRY(h->st_cut.ensure(sg * h->maxc * 8));
+    VS_TRY(h->spec_n.ensure(sg * 4));
+    VS_TRY(h->spec_exit.ensure(sg * 8));
+    VS_TRY(h->st_n.ensure(sg * 4));
+    VS_TRY(h->st_merge.ensure(sg * 4));
+    VS_TRY(h->st_total.ensure(sg * 4));
+    VS_TRY(h->exit_a.ensure(sg * 8));
+    VS_TRY(h->exit_b.ensure(sg * 8));
+    VS_TRY(h->seg_off.ensure((sg + 1 + sg / 4096 + 2) * 4));
+    VS_TRY(run_scan_kernels(h));
+    h->state = 1;
+    return 0;
+}
+
+static int cdc_stitch(vs_cdc *h, uint64_t entry, uint64_t *exit_pos, int *complete) {
+    if (!h || h->state < 1) return fail(VS_ERR_STATE, "vs_cdc_stitch before vs_cdc_scan");
+    if (entry < h->origin + h->own_lo)
+        return fail(VS_ERR_ARG, "entry before the scanned own range");
+    // entry >= own_hi is legal: a chunk of the previous shard spans this whole
+    // range, so this shard owns no chunk start and its exit is the entry
+    VS_TRY(set_dev(h));
+    h->entry = entry - h->origin;
+    for (int attempt = 0;; ++attempt) {
+        h->exit_old = h->exit_a.as<uint64_t>();
+        h->exit_new = h->exit_b.as<uint64_t>();
+        if (h->nseg)
+            VS_HIP(hipMemcpyAsync(h->exit_old, h->spec_exit.p, (size_t)h->nseg * 8,
+                                  hipMemcpyDeviceToDevice, h->stream));
+        bool redo = false;
+        for (uint32_t pass = 0; pass <= h->nseg + 1; ++pass) {
+            {
+                StageTimer t(h, kStSel);
+                // clear only the per-pass word; scan errors in flags[0] persist
+                VS_HIP(hipMemsetAsync(h->flags.as<uint32_t>() + 2, 0, 4, h->stream));
+                SelArgs s = sel_args(h);
+                VS_HIP(launch_stitch(s, h->stream));
+            }
+            VS_HIP(hipMemcpyAsync(h->pinned, h->flags.p, 16, hipMemcpyDeviceToHost, h->stream));
+            VS_TRY(sync_stream(h));
+            const uint32_t *fw = (const uint32_t *)h->pinned;
+            if (fw[0] & (kFlagPoolOverflow | kFlagDenseMissing)) {
+                redo = true;
+                break;
+            }
+            std::swap(h->exit_old, h->exit_new);  // exit_old = latest exits
+            if (!(fw[2] & kFlagChanged)) break;
+        }
+        if (!redo) break;
+        if (attempt > 0) return fail(VS_ERR_STATE, "dense candidate pool still overflowing");
+        // some strips were dense beyond the pool: size it for the worst case
+        h->pool_cap = (uint32_t)std::max<uint64_t>(h->nstrips, 16);
+        VS_TRY(run_scan_kernels(h));
+    }
+    // after the loop exit_old holds the converged exits (== exit_new)
+    uint64_t ex;
+    if (h->nseg) {
+        VS_HIP(hipMemcpyAsync(h->pinned, h->exit_old + (h->nseg - 1), 8, hipMemcpyDeviceToHost,
+                              h->stream));
+        VS_TRY(sync_stream(h));
+        ex = h->pinned[0];
+    } else {
+        ex = h->entry;
+    }
+    const bool done = ex != kIncomplete;
+    if (exit_pos) *exit_pos = done ? ex + h->origin : ~0ull;
+    if (complete) *complete = done ? 1 : 0;
+    h->state = 2;
+    return 0;
+}
+
+static int cdc_finish(vs_cdc *h, uint64_t *n_chunks) {
+    if (!h || h->state < 2) return fail(VS_ERR_STATE, "vs_cdc_finish before vs_cdc_stitch");
+    VS_TRY(set_dev(h));
+    VS_TRY(h->n_out.ensure(16));
+    SelArgs s = sel_args(h);
+    // upper bound of chunks: every segment's capacity
+    const uint64_t cap = std::max<uint64_t>((uint64_t)h->nseg * h->maxc, 1);
+    VS_TRY(h->ch_start.ensure(cap * 8));
+    VS_TRY(h->ch_end.ensure(cap * 8));
+    {
+        StageTimer t(h, kStSel);
+        VS_HIP(launch_emit(s, h->seg_off.as<uint32_t>(), h->ch_start.as<uint64_t>(),
+                           h->ch_end.as<uint64_t>(), h->n_out.as<uint64_t>(), h->stream));
+    }
+    VS_HIP(hipMemcpyAsync(h->pinned, h->n_out.p, 8, hipMemcpyDeviceToHost, h->stream));
+    VS_TRY(sync_stream(h));
+    const uint64_t n = h->pinned[0];
+    h->n_chunks = n;
+    VS_TRY(h->ch_cut.ensure(std::max<uint64_t>(n, 1) * 8));
+    VS_TRY(h->ch_id.ensure(std::max<uint64_t>(n, 1) * 32));
+    VS_TRY(h->order.ensure(std::max<uint64_t>(n, 1) * 4));
+    VS_TRY(h->hist.ensure((2 * 4096 + 16) * 4));
+    if (n) {
+        {
+            StageTimer t(h, kStOther);
+            VS_HIP(launch_cut_fp(h->data, n, h->ch_start.as<uint64_t>(), h->ch_end.as<uint64_t>(),
+                                 h->min_size, h->tabs.as<uint64_t>(), h->tabs.as<uint64_t>() + 256,
+                                 h->idx_shift, h->ch_cut.as<uint64_t>(), h->stream));
+            VS_HIP(launch_length_order(n, h->ch_start.as<uint64_t>(), h->ch_end.as<uint64_t>(),
+                                       nullptr, h->hist.as<uint32_t>(), h->order.as<uint32_t>(),
+                                       h->stream));
+        }
+        {
+            StageTimer t(h, kStSha);
+            ShaArgs a{};
+            a.data = h->data;
+            a.n = n;
+            a.starts = h->ch_start.as<uint64_t>();
+            a.ends = h->ch_end.as<uint64_t>();
+            a.order = h->order.as<uint32_t>();
+            a.ids = h->ch_id.as<uint8_t>();
+            VS_HIP(launch_sha256(a, h->stream));
+        }
+    }
+    VS_TRY(sync_stream(h));
+    if (n_chunks) *n_chunks = n;
+    h->state = 3;
+    return 0;
+}
+
+static int cdc_get_chunks(vs_cdc *h, uint64_t first, uint64_t n, vs_chunk *out) {
+    if (!h || h->state < 3) return fail(VS_ERR_STATE, "no finished batch");
+    if (first + n > h->n_chunks) return fail(VS_ERR_ARG, "chunk range out of bounds");
+    if (!n) return 0;
+    VS_TRY(set_dev(h));
+    std::vector<uint64_t> st(n), en(n), cu(n);
+    std::vector<uint8_t> id(n * 32);
+    VS_HIP(hipMemcpy(st.data(), h->ch_start.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost));
+    VS_HIP(hipMemcpy(en.data(), h->ch_end.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost));
+    VS_HIP(hipMemcpy(cu.data(), h->ch_cut.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost));
+    VS_HIP(hipMemcpy(id.data(), h->ch_id.as<uint8_t>() + first * 32, n * 32, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < n; ++i) {
+        out[i].start = h->origin + st[i];
+        out[i].length = (en[i] & kPosMask) - st[i] + 1;
+        out[i].cut = cu[i];
+        memcpy(out[i].id, &id[i * 32], 32);
+    }
+    return 0;
+}
+
+static int cdc_process(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t origin, int final,
+                       uint64_t *n_chunks, uint64_t *consumed) {
+    VS_TRY(cdc_scan(h, dev_data, len, origin, origin, origin + len, final));
+    uint64_t ex = 0;
+    int complete = 0;
+    VS_TRY(cdc_stitch(h, origin, &ex, &complete));
+    uint64_t n = 0;
+    VS_TRY(cdc_finish(h, &n));
+    if (n_chunks) *n_chunks = n;
+    if (consumed) {
+        if (complete) {
+            *consumed = ex - origin;
+        } else if (n) {
+            uint64_t e = 0;
+            VS_HIP(hipMemcpy(&e, h->ch_end.as<uint64_t>() + (n - 1), 8, hipMemcpyDeviceToHost));
+            *consumed = (e & kPosMask) + 1;
+        } else {
+            *consumed = 0;
+        }
+    }
+    return 0;
+}
+
+// streaming: run the pipeline over the staged bytes
+static int stream_run(vs_cdc *h, bool final) {
+    DevBuf &cur = h->sbuf[h->scur];
+    uint64_t n = 0, consumed = 0;
+    VS_TRY(cdc_process(h, cur.p ? cur.p : h->tabs.p, h->sfill, h->sorigin, final ? 1 : 0, &n,
+                       &consumed));
+    if (n) {
+        std::vector<vs_chunk> tmp(n);
+        VS_TRY(cdc_get_chunks(h, 0, n, tmp.data()));
+        for (auto &c : tmp) h->ready.push_back(c);
+    }
+    const uint64_t rest = h->sfill - consumed;
+    if (rest) {
+        DevBuf &nxt = h->sbuf[h->scur ^ 1];
+        VS_TRY(nxt.ensure(std::max<uint64_t>(rest, h->batch_bytes) + (1 << 20)));
+        VS_HIP(hipMemcpyAsync(nxt.p, (uint8_t *)cur.p + consumed, rest, hipMemcpyDeviceToDevice,
+                              h->stream));
+        VS_TRY(sync_stream(h));
+        h->scur ^= 1;
+    }
+    h->sorigin += consumed;
+    h->sfill = rest;
+    return 0;
+}
+
+}  // namespace vsgpu
+
+// ============================================================================
+// exported C ABI
+// ============================================================================
+VS_API const char *vs_last_error(void) { return g_err.c_str(); }
+VS_API const char *vs_version(void) { return "volsync_amd vsgpu 0.1 (gfx950)"; }
+
+VS_API int vs_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+VS_API int vs_pol_deg(uint64_t pol) { return pol_deg(pol); }
+VS_API int vs_pol_irreducible(uint64_t pol) { return pol_irreducible(pol) ? 1 : 0; }
+VS_API int vs_pol_tables(uint64_t pol, uint64_t out_tab[256], uint64_t mod_tab[256]) {
+    if (!pol) return fail(VS_ERR_POLY, "tables for polynomial computation not initialized");
+    if (pol_deg(pol) > 56) return fail(VS_ERR_POLY, "polynomial degree > 56");
+    pol_tables(pol, out_tab, mod_tab);
+    return 0;
+}
+
+VS_API int vs_cdc_open(int device, uint64_t pol, uint32_t min_size, uint32_t max_size,
+                       uint32_t avg_bits, vs_cdc **out) {
+    if (!out) return fail(VS_ERR_ARG, "null handle out-pointer");
+    *out = nullptr;
+    int ndev = vs_device_count();
+    if (ndev <= 0) return fail(VS_ERR_NO_DEVICE, "no HIP device available (no CPU fallback)");
+    if (device < 0 || device >= ndev) return fail(VS_ERR_ARG, "device index out of range");
+    vs_cdc *h = new vs_cdc();
+    h->device = device;
+    if (set_dev(h) < 0) {
+        delete h;
+        return VS_ERR_NO_DEVICE;
+    }
+    if (hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void **)&h->pinned, 64, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        delete h;
+        return fail(VS_ERR_HIP, "stream / pinned buffer creation failed");
+    }
+    h->stream = h->own;
+    int r = set_params(h, pol, min_size, max_size, avg_bits);
+    if (r < 0) {
+        std::string msg = g_err;
+        vs_cdc_close(h);
+        g_err = msg;
+        return r;
+    }
+    *out = h;
+    return 0;
+}
+
+VS_API int vs_cdc_reset(vs_cdc *h, uint64_t pol, uint32_t min_size, uint32_t max_size,
+                        uint32_t avg_bits) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    VS_TRY(set_dev(h));
+    VS_TRY(set_params(h, pol, min_size, max_size, avg_bits));
+    h->state = 0;
+    h->ready.clear();
+    h->sfill = 0;
+    h->sorigin = 0;
+    h->final_fed = false;
+    return 0;
+}
+
+VS_API int vs_cdc_set_batch_bytes(vs_cdc *h, uint64_t bytes) {
+    if (!h || bytes < 1) return fail(VS_ERR_ARG, "bad batch size");
+    h->batch_bytes = bytes;
+    return 0;
+}
+
+VS_API int vs_cdc_feed(vs_cdc *h, const void *buf, size_t n, int final) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    if (h->final_fed) return fail(VS_ERR_STATE, "stream already finalised (call vs_cdc_reset)");
+    if (n && !buf) return fail(VS_ERR_ARG, "null buffer");
+    VS_TRY(set_dev(h));
+    const uint8_t *src = (const uint8_t *)buf;
+    size_t left = n;
+    for (;;) {
+        // top up the staging buffer to batch_bytes, run a batch when full
+        DevBuf &cur = h->sbuf[h->scur];
+        // a batch of at least 2*MaxSize always determines its first chunk's cut,
+        // so every non-final run makes progress
+        const uint64_t batch = std::max<uint64_t>(h->batch_bytes, 2ull * h->max_size + (1 << 20));
+        const uint64_t room = (h->sfill < batch) ? batch - h->sfill : 0;
+        const uint64_t take = std::min<uint64_t>(room, left);
+        if (take) {
+            if (cur.cap < h->sfill + take) {
+                DevBuf bigger;
+                VS_TRY(bigger.ensure(std::max<uint64_t>(h->sfill + take, batch) + (1 << 20)));
+                if (h->sfill)
+                    VS_HIP(hipMemcpyAsync(bigger.p, cur.p, h->sfill, hipMemcpyDeviceToDevice,
+                                          h->stream));
+                VS_TRY(sync_stream(h));
+                cur.release();
+                cur = bigger;
+            }
+            VS_HIP(hipMemcpyAsync((uint8_t *)cur.p + h->sfill, src, take, hipMemcpyHostToDevice,
+                                  h->stream));
+            VS_TRY(sync_stream(h));
+            h->sfill += take;
+            src += take;
+            left -= take;
+        }
+        if (left == 0) break;
+        VS_TRY(stream_run(h, false));  // staging full, more input pending
+    }
+    if (final) {
+        VS_TRY(stream_run(h, true));
+        h->final_fed = true;
+    }
+    return 0;
+}
+
+VS_API int vs_cdc_next(vs_cdc *h, vs_chunk *out, size_t cap, size_t *n_out) {
+    if (!h || (!out && cap)) return fail(VS_ERR_ARG, "bad arguments");
+    size_t k = 0;
+    while (k < cap && !h->ready.empty()) {
+        out[k++] = h->ready.front();
+        h->ready.pop_front();
+    }
+    if (n_out) *n_out = k;
+    if (k == 0 && h->final_fed) return VS_EOF;
+    return 0;
+}
+
+VS_API void vs_cdc_close(vs_cdc *h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    DevBuf *bufs[] = {&h->tabs,     &h->counts,  &h->offs,     &h->dslot,   &h->pool,
+                      &h->flags,    &h->cstart,  &h->partials, &h->compact, &h->spec_cut,
+                      &h->spec_n,   &h->spec_exit, &h->st_cut, &h->st_n,    &h->st_merge,
+                      &h->st_total, &h->exit_a,  &h->exit_b,   &h->seg_off, &h->ch_start,
+                      &h->ch_end,   &h->ch_cut,  &h->ch_id,    &h->order,   &h->hist,
+                      &h->n_out,    &h->sbuf[0], &h->sbuf[1]};
+    for (DevBuf *b : bufs) b->release();
+    for (auto &p : h->pend) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+    if (h->pinned) (void)hipHostFree(h->pinned);
+    if (h->own) (void)hipStreamDestroy(h->own);
+    delete h;
+}
+
+VS_API int vs_cdc_set_stream(vs_cdc *h, void *hip_stream) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    h->stream = hip_stream ? (hipStream_t)hip_stream : h->own;
+    return 0;
+}
+
+VS_API int vs_cdc_scan(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t origin,
+                       uint64_t own_lo, uint64_t own_hi, int final) {
+    return cdc_scan(h, dev_data, len, origin, own_lo, own_hi, final);
+}
+
+VS_API int vs_cdc_stitch(vs_cdc *h, uint64_t entry, uint64_t *exit_pos, int *complete) {
+    return cdc_stitch(h, entry, exit_pos, complete);
+}
+
+VS_API int vs_cdc_finish(vs_cdc *h, uint64_t *n_chunks) { return cdc_finish(h, n_chunks); }
+
+VS_API int vs_cdc_process(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t origin,
+                          int final, uint64_t *n_chunks, uint64_t *consumed) {
+    return cdc_process(h, dev_data, len, origin, final, n_chunks, consumed);
+}
+
+VS_API int vs_cdc_get_chunks(vs_cdc *h, uint64_t first, uint64_t n, vs_chunk *out) {
+    return cdc_get_chunks(h, first, n, out);
+}
+
+VS_API int vs_cdc_timing(vs_cdc *h, int enable, double ms_out[4], uint64_t launches_out[4]) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    if (ms_out)
+        for (int i = 0; i < 4; ++i) ms_out[i] = h->ms[i];
+    if (launches_out)
+        for (int i = 0; i < 4; ++i) launches_out[i] = h->launches[i];
+    for (int i = 0; i < 4; ++i) {
+        h->ms[i] = 0;
+        h->launches[i] = 0;
+    }
+    h->timing = enable != 0;
+    return 0;
+}
+
+VS_API int vs_sha256_batch_device(int device, const void *dev_buf, const uint64_t *dev_off,
+                                  const uint32_t *dev_len, size_t n, uint8_t *dev_out,
+                                  void *hip_stream) {
+    if (vs_device_count() <= 0) return fail(VS_ERR_NO_DEVICE, "no HIP device available");
+    if (n && (!dev_buf || !dev_off || !dev_len || !dev_out))
+        return fail(VS_ERR_ARG, "null device pointer");
+    VS_HIP(hipSetDevice(device));
+    hipStream_t s = (hipStream_t)hip_stream;
+    ShaArgs a{};
+    a.data = (const uint8_t *)dev_buf;
+    a.n = n;
+    a.starts = dev_off;
+    a.lens = dev_len;
+    a.ids = dev_out;
+    VS_HIP(launch_sha256(a, s));
+    return 0;
+}
+
+VS_API int vs_sha256_batch(int device, const void *buf, size_t buf_len, const uint64_t *off,
+                           const uint32_t *len, size_t n, uint8_t (*out)[32]) {
+    if (vs_device_count() <= 0) return fail(VS_ERR_NO_DEVICE, "no HIP device available");
+    if (n && (!buf || !off || !len || !out)) return fail(VS_ERR_ARG, "null pointer");
+    for (size_t i = 0; i < n; ++i)
+        if (off[i] + len[i] > buf_len) return fail(VS_ERR_ARG, "blob outside the buffer");
+    VS_HIP(hipSetDevice(device));
+    DevBuf d, o, l, r, ord, hist;
+    VS_TRY(d.ensure(std::max<size_t>(buf_len, 16)));
+    VS_TRY(o.ensure(std::max<size_t>(n, 1) * 8));
+    VS_TRY(l.ensure(std::max<size_t>(n, 1) * 4));
+    VS_TRY(r.ensure(std::max<size_t>(n, 1) * 32));
+    VS_TRY(ord.ensure(std::max<size_t>(n, 1) * 4));
+    VS_TRY(hist.ensure((2 * 4096 + 16) * 4));
+    int rc = 0;
+    if (hipMemcpy(d.p, buf, buf_len, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(o.p, off, n * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(l.p, len, n * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        rc = fail(VS_ERR_HIP, "host to device copy failed");
+    } else if (n) {
+        ShaArgs a{};
+        a.data = d.as<uint8_t>();
+        a.n = n;
+        a.starts = o.as<uint64_t>();
+        a.lens = l.as<uint32_t>();
+        a.order = ord.as<uint32_t>();
+        a.ids = r.as<uint8_t>();
+        if (launch_length_order(n, a.starts, nullptr, a.lens, hist.as<uint32_t>(),
+                                ord.as<uint32_t>(), 0) != hipSuccess ||
+            launch_sha256(a, 0) != hipSuccess ||
+            hipMemcpy(out, r.p, n * 32, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = fail(VS_ERR_HIP, "SHA-256 batch failed");
+    }
+    d.release(); o.release(); l.release(); r.release(); ord.release(); hist.release();
+    return rc;
+}
+
+VS_API int vs_synth_fill_device(int device, uint64_t seed, uint64_t off, uint64_t n,
+                                void *dev_out, void *hip_stream) {
+    if (vs_device_count() <= 0) return fail(VS_ERR_NO_DEVICE, "no HIP device available");
+    VS_HIP(hipSetDevice(device));
+    VS_HIP(launch_synth(seed, off, n, (uint8_t *)dev_out, (hipStream_t)hip_stream));
+    return 0;
+}

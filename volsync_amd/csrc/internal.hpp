@@ -1,0 +1,137 @@
+// internal.hpp -- shared declarations of the gfx950 CDC + SHA-256 pipeline.
+// Public ABI: include/vsgpu.h.  Design: DESIGN.md.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/vsgpu.h"
+
+namespace vsgpu {
+
+// ---- error plumbing -------------------------------------------------------
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+#define VS_HIP(call)                                                                  \
+    do {                                                                              \
+        hipError_t e_ = (call);                                                       \
+        if (e_ != hipSuccess)                                                         \
+            return ::vsgpu::fail(VS_ERR_HIP, std::string(#call) + ": " +              \
+                                                 hipGetErrorString(e_));              \
+    } while (0)
+#define VS_TRY(expr)                 \
+    do {                             \
+        int r_ = (expr);             \
+        if (r_ < 0) return r_;       \
+    } while (0)
+
+// ---- Rabin tables (chunker.go fillTables) ----------------------------------
+int pol_deg(uint64_t p);
+uint64_t pol_mod(uint64_t x, uint64_t d);
+bool pol_irreducible(uint64_t p);
+void pol_tables(uint64_t pol, uint64_t out_tab[256], uint64_t mod_tab[256]);
+// out8[b] = b * x^512 mod P  (= appendByte(out[b], 0)): the evicted-byte term of
+// the rolling window written against the shifted digest.
+void pol_out8(uint64_t pol, const uint64_t out_tab[256], uint64_t out8[256]);
+
+// ---- fingerprint pass ------------------------------------------------------
+constexpr int kFpThreads = 1024;   // one 16-wave workgroup per CU (LDS: 128 KiB tables)
+constexpr int kFpCopies = 32;      // lane-private table copies: conflict-free ds_read_b64
+constexpr int kSlots = 3;          // candidate offsets kept per strip (dense strips: bitmask)
+constexpr uint32_t kNoSlot = 0xffffffffu;
+// flags words: [0] scan errors (pool overflow, dense strip without bitmask),
+// [1] dense pool bump cursor, [2] stitch pass "an exit changed"
+constexpr uint32_t kFlagPoolOverflow = 1u;
+constexpr uint32_t kFlagChanged = 2u;
+constexpr uint32_t kFlagDenseMissing = 4u;
+
+struct FpArgs {
+    const uint8_t *data;   // device bytes, 16-byte aligned base
+    uint64_t dlen;         // readable bytes at data
+    uint64_t base;         // data offset of strip 0 (multiple of 64)
+    uint64_t scan_end;     // candidates are recorded for positions < scan_end
+    uint64_t k_first;      // first strip of this launch
+    uint64_t k_count;      // strips in this launch
+    uint32_t strip;        // bytes per strip (multiple of 64)
+    uint32_t idx_shift;    // digest bit of the table index, minus 32 (deg - 40)
+    uint32_t mask_lo, mask_hi;
+    uint32_t *counts;      // [nstrips] candidates per strip
+    uint32_t *offs;        // [nstrips * kSlots] first offsets within the strip
+    uint32_t *dense_slot;  // [nstrips] pool slot of dense strips
+    uint32_t *pool;        // [pool_cap * strip/32] candidate bitmasks
+    uint32_t pool_cap;
+    uint32_t *pool_next;   // bump allocator
+    uint32_t *flags;
+    const uint64_t *mod_tab;   // [256]
+    const uint64_t *out8_tab;  // [256]
+};
+hipError_t launch_fingerprint(const FpArgs &a, bool guard, bool wide_mask, hipStream_t s);
+
+// ---- selection -------------------------------------------------------------
+constexpr uint64_t kPosMask = (1ull << 62) - 1;
+constexpr uint64_t kCutNormal = 0, kCutForced = 1ull << 62, kCutEof = 2ull << 62;
+constexpr uint64_t kIncomplete = ~0ull;   // exit marker: a cut needs more data
+
+struct SelArgs {
+    // candidate index (from the fingerprint pass)
+    uint64_t base;
+    uint32_t strip;
+    uint64_t nstrips;
+    const uint32_t *counts, *offs, *dense_slot, *pool;
+    const uint32_t *cstart;   // [nstrips+1] exclusive scan of min(count, kSlots)
+    const uint64_t *compact;  // [cstart[nstrips]] candidate positions (data offsets)
+    uint32_t *flags;
+    // chunk rule
+    uint64_t min_size, max_size;
+    uint64_t scan_end, dlen;
+    int final_eof;            // 1: the stream ends at dlen and scan_end == dlen
+    // segments tiling [own_lo, own_hi)
+    uint64_t own_lo, own_hi, seg_len;
+    uint32_t nseg, maxc;
+    uint64_t *spec_cut;       // [nseg * maxc]
+    uint32_t *spec_n;         // [nseg]
+    uint64_t *spec_exit;      // [nseg]
+    uint64_t *st_cut;         // [nseg * maxc]
+    uint32_t *st_n, *st_merge, *st_total;  // [nseg]
+    uint64_t *exit_old, *exit_new;         // [nseg]
+    uint64_t entry;
+};
+hipError_t launch_compact(const SelArgs &a, uint32_t *cstart_partials, uint64_t *compact,
+                          uint32_t *cstart, hipStream_t s);
+hipError_t launch_spec_walk(const SelArgs &a, hipStream_t s);
+hipError_t launch_stitch(const SelArgs &a, hipStream_t s);
+// chunk list: starts/ends (data offsets) + cut type, in stream order
+hipError_t launch_emit(const SelArgs &a, uint32_t *seg_off, uint64_t *ch_start,
+                       uint64_t *ch_end, uint64_t *n_out, hipStream_t s);
+hipError_t launch_cut_fp(const uint8_t *data, uint64_t n, const uint64_t *ch_start,
+                         const uint64_t *ch_end, uint64_t min_size, const uint64_t *mod_tab,
+                         const uint64_t *out8_tab, uint32_t idx_shift, uint64_t *cut_out,
+                         hipStream_t s);
+
+// ---- SHA-256 ---------------------------------------------------------------
+// Hash n blobs data[start[i] .. start[i]+len(i)) where len comes from either
+// (ends, inclusive end offsets) or (lens).  order: optional permutation
+// (longest first); ids: [n][32].
+struct ShaArgs {
+    const uint8_t *data;
+    uint64_t n;
+    const uint64_t *starts;
+    const uint64_t *ends;     // inclusive end offsets, or nullptr
+    const uint32_t *lens;     // lengths, or nullptr
+    const uint32_t *order;    // nullptr = identity
+    uint8_t *ids;
+};
+hipError_t launch_sha256(const ShaArgs &a, hipStream_t s);
+// Longest-first permutation of n blob lengths (bucketed by 64 KiB).
+hipError_t launch_length_order(uint64_t n, const uint64_t *starts, const uint64_t *ends,
+                               const uint32_t *lens, uint32_t *hist, uint32_t *order,
+                               hipStream_t s);
+
+// ---- synthetic data --------------------------------------------------------
+hipError_t launch_synth(uint64_t seed, uint64_t off, uint64_t n, uint8_t *out, hipStream_t s);
+
+// ---- misc ---------------------------------------------------------------------
+hipError_t launch_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *partials,
+                           uint32_t clamp, hipStream_t s);
+
+}  // namespace vsgpu

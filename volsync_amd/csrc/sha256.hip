@@ -1,0 +1,218 @@
+// sha256.hip -- batched SHA-256 blob IDs on gfx950.
+//
+// restic's blob ID is sha256.Sum256 of the chunk plaintext
+// (restic v0.13.1 internal/restic/id.go Hash, Go crypto/sha256 after
+// /root/reference/mover-restic/patch-sources.sh:16-27), computed for every
+// chunk in Repository.SaveBlob.
+//
+// One lane per blob: the Merkle-Damgard chain of a blob is sequential, so
+// parallelism is across blobs.  Lanes are fed longest-first (64 KiB buckets)
+// so a wave's lanes finish together.  Integer-VALU bound:
+// per 64-byte block 64 rounds x 14 ops + 48 schedule words x 10 ops with
+// v_bitop3_b32 for Ch / Maj / the three-way XORs, v_alignbit_b32 for
+// rotates and v_perm_b32 for the big-endian, byte-misaligned message words.
+#include "internal.hpp"
+
+namespace vsgpu {
+
+static constexpr uint32_t kK256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4,
+    0xab1c5ed5, 0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe,
+    0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f,
+    0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7,
+    0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc,
+    0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b,
+    0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116,
+    0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
+    0xc67178f2};
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
+    return __builtin_amdgcn_alignbit(x, x, n);
+}
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
+    return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);  // e ? f : g
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+
+__device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+    uint32_t e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+            const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+            const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+            wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+        }
+        const uint32_t t1 = h + xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)) + ch(e, f, g) +
+                            kK256[t] + wt;
+        const uint32_t t2 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)) + maj(a, b, c);
+        h = g;
+        g = f;
+        f = e;
+        e = d + t1;
+        d = c;
+        c = b;
+        b = a;
+        a = t1 + t2;
+    }
+    st[0] += a;
+    st[1] += b;
+    st[2] += c;
+    st[3] += d;
+    st[4] += e;
+    st[5] += f;
+    st[6] += g;
+    st[7] += h;
+}
+
+__device__ __forceinline__ void load_block(const uint32_t *wp, uint64_t wi, bool need17,
+                                           uint32_t (&d)[17]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) d[i] = wp[wi + i];
+    d[16] = need17 ? wp[wi + 16] : 0u;
+}
+
+__global__ __launch_bounds__(256) void sha256_kernel(ShaArgs a) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.n) return;
+    const uint64_t i = a.order ? a.order[t] : t;
+    const uint64_t start = a.starts[i];
+    const uint64_t len = a.ends ? ((a.ends[i] & kPosMask) - start + 1) : a.lens[i];
+    const uint32_t r = (uint32_t)(start & 3);
+    const uint32_t sel = (r << 24) | ((r + 1) << 16) | ((r + 2) << 8) | (r + 3);
+    const uint32_t *wp = (const uint32_t *)(a.data + (start - r));
+    uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                      0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    const uint64_t nfull = len >> 6;
+    const bool need17 = r != 0;
+    uint32_t cur[17], nxt[17];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) nxt[k] = 0;
+    if (nfull) load_block(wp, 0, need17, cur);
+    for (uint64_t b = 0; b < nfull; ++b) {
+        if (b + 1 < nfull) load_block(wp, 16 * (b + 1), need17, nxt);
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_perm(cur[k + 1], cur[k], sel);
+        compress(st, w);
+#pragma unroll
+        for (int k = 0; k < 17; ++k) cur[k] = nxt[k];
+    }
+    // tail: rem bytes + 0x80 + zeros + 64-bit big-endian bit length
+    const uint64_t rem = len - (nfull << 6);
+    const uint8_t *tp = a.data + start + (nfull << 6);
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = 0;
+    for (uint32_t j = 0; j < (uint32_t)rem; ++j) w[j >> 2] |= (uint32_t)tp[j] << (24 - 8 * (j & 3));
+    w[rem >> 2] |= 0x80u << (24 - 8 * (rem & 3));
+    const uint64_t bits = len << 3;
+    if (rem < 56) {
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+        compress(st, w);
+    } else {
+        compress(st, w);
+#pragma unroll
+        for (int k = 0; k < 14; ++k) w[k] = 0;
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+        compress(st, w);
+    }
+    uint4 *out = (uint4 *)(a.ids + 32 * i);
+    out[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]),
+                        __builtin_bswap32(st[2]), __builtin_bswap32(st[3]));
+    out[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]),
+                        __builtin_bswap32(st[6]), __builtin_bswap32(st[7]));
+}
+
+hipError_t launch_sha256(const ShaArgs &a, hipStream_t s) {
+    if (!a.n) return hipSuccess;
+    sha256_kernel<<<(uint32_t)((a.n + 255) / 256), 256, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+// ---- longest-first ordering ---------------------------------------------------
+constexpr uint32_t kLenBuckets = 4096;
+
+__device__ __forceinline__ uint32_t len_key(uint64_t i, const uint64_t *starts,
+                                            const uint64_t *ends, const uint32_t *lens) {
+    const uint64_t len = ends ? ((ends[i] & kPosMask) - starts[i] + 1) : lens[i];
+    const uint64_t b = len >> 16;
+    return kLenBuckets - 1 - (uint32_t)(b < kLenBuckets ? b : kLenBuckets - 1);
+}
+
+__global__ void len_hist_kernel(uint64_t n, const uint64_t *starts, const uint64_t *ends,
+                                const uint32_t *lens, uint32_t *hist) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(&hist[len_key(i, starts, ends, lens)], 1u);
+}
+
+__global__ void len_scatter_kernel(uint64_t n, const uint64_t *starts, const uint64_t *ends,
+                                   const uint32_t *lens, uint32_t *cursor, uint32_t *order) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) order[atomicAdd(&cursor[len_key(i, starts, ends, lens)], 1u)] = (uint32_t)i;
+}
+
+// hist: scratch of >= 2*kLenBuckets + 8 u32
+hipError_t launch_length_order(uint64_t n, const uint64_t *starts, const uint64_t *ends,
+                               const uint32_t *lens, uint32_t *hist, uint32_t *order,
+                               hipStream_t s) {
+    if (!n) return hipSuccess;
+    uint32_t *cursor = hist + kLenBuckets;
+    uint32_t *partials = cursor + kLenBuckets + 1;
+    hipError_t e = hipMemsetAsync(hist, 0, kLenBuckets * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    const uint32_t blocks = (uint32_t)((n + 255) / 256);
+    len_hist_kernel<<<blocks, 256, 0, s>>>(n, starts, ends, lens, hist);
+    e = launch_scan_u32(hist, cursor, kLenBuckets, partials, 0xffffffffu, s);
+    if (e != hipSuccess) return e;
+    len_scatter_kernel<<<blocks, 256, 0, s>>>(n, starts, ends, lens, cursor, order);
+    return hipGetLastError();
+}
+
+// ---- synthetic volume bytes -------------------------------------
+__device__ __forceinline__ uint64_t splitmix_word(uint64_t seed, uint64_t i) {
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void synth_kernel(uint64_t seed, uint64_t off, uint64_t n, uint8_t *out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint32_t a = (uint32_t)(off & 7);
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 8 * t < n; t += stride) {
+        const uint64_t w0 = (off >> 3) + t;
+        uint64_t v = splitmix_word(seed, w0);
+        if (a) v = (v >> (8 * a)) | (splitmix_word(seed, w0 + 1) << (64 - 8 * a));
+        const uint64_t o = 8 * t;
+        if (o + 8 <= n && (((uintptr_t)(out + o)) & 7) == 0) {
+            *(uint64_t *)(out + o) = v;
+        } else {
+            for (uint32_t k = 0; k < 8 && o + k < n; ++k) out[o + k] = (uint8_t)(v >> (8 * k));
+        }
+    }
+}
+
+hipError_t launch_synth(uint64_t seed, uint64_t off, uint64_t n, uint8_t *out, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint64_t words = (n + 7) / 8;
+    uint64_t blocks = (words + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    synth_kernel<<<(uint32_t)blocks, 256, 0, s>>>(seed, off, n, out);
+    return hipGetLastError();
+}
+
+}  // namespace vsgpu
