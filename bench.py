@@ -72,6 +72,8 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=int, default=4)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inflight", type=int, default=4,
+                    help="volumes in flight: handles on separate HIP streams, steps round-robin")
     args = ap.parse_args()
 
     import torch
@@ -96,32 +98,64 @@ def main():
     synth_fill_device(buf.data_ptr(), 2, spec.data_lo, dlen, device=local, stream=stream)
     torch.cuda.synchronize(dev)
 
-    dc = DeviceChunker(TestPol, MinSize, MaxSize, 20, device=local)
-    dc.set_stream(stream)
+    P = max(1, args.inflight)
+    streams = [torch.cuda.Stream(dev) for _ in range(P)]
+    handles = []
+    for st in streams:
+        h = DeviceChunker(TestPol, MinSize, MaxSize, 20, device=local)
+        h.set_stream(st.cuda_stream)
+        handles.append(h)
     coll = torch_collectives(dev) if world > 1 else None
+    counter = [0]
 
     def step():
+        # volume i runs on handle i % P; finish() leaves SHA-256 queued on that
+        # handle's stream, so up to P volumes overlap
+        dc = handles[counter[0] % P]
+        counter[0] += 1
         if world == 1:
             n, _ = dc.process(buf.data_ptr(), dlen, 0, True)
         else:
             n = run_shard(dc, spec, buf.data_ptr(), *coll)
         return n
 
+    def drain():
+        for h in handles:
+            h.wait()
+        torch.cuda.synchronize(dev)
+
     for _ in range(args.warmup):
         step()
+    drain()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
-    dc.timing(True)
+    for h in handles:
+        h.timing(True)
     t0 = time.perf_counter()
     nch = 0
     for _ in range(args.steps):
         nch = step()
-    torch.cuda.synchronize(dev)
+    drain()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    ms, launches = dc.timing(False)
+    ms = [0.0] * 4
+    launches = [0] * 4
+    for h in handles:
+        m, c = h.timing(False)
+        ms = [a + b for a, b in zip(ms, m)]
+        launches = [a + b for a, b in zip(launches, c)]
+    # one volume alone (no overlap): single-volume latency and isolated kernel times
+    h0 = handles[0]
+    h0.timing(True)
+    t1 = time.perf_counter()
+    if world == 1:
+        h0.process(buf.data_ptr(), dlen, 0, True)
+    else:
+        run_shard(h0, spec, buf.data_ptr(), *coll)
+    h0.wait()
+    lat = time.perf_counter() - t1
+    iso_ms, iso_launch = h0.timing(False)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -133,17 +167,16 @@ def main():
     own_bytes = spec.own_hi - spec.own_lo
     stages = ["fingerprint", "select", "sha256", "other"]
     per_step = {s: ms[i] / args.steps for i, s in enumerate(stages)}
-    dom = max(range(4), key=lambda i: ms[i])
-    fp_ms = ms[0] / max(1, launches[0]) if launches[0] else 0.0
+    # kernel roofline from the timed region (HIP events on each handle's stream,
+    # so overlapped volumes share the chip): algorithmic bytes per launch = the
+    # volume bytes -- the fingerprint pass reads each scanned byte once (plus a
+    # 64-byte warm-up per 12 KiB strip, not counted), SHA-256 reads each chunk
+    # byte once; one fingerprint stage and one SHA-256 launch per volume.
+    fp_ms = ms[0] / args.steps
     sha_ms = ms[2] / max(1, launches[2]) if launches[2] else 0.0
-    # algorithmic bytes per launch: the fingerprint pass reads each scanned byte
-    # once (plus a 64-byte warm-up per 12 KiB strip, not counted); SHA-256
-    # reads each chunk byte once.  One SHA launch per step; the fingerprint
-    # stage is one interior launch (+2 tiny guarded ones) per step.
-    fp_launch_bytes = own_bytes
-    sha_launch_bytes = own_bytes
-    fp_gbs = fp_launch_bytes / (ms[0] / args.steps) / 1e6 if ms[0] else 0.0
-    sha_gbs = sha_launch_bytes / sha_ms / 1e6 if sha_ms else 0.0
+    fp_gbs = own_bytes / fp_ms / 1e6 if fp_ms else 0.0
+    sha_gbs = own_bytes / sha_ms / 1e6 if sha_ms else 0.0
+    iso = {s: round(iso_ms[i], 3) for i, s in enumerate(stages)}
     roof = {
         "fingerprint": {"bound": "hbm", "achieved": round(fp_gbs, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(fp_gbs / HBM_PEAK_GBS, 4),
@@ -180,11 +213,16 @@ def main():
             "roofline": roofline,
             "stages_ms_per_step": {k: round(v, 3) for k, v in per_step.items()},
             "kernels": roof,
+            "inflight": P,
+            "single_volume": {"ms": round(lat * 1e3, 2),
+                              "GBps": round(total / lat / 1e9, 2),
+                              "stages_ms": iso},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_gib << 30, args.cpu_threads)
         print(json.dumps(out), flush=True)
-    dc.close()
+    for h in handles:
+        h.close()
     if world > 1:
         dist.destroy_process_group()
 

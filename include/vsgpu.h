@@ -104,8 +104,11 @@ int vs_cdc_scan(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t origin,
  * start of the first chunk at or beyond own_hi (or the stream end);
  * *complete = 0 when a chunk's cut depends on bytes not yet supplied. */
 int vs_cdc_stitch(vs_cdc *h, uint64_t entry, uint64_t *exit_pos, int *complete);
-/* Emits the chunk list, computes Cut values and SHA-256 blob IDs on device. */
+/* Emits the chunk list (the count is known on return) and queues the Cut
+ * values and SHA-256 blob IDs on the handle's stream without waiting. */
 int vs_cdc_finish(vs_cdc *h, uint64_t *n_chunks);
+/* Waits until the handle's queued work (blob IDs) is complete. */
+int vs_cdc_wait(vs_cdc *h);
 /* scan + stitch(own_lo) + finish for a single device (own range = whole buffer). */
 int vs_cdc_process(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t origin, int final,
                    uint64_t *n_chunks, uint64_t *consumed);

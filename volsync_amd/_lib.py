@@ -77,6 +77,7 @@ def _load() -> ctypes.CDLL:
         "vs_cdc_scan": (c_int, [vp, vp, c_u64, c_u64, c_u64, c_u64, c_int]),
         "vs_cdc_stitch": (c_int, [vp, c_u64, u64p, ctypes.POINTER(c_int)]),
         "vs_cdc_finish": (c_int, [vp, u64p]),
+        "vs_cdc_wait": (c_int, [vp]),
         "vs_cdc_process": (c_int, [vp, vp, c_u64, c_u64, c_int, u64p, u64p]),
         "vs_cdc_get_chunks": (c_int, [vp, c_u64, c_u64, ctypes.POINTER(VsChunk)]),
         "vs_cdc_timing": (c_int, [vp, c_int, ctypes.POINTER(ctypes.c_double), u64p]),

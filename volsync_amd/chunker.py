@@ -216,9 +216,13 @@ class DeviceChunker:
         return int(ex.value), bool(complete.value)
 
     def finish(self) -> int:
+        """Emit the chunk list; blob IDs stay queued (see wait())."""
         n = ctypes.c_uint64(0)
         check(lib.vs_cdc_finish(self._h, ctypes.byref(n)))
         return int(n.value)
+
+    def wait(self) -> None:
+        check(lib.vs_cdc_wait(self._h))
 
     def chunks(self, first: int = 0, n: Optional[int] = None, total: Optional[int] = None
                ) -> List[Chunk]:

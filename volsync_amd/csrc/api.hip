@@ -449,17 +449,25 @@ static int cdc_finish(vs_cdc *h, uint64_t *n_chunks) {
             VS_HIP(launch_sha256(a, h->stream));
         }
     }
-    VS_TRY(sync_stream(h));
+    // Cut values and blob IDs stay queued on the handle's stream: results are
+    // waited for by vs_cdc_wait / vs_cdc_get_chunks, so another handle's batch
+    // can run beside this one's SHA-256 tail.
     if (n_chunks) *n_chunks = n;
     h->state = 3;
     return 0;
+}
+
+static int cdc_wait(vs_cdc *h) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    VS_TRY(set_dev(h));
+    return sync_stream(h);
 }
 
 static int cdc_get_chunks(vs_cdc *h, uint64_t first, uint64_t n, vs_chunk *out) {
     if (!h || h->state < 3) return fail(VS_ERR_STATE, "no finished batch");
     if (first + n > h->n_chunks) return fail(VS_ERR_ARG, "chunk range out of bounds");
     if (!n) return 0;
-    VS_TRY(set_dev(h));
+    VS_TRY(cdc_wait(h));
     std::vector<uint64_t> st(n), en(n), cu(n);
     std::vector<uint8_t> id(n * 32);
     VS_HIP(hipMemcpy(st.data(), h->ch_start.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost));
@@ -697,12 +705,15 @@ VS_API int vs_cdc_process(vs_cdc *h, const void *dev_data, uint64_t len, uint64_
     return cdc_process(h, dev_data, len, origin, final, n_chunks, consumed);
 }
 
+VS_API int vs_cdc_wait(vs_cdc *h) { return cdc_wait(h); }
+
 VS_API int vs_cdc_get_chunks(vs_cdc *h, uint64_t first, uint64_t n, vs_chunk *out) {
     return cdc_get_chunks(h, first, n, out);
 }
 
 VS_API int vs_cdc_timing(vs_cdc *h, int enable, double ms_out[4], uint64_t launches_out[4]) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
+    VS_TRY(cdc_wait(h));
     if (ms_out)
         for (int i = 0; i < 4; ++i) ms_out[i] = h->ms[i];
     if (launches_out)
