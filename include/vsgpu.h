@@ -98,6 +98,9 @@ int vs_cdc_set_batch_bytes(vs_cdc *h, uint64_t bytes);
  * Multi-GPU: each rank scans its own byte range, exchanges the exit offset of
  * its last chunk (vs_cdc_stitch) and finishes; see DESIGN.md section 6. */
 int vs_cdc_set_stream(vs_cdc *h, void *hip_stream); /* NULL = handle's own stream */
+/* Stream for the SHA-256 stage.  NULL (default) = the main stream.  The
+ * streaming vs_cdc_feed path creates a private one on first use. */
+int vs_cdc_set_hash_stream(vs_cdc *h, void *hip_stream);
 int vs_cdc_scan(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t origin,
                 uint64_t own_lo, uint64_t own_hi, int final);
 /* Selects cuts given the true start of the first chunk (entry).  *exit_pos =
@@ -120,11 +123,16 @@ int vs_cdc_get_chunks(vs_cdc *h, uint64_t first, uint64_t n, vs_chunk *out);
 int vs_cdc_timing(vs_cdc *h, int enable, double ms_out[4], uint64_t launches_out[4]);
 
 /* ---- batched SHA-256 (restic.Hash over many blobs; C5 small files) ----
- * dev_buf: device bytes; off/len: device arrays of n entries; out: device
- * array of n*32 bytes.  Blob i = dev_buf[off[i] : off[i]+len[i]]. */
-int vs_sha256_batch_device(int device, const void *dev_buf, const uint64_t *dev_off,
-                           const uint32_t *dev_len, size_t n, uint8_t *dev_out,
-                           void *hip_stream);
+ * A vs_sha handle owns the scratch of the work-queue kernel.  run_device:
+ * dev_buf device bytes; dev_off/dev_len device arrays of n entries; dev_out a
+ * device array of n*32 bytes.  Blob i = dev_buf[off[i] : off[i]+len[i]].
+ * Asynchronous on hip_stream (NULL = default stream); one run in flight per
+ * handle. */
+typedef struct vs_sha vs_sha;
+int vs_sha256_open(int device, vs_sha **h);
+int vs_sha256_run_device(vs_sha *h, const void *dev_buf, const uint64_t *dev_off,
+                         const uint32_t *dev_len, size_t n, uint8_t *dev_out, void *hip_stream);
+void vs_sha256_close(vs_sha *h);
 /* Host-memory convenience form (copies in and out). */
 int vs_sha256_batch(int device, const void *buf, size_t buf_len, const uint64_t *off,
                     const uint32_t *len, size_t n, uint8_t (*out)[32]);

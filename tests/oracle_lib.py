@@ -81,3 +81,63 @@ def sha256(data) -> bytes:
     out = np.zeros(32, np.uint8)
     lib().ref_sha256(d.ctypes.data if len(d) else None, len(d), out.ctypes.data)
     return bytes(out)
+
+
+# ---- rsync restatement (oracle/rsync_ref.c) ---------------------------------
+def _rs():
+    L = lib()
+    if not getattr(L, "_rs_ready", False):
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        L.ref_rsync_checksum2.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int,
+                                          ctypes.c_uint32, ctypes.c_void_p]
+        L.ref_have_xxhash.restype = ctypes.c_int
+        L.ref_rsync_signatures.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                           ctypes.c_int32, ctypes.c_int, ctypes.c_uint32,
+                                           ctypes.c_void_p, ctypes.c_void_p]
+        L.ref_rsync_match.restype = ctypes.c_int64
+        L.ref_rsync_match.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                      ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                      ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+        L._rs_ready = True
+    return L
+
+
+def rsync_sizes(length: int, block_size: int = 0):
+    v = [ctypes.c_int32() for _ in range(4)]
+    rc = lib().ref_rsync_sum_sizes(length, block_size, *[ctypes.byref(x) for x in v])
+    if rc < 0:
+        raise ValueError("sum_sizes overflow")
+    return tuple(x.value for x in v)   # blength, s2length, count, remainder
+
+
+def rsync_signatures(basis: np.ndarray, blength: int, s2length: int, csum_type: int, seed: int):
+    n = len(basis)
+    count = (n + blength - 1) // blength
+    s1 = np.zeros(max(count, 1), np.uint32)
+    s2 = np.zeros(max(count, 1) * s2length, np.uint8)
+    rc = _rs().ref_rsync_signatures(basis.ctypes.data if n else None, n, blength, s2length,
+                                    csum_type, seed, s1.ctypes.data, s2.ctypes.data)
+    if rc < 0:
+        raise RuntimeError("signature restatement failed")
+    return s1[:count], s2[:count * s2length].reshape(count, s2length)
+
+
+def rsync_match(src: np.ndarray, sum1: np.ndarray, sum2: np.ndarray, blength: int,
+                remainder: int, csum_type: int, seed: int):
+    count = len(sum1)
+    s2length = sum2.shape[1] if count else 2
+    cap = len(src) // max(1, blength) + 8
+    mo = np.zeros(cap, np.int64)
+    mi = np.zeros(cap, np.int32)
+    fa = ctypes.c_int64(0)
+    s1 = np.ascontiguousarray(sum1, np.uint32)
+    s2 = np.ascontiguousarray(sum2, np.uint8)
+    n = _rs().ref_rsync_match(src.ctypes.data if len(src) else None, len(src), count, blength,
+                              remainder, s2length, s1.ctypes.data if count else None,
+                              s2.ctypes.data if count else None, csum_type, seed,
+                              mo.ctypes.data, mi.ctypes.data, cap, ctypes.byref(fa))
+    if n < 0:
+        raise RuntimeError("match restatement failed")
+    return [(int(mo[i]), int(mi[i])) for i in range(n)], int(fa.value)

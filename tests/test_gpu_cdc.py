@@ -163,6 +163,36 @@ def test_sha256_batch_vs_hashlib(gpu):
         assert g == hashlib.sha256(buf[o:o + n]).digest()
 
 
+def test_small_files_device_sha(gpu):
+    """C5 shape (scaled): many 4-64 KiB files packed in one device buffer, ~50%
+    duplicate payloads; one blob ID per file from the work-queue kernel."""
+    import torch
+    from volsync_amd import DeviceSha256
+    rng = np.random.default_rng(6)
+    nfiles = 20000
+    sizes = rng.integers(4096, 65537, nfiles)
+    sizes[::97] = rng.integers(0, 200, len(sizes[::97]))   # some tiny / empty files
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    total = int(sizes.sum())
+    pool = O.synth(8, 0, 4 << 20)
+    buf = np.empty(total, np.uint8)
+    for i, (o, n) in enumerate(zip(offs.tolist(), sizes.tolist())):
+        src = int(rng.integers(0, 2000)) * 1024      # dedup-heavy: few distinct payloads
+        buf[o:o + n] = pool[src:src + n]
+    d = to_dev(buf)
+    do = torch.from_numpy(offs.astype(np.int64)).cuda()
+    dl = torch.from_numpy(sizes.astype(np.int32)).cuda()
+    out = torch.zeros((nfiles, 32), dtype=torch.uint8, device="cuda")
+    sh = DeviceSha256()
+    sh.run(d.data_ptr(), do.data_ptr(), dl.data_ptr(), nfiles, out.data_ptr())
+    torch.cuda.synchronize()
+    sh.close()
+    got = out.cpu().numpy()
+    for i in range(0, nfiles, 7):
+        o, n = int(offs[i]), int(sizes[i])
+        assert bytes(got[i]) == hashlib.sha256(buf[o:o + n].tobytes()).digest(), i
+
+
 def test_synth_device_matches_oracle(gpu):
     import torch
     from volsync_amd import synth_fill_device

@@ -74,6 +74,7 @@ def _load() -> ctypes.CDLL:
         "vs_cdc_close": (None, [vp]),
         "vs_cdc_set_batch_bytes": (c_int, [vp, c_u64]),
         "vs_cdc_set_stream": (c_int, [vp, vp]),
+        "vs_cdc_set_hash_stream": (c_int, [vp, vp]),
         "vs_cdc_scan": (c_int, [vp, vp, c_u64, c_u64, c_u64, c_u64, c_int]),
         "vs_cdc_stitch": (c_int, [vp, c_u64, u64p, ctypes.POINTER(c_int)]),
         "vs_cdc_finish": (c_int, [vp, u64p]),
@@ -81,7 +82,9 @@ def _load() -> ctypes.CDLL:
         "vs_cdc_process": (c_int, [vp, vp, c_u64, c_u64, c_int, u64p, u64p]),
         "vs_cdc_get_chunks": (c_int, [vp, c_u64, c_u64, ctypes.POINTER(VsChunk)]),
         "vs_cdc_timing": (c_int, [vp, c_int, ctypes.POINTER(ctypes.c_double), u64p]),
-        "vs_sha256_batch_device": (c_int, [c_int, vp, vp, vp, c_size, vp, vp]),
+        "vs_sha256_open": (c_int, [c_int, ctypes.POINTER(vp)]),
+        "vs_sha256_run_device": (c_int, [vp, vp, vp, vp, c_size, vp, vp]),
+        "vs_sha256_close": (None, [vp]),
         "vs_sha256_batch": (c_int, [c_int, vp, c_size, vp, vp, c_size, vp]),
         "vs_synth_fill_device": (c_int, [c_int, c_u64, c_u64, c_u64, vp, vp]),
     }

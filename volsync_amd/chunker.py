@@ -34,6 +34,7 @@ AverageBits = 20
 TestPol = 0x3DA3358B4DC173  # chunker_test.go testPol
 
 __all__ = ["Chunk", "Chunker", "EOF", "New", "NewWithBoundaries", "Pol", "DeviceChunker",
+           "DeviceSha256",
            "MinSize", "MaxSize", "KiB", "MiB"]
 
 
@@ -197,6 +198,10 @@ class DeviceChunker:
     def set_stream(self, hip_stream: int) -> None:
         check(lib.vs_cdc_set_stream(self._h, ctypes.c_void_p(hip_stream or None)))
 
+    def set_hash_stream(self, hip_stream: int) -> None:
+        """Run the SHA-256 stage on another stream (0 = the main stream)."""
+        check(lib.vs_cdc_set_hash_stream(self._h, ctypes.c_void_p(hip_stream or None)))
+
     def process(self, dev_ptr: int, length: int, origin: int = 0, final: bool = True):
         n = ctypes.c_uint64(0)
         consumed = ctypes.c_uint64(0)
@@ -263,6 +268,33 @@ def sha256_batch(buf: bytes, offs, lens, device: int = 0) -> List[bytes]:
     check(lib.vs_sha256_batch(device, b.ctypes.data, len(buf), o.ctypes.data, ln.ctypes.data, n,
                               out.ctypes.data))
     return [bytes(out[i]) for i in range(n)]
+
+
+class DeviceSha256:
+    """restic.Hash over many device-resident blobs (vs_sha256_* work-queue
+    kernel): the C5 small-file path, one blob ID per file."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self._h = ctypes.c_void_p()
+        check(lib.vs_sha256_open(device, ctypes.byref(self._h)))
+
+    def run(self, dev_buf: int, dev_off: int, dev_len: int, n: int, dev_out: int,
+            stream: Optional[int] = None) -> None:
+        check(lib.vs_sha256_run_device(self._h, ctypes.c_void_p(dev_buf), ctypes.c_void_p(dev_off),
+                                       ctypes.c_void_p(dev_len), n, ctypes.c_void_p(dev_out),
+                                       ctypes.c_void_p(stream or None)))
+
+    def close(self) -> None:
+        if self._h:
+            lib.vs_sha256_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def synth_fill_device(dev_ptr: int, seed: int, off: int, n: int, device: int = 0,

@@ -88,7 +88,18 @@ struct vs_cdc {
     uint64_t *exit_old = nullptr, *exit_new = nullptr;
     uint64_t entry = 0;  // data offset
     // chunks
-    DevBuf ch_start, ch_end, ch_cut, ch_id, order, hist, n_out;
+    DevBuf ch_start, ch_end, ch_cut, ch_id, order, hist, n_out, sha_ctr;
+    // SHA-256 stream: the main stream unless one is set (vs_cdc_set_hash_stream)
+    // or the streaming feed path creates its own, so the next batch's
+    // fingerprint pass can overlap this batch's hashing tail; events order the
+    // shared chunk arrays.  Callers that pipeline several handles keep one
+    // stream per handle: with GPU_MAX_HW_QUEUES=4, extra streams share
+    // hardware queues with other handles' main streams and serialise them.
+    hipStream_t hstream = nullptr;
+    hipStream_t own_h = nullptr;
+    hipEvent_t ev_ready = nullptr;   // main stream: chunk list + order written
+    hipEvent_t ev_hashed = nullptr;  // hash stream: blob IDs written
+    bool hash_pending = false;
     uint64_t n_chunks = 0;
     int state = 0;  // 0 idle, 1 scanned, 2 stitched, 3 finished
     // host staging
@@ -135,18 +146,19 @@ static hipEvent_t get_event(vs_cdc *h) {
 struct StageTimer {
     vs_cdc *h;
     int st;
+    hipStream_t s;
     hipEvent_t a = nullptr;
-    StageTimer(vs_cdc *h_, int st_) : h(h_), st(st_) {
+    StageTimer(vs_cdc *h_, int st_, hipStream_t s_ = nullptr) : h(h_), st(st_), s(s_ ? s_ : h_->stream) {
         if (h->timing) {
             a = get_event(h);
-            if (a) (void)hipEventRecord(a, h->stream);
+            if (a) (void)hipEventRecord(a, s);
         }
     }
     ~StageTimer() {
         if (a) {
             hipEvent_t b = get_event(h);
             if (b) {
-                (void)hipEventRecord(b, h->stream);
+                (void)hipEventRecord(b, s);
                 h->pend.push_back({st, a, b});
             } else {
                 h->ev_pool.push_back(a);
@@ -169,9 +181,14 @@ static void drain_timers(vs_cdc *h) {
     h->pend.clear();
 }
 
-static int sync_stream(vs_cdc *h) {
+// waits for the main stream; also for the hash stream when `all`
+static int sync_stream(vs_cdc *h, bool all = false) {
     VS_HIP(hipStreamSynchronize(h->stream));
-    drain_timers(h);
+    if (all && h->hash_pending) {
+        if (h->hstream) VS_HIP(hipStreamSynchronize(h->hstream));
+        h->hash_pending = false;
+    }
+    if (all || !h->hash_pending) drain_timers(h);
     return 0;
 }
 
@@ -409,6 +426,8 @@ static int cdc_finish(vs_cdc *h, uint64_t *n_chunks) {
     if (!h || h->state < 2) return fail(VS_ERR_STATE, "vs_cdc_finish before vs_cdc_stitch");
     VS_TRY(set_dev(h));
     VS_TRY(h->n_out.ensure(16));
+    // the previous batch's SHA-256 reads the chunk arrays emit rewrites
+    if (h->hash_pending) VS_HIP(hipStreamWaitEvent(h->stream, h->ev_hashed, 0));
     SelArgs s = sel_args(h);
     // upper bound of chunks: every segment's capacity
     const uint64_t cap = std::max<uint64_t>((uint64_t)h->nseg * h->maxc, 1);
@@ -423,10 +442,14 @@ static int cdc_finish(vs_cdc *h, uint64_t *n_chunks) {
     VS_TRY(sync_stream(h));
     const uint64_t n = h->pinned[0];
     h->n_chunks = n;
+    if (h->hash_pending && (h->ch_cut.cap < n * 8 || h->ch_id.cap < n * 32 || h->order.cap < n * 4)) {
+        VS_TRY(sync_stream(h, true));  // about to reallocate arrays the hash stream reads
+    }
     VS_TRY(h->ch_cut.ensure(std::max<uint64_t>(n, 1) * 8));
     VS_TRY(h->ch_id.ensure(std::max<uint64_t>(n, 1) * 32));
     VS_TRY(h->order.ensure(std::max<uint64_t>(n, 1) * 4));
     VS_TRY(h->hist.ensure((2 * 4096 + 16) * 4));
+    VS_TRY(h->sha_ctr.ensure(16));
     if (n) {
         {
             StageTimer t(h, kStOther);
@@ -437,8 +460,13 @@ static int cdc_finish(vs_cdc *h, uint64_t *n_chunks) {
                                        nullptr, h->hist.as<uint32_t>(), h->order.as<uint32_t>(),
                                        h->stream));
         }
+        hipStream_t hs = h->hstream ? h->hstream : h->stream;
+        if (hs != h->stream) {
+            VS_HIP(hipEventRecord(h->ev_ready, h->stream));
+            VS_HIP(hipStreamWaitEvent(hs, h->ev_ready, 0));
+        }
         {
-            StageTimer t(h, kStSha);
+            StageTimer t(h, kStSha, hs);
             ShaArgs a{};
             a.data = h->data;
             a.n = n;
@@ -446,8 +474,11 @@ static int cdc_finish(vs_cdc *h, uint64_t *n_chunks) {
             a.ends = h->ch_end.as<uint64_t>();
             a.order = h->order.as<uint32_t>();
             a.ids = h->ch_id.as<uint8_t>();
-            VS_HIP(launch_sha256(a, h->stream));
+            a.counter = h->sha_ctr.as<uint32_t>();
+            VS_HIP(launch_sha256(a, hs));
         }
+        VS_HIP(hipEventRecord(h->ev_hashed, hs));
+        h->hash_pending = true;
     }
     // Cut values and blob IDs stay queued on the handle's stream: results are
     // waited for by vs_cdc_wait / vs_cdc_get_chunks, so another handle's batch
@@ -460,7 +491,7 @@ static int cdc_finish(vs_cdc *h, uint64_t *n_chunks) {
 static int cdc_wait(vs_cdc *h) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
     VS_TRY(set_dev(h));
-    return sync_stream(h);
+    return sync_stream(h, true);
 }
 
 static int cdc_get_chunks(vs_cdc *h, uint64_t first, uint64_t n, vs_chunk *out) {
@@ -571,6 +602,8 @@ VS_API int vs_cdc_open(int device, uint64_t pol, uint32_t min_size, uint32_t max
         return VS_ERR_NO_DEVICE;
     }
     if (hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_hashed, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void **)&h->pinned, 64, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         delete h;
@@ -612,6 +645,13 @@ VS_API int vs_cdc_feed(vs_cdc *h, const void *buf, size_t n, int final) {
     if (h->final_fed) return fail(VS_ERR_STATE, "stream already finalised (call vs_cdc_reset)");
     if (n && !buf) return fail(VS_ERR_ARG, "null buffer");
     VS_TRY(set_dev(h));
+    if (!h->hstream) {  // streaming: hash batch k while batch k+1 is fingerprinted
+        if (!h->own_h && hipStreamCreateWithFlags(&h->own_h, hipStreamNonBlocking) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(VS_ERR_HIP, "hash stream creation failed");
+        }
+        h->hstream = h->own_h;
+    }
     const uint8_t *src = (const uint8_t *)buf;
     size_t left = n;
     for (;;) {
@@ -666,12 +706,13 @@ VS_API void vs_cdc_close(vs_cdc *h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->hstream) (void)hipStreamSynchronize(h->hstream);
     DevBuf *bufs[] = {&h->tabs,     &h->counts,  &h->offs,     &h->dslot,   &h->pool,
                       &h->flags,    &h->cstart,  &h->partials, &h->compact, &h->spec_cut,
                       &h->spec_n,   &h->spec_exit, &h->st_cut, &h->st_n,    &h->st_merge,
                       &h->st_total, &h->exit_a,  &h->exit_b,   &h->seg_off, &h->ch_start,
                       &h->ch_end,   &h->ch_cut,  &h->ch_id,    &h->order,   &h->hist,
-                      &h->n_out,    &h->sbuf[0], &h->sbuf[1]};
+                      &h->n_out,    &h->sha_ctr, &h->sbuf[0], &h->sbuf[1]};
     for (DevBuf *b : bufs) b->release();
     for (auto &p : h->pend) {
         (void)hipEventDestroy(p.a);
@@ -679,6 +720,9 @@ VS_API void vs_cdc_close(vs_cdc *h) {
     }
     for (auto e : h->ev_pool) (void)hipEventDestroy(e);
     if (h->pinned) (void)hipHostFree(h->pinned);
+    if (h->ev_ready) (void)hipEventDestroy(h->ev_ready);
+    if (h->ev_hashed) (void)hipEventDestroy(h->ev_hashed);
+    if (h->own_h) (void)hipStreamDestroy(h->own_h);
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
 }
@@ -686,6 +730,14 @@ VS_API void vs_cdc_close(vs_cdc *h) {
 VS_API int vs_cdc_set_stream(vs_cdc *h, void *hip_stream) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
     h->stream = hip_stream ? (hipStream_t)hip_stream : h->own;
+    return 0;
+}
+
+VS_API int vs_cdc_set_hash_stream(vs_cdc *h, void *hip_stream) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    VS_TRY(set_dev(h));
+    VS_TRY(sync_stream(h, true));
+    h->hstream = (hipStream_t)hip_stream;
     return 0;
 }
 
@@ -726,22 +778,60 @@ VS_API int vs_cdc_timing(vs_cdc *h, int enable, double ms_out[4], uint64_t launc
     return 0;
 }
 
-VS_API int vs_sha256_batch_device(int device, const void *dev_buf, const uint64_t *dev_off,
-                                  const uint32_t *dev_len, size_t n, uint8_t *dev_out,
-                                  void *hip_stream) {
-    if (vs_device_count() <= 0) return fail(VS_ERR_NO_DEVICE, "no HIP device available");
+struct vs_sha {
+    int device = 0;
+    DevBuf order, hist, ctr;
+};
+
+VS_API int vs_sha256_open(int device, vs_sha **out) {
+    if (!out) return fail(VS_ERR_ARG, "null handle out-pointer");
+    *out = nullptr;
+    const int ndev = vs_device_count();
+    if (ndev <= 0) return fail(VS_ERR_NO_DEVICE, "no HIP device available (no CPU fallback)");
+    if (device < 0 || device >= ndev) return fail(VS_ERR_ARG, "device index out of range");
+    VS_HIP(hipSetDevice(device));
+    vs_sha *h = new vs_sha();
+    h->device = device;
+    if (h->hist.ensure((2 * 4096 + 16) * 4) < 0 || h->ctr.ensure(16) < 0) {
+        delete h;
+        return VS_ERR_NOMEM;
+    }
+    *out = h;
+    return 0;
+}
+
+VS_API int vs_sha256_run_device(vs_sha *h, const void *dev_buf, const uint64_t *dev_off,
+                                const uint32_t *dev_len, size_t n, uint8_t *dev_out,
+                                void *hip_stream) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
     if (n && (!dev_buf || !dev_off || !dev_len || !dev_out))
         return fail(VS_ERR_ARG, "null device pointer");
-    VS_HIP(hipSetDevice(device));
+    if (!n) return 0;
+    VS_HIP(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)hip_stream;
+    VS_TRY(h->order.ensure(n * 4));
     ShaArgs a{};
     a.data = (const uint8_t *)dev_buf;
     a.n = n;
     a.starts = dev_off;
     a.lens = dev_len;
     a.ids = dev_out;
+    a.order = h->order.as<uint32_t>();
+    a.counter = h->ctr.as<uint32_t>();
+    VS_HIP(launch_length_order(n, dev_off, nullptr, dev_len, h->hist.as<uint32_t>(),
+                               h->order.as<uint32_t>(), s));
     VS_HIP(launch_sha256(a, s));
     return 0;
+}
+
+VS_API void vs_sha256_close(vs_sha *h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipDeviceSynchronize();
+    h->order.release();
+    h->hist.release();
+    h->ctr.release();
+    delete h;
 }
 
 VS_API int vs_sha256_batch(int device, const void *buf, size_t buf_len, const uint64_t *off,
@@ -751,13 +841,14 @@ VS_API int vs_sha256_batch(int device, const void *buf, size_t buf_len, const ui
     for (size_t i = 0; i < n; ++i)
         if (off[i] + len[i] > buf_len) return fail(VS_ERR_ARG, "blob outside the buffer");
     VS_HIP(hipSetDevice(device));
-    DevBuf d, o, l, r, ord, hist;
+    DevBuf d, o, l, r, ord, hist, ctr;
     VS_TRY(d.ensure(std::max<size_t>(buf_len, 16)));
     VS_TRY(o.ensure(std::max<size_t>(n, 1) * 8));
     VS_TRY(l.ensure(std::max<size_t>(n, 1) * 4));
     VS_TRY(r.ensure(std::max<size_t>(n, 1) * 32));
     VS_TRY(ord.ensure(std::max<size_t>(n, 1) * 4));
     VS_TRY(hist.ensure((2 * 4096 + 16) * 4));
+    VS_TRY(ctr.ensure(16));
     int rc = 0;
     if (hipMemcpy(d.p, buf, buf_len, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(o.p, off, n * 8, hipMemcpyHostToDevice) != hipSuccess ||
@@ -771,6 +862,7 @@ VS_API int vs_sha256_batch(int device, const void *buf, size_t buf_len, const ui
         a.lens = l.as<uint32_t>();
         a.order = ord.as<uint32_t>();
         a.ids = r.as<uint8_t>();
+        a.counter = ctr.as<uint32_t>();
         if (launch_length_order(n, a.starts, nullptr, a.lens, hist.as<uint32_t>(),
                                 ord.as<uint32_t>(), 0) != hipSuccess ||
             launch_sha256(a, 0) != hipSuccess ||
@@ -778,6 +870,7 @@ VS_API int vs_sha256_batch(int device, const void *buf, size_t buf_len, const ui
             rc = fail(VS_ERR_HIP, "SHA-256 batch failed");
     }
     d.release(); o.release(); l.release(); r.release(); ord.release(); hist.release();
+    ctr.release();
     return rc;
 }
 

@@ -14,8 +14,6 @@
 // lane group always hit 32 distinct bank pairs, whatever the indices.
 // 8.5 VALU + 2 ds_read_b64 per byte; the OUT8 lookup is off the digest's
 // dependency chain.
-#include <cstdlib>
-
 #include "internal.hpp"
 
 namespace vsgpu {
@@ -24,7 +22,7 @@ constexpr uint32_t kTabEntries = 256 * kFpCopies;  // u64 entries per table
 constexpr uint32_t kOut8Byte = kTabEntries * 8;    // byte offset of OUT8 in LDS (0x10000)
 static_assert(kOut8Byte == 0x10000, "roll() builds OUT8 addresses with v_perm");
 
-typedef uint32_t Slot[4];  // 16 bytes of the stream as 4 little-endian words
+typedef uint32_t G16[16];  // one 64-byte group as 16 little-endian words
 
 template <bool GUARD>
 __device__ __forceinline__ uint4 load16(const uint8_t *data, int64_t off, uint64_t dlen) {
@@ -39,13 +37,16 @@ __device__ __forceinline__ uint4 load16(const uint8_t *data, int64_t off, uint64
 }
 
 template <bool GUARD>
-__device__ __forceinline__ void load_slot(Slot &sl, const uint8_t *data, int64_t off,
-                                          uint64_t dlen) {
-    const uint4 v = load16<GUARD>(data, off, dlen);
-    sl[0] = v.x;
-    sl[1] = v.y;
-    sl[2] = v.z;
-    sl[3] = v.w;
+__device__ __forceinline__ void load_group(G16 &g, const uint8_t *data, int64_t off,
+                                           uint64_t dlen) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint4 v = load16<GUARD>(data, off + 16 * q, dlen);
+        g[4 * q + 0] = v.x;
+        g[4 * q + 1] = v.y;
+        g[4 * q + 2] = v.z;
+        g[4 * q + 3] = v.w;
+    }
 }
 
 __device__ __forceinline__ uint64_t lds_u64(const char *lds, uint32_t byte_addr) {
@@ -92,27 +93,25 @@ __device__ __forceinline__ uint32_t cut_bits(uint32_t hi, uint32_t lo, uint32_t 
     return lo & mlo;
 }
 
-// 16 bytes for CH chains, interleaved byte by byte (independent dependency
-// chains for ILP).  m[c] collects the minimum masked digest of chain c:
-// m[c] == 0 <=> a candidate among these 16 positions.
-template <int CH, bool WIDE, int U, int R>
-__device__ __forceinline__ void process16(uint32_t (&hi)[CH], uint32_t (&lo)[CH],
-                                          const uint32_t (&S)[CH][R][4], uint32_t (&m)[CH],
-                                          uint32_t lane8, uint32_t sh, const char *lds,
-                                          uint32_t mlo, uint32_t mhi) {
-    constexpr int O = U, N = (U + 4) % R;  // evicted bytes / incoming bytes slots
+// 64 bytes for CH chains, interleaved byte by byte for ILP.  m[c] collects the
+// minimum masked digest: 0 <=> a candidate in this group.
+template <int CH, bool WIDE>
+__device__ __forceinline__ void process_group(uint32_t (&hi)[CH], uint32_t (&lo)[CH],
+                                              const G16 (&old)[CH], const G16 (&nw)[CH],
+                                              uint32_t (&m)[CH], uint32_t lane8, uint32_t sh,
+                                              const char *lds, uint32_t mlo, uint32_t mhi) {
 #pragma unroll
     for (int c = 0; c < CH; ++c) m[c] = 0xffffffffu;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < 16; ++w) {
 #define VS_ROLL2(J0, J1)                                                                 \
     {                                                                                    \
         uint32_t a_[CH], b_[CH];                                                         \
         _Pragma("unroll") for (int c = 0; c < CH; ++c) a_[c] =                           \
-            (roll<J0>(hi[c], lo[c], S[c][O][w], S[c][N][w], lane8, sh, lds),             \
+            (roll<J0>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds),                \
              cut_bits<WIDE>(hi[c], lo[c], mlo, mhi));                                    \
         _Pragma("unroll") for (int c = 0; c < CH; ++c) b_[c] =                           \
-            (roll<J1>(hi[c], lo[c], S[c][O][w], S[c][N][w], lane8, sh, lds),             \
+            (roll<J1>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds),                \
              cut_bits<WIDE>(hi[c], lo[c], mlo, mhi));                                    \
         _Pragma("unroll") for (int c = 0; c < CH; ++c) m[c] =                            \
             __builtin_elementwise_min(__builtin_elementwise_min(m[c], a_[c]), b_[c]);    \
@@ -120,9 +119,6 @@ __device__ __forceinline__ void process16(uint32_t (&hi)[CH], uint32_t (&lo)[CH]
         VS_ROLL2(0, 1)
         VS_ROLL2(2, 3)
 #undef VS_ROLL2
-        // bound the scheduler's look-ahead to 4 bytes x CH chains: hoisting the
-        // chain-independent OUT8 lookups of a whole step costs 2 VGPRs each
-        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -159,23 +155,12 @@ __device__ void rec_dense_alloc(const FpArgs &a, StripRec &r) {
 }
 
 template <bool GUARD, bool WIDE>
-__device__ void rare_span(const FpArgs &a, StripRec &r, int64_t gpos, uint32_t sh, uint32_t lane8,
-                          const char *lds, uint64_t strip_base) {
-    // re-roll the 16 positions of a span that holds a candidate, recording each
-    // (gpos: data offset of the span, 16-aligned in the strip).  The digest
-    // before the span is recomputed from the 64 bytes that precede it (the
-    // fingerprint is position-independent), so the hot loop keeps no copy.
-    uint32_t hi = 0, lo = 0;
-    for (int j = -64; j < 0; ++j) {
-        const uint32_t bn = byte_at<GUARD>(a.data, gpos + j, a.dlen);
-        const uint32_t idx = __builtin_amdgcn_ubfe(hi, sh, 8);
-        const uint64_t mv = lds_u64(lds, (idx << 8) | lane8);
-        const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 24);
-        hi = nhi ^ (uint32_t)(mv >> 32);
-        lo = ((lo << 8) | bn) ^ (uint32_t)mv;
-    }
-    uint32_t bits = 0;
-    for (int j = 0; j < 16; ++j) {
+__device__ void rare_group(const FpArgs &a, StripRec &r, int64_t gpos, uint32_t hi,
+                           uint32_t lo, uint32_t sh, uint32_t lane8, const char *lds,
+                           uint64_t strip_base) {
+    // gpos: data offset of the group's first byte; (hi,lo): digest before it
+    uint64_t bits = 0;
+    for (int j = 0; j < 64; ++j) {
         const int64_t p = gpos + j;
         const uint32_t bo = byte_at<GUARD>(a.data, p - 64, a.dlen);
         const uint32_t bn = byte_at<GUARD>(a.data, p, a.dlen);
@@ -193,23 +178,22 @@ __device__ void rare_span(const FpArgs &a, StripRec &r, int64_t gpos, uint32_t s
                 a.offs[r.k * kSlots + r.cnt] = off;
             } else {
                 if (r.cnt == (uint32_t)kSlots) rec_dense_alloc(a, r);
-                bits |= 1u << j;
+                bits |= 1ull << j;
             }
             r.cnt++;
         }
     }
     if (bits && r.slot != kNoSlot) {
         const uint32_t words = a.strip / 32;
-        const uint32_t o = (uint32_t)((uint64_t)gpos - strip_base);  // multiple of 16
-        a.pool[(uint64_t)r.slot * words + (o >> 5)] |= bits << (o & 31);
+        uint32_t *bw = a.pool + (uint64_t)r.slot * words;
+        const uint32_t w0 = (uint32_t)(((uint64_t)gpos - strip_base) >> 5);
+        bw[w0] |= (uint32_t)bits;
+        bw[w0 + 1] |= (uint32_t)(bits >> 32);
     }
 }
 
-// CH independent chains per lane; R-slot ring of 16-byte registers per chain
-// (R = 8: refills run 3 steps ahead; R = 6: 1 step ahead, 16 fewer VGPRs).
-template <int CH, int R, bool GUARD, bool WIDE>
+template <int CH, bool GUARD, bool WIDE>
 __global__ __launch_bounds__(kFpThreads) void fp_kernel(FpArgs a) {
-    static_assert(R == 6 || R == 8, "ring of 6 or 8 slots");
     __shared__ __attribute__((aligned(16))) uint64_t tabs[2 * kTabEntries];  // 128 KiB
     for (uint32_t i = threadIdx.x; i < kTabEntries; i += blockDim.x) {
         const uint32_t e = i / kFpCopies;
@@ -222,7 +206,7 @@ __global__ __launch_bounds__(kFpThreads) void fp_kernel(FpArgs a) {
     const uint32_t sh = a.idx_shift;
     const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t NS = a.strip / 16;  // 16-byte steps per strip (multiple of 24)
+    const uint32_t G = a.strip / 64;  // checked groups per strip (multiple of 3)
 
     StripRec rec[CH];
     int64_t sb[CH];  // strip base (data offset)
@@ -237,69 +221,55 @@ __global__ __launch_bounds__(kFpThreads) void fp_kernel(FpArgs a) {
         sb[c] = (int64_t)(a.base + rec[c].k * a.strip);
     }
 
-    // Ring of R 16-byte slots per chain: step s (bytes sb+16s..+15) reads its
-    // evicted bytes (step s-4) from slot s%R and its new bytes from slot
-    // (s+4)%R; after the step, slot s%R is refilled with step s+R-4.
-    uint32_t S[CH][R][4];
-#pragma unroll
-    for (int c = 0; c < CH; ++c)
-#pragma unroll
-        for (int j = 0; j < R; ++j) load_slot<GUARD>(S[c][j], a.data, sb[c] - 64 + 16 * j, a.dlen);
-
-    // warm-up over the 64 bytes before the strip: window of virtual zeros, digest 0
     uint32_t hi[CH], lo[CH], m[CH];
+    G16 X[CH], Y[CH], Z[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        load_group<GUARD>(X[c], a.data, sb[c] - 64, a.dlen);  // warm-up bytes
+        load_group<GUARD>(Y[c], a.data, sb[c], a.dlen);       // group 1
+    }
+    // warm-up: the window starts as 64 virtual zero bytes, digest 0
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
         hi[c] = 0;
         lo[c] = 0;
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int w = 0; w < 16; ++w) {
 #pragma unroll
-        for (int w = 0; w < 4; ++w)
-#pragma unroll
-            for (int c = 0; c < CH; ++c) {
-                roll_warm<0>(hi[c], lo[c], S[c][j][w], lane8, sh, lds);
-                roll_warm<1>(hi[c], lo[c], S[c][j][w], lane8, sh, lds);
-                roll_warm<2>(hi[c], lo[c], S[c][j][w], lane8, sh, lds);
-                roll_warm<3>(hi[c], lo[c], S[c][j][w], lane8, sh, lds);
-            }
+        for (int c = 0; c < CH; ++c) {
+            roll_warm<0>(hi[c], lo[c], X[c][w], lane8, sh, lds);
+            roll_warm<1>(hi[c], lo[c], X[c][w], lane8, sh, lds);
+            roll_warm<2>(hi[c], lo[c], X[c][w], lane8, sh, lds);
+            roll_warm<3>(hi[c], lo[c], X[c][w], lane8, sh, lds);
+        }
+    }
 
-#define VS_STEP(U)                                                                        \
+#define VS_GROUP(OLD, NEW, NEXT, GI)                                                      \
     {                                                                                     \
-        process16<CH, WIDE, U, R>(hi, lo, S, m, lane8, sh, lds, a.mask_lo, a.mask_hi);       \
+        if ((GI) + 1 <= G) {                                                              \
+            _Pragma("unroll") for (int c = 0; c < CH; ++c)                                \
+                load_group<GUARD>(NEXT[c], a.data, sb[c] + 64 * (int64_t)(GI), a.dlen);   \
+        }                                                                                 \
+        uint32_t h0[CH], l0[CH];                                                          \
+        _Pragma("unroll") for (int c = 0; c < CH; ++c) {                                  \
+            h0[c] = hi[c];                                                                \
+            l0[c] = lo[c];                                                                \
+        }                                                                                 \
+        process_group<CH, WIDE>(hi, lo, OLD, NEW, m, lane8, sh, lds, a.mask_lo, a.mask_hi); \
         _Pragma("unroll") for (int c = 0; c < CH; ++c) {                                  \
             if (m[c] == 0)                                                                \
-                rare_span<GUARD, WIDE>(a, rec[c], sb[c] + 16 * (int64_t)(s0 + U), sh, lane8, \
-                                       lds, (uint64_t)sb[c]);                             \
-        }                                                                                 \
-        if (s0 + U + R - 4 < NS) {                                                        \
-            _Pragma("unroll") for (int c = 0; c < CH; ++c) {                              \
-                if (GUARD) {                                                              \
-                    load_slot<GUARD>(S[c][U], a.data, sb[c] + 16 * (int64_t)(s0 + U + R - 4), \
-                                     a.dlen);                                             \
-                } else {                                                                  \
-                    const uint4 v_ = q[c][U + R - 4]; /* base + immediate offset */   \
-                    S[c][U][0] = v_.x;                                                    \
-                    S[c][U][1] = v_.y;                                                    \
-                    S[c][U][2] = v_.z;                                                    \
-                    S[c][U][3] = v_.w;                                                    \
-                }                                                                         \
-            }                                                                             \
+                rare_group<GUARD, WIDE>(a, rec[c], sb[c] + 64 * (int64_t)((GI) - 1), h0[c], \
+                                        l0[c], sh, lane8, lds, (uint64_t)sb[c]);          \
         }                                                                                 \
     }
-    const uint4 *q[CH];  // 16-byte step s0 of each strip (advances 128 B per iteration)
-#pragma unroll
-    for (int c = 0; c < CH; ++c) q[c] = (const uint4 *)(a.data + sb[c]);
-    for (uint32_t s0 = 0; s0 < NS; s0 += R) {
-        VS_STEP(0) VS_STEP(1) VS_STEP(2) VS_STEP(3) VS_STEP(4) VS_STEP(5)
-        if constexpr (R == 8) {
-            VS_STEP(6) VS_STEP(7)
-        }
-#pragma unroll
-        for (int c = 0; c < CH; ++c) q[c] += R;
+
+    for (uint32_t g = 1; g <= G; g += 3) {
+        VS_GROUP(X, Y, Z, g)
+        VS_GROUP(Y, Z, X, g + 1)
+        VS_GROUP(Z, X, Y, g + 2)
     }
-#undef VS_STEP
+#undef VS_GROUP
 
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
@@ -310,39 +280,26 @@ __global__ __launch_bounds__(kFpThreads) void fp_kernel(FpArgs a) {
     }
 }
 
-template <int CH, int R>
-static void launch_variant(const FpArgs &a, bool guard, bool wide, hipStream_t s) {
+#ifndef VS_FP_CHAINS
+#define VS_FP_CHAINS 1
+#endif
+
+hipError_t launch_fingerprint(const FpArgs &a, bool guard, bool wide, hipStream_t s) {
+    if (a.k_count == 0) return hipSuccess;
+    constexpr int CH = VS_FP_CHAINS;
     const uint64_t threads = (a.k_count + CH - 1) / CH;
     const uint32_t blocks = (uint32_t)((threads + kFpThreads - 1) / kFpThreads);
     if (guard) {
         if (wide)
-            fp_kernel<CH, R, true, true><<<blocks, kFpThreads, 0, s>>>(a);
+            fp_kernel<CH, true, true><<<blocks, kFpThreads, 0, s>>>(a);
         else
-            fp_kernel<CH, R, true, false><<<blocks, kFpThreads, 0, s>>>(a);
+            fp_kernel<CH, true, false><<<blocks, kFpThreads, 0, s>>>(a);
     } else {
         if (wide)
-            fp_kernel<CH, R, false, true><<<blocks, kFpThreads, 0, s>>>(a);
+            fp_kernel<CH, false, true><<<blocks, kFpThreads, 0, s>>>(a);
         else
-            fp_kernel<CH, R, false, false><<<blocks, kFpThreads, 0, s>>>(a);
+            fp_kernel<CH, false, false><<<blocks, kFpThreads, 0, s>>>(a);
     }
-}
-
-// VSGPU_FP_VARIANT: "2x6" (default: two chains per lane, 6-slot rings, 128
-// VGPRs) or "1x8" (one chain, 8-slot ring, 80 VGPRs).  Both are bit-identical.
-static int fp_variant() {
-    static int v = [] {
-        const char *e = getenv("VSGPU_FP_VARIANT");
-        return (e && e[0] == '1') ? 1 : 2;
-    }();
-    return v;
-}
-
-hipError_t launch_fingerprint(const FpArgs &a, bool guard, bool wide, hipStream_t s) {
-    if (a.k_count == 0) return hipSuccess;
-    if (fp_variant() == 1)
-        launch_variant<1, 8>(a, guard, wide, s);
-    else
-        launch_variant<2, 6>(a, guard, wide, s);
     return hipGetLastError();
 }
 

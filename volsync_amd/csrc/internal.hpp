@@ -120,6 +120,7 @@ struct ShaArgs {
     const uint32_t *lens;     // lengths, or nullptr
     const uint32_t *order;    // nullptr = identity
     uint8_t *ids;
+    uint32_t *counter;        // work-queue head (device word; zeroed by launch_sha256)
 };
 hipError_t launch_sha256(const ShaArgs &a, hipStream_t s);
 // Longest-first permutation of n blob lengths (bucketed by 64 KiB).

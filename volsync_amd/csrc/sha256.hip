@@ -11,6 +11,8 @@
 // per 64-byte block 64 rounds x 14 ops + 48 schedule words x 10 ops with
 // v_bitop3_b32 for Ch / Maj / the three-way XORs, v_alignbit_b32 for
 // rotates and v_perm_b32 for the big-endian, byte-misaligned message words.
+#include <algorithm>
+
 #include "internal.hpp"
 
 namespace vsgpu {
@@ -76,70 +78,131 @@ __device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
     st[7] += h;
 }
 
-__device__ __forceinline__ void load_block(const uint32_t *wp, uint64_t wi, bool need17,
-                                           uint32_t (&d)[17]) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) d[i] = wp[wi + i];
-    d[16] = need17 ? wp[wi + 16] : 0u;
+// Work-queue SHA-256.  A fixed grid of lanes pulls blobs
+// longest-first from a global counter; every loop iteration each busy lane
+// compresses exactly one 64-byte block -- a data block, or one of the one or
+// two padding blocks it builds from the blob's tail -- so a wave stays full
+// until the queue drains and only the fetch / padding build diverge.  Waves
+// whose blobs have the most blocks left raise their issue priority, so the
+// longest blobs (the latency tail) run at the single-wave issue rate while
+// co-resident waves fill the SIMD's remaining issue slots.
+__device__ __forceinline__ uint64_t blob_len(const ShaArgs &a, uint64_t i, uint64_t start) {
+    return a.ends ? ((a.ends[i] & kPosMask) - start + 1) : a.lens[i];
 }
 
-__global__ __launch_bounds__(256) void sha256_kernel(ShaArgs a) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= a.n) return;
-    const uint64_t i = a.order ? a.order[t] : t;
-    const uint64_t start = a.starts[i];
-    const uint64_t len = a.ends ? ((a.ends[i] & kPosMask) - start + 1) : a.lens[i];
-    const uint32_t r = (uint32_t)(start & 3);
-    const uint32_t sel = (r << 24) | ((r + 1) << 16) | ((r + 2) << 8) | (r + 3);
-    const uint32_t *wp = (const uint32_t *)(a.data + (start - r));
-    uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
-                      0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
-    const uint64_t nfull = len >> 6;
-    const bool need17 = r != 0;
-    uint32_t cur[17], nxt[17];
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
-    for (int k = 0; k < 17; ++k) nxt[k] = 0;
-    if (nfull) load_block(wp, 0, need17, cur);
-    for (uint64_t b = 0; b < nfull; ++b) {
-        if (b + 1 < nfull) load_block(wp, 16 * (b + 1), need17, nxt);
-        uint32_t w[16];
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+
+// The next block's words are loaded while the current block is compressed
+// (one wave per SIMD in a latency tail has nothing else to hide the load).
+__device__ __forceinline__ void load_words(uint32_t (&d)[17], const uint32_t *wp, uint32_t lim) {
+    if (lim >= 64) {
+        // data block: one unconditional 64-byte load (merged into 4 x dwordx4)
 #pragma unroll
-        for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_perm(cur[k + 1], cur[k], sel);
-        compress(st, w);
-#pragma unroll
-        for (int k = 0; k < 17; ++k) cur[k] = nxt[k];
-    }
-    // tail: rem bytes + 0x80 + zeros + 64-bit big-endian bit length
-    const uint64_t rem = len - (nfull << 6);
-    const uint8_t *tp = a.data + start + (nfull << 6);
-    uint32_t w[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] = 0;
-    for (uint32_t j = 0; j < (uint32_t)rem; ++j) w[j >> 2] |= (uint32_t)tp[j] << (24 - 8 * (j & 3));
-    w[rem >> 2] |= 0x80u << (24 - 8 * (rem & 3));
-    const uint64_t bits = len << 3;
-    if (rem < 56) {
-        w[14] = (uint32_t)(bits >> 32);
-        w[15] = (uint32_t)bits;
-        compress(st, w);
+        for (int k = 0; k < 16; ++k) d[k] = wp[k];
+        d[16] = (lim > 64) ? wp[16] : 0u;
     } else {
-        compress(st, w);
+        // padding block (once per blob): only the words that hold tail bytes
 #pragma unroll
-        for (int k = 0; k < 14; ++k) w[k] = 0;
-        w[14] = (uint32_t)(bits >> 32);
-        w[15] = (uint32_t)bits;
-        compress(st, w);
+        for (int k = 0; k < 17; ++k) d[k] = (4u * k < lim) ? wp[k] : 0u;
     }
-    uint4 *out = (uint4 *)(a.ids + 32 * i);
-    out[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]),
-                        __builtin_bswap32(st[2]), __builtin_bswap32(st[3]));
-    out[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]),
-                        __builtin_bswap32(st[6]), __builtin_bswap32(st[7]));
 }
 
+// words of block j: data blocks read 64 B (+4 when misaligned); the first
+// padding block reads only the words holding tail bytes (never past the blob)
+__device__ __forceinline__ uint32_t block_lim(uint32_t j, uint32_t nfull, uint32_t r,
+                                              uint32_t rem) {
+    return (j < nfull) ? (r ? 68u : 64u) : (j == nfull ? r + rem : 0u);
+}
+
+__global__ __launch_bounds__(256, 4) void sha256_kernel(ShaArgs a) {
+    bool has = false, done = false;
+    uint32_t ci = 0;               // blob index
+    const uint32_t *wp = nullptr;  // 4-aligned words of block b+1 (the prefetch target)
+    uint32_t sel = 0;              // v_perm selector: byte misalignment r in its top byte
+    uint32_t nfull = 0, b = 0, rem = 0;  // full data blocks, current block, tail bytes
+    uint32_t st[8];
+    uint32_t d[17];                // raw words of block b
+    for (;;) {
+        if (!has && !done) {
+            const uint32_t t = atomicAdd(a.counter, 1u);
+            if (t < a.n) {
+                ci = a.order ? a.order[t] : t;
+                const uint64_t start = a.starts[ci];
+                const uint64_t len = blob_len(a, ci, start);
+                const uint32_t r = (uint32_t)(start & 3);
+                sel = (r << 24) | ((r + 1) << 16) | ((r + 2) << 8) | (r + 3);
+                wp = (const uint32_t *)(a.data + (start - r));
+                nfull = (uint32_t)(len >> 6);
+                rem = (uint32_t)(len & 63);
+                b = 0;
+                load_words(d, wp, block_lim(0, nfull, r, rem));
+                wp += 16;
+                st[0] = 0x6a09e667; st[1] = 0xbb67ae85; st[2] = 0x3c6ef372; st[3] = 0xa54ff53a;
+                st[4] = 0x510e527f; st[5] = 0x9b05688c; st[6] = 0x1f83d9ab; st[7] = 0x5be0cd19;
+                has = true;
+                // raise the issue priority of waves that hold the longest blobs
+                const uint32_t left = wave_max_u32(min(nfull >> 13, 3u));
+                const uint32_t pr = __builtin_amdgcn_readfirstlane(left);
+                if (pr >= 3) __builtin_amdgcn_s_setprio(3);
+                else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+                else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            } else {
+                done = true;
+            }
+        }
+        if (__all(done)) break;
+        if (has) {
+            const uint32_t r = sel >> 24;
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_perm(d[k + 1], d[k], sel);
+            if (b >= nfull) {
+                // padding: [tail bytes, 0x80, zeros] (+ big-endian bit length)
+                const uint32_t tl = (b == nfull) ? rem : 0u;
+                const bool mark = b == nfull;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const int v = min(max((int)tl - 4 * k, 0), 4);  // tail bytes in word k
+                    const uint32_t keep = (v == 4) ? 0xffffffffu : ~(0xffffffffu >> (8 * v));
+                    const uint32_t m80 =
+                        (mark && v < 4 && (int)tl >= 4 * k) ? (0x80u << (24 - 8 * v)) : 0u;
+                    w[k] = (w[k] & keep) | m80;
+                }
+                if (b > nfull || rem < 56) {
+                    const uint64_t bits = ((uint64_t)nfull * 64 + rem) << 3;
+                    w[14] = (uint32_t)(bits >> 32);
+                    w[15] = (uint32_t)bits;
+                }
+            }
+            load_words(d, wp, block_lim(b + 1, nfull, r, rem));  // prefetch block b+1
+            wp += 16;
+            compress(st, w);
+            ++b;
+            if (b == nfull + (rem < 56 ? 1u : 2u)) {
+                uint4 *out = (uint4 *)(a.ids + 32ull * ci);
+                out[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]),
+                                    __builtin_bswap32(st[2]), __builtin_bswap32(st[3]));
+                out[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]),
+                                    __builtin_bswap32(st[6]), __builtin_bswap32(st[7]));
+                has = false;
+            }
+        }
+    }
+}
+
+// grid: one lane per blob up to two waves per SIMD (256 CUs x 4 SIMDs x 2);
+// counter: a device word, zeroed here on the stream before the launch
 hipError_t launch_sha256(const ShaArgs &a, hipStream_t s) {
     if (!a.n) return hipSuccess;
-    sha256_kernel<<<(uint32_t)((a.n + 255) / 256), 256, 0, s>>>(a);
+    hipError_t e = hipMemsetAsync(a.counter, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    const uint64_t lanes = std::min<uint64_t>(a.n, 2048ull * 64);
+    sha256_kernel<<<(uint32_t)((lanes + 255) / 256), 256, 0, s>>>(a);
     return hipGetLastError();
 }
 
