@@ -72,7 +72,7 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=int, default=4)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=4,
+    ap.add_argument("--inflight", type=int, default=2,
                     help="volumes in flight: handles on separate HIP streams, steps round-robin")
     args = ap.parse_args()
 

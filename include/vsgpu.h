@@ -97,6 +97,9 @@ int vs_cdc_set_batch_bytes(vs_cdc *h, uint64_t bytes);
  * clipped to the stream, and final = 1 when origin + len is the stream end.
  * Multi-GPU: each rank scans its own byte range, exchanges the exit offset of
  * its last chunk (vs_cdc_stitch) and finishes; see DESIGN.md section 6. */
+/* Ordering: with the handle's own stream (default) a scan waits for work
+ * already queued on the null stream; with vs_cdc_set_stream the caller's
+ * stream must already order the producer of dev_data before the scan. */
 int vs_cdc_set_stream(vs_cdc *h, void *hip_stream); /* NULL = handle's own stream */
 /* Stream for the SHA-256 stage.  NULL (default) = the main stream.  The
  * streaming vs_cdc_feed path creates a private one on first use. */
@@ -139,7 +142,8 @@ int vs_sha256_batch(int device, const void *buf, size_t buf_len, const uint64_t 
 
 /* ---- device utilities for benches and tests --------------------------- */
 /* Fill dev_out[0:n] with bytes [off, off+n) of the synthetic splitmix64
- * volume stream. */
+ * volume stream.  hip_stream NULL: returns when the fill is
+ * complete; otherwise queued on that stream. */
 int vs_synth_fill_device(int device, uint64_t seed, uint64_t off, uint64_t n, void *dev_out,
                          void *hip_stream);
 

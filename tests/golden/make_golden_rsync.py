@@ -26,36 +26,10 @@ sys.path.insert(0, ROOT)
 from oracle import cdc_ref as P  # noqa: E402
 from oracle import rsync_ref as R  # noqa: E402
 from tests import oracle_lib as O  # noqa: E402
+from tests.golden_util import rsync_pair as make_pair  # noqa: E402
 
 OUT = os.path.dirname(os.path.abspath(__file__))
 SEED = 0x5EED5EED
-
-
-def make_pair(spec: dict):
-    """(basis, source) byte arrays for a fixture spec (shared with the tests)."""
-    kind = spec["kind"]
-    n = spec["basis_len"]
-    if kind == "dup_blocks":
-        unit = P.synth(spec["seed"], 0, spec["period"])
-        basis = np.tile(unit, -(-n // spec["period"]))[:n].copy()
-    else:
-        basis = P.synth(spec["seed"], 0, n)
-    if kind in ("mutate", "dup_blocks"):
-        bl = O.rsync_sizes(n, spec.get("block_size", 0))[0]
-        src = R.mutate(basis, bl, spec["edit_seed"], spec["frac"])
-        if spec.get("shift"):
-            src = np.concatenate([P.synth(99, 0, spec["shift"]), src])
-    elif kind == "identical":
-        src = basis.copy()
-    elif kind == "disjoint":
-        src = P.synth(spec["seed"] + 1000, 0, spec["src_len"])
-    elif kind == "prefix":
-        src = basis[: spec["src_len"]].copy()
-    else:
-        raise ValueError(kind)
-    if "src_len" in spec and kind == "mutate":
-        src = src[: spec["src_len"]]
-    return basis, src
 
 
 def case(name, spec, csum_type=R.CSUM_XXH3_128, seed=SEED, note=""):

@@ -39,6 +39,36 @@ def make_input(spec: dict) -> np.ndarray:
     raise ValueError(kind)
 
 
+def rsync_pair(spec: dict):
+    """(basis, source) byte arrays for an rsync fixture spec (make_golden_rsync.py)."""
+    from oracle import cdc_ref as P
+    from oracle import rsync_ref as R
+    from tests import oracle_lib as O
+    kind = spec["kind"]
+    n = spec["basis_len"]
+    if kind == "dup_blocks":
+        unit = P.synth(spec["seed"], 0, spec["period"])
+        basis = np.tile(unit, -(-n // spec["period"]))[:n].copy()
+    else:
+        basis = P.synth(spec["seed"], 0, n)
+    if kind in ("mutate", "dup_blocks"):
+        bl = O.rsync_sizes(n, spec.get("block_size", 0))[0]
+        src = R.mutate(basis, bl, spec["edit_seed"], spec["frac"])
+        if spec.get("shift"):
+            src = np.concatenate([P.synth(99, 0, spec["shift"]), src])
+    elif kind == "identical":
+        src = basis.copy()
+    elif kind == "disjoint":
+        src = P.synth(spec["seed"] + 1000, 0, spec["src_len"])
+    elif kind == "prefix":
+        src = basis[: spec["src_len"]].copy()
+    else:
+        raise ValueError(kind)
+    if "src_len" in spec and kind == "mutate":
+        src = src[: spec["src_len"]]
+    return basis, src
+
+
 def params(doc):
     p = doc["params"]
     return int(p["pol"], 16), int(p["min"]), int(p["max"]), int(p["avg_bits"])

@@ -99,6 +99,7 @@ struct vs_cdc {
     hipStream_t own_h = nullptr;
     hipEvent_t ev_ready = nullptr;   // main stream: chunk list + order written
     hipEvent_t ev_hashed = nullptr;  // hash stream: blob IDs written
+    hipEvent_t ev_null = nullptr;    // orders a scan after prior null-stream work
     bool hash_pending = false;
     uint64_t n_chunks = 0;
     int state = 0;  // 0 idle, 1 scanned, 2 stitched, 3 finished
@@ -325,6 +326,13 @@ static int cdc_scan(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t orig
     if (own_lo < origin || own_hi < own_lo || own_hi > origin + len)
         return fail(VS_ERR_ARG, "own range must lie inside [origin, origin + len)");
     VS_TRY(set_dev(h));
+    if (h->stream == h->own) {
+        // the handle's own stream is non-blocking: order the scan after work the
+        // caller queued on the null stream (e.g. the kernel that wrote the data).
+        // With vs_cdc_set_stream the caller's stream carries that order instead.
+        VS_HIP(hipEventRecord(h->ev_null, nullptr));
+        VS_HIP(hipStreamWaitEvent(h->stream, h->ev_null, 0));
+    }
     h->data = (const uint8_t *)dev_data;
     h->dlen = len;
     h->origin = origin;
@@ -604,6 +612,7 @@ VS_API int vs_cdc_open(int device, uint64_t pol, uint32_t min_size, uint32_t max
     if (hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_ready, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_hashed, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_null, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void **)&h->pinned, 64, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         delete h;
@@ -722,6 +731,7 @@ VS_API void vs_cdc_close(vs_cdc *h) {
     if (h->pinned) (void)hipHostFree(h->pinned);
     if (h->ev_ready) (void)hipEventDestroy(h->ev_ready);
     if (h->ev_hashed) (void)hipEventDestroy(h->ev_hashed);
+    if (h->ev_null) (void)hipEventDestroy(h->ev_null);
     if (h->own_h) (void)hipStreamDestroy(h->own_h);
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
@@ -879,5 +889,6 @@ VS_API int vs_synth_fill_device(int device, uint64_t seed, uint64_t off, uint64_
     if (vs_device_count() <= 0) return fail(VS_ERR_NO_DEVICE, "no HIP device available");
     VS_HIP(hipSetDevice(device));
     VS_HIP(launch_synth(seed, off, n, (uint8_t *)dev_out, (hipStream_t)hip_stream));
+    if (!hip_stream) VS_HIP(hipStreamSynchronize(nullptr));  // NULL stream: blocking fill
     return 0;
 }
