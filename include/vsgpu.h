@@ -1,15 +1,20 @@
 /*
  * vsgpu.h -- C ABI of the MI355X data-movement hot path behind VolSync's
- * restic mover: content-defined chunking (restic chunker, Rabin fingerprint
- * over a 64-byte window) plus SHA-256 blob IDs, as hand-written gfx950 HIP
- * kernels.
+ * restic and rsync movers: content-defined chunking (restic chunker, Rabin
+ * fingerprint over a 64-byte window) plus SHA-256 blob IDs, and rsync's
+ * rolling weak checksum + strong-sum block matching, as hand-written gfx950
+ * HIP kernels.
  *
  * The reference binds this path in Go.  The restic mover image
  * (/root/reference/mover-restic/Dockerfile:8-27) builds restic v0.13.1, whose
  * archiver calls github.com/restic/chunker@v0.4.0 and crypto/sha256 (patched
  * in by mover-restic/patch-sources.sh:16-27); restic runs from
- * mover-restic/entry.sh:60-65 ("restic backup").  Each entry point below names
- * the upstream interface it replaces; INTEGRATION.md shows the cgo binding.
+ * mover-restic/entry.sh:60-65 ("restic backup").  The rsync mover image
+ * (mover-rsync/Dockerfile:11-12) installs rsync 3.2.3, run by
+ * mover-rsync/source.sh:54 (rsync -aAhHSxz --delete ...); its sender's
+ * match.c/checksum.c/generator.c functions are the vs_rsync_* entry points.
+ * Each entry point below names the upstream interface it replaces;
+ * INTEGRATION.md shows the cgo binding.
  *
  * Conventions:
  *  - return 0 on success, a negative VS_ERR_* on failure, VS_EOF (1) when a
@@ -139,6 +144,77 @@ void vs_sha256_close(vs_sha *h);
 /* Host-memory convenience form (copies in and out). */
 int vs_sha256_batch(int device, const void *buf, size_t buf_len, const uint64_t *off,
                     const uint32_t *len, size_t n, uint8_t (*out)[32]);
+
+/* ---- rsync delta matching (rsync 3.2.3) -----
+ * csum_type: the negotiated xfersum (checksum.c): VS_CSUM_MD5 (seed
+ * prepended as LE u32 when non-zero), VS_CSUM_XXH64, VS_CSUM_XXH3_64,
+ * VS_CSUM_XXH3_128 (the 3.2.3 <-> 3.2.3 default).  seed = checksum_seed. */
+#define VS_CSUM_MD5 5
+#define VS_CSUM_XXH64 6
+#define VS_CSUM_XXH3_64 7
+#define VS_CSUM_XXH3_128 8
+
+/* One match: match.c matched(offset, i) -- source bytes [offset, offset +
+ * len_i) equal destination block i; literals are the gaps between matches. */
+typedef struct vs_match {
+    int64_t offset;
+    int32_t block_index;
+    int32_t reserved;
+} vs_match;
+
+/* Replaces generator.c sum_sizes_sqroot (protocol >= 30): block length,
+ * strong-sum bytes sent, block count and last-block remainder for a
+ * destination of len bytes; block_size != 0 is --block-size. */
+int vs_rsync_sizes(int64_t len, int32_t block_size, int32_t *blength, int32_t *s2length,
+                   int32_t *count, int32_t *remainder);
+
+typedef struct vs_rsync vs_rsync;
+int vs_rsync_open(int device, vs_rsync **h);
+int vs_rsync_set_stream(vs_rsync *h, void *hip_stream); /* NULL = handle's own stream */
+void vs_rsync_close(vs_rsync *h);
+/* Replaces generator.c generate_and_send_sums (get_checksum1 + get_checksum2
+ * per block): signatures of a device-resident destination file.  dev_sum1
+ * [count] u32 and dev_sum2 [count * s2length] bytes are device arrays.
+ * Returns after queueing on the handle's stream. */
+int vs_rsync_signatures_device(vs_rsync *h, const void *dev_basis, int64_t len, int32_t blength,
+                               int32_t s2length, int csum_type, uint32_t seed,
+                               uint32_t *dev_sum1, uint8_t *dev_sum2);
+/* Replaces match.c build_hash_table: load the signature table the sender
+ * received (read_sum_head + per-block sum1/sum2).  Host arrays (copied) or,
+ * in the _device form, device arrays. */
+int vs_rsync_load_sums(vs_rsync *h, int32_t count, int32_t blength, int32_t s2length,
+                       int32_t remainder, const uint32_t *sum1, const uint8_t *sum2,
+                       int csum_type, uint32_t seed);
+int vs_rsync_load_sums_device(vs_rsync *h, int32_t count, int32_t blength, int32_t s2length,
+                              int32_t remainder, const uint32_t *dev_sum1,
+                              const uint8_t *dev_sum2, int csum_type, uint32_t seed);
+/* Replaces match.c match_sums -> hash_search: the greedy match list of a
+ * device-resident source against the loaded table (identical to rsync's,
+ * including chain order, the want_i preference and false-alarm handling).
+ * Blocks until done; *n_matches = number of matches. */
+int vs_rsync_match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_matches);
+/* Copy matches [first, first+n) of the last match run to host. */
+int vs_rsync_get_matches(vs_rsync *h, int64_t first, int64_t n, vs_match *out);
+/* Counters of the last match run: weak candidates found by the scan,
+ * false alarms (strong mismatches the walk visited, rsync's stats), windows
+ * strong-hashed on the device, walk rounds. */
+int vs_rsync_stats(vs_rsync *h, int64_t *candidates, int64_t *false_alarms,
+                   int64_t *strong_hashed, int32_t *rounds);
+/* Device time (ms) of the last run's stages: 0 signatures, 1 table, 2 scan
+ * (prefix + weak scan + sort), 3 strong verification, 4 host walk. */
+int vs_rsync_timing(vs_rsync *h, double ms_out[5]);
+
+/* Host-memory one-shot forms: copy in, run, copy out. */
+int vs_rsync_signatures(int device, const void *basis, int64_t len, int32_t blength,
+                        int32_t s2length, int csum_type, uint32_t seed, uint32_t *sum1,
+                        uint8_t *sum2);
+typedef struct vs_sigtable {
+    int32_t count, blength, s2length, remainder;
+    const uint32_t *sum1; /* [count] */
+    const uint8_t *sum2;  /* [count * s2length] */
+} vs_sigtable;
+int vs_rsync_match(int device, const void *src, int64_t len, const vs_sigtable *t,
+                   int csum_type, uint32_t seed, vs_match *out, size_t cap, size_t *n_out);
 
 /* ---- device utilities for benches and tests --------------------------- */
 /* Fill dev_out[0:n] with bytes [off, off+n) of the synthetic splitmix64

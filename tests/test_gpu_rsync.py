@@ -1,0 +1,196 @@
+"""GPU parity tests of rsync delta matching (R1-R6) through the C ABI.
+
+Bar: bit-exact sum1/sum2 signatures and match lists (offset, block index)
+against the committed golden fixtures and the C restatement of hash_search
+(oracle/rsync_ref.c) on seeded inputs; at larger sizes, properties (every
+match is a byte-exact copy, matches tile without overlap, the unedited blocks
+are found).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import rsync_ref as R
+from tests import golden_util as G
+from tests import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+FIX = G.fixtures("rsync_*.json")
+
+
+def to_dev(arr: np.ndarray):
+    import torch
+    t = torch.empty(max(len(arr), 16), dtype=torch.uint8, device="cuda")
+    if len(arr):
+        t[: len(arr)].copy_(torch.from_numpy(np.ascontiguousarray(arr)))
+    torch.cuda.synchronize()
+    return t
+
+
+def load_fixture(path):
+    doc = G.load(path)
+    basis, src = G.rsync_pair(doc["input"])
+    return doc, basis, src
+
+
+@pytest.mark.parametrize("path", FIX, ids=os.path.basename)
+def test_signatures_vs_golden(gpu, path):
+    from volsync_amd import generate_sums
+    doc, basis, _ = load_fixture(path)
+    p, z = doc["params"], doc["sizes"]
+    s = generate_sums(basis, p["csum_type"], p["seed"], p["block_size"])
+    assert (s.blength, s.s2length, s.count, s.remainder) == \
+        (z["blength"], z["s2length"], z["count"], z["remainder"])
+    assert [int(x) for x in s.sum1] == doc["sum1"]
+    assert [bytes(r).hex() for r in s.sum2] == doc["sum2"]
+
+
+@pytest.mark.parametrize("path", FIX, ids=os.path.basename)
+def test_match_vs_golden(gpu, path):
+    from volsync_amd import SumStruct, match_sums
+    doc, _, src = load_fixture(path)
+    p, z = doc["params"], doc["sizes"]
+    s = SumStruct(flength=0, count=z["count"], blength=z["blength"], s2length=z["s2length"],
+                  remainder=z["remainder"], sum1=np.array(doc["sum1"], np.uint32),
+                  sum2=np.array([list(bytes.fromhex(h)) for h in doc["sum2"]], np.uint8).reshape(
+                      z["count"], z["s2length"]))
+    got = match_sums(src, s, p["csum_type"], p["seed"])
+    assert got == [tuple(m) for m in doc["matches"]]
+
+
+@pytest.mark.parametrize("csum_type,seed,n,frac,block_size", [
+    (R.CSUM_XXH3_128, 0x5EED5EED, 48 << 20, 0.10, 0),
+    (R.CSUM_MD5, 0x5EED5EED, 24 << 20, 0.10, 0),
+    (R.CSUM_XXH3_64, 7, 16 << 20, 0.30, 0),
+    (R.CSUM_XXH64, 0, 16 << 20, 0.05, 0),
+    (R.CSUM_XXH3_128, 1, 8 << 20, 0.20, 1000),        # odd block size: unaligned blocks
+    (R.CSUM_XXH3_128, 2, (5 << 20) + 777, 0.10, 0),   # short last block
+])
+def test_device_path_vs_c_oracle(gpu, csum_type, seed, n, frac, block_size):
+    """Signatures on the device (vs_rsync_signatures_device), table loaded from
+    device arrays, match on a device-resident source: == the C hash_search."""
+    import torch
+    from volsync_amd import Matcher, sum_sizes_sqroot
+    basis = O.synth(100 + n % 97, 0, n)
+    hdr = sum_sizes_sqroot(n, block_size)
+    src = R.mutate(basis, hdr.blength, seed=n % 1000, frac=frac)
+    db, ds = to_dev(basis), to_dev(src)
+    s1 = torch.zeros(max(hdr.count, 1), dtype=torch.int32, device="cuda")
+    s2 = torch.zeros(max(hdr.count, 1) * hdr.s2length, dtype=torch.uint8, device="cuda")
+    m = Matcher()
+    m.signatures_device(db.data_ptr(), n, hdr.blength, hdr.s2length, csum_type, seed,
+                        s1.data_ptr(), s2.data_ptr())
+    m.load_sums_device(hdr.count, hdr.blength, hdr.s2length, hdr.remainder, s1.data_ptr(),
+                       s2.data_ptr(), csum_type, seed)
+    got = m.match_sums(ds.data_ptr(), len(src))
+    st = m.stats()
+    m.close()
+    c1, c2 = O.rsync_signatures(basis, hdr.blength, hdr.s2length, csum_type, seed)
+    assert (s1.cpu().numpy().view(np.uint32)[: hdr.count] == c1).all()
+    assert (s2.cpu().numpy()[: hdr.count * hdr.s2length].reshape(-1, hdr.s2length) == c2).all()
+    want, fa = O.rsync_match(src, c1, c2, hdr.blength, hdr.remainder, csum_type, seed)
+    assert got == want
+    assert st["false_alarms"] == fa
+
+
+def test_weak_collisions_and_false_alarms(gpu):
+    """Tiny strong sums (s2length 2, the minimum) over a small-block table make
+    false alarms and strong collisions likely: the walk must follow rsync
+    exactly through them (want_i, chain order, false-alarm continue)."""
+    from volsync_amd import SumStruct, match_sums
+    rng = np.random.default_rng(11)
+    # low-entropy data: weak sums collide often
+    basis = rng.integers(0, 3, 300_000, dtype=np.uint8)
+    src = np.concatenate([basis[1000:150_000], rng.integers(0, 3, 20_000, dtype=np.uint8),
+                          basis[:100_000]])
+    for csum_type, seed in [(R.CSUM_XXH3_128, 3), (R.CSUM_MD5, 0), (R.CSUM_XXH64, 9)]:
+        bl, s2l, cnt, rem = O.rsync_sizes(len(basis), 700)
+        c1, c2 = O.rsync_signatures(basis, bl, s2l, csum_type, seed)
+        want, fa = O.rsync_match(src, c1, c2, bl, rem, csum_type, seed)
+        s = SumStruct(0, cnt, bl, s2l, rem, c1, c2)
+        assert match_sums(src, s, csum_type, seed) == want
+
+
+def test_repeated_blocks_prefer_adjacent(gpu):
+    """Identical blocks: rsync's chain offers the highest index first and the
+    want_i rule then prefers the block after the previous match."""
+    from volsync_amd import generate_sums, match_sums
+    unit = O.synth(5, 0, 700)
+    basis = np.tile(unit, 64)
+    src = np.concatenate([basis[:7000], O.synth(6, 0, 333), basis[:14000]])
+    s = generate_sums(basis, R.CSUM_XXH3_128, 77)
+    want, _ = O.rsync_match(src, s.sum1, s.sum2, s.blength, s.remainder, R.CSUM_XXH3_128, 77)
+    assert match_sums(src, s, R.CSUM_XXH3_128, 77) == want
+
+
+def test_empty_inputs(gpu):
+    from volsync_amd import generate_sums, match_sums
+    s = generate_sums(np.zeros(0, np.uint8))
+    assert s.count == 0
+    assert match_sums(O.synth(1, 0, 5000), s) == []
+    s = generate_sums(O.synth(1, 0, 5000))
+    assert match_sums(np.zeros(0, np.uint8), s) == []
+
+
+def test_c4_shape_properties(gpu):
+    """C4 shape at 4 GiB on one device (blength 65536): every match is a
+    byte-exact copy of its block, matches never overlap, >= 85% of the blocks
+    are found, and the list equals the C oracle on a 256 MiB window pair."""
+    import torch
+    from volsync_amd import Matcher, sum_sizes_sqroot, synth_fill_device
+    n = 4 << 30
+    hdr = sum_sizes_sqroot(n)
+    db = torch.empty(n, dtype=torch.uint8, device="cuda")
+    synth_fill_device(db.data_ptr(), 4, 0, n)
+    # source: basis with edits at 10% of the blocks, assembled on the device
+    rng = np.random.default_rng(5)
+    edits = np.sort(rng.choice(hdr.count, hdr.count // 10, replace=False))
+    pieces, pos = [], 0
+    for b in edits.tolist():
+        at = b * hdr.blength + int(rng.integers(0, hdr.blength - 4096))
+        pieces.append(db[pos:at])
+        kind = int(rng.integers(0, 3))
+        if kind == 0:
+            pieces.append(torch.randint(0, 256, (4096,), dtype=torch.uint8, device="cuda"))
+            pos = at + 4096
+        elif kind == 1:
+            pieces.append(torch.randint(0, 256, (int(rng.integers(1, 65)),), dtype=torch.uint8,
+                                        device="cuda"))
+            pos = at
+        else:
+            pos = at + int(rng.integers(1, 65))
+    pieces.append(db[pos:])
+    ds = torch.cat(pieces)
+    del pieces
+    s1 = torch.zeros(hdr.count, dtype=torch.int32, device="cuda")
+    s2 = torch.zeros(hdr.count * hdr.s2length, dtype=torch.uint8, device="cuda")
+    m = Matcher()
+    m.signatures_device(db.data_ptr(), n, hdr.blength, hdr.s2length, R.CSUM_XXH3_128,
+                        0x5EED5EED, s1.data_ptr(), s2.data_ptr())
+    m.load_sums_device(hdr.count, hdr.blength, hdr.s2length, hdr.remainder, s1.data_ptr(),
+                       s2.data_ptr(), R.CSUM_XXH3_128, 0x5EED5EED)
+    got = m.match_sums(ds.data_ptr(), ds.numel())
+    m.close()
+    assert len(got) >= 0.85 * hdr.count
+    prev = 0
+    rng2 = np.random.default_rng(1)
+    picks = set(rng2.integers(0, len(got), 200).tolist())
+    for j, (o, i) in enumerate(got):
+        assert o >= prev
+        prev = o + hdr.blength
+        if j in picks:
+            assert torch.equal(ds[o:o + hdr.blength], db[i * hdr.blength:(i + 1) * hdr.blength])
+    # exact list on a window pair that fits the CPU oracle
+    w = 256 << 20
+    bw = db[:w].cpu().numpy()
+    sw = ds[:w].cpu().numpy()
+    del db, ds
+    torch.cuda.empty_cache()
+    hw = sum_sizes_sqroot(w)
+    c1, c2 = O.rsync_signatures(bw, hw.blength, hw.s2length, R.CSUM_XXH3_128, 0x5EED5EED)
+    want, _ = O.rsync_match(sw, c1, c2, hw.blength, hw.remainder, R.CSUM_XXH3_128, 0x5EED5EED)
+    from volsync_amd import SumStruct, match_sums
+    s = SumStruct(0, hw.count, hw.blength, hw.s2length, hw.remainder, c1, c2)
+    assert match_sums(sw, s, R.CSUM_XXH3_128, 0x5EED5EED) == want

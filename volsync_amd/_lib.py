@@ -29,10 +29,25 @@ c_u64 = ctypes.c_uint64
 c_u32 = ctypes.c_uint32
 c_int = ctypes.c_int
 c_size = ctypes.c_size_t
+i32 = ctypes.c_int32
+i64 = ctypes.c_int64
+i32p = ctypes.POINTER(ctypes.c_int32)
+i64p = ctypes.POINTER(ctypes.c_int64)
 
 
 class VsChunk(ctypes.Structure):
     _fields_ = [("start", c_u64), ("length", c_u64), ("cut", c_u64), ("id", ctypes.c_uint8 * 32)]
+
+
+class VsMatch(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_int64), ("block_index", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+class VsSigTable(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_int32), ("blength", ctypes.c_int32),
+                ("s2length", ctypes.c_int32), ("remainder", ctypes.c_int32),
+                ("sum1", vp), ("sum2", vp)]
 
 
 class VsError(RuntimeError):
@@ -87,6 +102,20 @@ def _load() -> ctypes.CDLL:
         "vs_sha256_close": (None, [vp]),
         "vs_sha256_batch": (c_int, [c_int, vp, c_size, vp, vp, c_size, vp]),
         "vs_synth_fill_device": (c_int, [c_int, c_u64, c_u64, c_u64, vp, vp]),
+        "vs_rsync_sizes": (c_int, [i64, i32, i32p, i32p, i32p, i32p]),
+        "vs_rsync_open": (c_int, [c_int, ctypes.POINTER(vp)]),
+        "vs_rsync_set_stream": (c_int, [vp, vp]),
+        "vs_rsync_close": (None, [vp]),
+        "vs_rsync_signatures_device": (c_int, [vp, vp, i64, i32, i32, c_int, c_u32, vp, vp]),
+        "vs_rsync_load_sums": (c_int, [vp, i32, i32, i32, i32, vp, vp, c_int, c_u32]),
+        "vs_rsync_load_sums_device": (c_int, [vp, i32, i32, i32, i32, vp, vp, c_int, c_u32]),
+        "vs_rsync_match_device": (c_int, [vp, vp, i64, i64p]),
+        "vs_rsync_get_matches": (c_int, [vp, i64, i64, ctypes.POINTER(VsMatch)]),
+        "vs_rsync_stats": (c_int, [vp, i64p, i64p, i64p, i32p]),
+        "vs_rsync_timing": (c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
+        "vs_rsync_signatures": (c_int, [c_int, vp, i64, i32, i32, c_int, c_u32, vp, vp]),
+        "vs_rsync_match": (c_int, [c_int, vp, i64, ctypes.POINTER(VsSigTable), c_int, c_u32,
+                                   ctypes.POINTER(VsMatch), c_size, ctypes.POINTER(c_size)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -26,34 +26,6 @@ int fail(int code, const std::string &msg) {
     return code;
 }
 
-struct DevBuf {
-    void *p = nullptr;
-    size_t cap = 0;
-    int ensure(size_t bytes) {
-        if (bytes <= cap) return 0;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-        size_t want = std::max<size_t>(bytes, 256);
-        if (hipMalloc(&p, want) != hipSuccess) {
-            p = nullptr;
-            (void)hipGetLastError();
-            return fail(VS_ERR_NOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
-        }
-        cap = want;
-        return 0;
-    }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-    template <class T>
-    T *as() const {
-        return (T *)p;
-    }
-};
-
 // strip = 64 * G with G % 3 == 0 (fingerprint.hip rotates three group buffers)
 constexpr uint32_t kStrip = 12288;
 

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <algorithm>
 #include <string>
 
 #include "../../include/vsgpu.h"
@@ -24,6 +25,35 @@ int fail(int code, const std::string &msg);
         int r_ = (expr);             \
         if (r_ < 0) return r_;       \
     } while (0)
+
+// ---- device buffer that only grows ------------------------------------------
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 256);
+        if (hipMalloc(&p, want) != hipSuccess) {
+            p = nullptr;
+            (void)hipGetLastError();
+            return fail(VS_ERR_NOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
+        }
+        cap = want;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T *as() const {
+        return (T *)p;
+    }
+};
 
 // ---- Rabin tables (chunker.go fillTables) ----------------------------------
 int pol_deg(uint64_t p);
@@ -134,5 +164,55 @@ hipError_t launch_synth(uint64_t seed, uint64_t off, uint64_t n, uint8_t *out, h
 // ---- misc ---------------------------------------------------------------------
 hipError_t launch_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *partials,
                            uint32_t clamp, hipStream_t s);
+
+// ---- rsync delta matching (rsync.hip) ------------------------------------------
+constexpr uint64_t kRsG = 4096;       // coarse prefix granularity (bytes)
+constexpr uint64_t kRsStrip = 4096;   // offsets per scan lane (multiple of kRsG and 16)
+
+struct RsSigArgs {
+    const uint8_t *data;   // basis bytes
+    uint64_t len;
+    uint64_t count;        // blocks
+    uint32_t blength, remainder, s2length;
+    int csum_type;
+    uint32_t seed;
+    uint32_t *sum1;        // [count]
+    uint8_t *sum2;         // [count * s2length]
+};
+hipError_t launch_rs_signatures(const RsSigArgs &a, hipStream_t s);
+hipError_t launch_rs_strong(const uint8_t *data, const uint64_t *offs, const uint32_t *lens,
+                            uint64_t n, int csum_type, uint32_t seed, uint32_t s2length,
+                            uint8_t *out, hipStream_t s);
+// sort keys (sum1 << 32 | ~index) -> tkey, directory over the top dbits of sum1
+// (2^dbits + 1 entries) and a 2^fbits-bit filter over the top fbits
+hipError_t launch_rs_table(const uint32_t *sum1, uint32_t count, uint64_t *keys, uint64_t *tkey,
+                           void *tmp, size_t tmp_bytes, uint32_t dbits, uint32_t *dir,
+                           uint32_t fbits, uint32_t *filt, hipStream_t s);
+size_t rs_sort_tmp_bytes(uint64_t n_keys, bool pairs);
+// coarse prefixes: px/pt per kRsG block, *_scan exclusive (n+1 entries)
+hipError_t launch_rs_prefix(const uint8_t *data, uint64_t len, uint32_t *px, uint32_t *pt,
+                            uint32_t *px_scan, uint32_t *pt_scan, uint32_t *partials,
+                            hipStream_t s);
+
+struct RsScanArgs {
+    const uint8_t *data;   // source bytes
+    uint64_t len;
+    uint64_t nfull;        // offsets with a full blength window: len - blength + 1 (or 0)
+    uint64_t blength;
+    uint32_t count, remainder;
+    const uint32_t *px_scan, *pt_scan;
+    const uint64_t *tkey;  // sorted (sum1 << 32 | ~index)
+    const uint32_t *dir;
+    const uint32_t *filt;
+    uint32_t dbits, fbits;
+    unsigned long long *n_cand;
+    uint64_t cap;
+    uint64_t *cand_off;    // [cap]
+    uint32_t *cand_sum;    // [cap]
+};
+hipError_t launch_rs_scan(const RsScanArgs &a, hipStream_t s);
+hipError_t launch_rs_sort_cands(void *tmp, size_t tmp_bytes, const uint64_t *off_in,
+                                uint64_t *off_out, const uint32_t *sum_in, uint32_t *sum_out,
+                                uint64_t n, int end_bit, hipStream_t s);
 
 }  // namespace vsgpu

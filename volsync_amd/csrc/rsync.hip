@@ -1,0 +1,308 @@
+// rsync.hip -- rsync 3.2.3 delta matching on gfx950.
+//
+//   R1 weak sum   get_checksum1 over signed bytes: s1 = sum b, s2 = sum (k-j) b_j,
+//                 sum = (s1 & 0xffff) | (s2 << 16).  Four bytes per v_dot4c_i32_i8.
+//   R2 strong sum get_checksum2 (strong.hpp: XXH3-128/64, XXH64, MD5).
+//   R4 signatures one lane per destination block: weak + strong.
+//   R5 table      blocks sorted by (sum1 ascending, index descending) -- the
+//                 order in which match.c build_hash_table's chains present the
+//                 blocks of one weak sum -- plus a bucket directory on the top
+//                 bits of sum1 and a bit filter in front of it.
+//   R6 scan       every source offset's weak sum: coarse prefix sums give a
+//                 lane the window sum at its strip start, the lane then rolls
+//                 (hash_search's s1/s2 update) and probes filter -> directory ->
+//                 entries; offsets with a block of equal sum1 and length are
+//                 appended as candidates.  Strong sums of candidates the greedy
+//                 walk visits are computed in batches (rs_strong_kernel).
+// HBM layout: source/basis bytes as given (16-byte aligned base); candidates
+// (offset u64, sum u32) appended then radix-sorted by offset.  DESIGN.md 4.
+#include <hipcub/hipcub.hpp>
+
+#include "internal.hpp"
+#include "strong.hpp"
+
+namespace vsgpu {
+
+// ---- weak sums ------------------------------------------------------------------
+// signed-byte dot products: sum of 4 bytes, and 4 bytes weighted by w (int8 lanes)
+__device__ __forceinline__ int dot4(uint32_t word, uint32_t w, int acc) {
+    return __builtin_amdgcn_sdot4((int)word, (int)w, acc, false);
+}
+
+// 16 bytes at p (any alignment), bounds-checked against [0, lim)
+__device__ __forceinline__ void load16(const uint8_t *p, uint64_t pos, uint64_t lim,
+                                       uint32_t (&w)[4]) {
+    if (pos + 16 <= lim) {
+        memcpy(w, p + pos, 16);
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t v = 0;
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t q = pos + 4 * i + j;
+            if (q < lim) v |= (uint32_t)p[q] << (8 * j);
+        }
+        w[i] = v;
+    }
+}
+
+// (sum b, sum u*b) over bytes [pos, pos+n) with u = position - pos (local weights)
+__device__ void weak_parts(const uint8_t *p, uint64_t pos, uint64_t n, uint64_t lim,
+                           uint32_t &sx, uint32_t &sux) {
+    uint32_t a = 0, b = 0;
+    uint64_t u = 0;
+    for (; u + 16 <= n; u += 16) {
+        uint32_t w[4];
+        load16(p, pos + u, lim, w);
+        int s = 0, t = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            s = dot4(w[i], 0x01010101u, s);
+            // weights 4i .. 4i+3 for bytes 0..3 of word i (little endian)
+            t = dot4(w[i], (uint32_t)(4 * i) * 0x01010101u + 0x03020100u, t);
+        }
+        b += (uint32_t)u * (uint32_t)s + (uint32_t)t;
+        a += (uint32_t)s;
+    }
+    for (; u < n; ++u) {
+        const uint32_t x = (uint32_t)(int32_t)(int8_t)p[pos + u];
+        a += x;
+        b += (uint32_t)u * x;
+    }
+    sx = a;
+    sux = b;
+}
+
+// get_checksum1 of [pos, pos+n): s1 = sum x, s2 = sum (n - u) x = n*s1 - sum u*x
+__device__ __forceinline__ uint32_t weak_sum(const uint8_t *p, uint64_t pos, uint64_t n,
+                                             uint64_t lim) {
+    uint32_t sx, sux;
+    weak_parts(p, pos, n, lim, sx, sux);
+    const uint32_t s2 = (uint32_t)n * sx - sux;
+    return (sx & 0xffffu) | (s2 << 16);
+}
+
+// ---- R4 signatures: one lane per block ------------------------------------------
+__global__ void rs_sig_kernel(RsSigArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.count) return;
+    const uint64_t pos = i * a.blength;
+    const uint64_t n = (i == a.count - 1 && a.remainder) ? a.remainder : a.blength;
+    a.sum1[i] = weak_sum(a.data, pos, n, a.len);
+    uint8_t s[16];
+    vsstrong::checksum2(a.data + pos, n, a.csum_type, a.seed, s);
+    for (uint32_t j = 0; j < a.s2length; ++j) a.sum2[i * a.s2length + j] = s[j];
+}
+
+hipError_t launch_rs_signatures(const RsSigArgs &a, hipStream_t s) {
+    if (!a.count) return hipSuccess;
+    rs_sig_kernel<<<(uint32_t)((a.count + 127) / 128), 128, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+// ---- strong sums of arbitrary windows (candidate verification) --------------------
+__global__ void rs_strong_kernel(const uint8_t *data, const uint64_t *offs, const uint32_t *lens,
+                                 uint64_t n, int csum_type, uint32_t seed, uint32_t s2length,
+                                 uint8_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t s[16];
+    vsstrong::checksum2(data + offs[i], lens[i], csum_type, seed, s);
+    for (uint32_t j = 0; j < s2length; ++j) out[i * s2length + j] = s[j];
+}
+
+hipError_t launch_rs_strong(const uint8_t *data, const uint64_t *offs, const uint32_t *lens,
+                            uint64_t n, int csum_type, uint32_t seed, uint32_t s2length,
+                            uint8_t *out, hipStream_t s) {
+    if (!n) return hipSuccess;
+    rs_strong_kernel<<<(uint32_t)((n + 127) / 128), 128, 0, s>>>(data, offs, lens, n, csum_type,
+                                                                 seed, s2length, out);
+    return hipGetLastError();
+}
+
+// ---- R5 table: sort keys, directory, filter ----------------------------------------
+__global__ void rs_keys_kernel(const uint32_t *sum1, uint32_t count, uint64_t *keys) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) keys[i] = ((uint64_t)sum1[i] << 32) | (uint32_t)~i;
+}
+
+// dir[b] = first sorted position whose bucket (sum1 >> (32 - dbits)) >= b, b in [0, 2^dbits]
+__global__ void rs_dir_kernel(const uint64_t *tkey, uint32_t count, uint32_t dbits, uint32_t *dir,
+                              uint32_t fbits, uint32_t *filt) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nb = 1ull << dbits;
+    if (p > count) return;
+    const uint64_t b = (p < count) ? (tkey[p] >> (64 - dbits)) : nb;
+    const uint64_t bp = (p == 0) ? 0 : (tkey[p - 1] >> (64 - dbits)) + 1;
+    for (uint64_t q = bp; q <= b; ++q) dir[q] = (uint32_t)p;
+    if (p < count) {
+        const uint32_t f = (uint32_t)(tkey[p] >> (64 - fbits));
+        atomicOr(&filt[f >> 5], 1u << (f & 31));
+    }
+}
+
+hipError_t launch_rs_table(const uint32_t *sum1, uint32_t count, uint64_t *keys, uint64_t *tkey,
+                           void *tmp, size_t tmp_bytes, uint32_t dbits, uint32_t *dir,
+                           uint32_t fbits, uint32_t *filt, hipStream_t s) {
+    if (!count) return hipSuccess;
+    rs_keys_kernel<<<(count + 255) / 256, 256, 0, s>>>(sum1, count, keys);
+    hipError_t e = hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, keys, tkey, (int)count, 0, 64,
+                                                     s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(filt, 0, ((1ull << fbits) / 32) * 4, s);
+    if (e != hipSuccess) return e;
+    rs_dir_kernel<<<(count + 1 + 255) / 256, 256, 0, s>>>(tkey, count, dbits, dir, fbits, filt);
+    return hipGetLastError();
+}
+
+size_t rs_sort_tmp_bytes(uint64_t n_keys, bool pairs) {
+    size_t b = 0;
+    if (pairs)
+        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint64_t *)nullptr,
+                                                 (uint64_t *)nullptr, (const uint32_t *)nullptr,
+                                                 (uint32_t *)nullptr, (int)n_keys, 0, 64);
+    else
+        (void)hipcub::DeviceRadixSort::SortKeys(nullptr, b, (const uint64_t *)nullptr,
+                                                (uint64_t *)nullptr, (int)n_keys, 0, 64);
+    return b;
+}
+
+// ---- R6 coarse prefix sums of the source ------------------------------------------
+// per kRsG-byte block j: px[j] = sum x, pt[j] = sum t*x (t absolute, mod 2^32)
+__global__ void rs_block_sums_kernel(const uint8_t *data, uint64_t len, uint64_t nblk,
+                                     uint32_t *px, uint32_t *pt) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nblk) return;
+    const uint64_t pos = j * kRsG;
+    const uint64_t n = min((uint64_t)kRsG, len - pos);
+    uint32_t sx, sux;
+    weak_parts(data, pos, n, len, sx, sux);
+    px[j] = sx;
+    pt[j] = (uint32_t)pos * sx + sux;
+}
+
+hipError_t launch_rs_prefix(const uint8_t *data, uint64_t len, uint32_t *px, uint32_t *pt,
+                            uint32_t *px_scan, uint32_t *pt_scan, uint32_t *partials,
+                            hipStream_t s) {
+    const uint64_t nblk = (len + kRsG - 1) / kRsG;
+    if (nblk) {
+        rs_block_sums_kernel<<<(uint32_t)((nblk + 255) / 256), 256, 0, s>>>(data, len, nblk, px,
+                                                                            pt);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = launch_scan_u32(px, px_scan, nblk, partials, 0xffffffffu, s);
+    if (e != hipSuccess) return e;
+    return launch_scan_u32(pt, pt_scan, nblk, partials, 0xffffffffu, s);
+}
+
+// ---- R6 weak scan ----------------------------------------------------------------------
+// prefix (sum x, sum t*x) of bytes [0, q)
+__device__ __forceinline__ void prefix_at(const RsScanArgs &a, uint64_t q, uint32_t &sx,
+                                          uint32_t &stx) {
+    const uint64_t j = q / kRsG;
+    const uint64_t q0 = j * kRsG;
+    uint32_t x = a.px_scan[j], t = a.pt_scan[j];
+    if (q > q0) {
+        uint32_t bx, bux;
+        weak_parts(a.data, q0, q - q0, a.len, bx, bux);
+        x += bx;
+        t += (uint32_t)q0 * bx + bux;
+    }
+    sx = x;
+    stx = t;
+}
+
+// does a block with sum1 == sum and length k exist?
+__device__ __forceinline__ bool probe(const RsScanArgs &a, uint32_t sum, bool full) {
+    const uint32_t f = sum >> (32 - a.fbits);
+    if (!((a.filt[f >> 5] >> (f & 31)) & 1u)) return false;
+    const uint32_t b = sum >> (32 - a.dbits);
+    const uint32_t p0 = a.dir[b], p1 = a.dir[b + 1];
+    for (uint32_t p = p0; p < p1; ++p) {
+        const uint64_t key = a.tkey[p];
+        const uint32_t s1 = (uint32_t)(key >> 32);
+        if (s1 > sum) break;
+        if (s1 < sum) continue;
+        const uint32_t i = ~(uint32_t)key;
+        const bool last_short = (i == a.count - 1) && a.remainder;
+        if (full ? !last_short : last_short) return true;
+    }
+    return false;
+}
+
+__device__ __forceinline__ void emit(const RsScanArgs &a, uint64_t o, uint32_t sum) {
+    const unsigned long long slot = atomicAdd((unsigned long long *)a.n_cand, 1ull);
+    if (slot < a.cap) {
+        a.cand_off[slot] = o;
+        a.cand_sum[slot] = sum;
+    }
+}
+
+// lane per strip of kRsStrip offsets in [0, nfull): full windows of blength bytes
+__global__ void rs_scan_kernel(RsScanArgs a) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t o0 = k * kRsStrip;
+    if (o0 >= a.nfull) return;
+    const uint64_t o1 = min(o0 + kRsStrip, a.nfull);
+    const uint64_t n = a.blength;
+    // window sum at o0 from the coarse prefixes (o0 is a multiple of kRsG)
+    uint32_t xa, ta, xb, tb;
+    prefix_at(a, o0, xa, ta);
+    prefix_at(a, o0 + n, xb, tb);
+    uint32_t s1 = xb - xa;
+    uint32_t s2 = (uint32_t)(n + o0) * s1 - (tb - ta);
+    const uint8_t *d = a.data;
+    const uint32_t nn = (uint32_t)n;
+    for (uint64_t o = o0; o < o1; o += 16) {
+        uint32_t wo[4], wi[4];
+        load16(d, o, a.len, wo);       // bytes leaving: o .. o+15
+        load16(d, o + n, a.len, wi);   // bytes entering: o+n .. o+n+15
+        uint32_t sums[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            sums[j] = (s1 & 0xffffu) | (s2 << 16);
+            const uint32_t xo = (uint32_t)__builtin_amdgcn_sbfe(wo[j >> 2], 8 * (j & 3), 8);
+            const uint32_t xi = (uint32_t)__builtin_amdgcn_sbfe(wi[j >> 2], 8 * (j & 3), 8);
+            // hash_search's roll: s1 -= out; s2 -= k*out; s1 += in; s2 += s1
+            s1 = s1 - xo + xi;
+            s2 = s2 - nn * xo + s1;
+        }
+        uint32_t hit = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t f = sums[j] >> (32 - a.fbits);
+            hit |= ((a.filt[f >> 5] >> (f & 31)) & 1u) << j;
+        }
+        while (hit) {
+            const int j = __builtin_ctz(hit);
+            hit &= hit - 1;
+            if (o + j < o1 && probe(a, sums[j], true)) emit(a, o + j, sums[j]);
+        }
+    }
+}
+
+// the one shrunk-window offset that can match (the short last block), on one lane
+__global__ void rs_scan_tail_kernel(RsScanArgs a, uint64_t o) {
+    const uint32_t sum = weak_sum(a.data, o, a.len - o, a.len);
+    if (probe(a, sum, false)) emit(a, o, sum);
+}
+
+hipError_t launch_rs_scan(const RsScanArgs &a, hipStream_t s) {
+    const uint64_t strips = (a.nfull + kRsStrip - 1) / kRsStrip;
+    if (strips) rs_scan_kernel<<<(uint32_t)((strips + 127) / 128), 128, 0, s>>>(a);
+    if (a.remainder && a.count && a.len >= a.remainder)
+        rs_scan_tail_kernel<<<1, 1, 0, s>>>(a, a.len - a.remainder);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_sort_cands(void *tmp, size_t tmp_bytes, const uint64_t *off_in,
+                                uint64_t *off_out, const uint32_t *sum_in, uint32_t *sum_out,
+                                uint64_t n, int end_bit, hipStream_t s) {
+    if (!n) return hipSuccess;
+    return hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, off_in, off_out, sum_in, sum_out,
+                                              (int)n, 0, end_bit, s);
+}
+
+}  // namespace vsgpu

@@ -1,0 +1,162 @@
+"""Host-side mirror of rsync 3.2.3's sender-side delta interface over the C ABI.
+
+rsync (installed by /root/reference/mover-rsync/Dockerfile:11-12, run from
+mover-rsync/source.sh:54) is C; its delta stage is a handful of functions over
+`struct sum_struct`.  Names and argument meaning follow them:
+
+  sum_sizes_sqroot(len)            generator.c  -> SumStruct header
+  generate_sums(basis, ...)        generator.c generate_and_send_sums
+                                   (get_checksum1 + get_checksum2 per block)
+  Matcher.load_sums(sums)          match.c build_hash_table
+  Matcher.match_sums(src)          match.c match_sums -> hash_search
+                                   -> [(offset, block_index)] = matched() calls
+
+All compute runs in volsync_amd/lib/libvsgpu.so on a gfx950 device; there is
+no CPU fallback (a missing library raises ImportError, a missing device
+VsError(VS_ERR_NO_DEVICE)).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from ._lib import VsMatch, VsSigTable, check, lib
+
+CSUM_MD5, CSUM_XXH64, CSUM_XXH3_64, CSUM_XXH3_128 = 5, 6, 7, 8
+
+
+@dataclass
+class SumStruct:
+    """match.c / rsync.h `struct sum_struct`: header plus per-block sums."""
+    flength: int
+    count: int
+    blength: int
+    s2length: int
+    remainder: int
+    sum1: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
+    sum2: np.ndarray = field(default_factory=lambda: np.zeros((0, 2), np.uint8))
+
+    def block_len(self, i: int) -> int:
+        return self.remainder if (i == self.count - 1 and self.remainder) else self.blength
+
+
+def sum_sizes_sqroot(length: int, block_size: int = 0) -> SumStruct:
+    v = [ctypes.c_int32() for _ in range(4)]
+    check(lib.vs_rsync_sizes(int(length), int(block_size), *[ctypes.byref(x) for x in v]))
+    bl, s2, cnt, rem = (x.value for x in v)
+    return SumStruct(flength=int(length), count=cnt, blength=bl, s2length=s2, remainder=rem)
+
+
+def _host_bytes(buf) -> np.ndarray:
+    if isinstance(buf, np.ndarray):
+        return np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+    return np.frombuffer(bytes(buf), dtype=np.uint8)
+
+
+def generate_sums(basis, csum_type: int = CSUM_XXH3_128, seed: int = 0, block_size: int = 0,
+                  device: int = 0) -> SumStruct:
+    """Signatures of a host buffer (copied to the device)."""
+    b = _host_bytes(basis)
+    s = sum_sizes_sqroot(len(b), block_size)
+    s.sum1 = np.zeros(max(s.count, 1), np.uint32)
+    s.sum2 = np.zeros((max(s.count, 1), s.s2length), np.uint8)
+    check(lib.vs_rsync_signatures(device, b.ctypes.data if len(b) else None, len(b), s.blength,
+                                  s.s2length, csum_type, seed & 0xFFFFFFFF, s.sum1.ctypes.data,
+                                  s.sum2.ctypes.data))
+    s.sum1, s.sum2 = s.sum1[: s.count], s.sum2[: s.count]
+    return s
+
+
+class Matcher:
+    """A vs_rsync handle: device signatures, table and match runs."""
+
+    def __init__(self, device: int = 0):
+        self._h = ctypes.c_void_p()
+        check(lib.vs_rsync_open(device, ctypes.byref(self._h)))
+
+    def close(self) -> None:
+        if self._h:
+            lib.vs_rsync_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, hip_stream: int) -> None:
+        check(lib.vs_rsync_set_stream(self._h, ctypes.c_void_p(hip_stream or None)))
+
+    def signatures_device(self, dev_basis: int, length: int, blength: int, s2length: int,
+                          csum_type: int, seed: int, dev_sum1: int, dev_sum2: int) -> None:
+        check(lib.vs_rsync_signatures_device(self._h, ctypes.c_void_p(dev_basis or None), length,
+                                             blength, s2length, csum_type, seed & 0xFFFFFFFF,
+                                             ctypes.c_void_p(dev_sum1 or None),
+                                             ctypes.c_void_p(dev_sum2 or None)))
+
+    def load_sums(self, s: SumStruct, csum_type: int = CSUM_XXH3_128, seed: int = 0) -> None:
+        s1 = np.ascontiguousarray(s.sum1, np.uint32)
+        s2 = np.ascontiguousarray(s.sum2, np.uint8)
+        check(lib.vs_rsync_load_sums(self._h, s.count, s.blength, s.s2length, s.remainder,
+                                     s1.ctypes.data if s.count else None,
+                                     s2.ctypes.data if s.count else None, csum_type,
+                                     seed & 0xFFFFFFFF))
+
+    def load_sums_device(self, count: int, blength: int, s2length: int, remainder: int,
+                         dev_sum1: int, dev_sum2: int, csum_type: int, seed: int) -> None:
+        check(lib.vs_rsync_load_sums_device(self._h, count, blength, s2length, remainder,
+                                            ctypes.c_void_p(dev_sum1 or None),
+                                            ctypes.c_void_p(dev_sum2 or None), csum_type,
+                                            seed & 0xFFFFFFFF))
+
+    def match_device(self, dev_src: int, length: int) -> int:
+        n = ctypes.c_int64(0)
+        check(lib.vs_rsync_match_device(self._h, ctypes.c_void_p(dev_src or None), length,
+                                        ctypes.byref(n)))
+        self._last_n = n.value
+        return n.value
+
+    def matches(self, first: int = 0, n: Optional[int] = None) -> List[Tuple[int, int]]:
+        if n is None:
+            n = self.stats()["matches"] - first
+        arr = (VsMatch * max(n, 1))()
+        check(lib.vs_rsync_get_matches(self._h, first, n, arr))
+        return [(arr[i].offset, arr[i].block_index) for i in range(n)]
+
+    def stats(self) -> dict:
+        c, fa, sh = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        r = ctypes.c_int32()
+        check(lib.vs_rsync_stats(self._h, ctypes.byref(c), ctypes.byref(fa), ctypes.byref(sh),
+                                 ctypes.byref(r)))
+        return {"candidates": c.value, "false_alarms": fa.value, "strong_hashed": sh.value,
+                "rounds": r.value, "matches": self._last_n}
+
+    def timing(self) -> dict:
+        ms = (ctypes.c_double * 5)()
+        check(lib.vs_rsync_timing(self._h, ms))
+        return dict(zip(["signatures", "table", "scan", "verify", "walk"], list(ms)))
+
+    def match_sums(self, dev_src: int, length: int) -> List[Tuple[int, int]]:
+        return self.matches(0, self.match_device(dev_src, length))
+
+    _last_n = 0
+
+
+def match_sums(src, s: SumStruct, csum_type: int = CSUM_XXH3_128, seed: int = 0,
+               device: int = 0) -> List[Tuple[int, int]]:
+    """One-shot host form: the greedy match list of `src` against `s`."""
+    b = _host_bytes(src)
+    s1 = np.ascontiguousarray(s.sum1, np.uint32)
+    s2 = np.ascontiguousarray(s.sum2, np.uint8)
+    t = VsSigTable(s.count, s.blength, s.s2length, s.remainder,
+                   s1.ctypes.data if s.count else None, s2.ctypes.data if s.count else None)
+    cap = len(b) // max(1, min(s.blength, s.remainder or s.blength)) + 8
+    out = (VsMatch * cap)()
+    n = ctypes.c_size_t(0)
+    check(lib.vs_rsync_match(device, b.ctypes.data if len(b) else None, len(b), ctypes.byref(t),
+                             csum_type, seed & 0xFFFFFFFF, out, cap, ctypes.byref(n)))
+    return [(out[i].offset, out[i].block_index) for i in range(n.value)]
