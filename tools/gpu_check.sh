@@ -16,8 +16,8 @@ step() {  # step <name> <timeout> <cmd...>
 for s in "$@"; do
   case $s in
     smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step gputests 1500 python -m pytest tests -q -m gpu -x ;;
-    testsk) step gputests 1500 python -m pytest tests -q -m gpu ;;
+    tests) step gputests 1500 python -u -m pytest tests -v -m gpu -x --timeout 120 --timeout-method thread ;;
+    testsk) step gputests 1500 python -u -m pytest tests -v -m gpu --timeout 120 --timeout-method thread ;;
     bench_small) step bench_small 600 python bench.py --steps 2 --warmup 1 --per-gpu-gib 8 --no-cpu-baseline ;;
     bench) step bench 900 python bench.py ;;
   esac
