@@ -8,8 +8,11 @@ python bench.py --gpus N --steps K --warmup W
        scaling, per-GPU work fixed); the only exchange is an RCCL all-gather of
        one u64 per rank per stitch round (volsync_amd/shard.py).
 A step = one full pass of the hot path over the volume: fingerprint, cut
-selection, Cut values, SHA-256 of every chunk.  Inputs are generated in HBM
-before the timed region.  Prints one JSON line (rank 0).
+selection, Cut values, SHA-256 of every chunk.  Steps are pipelined: the
+time-sliced SHA-256 engine keeps hashing step k's chunks while step k+1 is
+chunked, and the timed region ends only after the engine has drained, so every
+blob ID of all K volumes is final inside it.  Inputs are
+generated in HBM before the timed region.  Prints one JSON line (rank 0).
 """
 from __future__ import annotations
 
@@ -66,14 +69,14 @@ def _cpu_model() -> str:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--per-gpu-gib", type=float, default=64.0)
     ap.add_argument("--cpu-sample-gib", type=int, default=4)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="volumes in flight: handles on separate HIP streams, steps round-robin")
+    ap.add_argument("--hash-slice", type=int, default=8192,
+                    help="SHA-256 blocks per chunk per step (time-sliced engine; 0 = unbounded)")
     args = ap.parse_args()
 
     import torch
@@ -98,64 +101,47 @@ def main():
     synth_fill_device(buf.data_ptr(), 2, spec.data_lo, dlen, device=local, stream=stream)
     torch.cuda.synchronize(dev)
 
-    P = max(1, args.inflight)
-    streams = [torch.cuda.Stream(dev) for _ in range(P)]
-    handles = []
-    for st in streams:
-        h = DeviceChunker(TestPol, MinSize, MaxSize, 20, device=local)
-        h.set_stream(st.cuda_stream)
-        handles.append(h)
+    dc = DeviceChunker(TestPol, MinSize, MaxSize, 20, device=local)
+    dc.set_hash_slice(args.hash_slice)
     coll = torch_collectives(dev) if world > 1 else None
-    counter = [0]
 
     def step():
-        # volume i runs on handle i % P; finish() leaves SHA-256 queued on that
-        # handle's stream, so up to P volumes overlap
-        dc = handles[counter[0] % P]
-        counter[0] += 1
+        # one volume pass: fingerprint + cut selection + Cut values on the main
+        # stream; its chunks join the time-sliced SHA-256 engine on the hash
+        # stream, which keeps hashing them while the next volume is chunked
+        # (DESIGN.md 3.4).  wait() hashes everything still queued.
         if world == 1:
             n, _ = dc.process(buf.data_ptr(), dlen, 0, True)
         else:
             n = run_shard(dc, spec, buf.data_ptr(), *coll)
         return n
 
-    def drain():
-        for h in handles:
-            h.wait()
-        torch.cuda.synchronize(dev)
-
     for _ in range(args.warmup):
         step()
-    drain()
+    dc.wait()
+    torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    for h in handles:
-        h.timing(True)
+    torch.cuda.synchronize(dev)
+    dc.timing(True)
     t0 = time.perf_counter()
     nch = 0
     for _ in range(args.steps):
         nch = step()
-    drain()
+    dc.wait()
+    torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    ms = [0.0] * 4
-    launches = [0] * 4
-    for h in handles:
-        m, c = h.timing(False)
-        ms = [a + b for a, b in zip(ms, m)]
-        launches = [a + b for a, b in zip(launches, c)]
-    # one volume alone (no overlap): single-volume latency and isolated kernel times
-    h0 = handles[0]
-    h0.timing(True)
+    ms, launches = dc.timing(False)
+    # one volume alone: single-volume latency and isolated stage times
+    dc.timing(True)
     t1 = time.perf_counter()
-    if world == 1:
-        h0.process(buf.data_ptr(), dlen, 0, True)
-    else:
-        run_shard(h0, spec, buf.data_ptr(), *coll)
-    h0.wait()
+    step()
+    dc.wait()
     lat = time.perf_counter() - t1
-    iso_ms, iso_launch = h0.timing(False)
+    iso_ms, iso_launch = dc.timing(False)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -172,8 +158,10 @@ def main():
     # volume bytes -- the fingerprint pass reads each scanned byte once (plus a
     # 64-byte warm-up per 12 KiB strip, not counted), SHA-256 reads each chunk
     # byte once; one fingerprint stage and one SHA-256 launch per volume.
+    # fingerprint: one launch per volume; SHA-256: slices (one per step plus the
+    # final drain) -- bytes hashed in the timed region / summed slice time
     fp_ms = ms[0] / args.steps
-    sha_ms = ms[2] / max(1, launches[2]) if launches[2] else 0.0
+    sha_ms = ms[2] / args.steps
     fp_gbs = own_bytes / fp_ms / 1e6 if fp_ms else 0.0
     sha_gbs = own_bytes / sha_ms / 1e6 if sha_ms else 0.0
     iso = {s: round(iso_ms[i], 3) for i, s in enumerate(stages)}
@@ -213,7 +201,8 @@ def main():
             "roofline": roofline,
             "stages_ms_per_step": {k: round(v, 3) for k, v in per_step.items()},
             "kernels": roof,
-            "inflight": P,
+            "hash_slice_blocks": args.hash_slice,
+            "sha_slices": launches[2],
             "single_volume": {"ms": round(lat * 1e3, 2),
                               "GBps": round(total / lat / 1e9, 2),
                               "stages_ms": iso},
@@ -221,8 +210,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_gib << 30, args.cpu_threads)
         print(json.dumps(out), flush=True)
-    for h in handles:
-        h.close()
+    dc.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -106,24 +106,37 @@ int vs_cdc_set_batch_bytes(vs_cdc *h, uint64_t bytes);
  * already queued on the null stream; with vs_cdc_set_stream the caller's
  * stream must already order the producer of dev_data before the scan. */
 int vs_cdc_set_stream(vs_cdc *h, void *hip_stream); /* NULL = handle's own stream */
-/* Stream for the SHA-256 stage.  NULL (default) = the main stream.  The
- * streaming vs_cdc_feed path creates a private one on first use. */
+/* Stream of the SHA-256 stage.  NULL (default) = the handle's own hash
+ * stream, so batch k+1's fingerprint pass runs beside batch k's hashing. */
 int vs_cdc_set_hash_stream(vs_cdc *h, void *hip_stream);
+/* Time slicing of the SHA-256 engine: each vs_cdc_finish
+ * advances every queued chunk by at most `blocks` 64-byte blocks and carries
+ * the midstate of unfinished chunks to the next batch's launch; vs_cdc_wait
+ * hashes the rest.  0 = unbounded (every batch hashed to the end in one
+ * launch).  Default 8192 (512 KiB per chunk per batch). */
+int vs_cdc_set_hash_slice(vs_cdc *h, uint32_t blocks);
+/* Pipelined batches: batch numbers count vs_cdc_finish calls from 0; the ring
+ * keeps the last *ring batches' chunk lists.  Data passed to vs_cdc_scan must
+ * stay valid until its batch's blob IDs are final (vs_cdc_wait). */
+int vs_cdc_batches(vs_cdc *h, uint64_t *finished, uint64_t *ring);
+int vs_cdc_get_batch_chunks(vs_cdc *h, uint64_t batch, uint64_t first, uint64_t n,
+                            vs_chunk *out);
 int vs_cdc_scan(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t origin,
                 uint64_t own_lo, uint64_t own_hi, int final);
 /* Selects cuts given the true start of the first chunk (entry).  *exit_pos =
  * start of the first chunk at or beyond own_hi (or the stream end);
  * *complete = 0 when a chunk's cut depends on bytes not yet supplied. */
 int vs_cdc_stitch(vs_cdc *h, uint64_t entry, uint64_t *exit_pos, int *complete);
-/* Emits the chunk list (the count is known on return) and queues the Cut
- * values and SHA-256 blob IDs on the handle's stream without waiting. */
+/* Emits the chunk list (the count is known on return), queues the Cut values
+ * and hands the chunks to the SHA-256 engine without waiting for their IDs. */
 int vs_cdc_finish(vs_cdc *h, uint64_t *n_chunks);
-/* Waits until the handle's queued work (blob IDs) is complete. */
+/* Hashes every queued chunk to the end and waits until all blob IDs of all
+ * finished batches are final. */
 int vs_cdc_wait(vs_cdc *h);
 /* scan + stitch(own_lo) + finish for a single device (own range = whole buffer). */
 int vs_cdc_process(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t origin, int final,
                    uint64_t *n_chunks, uint64_t *consumed);
-/* Copy chunks [first, first+n) of the last finish() to host. */
+/* Copy chunks [first, first+n) of the last finish() to host (waits). */
 int vs_cdc_get_chunks(vs_cdc *h, uint64_t first, uint64_t n, vs_chunk *out);
 /* Accumulated device time (ms) per pipeline stage since the last reset of the
  * timers, measured with HIP events on the handle's stream when enabled.

@@ -241,3 +241,46 @@ def test_full_size_c2_properties(gpu):
         assert (c.Start + ref[0], ref[1], ref[2], ref[3]) == (c.Start, c.Length, c.Cut, c.ID.hex())
     del t
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("budget", [1, 2, 3, 7, 100, 0])
+def test_hash_slice_budgets(gpu, budget):
+    """Time-sliced SHA-256 engine: chains carry their midstate across slices
+    of `budget` blocks (1 block per batch = the most slices); the blob IDs
+    must not depend on the slicing."""
+    from volsync_amd import DeviceChunker
+    mn, mx, ab = 4096, 65536, 13
+    dc = DeviceChunker(P.TEST_POL, mn, mx, ab)
+    dc.set_hash_slice(budget)
+    for seed, n in [(80, (3 << 20) + 5), (81, 70000), (82, 1 << 20)]:
+        data = O.synth(seed, 0, n)
+        assert dev_chunks(data, P.TEST_POL, mn, mx, ab, dc=dc) == O.cdc_hash(data, P.TEST_POL, mn, mx, ab)
+    dc.close()
+
+
+@pytest.mark.parametrize("budget", [5, 8192])
+def test_pipelined_batches(gpu, budget):
+    """Batches finished back to back on one handle without waiting (the bench
+    pattern): each batch's chunk list and blob IDs equal the oracle's, read
+    back after the engine drained."""
+    from volsync_amd import DeviceChunker
+    mn, mx, ab = 16384, 1 << 18, 15
+    dc = DeviceChunker(P.TEST_POL, mn, mx, ab)
+    dc.set_hash_slice(budget)
+    datas, bufs, counts = [], [], []
+    first, ring = dc.batches()
+    for i in range(6):
+        data = O.synth(90 + i, 0, (4 << 20) + 977 * i)
+        t = to_dev(data)
+        n, consumed = dc.process(t.data_ptr(), len(data), 0, True)
+        assert consumed == len(data)
+        datas.append(data)
+        bufs.append(t)      # device data must outlive its batch's hashing
+        counts.append(n)
+    done, ring = dc.batches()
+    assert done == first + 6
+    for i in range(max(0, 6 - ring), 6):
+        got = [(c.Start, c.Length, c.Cut, c.ID.hex())
+               for c in dc.batch_chunks(first + i, 0, counts[i])]
+        assert got == O.cdc_hash(datas[i], P.TEST_POL, mn, mx, ab)
+    dc.close()

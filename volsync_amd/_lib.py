@@ -90,6 +90,9 @@ def _load() -> ctypes.CDLL:
         "vs_cdc_set_batch_bytes": (c_int, [vp, c_u64]),
         "vs_cdc_set_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_stream": (c_int, [vp, vp]),
+        "vs_cdc_set_hash_slice": (c_int, [vp, c_u32]),
+        "vs_cdc_batches": (c_int, [vp, u64p, u64p]),
+        "vs_cdc_get_batch_chunks": (c_int, [vp, c_u64, c_u64, c_u64, ctypes.POINTER(VsChunk)]),
         "vs_cdc_scan": (c_int, [vp, vp, c_u64, c_u64, c_u64, c_u64, c_int]),
         "vs_cdc_stitch": (c_int, [vp, c_u64, u64p, ctypes.POINTER(c_int)]),
         "vs_cdc_finish": (c_int, [vp, u64p]),

@@ -199,8 +199,27 @@ class DeviceChunker:
         check(lib.vs_cdc_set_stream(self._h, ctypes.c_void_p(hip_stream or None)))
 
     def set_hash_stream(self, hip_stream: int) -> None:
-        """Run the SHA-256 stage on another stream (0 = the main stream)."""
+        """Run the SHA-256 stage on another stream (0 = the handle's own)."""
         check(lib.vs_cdc_set_hash_stream(self._h, ctypes.c_void_p(hip_stream or None)))
+
+    def set_hash_slice(self, blocks: int) -> None:
+        """Blocks per chunk per batch of the time-sliced SHA-256 engine (0 = unbounded)."""
+        check(lib.vs_cdc_set_hash_slice(self._h, int(blocks)))
+
+    def batches(self):
+        """(batches finished so far, batches the ring keeps)."""
+        f = ctypes.c_uint64(0)
+        r = ctypes.c_uint64(0)
+        check(lib.vs_cdc_batches(self._h, ctypes.byref(f), ctypes.byref(r)))
+        return int(f.value), int(r.value)
+
+    def batch_chunks(self, batch: int, first: int, n: int) -> List[Chunk]:
+        """Chunks of an earlier batch (pipelined use; waits for its blob IDs)."""
+        if n <= 0:
+            return []
+        arr = (VsChunk * n)()
+        check(lib.vs_cdc_get_batch_chunks(self._h, batch, first, n, arr))
+        return [_chunk_from(c) for c in arr]
 
     def process(self, dev_ptr: int, length: int, origin: int = 0, final: bool = True):
         n = ctypes.c_uint64(0)

@@ -59,21 +59,33 @@ struct vs_cdc {
         seg_off;
     uint64_t *exit_old = nullptr, *exit_new = nullptr;
     uint64_t entry = 0;  // data offset
-    // chunks
-    DevBuf ch_start, ch_end, ch_cut, ch_id, order, hist, n_out, sha_ctr;
-    // SHA-256 stream: the main stream unless one is set (vs_cdc_set_hash_stream)
-    // or the streaming feed path creates its own, so the next batch's
-    // fingerprint pass can overlap this batch's hashing tail; events order the
-    // shared chunk arrays.  Callers that pipeline several handles keep one
-    // stream per handle: with GPU_MAX_HW_QUEUES=4, extra streams share
-    // hardware queues with other handles' main streams and serialise them.
+    // chunk batches: a ring of per-batch chunk arrays.  The
+    // hash engine keeps hashing batch q's chunks (IDs into its slot) while
+    // batches q+1, q+2, ... are chunked; a slot is reused only once every
+    // chain of its previous batch is complete.
+    struct Slot {
+        DevBuf start, end, cut, id;
+        uint64_t n = 0, origin = 0;
+        uint64_t seq = ~0ull;     // batch number held, ~0 = never used
+        uint64_t done_slice = 0;  // slice index after which its blob IDs are final
+    };
+    std::vector<Slot> slots;
+    uint64_t seq = 0;             // batches finished so far
+    int last = -1;                // slot of the last finished batch
+    uint64_t n_chunks = 0;
+    DevBuf n_out;
+    // SHA-256: time-sliced engine on its own stream (hstream)
+    ShaEngine sha;
+    uint32_t hash_budget = 8192;  // blocks per chain per slice (0xffffffff: unbounded)
+    uint32_t chain_slices = 1;    // slices that finish any chain: ceil(max blocks / budget)
+    uint64_t slices = 0;          // slices launched
+    static constexpr int kSliceEv = 32;
+    hipEvent_t slice_ev[kSliceEv] = {};  // event after slice i at [i % kSliceEv]
     hipStream_t hstream = nullptr;
     hipStream_t own_h = nullptr;
-    hipEvent_t ev_ready = nullptr;   // main stream: chunk list + order written
-    hipEvent_t ev_hashed = nullptr;  // hash stream: blob IDs written
+    hipEvent_t ev_ready = nullptr;   // main stream: a batch's chunk list written
     hipEvent_t ev_null = nullptr;    // orders a scan after prior null-stream work
     bool hash_pending = false;
-    uint64_t n_chunks = 0;
     int state = 0;  // 0 idle, 1 scanned, 2 stitched, 3 finished
     // host staging
     uint64_t *pinned = nullptr;  // 8 u64 of pinned host memory
@@ -158,10 +170,68 @@ static void drain_timers(vs_cdc *h) {
 static int sync_stream(vs_cdc *h, bool all = false) {
     VS_HIP(hipStreamSynchronize(h->stream));
     if (all && h->hash_pending) {
-        if (h->hstream) VS_HIP(hipStreamSynchronize(h->hstream));
+        VS_HIP(hipStreamSynchronize(h->hstream));
         h->hash_pending = false;
     }
     if (all || !h->hash_pending) drain_timers(h);
+    return 0;
+}
+
+// one slice of the hash engine on the hash stream, followed by its event.
+// Flow control: before slice i reuses event slot i % kSliceEv the host waits
+// for slice i - kSliceEv, so "c + kSliceEv <= slices" implies slice c is done.
+static int run_slice(vs_cdc *h, uint32_t budget) {
+    if (h->sha.idle()) return 0;
+    const uint64_t i = h->slices + 1;
+    hipEvent_t &e = h->slice_ev[i % vs_cdc::kSliceEv];
+    if (!e) {
+        VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    } else if (i > (uint64_t)vs_cdc::kSliceEv) {
+        VS_HIP(hipEventSynchronize(e));
+    }
+    {
+        StageTimer t(h, kStSha, h->hstream);
+        VS_TRY(h->sha.slice(budget, h->hstream));
+    }
+    VS_HIP(hipEventRecord(e, h->hstream));
+    h->slices = i;
+    if (budget == 0xffffffffu)
+        for (auto &s : h->slots)
+            if (s.seq != ~0ull && s.done_slice > i) s.done_slice = i;
+    return 0;
+}
+
+// hash every queued chain to the end (one unbounded slice)
+static int drain_hash(vs_cdc *h) { return run_slice(h, 0xffffffffu); }
+
+// make the main stream wait until slot k's previous batch is fully hashed
+static int slot_free(vs_cdc *h, size_t k) {
+    vs_cdc::Slot &s = h->slots[k];
+    if (s.seq == ~0ull) return 0;
+    if (s.done_slice > h->slices) VS_TRY(drain_hash(h));  // ring shorter than a chain's slices
+    const uint64_t c = s.done_slice;
+    if (c == 0 || c + vs_cdc::kSliceEv <= h->slices) return 0;
+    VS_HIP(hipStreamWaitEvent(h->stream, h->slice_ev[c % vs_cdc::kSliceEv], 0));
+    return 0;
+}
+
+// (re)size the batch ring for the current parameters and slice budget
+static int size_ring(vs_cdc *h) {
+    const uint64_t mb = sha_blocks(h->max_size);
+    const uint64_t L = (h->hash_budget == 0xffffffffu) ? 1 : (mb + h->hash_budget - 1) / h->hash_budget;
+    h->chain_slices = (uint32_t)std::min<uint64_t>(L, 1u << 30);
+    const size_t want = (size_t)std::min<uint64_t>(L + 2, 24);
+    if (h->slots.size() != want) {
+        VS_TRY(sync_stream(h, true));
+        for (auto &s : h->slots) {
+            s.start.release();
+            s.end.release();
+            s.cut.release();
+            s.id.release();
+        }
+        h->slots.assign(want, vs_cdc::Slot());
+        h->last = -1;
+    }
     return 0;
 }
 
@@ -406,63 +476,58 @@ static int cdc_finish(vs_cdc *h, uint64_t *n_chunks) {
     if (!h || h->state < 2) return fail(VS_ERR_STATE, "vs_cdc_finish before vs_cdc_stitch");
     VS_TRY(set_dev(h));
     VS_TRY(h->n_out.ensure(16));
-    // the previous batch's SHA-256 reads the chunk arrays emit rewrites
-    if (h->hash_pending) VS_HIP(hipStreamWaitEvent(h->stream, h->ev_hashed, 0));
+    VS_TRY(size_ring(h));
+    const size_t k = (size_t)(h->seq % h->slots.size());
+    vs_cdc::Slot &sl = h->slots[k];
+    // the slot's previous batch must be fully hashed before emit rewrites it
+    VS_TRY(slot_free(h, k));
     SelArgs s = sel_args(h);
     // upper bound of chunks: every segment's capacity
     const uint64_t cap = std::max<uint64_t>((uint64_t)h->nseg * h->maxc, 1);
-    VS_TRY(h->ch_start.ensure(cap * 8));
-    VS_TRY(h->ch_end.ensure(cap * 8));
+    if (sl.start.cap < cap * 8 || sl.end.cap < cap * 8) {
+        VS_TRY(sync_stream(h, true));  // growing arrays the hash stream may read
+        VS_TRY(sl.start.ensure(cap * 8));
+        VS_TRY(sl.end.ensure(cap * 8));
+    }
     {
         StageTimer t(h, kStSel);
-        VS_HIP(launch_emit(s, h->seg_off.as<uint32_t>(), h->ch_start.as<uint64_t>(),
-                           h->ch_end.as<uint64_t>(), h->n_out.as<uint64_t>(), h->stream));
+        VS_HIP(launch_emit(s, h->seg_off.as<uint32_t>(), sl.start.as<uint64_t>(),
+                           sl.end.as<uint64_t>(), h->n_out.as<uint64_t>(), h->stream));
     }
     VS_HIP(hipMemcpyAsync(h->pinned, h->n_out.p, 8, hipMemcpyDeviceToHost, h->stream));
     VS_TRY(sync_stream(h));
     const uint64_t n = h->pinned[0];
-    h->n_chunks = n;
-    if (h->hash_pending && (h->ch_cut.cap < n * 8 || h->ch_id.cap < n * 32 || h->order.cap < n * 4)) {
-        VS_TRY(sync_stream(h, true));  // about to reallocate arrays the hash stream reads
+    if (sl.cut.cap < n * 8 || sl.id.cap < n * 32) {
+        VS_TRY(sync_stream(h, true));
+        VS_TRY(sl.cut.ensure(std::max<uint64_t>(n, 1) * 8));
+        VS_TRY(sl.id.ensure(std::max<uint64_t>(n, 1) * 32));
     }
-    VS_TRY(h->ch_cut.ensure(std::max<uint64_t>(n, 1) * 8));
-    VS_TRY(h->ch_id.ensure(std::max<uint64_t>(n, 1) * 32));
-    VS_TRY(h->order.ensure(std::max<uint64_t>(n, 1) * 4));
-    VS_TRY(h->hist.ensure((2 * 4096 + 16) * 4));
-    VS_TRY(h->sha_ctr.ensure(16));
     if (n) {
         {
             StageTimer t(h, kStOther);
-            VS_HIP(launch_cut_fp(h->data, n, h->ch_start.as<uint64_t>(), h->ch_end.as<uint64_t>(),
+            VS_HIP(launch_cut_fp(h->data, n, sl.start.as<uint64_t>(), sl.end.as<uint64_t>(),
                                  h->min_size, h->tabs.as<uint64_t>(), h->tabs.as<uint64_t>() + 256,
-                                 h->idx_shift, h->ch_cut.as<uint64_t>(), h->stream));
-            VS_HIP(launch_length_order(n, h->ch_start.as<uint64_t>(), h->ch_end.as<uint64_t>(),
-                                       nullptr, h->hist.as<uint32_t>(), h->order.as<uint32_t>(),
-                                       h->stream));
+                                 h->idx_shift, sl.cut.as<uint64_t>(), h->stream));
         }
-        hipStream_t hs = h->hstream ? h->hstream : h->stream;
-        if (hs != h->stream) {
-            VS_HIP(hipEventRecord(h->ev_ready, h->stream));
-            VS_HIP(hipStreamWaitEvent(hs, h->ev_ready, 0));
-        }
-        {
-            StageTimer t(h, kStSha, hs);
-            ShaArgs a{};
-            a.data = h->data;
-            a.n = n;
-            a.starts = h->ch_start.as<uint64_t>();
-            a.ends = h->ch_end.as<uint64_t>();
-            a.order = h->order.as<uint32_t>();
-            a.ids = h->ch_id.as<uint8_t>();
-            a.counter = h->sha_ctr.as<uint32_t>();
-            VS_HIP(launch_sha256(a, hs));
-        }
-        VS_HIP(hipEventRecord(h->ev_hashed, hs));
+        // the hash stream picks the chunk list up once emit has written it
+        VS_HIP(hipEventRecord(h->ev_ready, h->stream));
+        VS_HIP(hipStreamWaitEvent(h->hstream, h->ev_ready, 0));
+        VS_TRY(h->sha.append_chunks(h->data, sl.start.as<uint64_t>(), sl.end.as<uint64_t>(), n,
+                                    sl.id.as<uint8_t>(), (uint32_t)sha_blocks(h->max_size),
+                                    h->hstream));
+        VS_TRY(run_slice(h, h->hash_budget));
         h->hash_pending = true;
     }
-    // Cut values and blob IDs stay queued on the handle's stream: results are
-    // waited for by vs_cdc_wait / vs_cdc_get_chunks, so another handle's batch
-    // can run beside this one's SHA-256 tail.
+    sl.n = n;
+    sl.origin = h->origin;
+    sl.seq = h->seq;
+    sl.done_slice = n ? h->slices + h->chain_slices - 1 : 0;
+    h->last = (int)k;
+    h->n_chunks = n;
+    h->seq++;
+    // Cut values and blob IDs stay queued: results are waited for by
+    // vs_cdc_wait / vs_cdc_get_chunks, so the next batch's fingerprint pass
+    // runs beside this batch's hashing.
     if (n_chunks) *n_chunks = n;
     h->state = 3;
     return 0;
@@ -471,27 +536,38 @@ static int cdc_finish(vs_cdc *h, uint64_t *n_chunks) {
 static int cdc_wait(vs_cdc *h) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
     VS_TRY(set_dev(h));
+    VS_TRY(drain_hash(h));
     return sync_stream(h, true);
 }
 
-static int cdc_get_chunks(vs_cdc *h, uint64_t first, uint64_t n, vs_chunk *out) {
-    if (!h || h->state < 3) return fail(VS_ERR_STATE, "no finished batch");
-    if (first + n > h->n_chunks) return fail(VS_ERR_ARG, "chunk range out of bounds");
+// chunks [first, first+n) of batch `seq` (while its ring slot still holds it)
+static int cdc_get_batch(vs_cdc *h, uint64_t seq, uint64_t first, uint64_t n, vs_chunk *out) {
+    if (!h || h->slots.empty() || seq >= h->seq) return fail(VS_ERR_STATE, "no such finished batch");
+    const vs_cdc::Slot &sl = h->slots[seq % h->slots.size()];
+    if (sl.seq != seq) return fail(VS_ERR_STATE, "batch already recycled (ring holds the last " +
+                                                     std::to_string(h->slots.size()) + ")");
+    if (first + n > sl.n) return fail(VS_ERR_ARG, "chunk range out of bounds");
     if (!n) return 0;
     VS_TRY(cdc_wait(h));
     std::vector<uint64_t> st(n), en(n), cu(n);
     std::vector<uint8_t> id(n * 32);
-    VS_HIP(hipMemcpy(st.data(), h->ch_start.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost));
-    VS_HIP(hipMemcpy(en.data(), h->ch_end.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost));
-    VS_HIP(hipMemcpy(cu.data(), h->ch_cut.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost));
-    VS_HIP(hipMemcpy(id.data(), h->ch_id.as<uint8_t>() + first * 32, n * 32, hipMemcpyDeviceToHost));
+    VS_HIP(hipMemcpy(st.data(), sl.start.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost));
+    VS_HIP(hipMemcpy(en.data(), sl.end.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost));
+    VS_HIP(hipMemcpy(cu.data(), sl.cut.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost));
+    VS_HIP(hipMemcpy(id.data(), sl.id.as<uint8_t>() + first * 32, n * 32, hipMemcpyDeviceToHost));
     for (uint64_t i = 0; i < n; ++i) {
-        out[i].start = h->origin + st[i];
+        out[i].start = sl.origin + st[i];
         out[i].length = (en[i] & kPosMask) - st[i] + 1;
         out[i].cut = cu[i];
         memcpy(out[i].id, &id[i * 32], 32);
     }
     return 0;
+}
+
+static int cdc_get_chunks(vs_cdc *h, uint64_t first, uint64_t n, vs_chunk *out) {
+    if (!h || h->state < 3 || h->last < 0) return fail(VS_ERR_STATE, "no finished batch");
+    if (first + n > h->n_chunks) return fail(VS_ERR_ARG, "chunk range out of bounds");
+    return cdc_get_batch(h, h->seq - 1, first, n, out);
 }
 
 static int cdc_process(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t origin, int final,
@@ -508,7 +584,8 @@ static int cdc_process(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t o
             *consumed = ex - origin;
         } else if (n) {
             uint64_t e = 0;
-            VS_HIP(hipMemcpy(&e, h->ch_end.as<uint64_t>() + (n - 1), 8, hipMemcpyDeviceToHost));
+            VS_HIP(hipMemcpy(&e, h->slots[h->last].end.as<uint64_t>() + (n - 1), 8,
+                             hipMemcpyDeviceToHost));
             *consumed = (e & kPosMask) + 1;
         } else {
             *consumed = 0;
@@ -582,15 +659,22 @@ VS_API int vs_cdc_open(int device, uint64_t pol, uint32_t min_size, uint32_t max
         return VS_ERR_NO_DEVICE;
     }
     if (hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->own_h, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_ready, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_hashed, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_null, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void **)&h->pinned, 64, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
-        delete h;
+        vs_cdc_close(h);
         return fail(VS_ERR_HIP, "stream / pinned buffer creation failed");
     }
     h->stream = h->own;
+    h->hstream = h->own_h;
+    if (h->sha.init(device) < 0) {
+        std::string msg = g_err;
+        vs_cdc_close(h);
+        g_err = msg;
+        return VS_ERR_NOMEM;
+    }
     int r = set_params(h, pol, min_size, max_size, avg_bits);
     if (r < 0) {
         std::string msg = g_err;
@@ -626,13 +710,6 @@ VS_API int vs_cdc_feed(vs_cdc *h, const void *buf, size_t n, int final) {
     if (h->final_fed) return fail(VS_ERR_STATE, "stream already finalised (call vs_cdc_reset)");
     if (n && !buf) return fail(VS_ERR_ARG, "null buffer");
     VS_TRY(set_dev(h));
-    if (!h->hstream) {  // streaming: hash batch k while batch k+1 is fingerprinted
-        if (!h->own_h && hipStreamCreateWithFlags(&h->own_h, hipStreamNonBlocking) != hipSuccess) {
-            (void)hipGetLastError();
-            return fail(VS_ERR_HIP, "hash stream creation failed");
-        }
-        h->hstream = h->own_h;
-    }
     const uint8_t *src = (const uint8_t *)buf;
     size_t left = n;
     for (;;) {
@@ -688,21 +765,28 @@ VS_API void vs_cdc_close(vs_cdc *h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->hstream) (void)hipStreamSynchronize(h->hstream);
-    DevBuf *bufs[] = {&h->tabs,     &h->counts,  &h->offs,     &h->dslot,   &h->pool,
-                      &h->flags,    &h->cstart,  &h->partials, &h->compact, &h->spec_cut,
+    DevBuf *bufs[] = {&h->tabs,     &h->counts,    &h->offs,   &h->dslot,   &h->pool,
+                      &h->flags,    &h->cstart,    &h->partials, &h->compact, &h->spec_cut,
                       &h->spec_n,   &h->spec_exit, &h->st_cut, &h->st_n,    &h->st_merge,
-                      &h->st_total, &h->exit_a,  &h->exit_b,   &h->seg_off, &h->ch_start,
-                      &h->ch_end,   &h->ch_cut,  &h->ch_id,    &h->order,   &h->hist,
-                      &h->n_out,    &h->sha_ctr, &h->sbuf[0], &h->sbuf[1]};
+                      &h->st_total, &h->exit_a,    &h->exit_b, &h->seg_off, &h->n_out,
+                      &h->sbuf[0],  &h->sbuf[1]};
     for (DevBuf *b : bufs) b->release();
+    for (auto &s : h->slots) {
+        s.start.release();
+        s.end.release();
+        s.cut.release();
+        s.id.release();
+    }
+    h->sha.release();
     for (auto &p : h->pend) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
     }
     for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+    for (auto e : h->slice_ev)
+        if (e) (void)hipEventDestroy(e);
     if (h->pinned) (void)hipHostFree(h->pinned);
     if (h->ev_ready) (void)hipEventDestroy(h->ev_ready);
-    if (h->ev_hashed) (void)hipEventDestroy(h->ev_hashed);
     if (h->ev_null) (void)hipEventDestroy(h->ev_null);
     if (h->own_h) (void)hipStreamDestroy(h->own_h);
     if (h->own) (void)hipStreamDestroy(h->own);
@@ -717,9 +801,29 @@ VS_API int vs_cdc_set_stream(vs_cdc *h, void *hip_stream) {
 
 VS_API int vs_cdc_set_hash_stream(vs_cdc *h, void *hip_stream) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
+    VS_TRY(cdc_wait(h));  // the engine's queued work stays on the old stream
+    h->hstream = hip_stream ? (hipStream_t)hip_stream : h->own_h;
+    return 0;
+}
+
+VS_API int vs_cdc_set_hash_slice(vs_cdc *h, uint32_t blocks) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    VS_TRY(cdc_wait(h));
+    h->hash_budget = blocks ? blocks : 0xffffffffu;
+    return size_ring(h);
+}
+
+VS_API int vs_cdc_get_batch_chunks(vs_cdc *h, uint64_t batch, uint64_t first, uint64_t n,
+                                   vs_chunk *out) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
     VS_TRY(set_dev(h));
-    VS_TRY(sync_stream(h, true));
-    h->hstream = (hipStream_t)hip_stream;
+    return cdc_get_batch(h, batch, first, n, out);
+}
+
+VS_API int vs_cdc_batches(vs_cdc *h, uint64_t *finished, uint64_t *ring) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    if (finished) *finished = h->seq;
+    if (ring) *ring = h->slots.size();
     return 0;
 }
 
@@ -762,7 +866,9 @@ VS_API int vs_cdc_timing(vs_cdc *h, int enable, double ms_out[4], uint64_t launc
 
 struct vs_sha {
     int device = 0;
-    DevBuf order, hist, ctr;
+    ShaEngine eng;
+    hipEvent_t done = nullptr;  // after the last run, on its stream
+    bool ran = false;
 };
 
 VS_API int vs_sha256_open(int device, vs_sha **out) {
@@ -774,11 +880,25 @@ VS_API int vs_sha256_open(int device, vs_sha **out) {
     VS_HIP(hipSetDevice(device));
     vs_sha *h = new vs_sha();
     h->device = device;
-    if (h->hist.ensure((2 * 4096 + 16) * 4) < 0 || h->ctr.ensure(16) < 0) {
-        delete h;
+    if (h->eng.init(device) < 0 ||
+        hipEventCreateWithFlags(&h->done, hipEventDisableTiming) != hipSuccess) {
+        std::string msg = g_err;
+        vs_sha256_close(h);
+        g_err = msg;
         return VS_ERR_NOMEM;
     }
     *out = h;
+    return 0;
+}
+
+// blob IDs of n device blobs with the hash engine: append + one unbounded slice
+static int sha_run(vs_sha *h, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
+                   size_t n, uint8_t *out, hipStream_t s) {
+    if (h->ran) VS_HIP(hipStreamWaitEvent(s, h->done, 0));  // engine buffers of the last run
+    VS_TRY(h->eng.append_blobs(buf, off, len, n, out, s));
+    VS_TRY(h->eng.slice(0xffffffffu, s));
+    VS_HIP(hipEventRecord(h->done, s));
+    h->ran = true;
     return 0;
 }
 
@@ -790,29 +910,18 @@ VS_API int vs_sha256_run_device(vs_sha *h, const void *dev_buf, const uint64_t *
         return fail(VS_ERR_ARG, "null device pointer");
     if (!n) return 0;
     VS_HIP(hipSetDevice(h->device));
-    hipStream_t s = (hipStream_t)hip_stream;
-    VS_TRY(h->order.ensure(n * 4));
-    ShaArgs a{};
-    a.data = (const uint8_t *)dev_buf;
-    a.n = n;
-    a.starts = dev_off;
-    a.lens = dev_len;
-    a.ids = dev_out;
-    a.order = h->order.as<uint32_t>();
-    a.counter = h->ctr.as<uint32_t>();
-    VS_HIP(launch_length_order(n, dev_off, nullptr, dev_len, h->hist.as<uint32_t>(),
-                               h->order.as<uint32_t>(), s));
-    VS_HIP(launch_sha256(a, s));
-    return 0;
+    return sha_run(h, (const uint8_t *)dev_buf, dev_off, dev_len, n, dev_out,
+                   (hipStream_t)hip_stream);
 }
 
 VS_API void vs_sha256_close(vs_sha *h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
-    (void)hipDeviceSynchronize();
-    h->order.release();
-    h->hist.release();
-    h->ctr.release();
+    if (h->done) {
+        (void)hipEventSynchronize(h->done);
+        (void)hipEventDestroy(h->done);
+    }
+    h->eng.release();
     delete h;
 }
 
@@ -822,37 +931,27 @@ VS_API int vs_sha256_batch(int device, const void *buf, size_t buf_len, const ui
     if (n && (!buf || !off || !len || !out)) return fail(VS_ERR_ARG, "null pointer");
     for (size_t i = 0; i < n; ++i)
         if (off[i] + len[i] > buf_len) return fail(VS_ERR_ARG, "blob outside the buffer");
-    VS_HIP(hipSetDevice(device));
-    DevBuf d, o, l, r, ord, hist, ctr;
-    VS_TRY(d.ensure(std::max<size_t>(buf_len, 16)));
-    VS_TRY(o.ensure(std::max<size_t>(n, 1) * 8));
-    VS_TRY(l.ensure(std::max<size_t>(n, 1) * 4));
-    VS_TRY(r.ensure(std::max<size_t>(n, 1) * 32));
-    VS_TRY(ord.ensure(std::max<size_t>(n, 1) * 4));
-    VS_TRY(hist.ensure((2 * 4096 + 16) * 4));
-    VS_TRY(ctr.ensure(16));
+    if (!n) return 0;
+    vs_sha *h = nullptr;
+    VS_TRY(vs_sha256_open(device, &h));
+    DevBuf d, o, l, r;
     int rc = 0;
-    if (hipMemcpy(d.p, buf, buf_len, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(o.p, off, n * 8, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(l.p, len, n * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    if ((rc = d.ensure(std::max<size_t>(buf_len, 16))) < 0 || (rc = o.ensure(n * 8)) < 0 ||
+        (rc = l.ensure(n * 4)) < 0 || (rc = r.ensure(n * 32)) < 0) {
+    } else if (hipMemcpy(d.p, buf, buf_len, hipMemcpyHostToDevice) != hipSuccess ||
+               hipMemcpy(o.p, off, n * 8, hipMemcpyHostToDevice) != hipSuccess ||
+               hipMemcpy(l.p, len, n * 4, hipMemcpyHostToDevice) != hipSuccess) {
         rc = fail(VS_ERR_HIP, "host to device copy failed");
-    } else if (n) {
-        ShaArgs a{};
-        a.data = d.as<uint8_t>();
-        a.n = n;
-        a.starts = o.as<uint64_t>();
-        a.lens = l.as<uint32_t>();
-        a.order = ord.as<uint32_t>();
-        a.ids = r.as<uint8_t>();
-        a.counter = ctr.as<uint32_t>();
-        if (launch_length_order(n, a.starts, nullptr, a.lens, hist.as<uint32_t>(),
-                                ord.as<uint32_t>(), 0) != hipSuccess ||
-            launch_sha256(a, 0) != hipSuccess ||
-            hipMemcpy(out, r.p, n * 32, hipMemcpyDeviceToHost) != hipSuccess)
+    } else if ((rc = sha_run(h, d.as<uint8_t>(), o.as<uint64_t>(), l.as<uint32_t>(), n,
+                             r.as<uint8_t>(), nullptr)) == 0) {
+        if (hipMemcpy(out, r.p, n * 32, hipMemcpyDeviceToHost) != hipSuccess)
             rc = fail(VS_ERR_HIP, "SHA-256 batch failed");
     }
-    d.release(); o.release(); l.release(); r.release(); ord.release(); hist.release();
-    ctr.release();
+    vs_sha256_close(h);
+    d.release();
+    o.release();
+    l.release();
+    r.release();
     return rc;
 }
 

@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <algorithm>
 #include <string>
+#include <vector>
 
 #include "../../include/vsgpu.h"
 
@@ -138,25 +139,56 @@ hipError_t launch_cut_fp(const uint8_t *data, uint64_t n, const uint64_t *ch_sta
                          const uint64_t *out8_tab, uint32_t idx_shift, uint64_t *cut_out,
                          hipStream_t s);
 
-// ---- SHA-256 ---------------------------------------------------------------
-// Hash n blobs data[start[i] .. start[i]+len(i)) where len comes from either
-// (ends, inclusive end offsets) or (lens).  order: optional permutation
-// (longest first); ids: [n][32].
-struct ShaArgs {
-    const uint8_t *data;
-    uint64_t n;
-    const uint64_t *starts;
-    const uint64_t *ends;     // inclusive end offsets, or nullptr
-    const uint32_t *lens;     // lengths, or nullptr
-    const uint32_t *order;    // nullptr = identity
-    uint8_t *ids;
-    uint32_t *counter;        // work-queue head (device word; zeroed by launch_sha256)
+// ---- SHA-256 hash engine (sha256.hip) --------------------------
+// One active hash chain: a blob data[ptr0 .. end) of len bytes, advanced to
+// ptr (ptr - ptr0 is a multiple of 64; ptr > end while only the second
+// padding block is left), midstate st, digest destination out.  64 bytes.
+struct ShaChain {
+    uint64_t ptr, end, len;
+    uint8_t *out;
+    uint32_t st[8];
 };
-hipError_t launch_sha256(const ShaArgs &a, hipStream_t s);
-// Longest-first permutation of n blob lengths (bucketed by 64 KiB).
-hipError_t launch_length_order(uint64_t n, const uint64_t *starts, const uint64_t *ends,
-                               const uint32_t *lens, uint32_t *hist, uint32_t *order,
-                               hipStream_t s);
+static_assert(sizeof(ShaChain) == 64, "ShaChain is one 64-byte record");
+
+struct ShaSliceArgs {
+    const ShaChain *cur;
+    ShaChain *next;
+    const uint32_t *order;   // longest-first permutation of cur
+    const uint32_t *n_cur;   // device counts
+    uint32_t *n_next;
+    uint32_t *tile_ctr;
+    uint32_t budget;         // max blocks per chain in this slice (0xffffffff: all)
+};
+
+// Host side of the engine: a double-buffered active list on the device, fed by
+// append_*() and advanced by slice(); every call queues on the given stream
+// (always the same one) without synchronising.
+struct ShaEngine {
+    struct Group {
+        uint64_t n;
+        uint32_t max_blocks;  // upper bound on any chain's remaining blocks
+    };
+    int device = 0;
+    int cus = 256;
+    DevBuf list[2], order, hist, ctl;  // ctl: u32 counts [0], [1] (list parity), [2] tile counter
+    int cur = 0;
+    uint64_t cap = 0;  // chains per list
+    uint64_t ub = 0;   // upper bound on the active chains
+    std::vector<Group> groups;
+    int init(int dev);
+    void release();
+    uint32_t *count(int which);
+    int reserve(uint64_t n_new, hipStream_t s);
+    // chunks [starts[i], (ends[i] & kPosMask)] of data; digest i -> ids + 32 i
+    int append_chunks(const uint8_t *data, const uint64_t *starts, const uint64_t *ends, uint64_t n,
+                      uint8_t *ids, uint32_t max_blocks, hipStream_t s);
+    int append_blobs(const uint8_t *data, const uint64_t *off, const uint32_t *lens, uint64_t n,
+                     uint8_t *ids, hipStream_t s);
+    int slice(uint32_t budget, hipStream_t s);
+    bool idle() const { return ub == 0; }
+};
+// SHA-256 blocks of a blob of len bytes (data + padding)
+inline uint64_t sha_blocks(uint64_t len) { return (len >> 6) + ((len & 63) < 56 ? 1 : 2); }
 
 // ---- synthetic data --------------------------------------------------------
 hipError_t launch_synth(uint64_t seed, uint64_t off, uint64_t n, uint8_t *out, hipStream_t s);

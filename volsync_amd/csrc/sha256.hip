@@ -1,16 +1,32 @@
-// sha256.hip -- batched SHA-256 blob IDs on gfx950.
+// sha256.hip -- batched SHA-256 blob IDs on gfx950: the time-sliced
+// producer/consumer hash engine.
 //
 // restic's blob ID is sha256.Sum256 of the chunk plaintext
 // (restic v0.13.1 internal/restic/id.go Hash, Go crypto/sha256 after
 // /root/reference/mover-restic/patch-sources.sh:16-27), computed for every
 // chunk in Repository.SaveBlob.
 //
-// One lane per blob: the Merkle-Damgard chain of a blob is sequential, so
-// parallelism is across blobs.  Lanes are fed longest-first (64 KiB buckets)
-// so a wave's lanes finish together.  Integer-VALU bound:
-// per 64-byte block 64 rounds x 14 ops + 48 schedule words x 10 ops with
-// v_bitop3_b32 for Ch / Maj / the three-way XORs, v_alignbit_b32 for
-// rotates and v_perm_b32 for the big-endian, byte-misaligned message words.
+// A blob's Merkle-Damgard chain is sequential, so parallelism is across
+// blobs ("chains").  Two facts shape the kernel:
+//   * a wave alone on its SIMD issues one VALU instruction per 4 cycles, so a
+//     chain's latency is its per-lane instruction count: the longest chunk
+//     (MaxSize = 8 MiB = 131072 blocks) is the critical path of a volume;
+//   * chains of one volume (~44 K at 64 GiB) fill only a fraction of the
+//     256 CU x 4 SIMD x 2 waves x 64 lanes the chip can keep busy.
+// Hence:
+//   * producer/consumer split: per 64 chains a workgroup of two waves; the
+//     producer loads message blocks and expands the schedule W[0..63] + K into
+//     an LDS double buffer, the consumer runs only the 64 rounds (14 VALU per
+//     round + 16 ds_read_b128 per block instead of ~1460 VALU per block), so a
+//     chain advances ~1.6x faster than with one lane doing both;
+//   * time slicing: a launch advances every active chain by at most `budget`
+//     blocks and writes the midstate of unfinished chains to the next active
+//     list, so the chains of consecutive volumes share launches on one stream
+//     (no hardware-queue serialisation) and the chip stays full in steady
+//     state.
+// Chains are processed in tiles of 64 taken longest-first from a work queue;
+// v_bitop3_b32 does Ch / Maj / three-way XORs, v_alignbit_b32 the rotates and
+// v_perm_b32 the big-endian, byte-misaligned message words.
 #include <algorithm>
 
 #include "internal.hpp"
@@ -29,6 +45,9 @@ static constexpr uint32_t kK256[64] = {
     0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
     0xc67178f2};
 
+static constexpr uint32_t kIV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                    0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+
 __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
     return __builtin_amdgcn_alignbit(x, x, n);
 }
@@ -42,31 +61,113 @@ __device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
 }
 
-__device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
+// Blocks (data + padding) still to compress for a chain whose next unread
+// byte is ptr and whose data ends at end.  end - ptr < 0 only while the
+// second padding block (tail >= 56 bytes) is pending.
+__device__ __forceinline__ uint32_t blocks_left(uint64_t ptr, uint64_t end) {
+    const int64_t d = (int64_t)(end - ptr);
+    if (d < 0) return 1;
+    const uint64_t b = ((uint64_t)d >> 6) + (((uint64_t)d & 63) < 56 ? 1u : 2u);
+    return b > 0xffffffffull ? 0xffffffffu : (uint32_t)b;
+}
+
+// Raw little-endian words of the block at ptr: 16 words (+1 when ptr is not
+// 4-byte aligned) of a data block; only the words holding tail bytes of the
+// first padding block (never reading past the blob); none for the second.
+__device__ __forceinline__ void load_raw(uint32_t (&d)[17], uint64_t ptr, uint64_t end) {
+    const uint32_t r = (uint32_t)(ptr & 3);
+    const uint32_t *wp = (const uint32_t *)(uintptr_t)(ptr - r);
+    const int64_t left = (int64_t)(end - ptr);
+    if (left >= 64) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d[k] = wp[k];
+        d[16] = r ? wp[16] : 0u;
+    } else if (left > 0) {
+        const uint32_t lim = r + (uint32_t)left;  // bytes of wp[] that belong to the blob
+#pragma unroll
+        for (int k = 0; k < 17; ++k) d[k] = (4u * k < lim) ? wp[k] : 0u;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 17; ++k) d[k] = 0u;
+    }
+}
+
+// Big-endian message words W[0..15] of the block at ptr from its raw words.
+__device__ __forceinline__ void message(uint32_t (&w)[16], const uint32_t (&d)[17], uint64_t ptr,
+                                        uint64_t end, uint64_t len) {
+    const uint32_t r = (uint32_t)(ptr & 3);
+    const uint32_t sel = (r << 24) | ((r + 1) << 16) | ((r + 2) << 8) | (r + 3);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_perm(d[k + 1], d[k], sel);
+    const int64_t left = (int64_t)(end - ptr);
+    if (left < 64) {
+        // padding: [tail bytes, 0x80, zeros] (+ big-endian bit length)
+        const int tl = left > 0 ? (int)left : 0;
+        const bool mark = left >= 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int v = min(max(tl - 4 * k, 0), 4);  // tail bytes in word k
+            const uint32_t keep = (v == 4) ? 0xffffffffu : ~(0xffffffffu >> (8 * v));
+            const uint32_t m80 = (mark && v < 4 && tl >= 4 * k) ? (0x80u << (24 - 8 * v)) : 0u;
+            w[k] = (w[k] & keep) | m80;
+        }
+        if (left < 56) {
+            const uint64_t bits = len << 3;
+            w[14] = (uint32_t)(bits >> 32);
+            w[15] = (uint32_t)bits;
+        }
+    }
+}
+
+// Producer: W[t] + K[t] for t = 0..63 into the LDS slot (word group q of
+// lane l at uint4 index q*64 + l: conflict-free ds_write_b128 / ds_read_b128).
+__device__ __forceinline__ void schedule_to_lds(uint32_t (&w)[16], uint4 *slot, uint32_t lane) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int t = 4 * q + i;
+            uint32_t wt;
+            if (t < 16) {
+                wt = w[t];
+            } else {
+                const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+                const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+                const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+                wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+            }
+            o[i] = wt + kK256[t];
+        }
+        slot[q * 64 + lane] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+#define VS_SHA_ROUND(a, b, c, d, e, f, g, h, wk)                                   \
+    {                                                                              \
+        const uint32_t t1_ = h + xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)) +       \
+                             ch(e, f, g) + (wk);                                   \
+        const uint32_t t2_ = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)) + maj(a, b, c); \
+        d += t1_;                                                                  \
+        h = t1_ + t2_;                                                             \
+    }
+
+// Consumer: the 64 rounds of one block from the LDS slot.
+__device__ __forceinline__ void compress_lds(uint32_t (&st)[8], const uint4 *slot, uint32_t lane) {
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
     uint32_t e = st[4], f = st[5], g = st[6], h = st[7];
 #pragma unroll
-    for (int t = 0; t < 64; ++t) {
-        uint32_t wt;
-        if (t < 16) {
-            wt = w[t];
-        } else {
-            const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-            const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
-            const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
-            wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
-        }
-        const uint32_t t1 = h + xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)) + ch(e, f, g) +
-                            kK256[t] + wt;
-        const uint32_t t2 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)) + maj(a, b, c);
-        h = g;
-        g = f;
-        f = e;
-        e = d + t1;
-        d = c;
-        c = b;
-        b = a;
-        a = t1 + t2;
+    for (int q = 0; q < 16; q += 2) {
+        const uint4 v = slot[q * 64 + lane];
+        const uint4 u = slot[(q + 1) * 64 + lane];
+        VS_SHA_ROUND(a, b, c, d, e, f, g, h, v.x)
+        VS_SHA_ROUND(h, a, b, c, d, e, f, g, v.y)
+        VS_SHA_ROUND(g, h, a, b, c, d, e, f, v.z)
+        VS_SHA_ROUND(f, g, h, a, b, c, d, e, v.w)
+        VS_SHA_ROUND(e, f, g, h, a, b, c, d, u.x)
+        VS_SHA_ROUND(d, e, f, g, h, a, b, c, u.y)
+        VS_SHA_ROUND(c, d, e, f, g, h, a, b, u.z)
+        VS_SHA_ROUND(b, c, d, e, f, g, h, a, u.w)
     }
     st[0] += a;
     st[1] += b;
@@ -77,172 +178,272 @@ __device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
     st[6] += g;
     st[7] += h;
 }
+#undef VS_SHA_ROUND
 
-// Work-queue SHA-256.  A fixed grid of lanes pulls blobs
-// longest-first from a global counter; every loop iteration each busy lane
-// compresses exactly one 64-byte block -- a data block, or one of the one or
-// two padding blocks it builds from the blob's tail -- so a wave stays full
-// until the queue drains and only the fetch / padding build diverge.  Waves
-// whose blobs have the most blocks left raise their issue priority, so the
-// longest blobs (the latency tail) run at the single-wave issue rate while
-// co-resident waves fill the SIMD's remaining issue slots.
-__device__ __forceinline__ uint64_t blob_len(const ShaArgs &a, uint64_t i, uint64_t start) {
-    return a.ends ? ((a.ends[i] & kPosMask) - start + 1) : a.lens[i];
-}
-
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
-}
-
-// The next block's words are loaded while the current block is compressed
-// (one wave per SIMD in a latency tail has nothing else to hide the load).
-__device__ __forceinline__ void load_words(uint32_t (&d)[17], const uint32_t *wp, uint32_t lim) {
-    if (lim >= 64) {
-        // data block: one unconditional 64-byte load (merged into 4 x dwordx4)
-#pragma unroll
-        for (int k = 0; k < 16; ++k) d[k] = wp[k];
-        d[16] = (lim > 64) ? wp[16] : 0u;
-    } else {
-        // padding block (once per blob): only the words that hold tail bytes
-#pragma unroll
-        for (int k = 0; k < 17; ++k) d[k] = (4u * k < lim) ? wp[k] : 0u;
-    }
-}
-
-// words of block j: data blocks read 64 B (+4 when misaligned); the first
-// padding block reads only the words holding tail bytes (never past the blob)
-__device__ __forceinline__ uint32_t block_lim(uint32_t j, uint32_t nfull, uint32_t r,
-                                              uint32_t rem) {
-    return (j < nfull) ? (r ? 68u : 64u) : (j == nfull ? r + rem : 0u);
-}
-
-__global__ __launch_bounds__(256, 4) void sha256_kernel(ShaArgs a) {
-    bool has = false, done = false;
-    uint32_t ci = 0;               // blob index
-    const uint32_t *wp = nullptr;  // 4-aligned words of block b+1 (the prefetch target)
-    uint32_t sel = 0;              // v_perm selector: byte misalignment r in its top byte
-    uint32_t nfull = 0, b = 0, rem = 0;  // full data blocks, current block, tail bytes
-    uint32_t st[8];
-    uint32_t d[17];                // raw words of block b
+// One slice over the active chains.  Workgroup = 2 waves:
+// wave 0 produces, wave 1 consumes; both hold the same 64 chains (lane l of
+// each wave = chain l of the tile) and step through the same block loop, one
+// workgroup barrier per block.
+__global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
+    __shared__ uint4 wk[2][16 * 64];  // 2 x 16 KiB: W+K of one block of 64 chains
+    __shared__ uint32_t tile_sh;
+    const uint32_t lane = threadIdx.x & 63;
+    const bool producer = threadIdx.x < 64;
+    const uint32_t n = *a.n_cur;
+    const uint32_t ntiles = (n + 63) / 64;
+    if (!producer) __builtin_amdgcn_s_setprio(2);  // the rounds are the critical path
     for (;;) {
-        if (!has && !done) {
-            const uint32_t t = atomicAdd(a.counter, 1u);
-            if (t < a.n) {
-                ci = a.order ? a.order[t] : t;
-                const uint64_t start = a.starts[ci];
-                const uint64_t len = blob_len(a, ci, start);
-                const uint32_t r = (uint32_t)(start & 3);
-                sel = (r << 24) | ((r + 1) << 16) | ((r + 2) << 8) | (r + 3);
-                wp = (const uint32_t *)(a.data + (start - r));
-                nfull = (uint32_t)(len >> 6);
-                rem = (uint32_t)(len & 63);
-                b = 0;
-                load_words(d, wp, block_lim(0, nfull, r, rem));
-                wp += 16;
-                st[0] = 0x6a09e667; st[1] = 0xbb67ae85; st[2] = 0x3c6ef372; st[3] = 0xa54ff53a;
-                st[4] = 0x510e527f; st[5] = 0x9b05688c; st[6] = 0x1f83d9ab; st[7] = 0x5be0cd19;
-                has = true;
-                // raise the issue priority of waves that hold the longest blobs
-                const uint32_t left = wave_max_u32(min(nfull >> 13, 3u));
-                const uint32_t pr = __builtin_amdgcn_readfirstlane(left);
-                if (pr >= 3) __builtin_amdgcn_s_setprio(3);
-                else if (pr == 2) __builtin_amdgcn_s_setprio(2);
-                else if (pr == 1) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            } else {
-                done = true;
-            }
-        }
-        if (__all(done)) break;
-        if (has) {
-            const uint32_t r = sel >> 24;
-            uint32_t w[16];
+        if (threadIdx.x == 0) tile_sh = atomicAdd(a.tile_ctr, 1u);
+        __syncthreads();
+        const uint32_t t = tile_sh;
+        __syncthreads();
+        if (t >= ntiles) break;
+        const uint32_t idx = t * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t ci = valid ? (a.order ? a.order[idx] : idx) : 0u;
+        const ShaChain ch0 = a.cur[ci];
+        const uint32_t left = valid ? blocks_left(ch0.ptr, ch0.end) : 0u;
+        const uint32_t mine = min(left, a.budget);
+        // steps = max over the tile's lanes (identical in both waves)
+        uint32_t steps = mine;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_perm(d[k + 1], d[k], sel);
-            if (b >= nfull) {
-                // padding: [tail bytes, 0x80, zeros] (+ big-endian bit length)
-                const uint32_t tl = (b == nfull) ? rem : 0u;
-                const bool mark = b == nfull;
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const int v = min(max((int)tl - 4 * k, 0), 4);  // tail bytes in word k
-                    const uint32_t keep = (v == 4) ? 0xffffffffu : ~(0xffffffffu >> (8 * v));
-                    const uint32_t m80 =
-                        (mark && v < 4 && (int)tl >= 4 * k) ? (0x80u << (24 - 8 * v)) : 0u;
-                    w[k] = (w[k] & keep) | m80;
-                }
-                if (b > nfull || rem < 56) {
-                    const uint64_t bits = ((uint64_t)nfull * 64 + rem) << 3;
-                    w[14] = (uint32_t)(bits >> 32);
-                    w[15] = (uint32_t)bits;
-                }
+        for (int o = 32; o > 0; o >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, o, 64));
+        steps = __builtin_amdgcn_readfirstlane(steps);
+        if (steps == 0) continue;
+        if (producer) {
+            uint32_t dr[17], w[16];
+            uint64_t p = ch0.ptr;
+            if (mine > 0) load_raw(dr, p, ch0.end);
+            uint32_t dn[17];
+            if (mine > 1) load_raw(dn, p + 64, ch0.end);
+            if (mine > 0) {
+                message(w, dr, p, ch0.end, ch0.len);
+                schedule_to_lds(w, wk[0], lane);
             }
-            load_words(d, wp, block_lim(b + 1, nfull, r, rem));  // prefetch block b+1
-            wp += 16;
-            compress(st, w);
-            ++b;
-            if (b == nfull + (rem < 56 ? 1u : 2u)) {
-                uint4 *out = (uint4 *)(a.ids + 32ull * ci);
+            __syncthreads();
+            for (uint32_t j = 0; j < steps; ++j) {
+                // produce block j+1 while the consumer runs block j
+                if (j + 1 < mine) {
+                    const uint64_t pj = p + 64ull * (j + 1);
+#pragma unroll
+                    for (int k = 0; k < 17; ++k) dr[k] = dn[k];
+                    if (j + 2 < mine) load_raw(dn, pj + 64, ch0.end);  // prefetch j+2
+                    message(w, dr, pj, ch0.end, ch0.len);
+                    schedule_to_lds(w, wk[(j + 1) & 1], lane);
+                }
+                __syncthreads();
+            }
+        } else {
+            uint32_t st[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) st[i] = ch0.st[i];
+            __syncthreads();
+            for (uint32_t j = 0; j < steps; ++j) {
+                if (j < mine) compress_lds(st, wk[j & 1], lane);
+                __syncthreads();
+            }
+            const bool finished = valid && mine == left;
+            const bool survive = valid && !finished;
+            if (finished) {
+                uint4 *out = (uint4 *)ch0.out;
                 out[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]),
                                     __builtin_bswap32(st[2]), __builtin_bswap32(st[3]));
                 out[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]),
                                     __builtin_bswap32(st[6]), __builtin_bswap32(st[7]));
-                has = false;
+            }
+            // survivors: wave-aggregated append to the next active list
+            const uint64_t bal = __ballot(survive);
+            if (bal) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(a.n_next, (uint32_t)__popcll(bal));
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (survive) {
+                    const uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+                    ShaChain nc = ch0;
+                    nc.ptr = ch0.ptr + 64ull * mine;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) nc.st[i] = st[i];
+                    a.next[pos] = nc;
+                }
             }
         }
     }
 }
 
-// grid: one lane per blob up to two waves per SIMD (256 CUs x 4 SIMDs x 2);
-// counter: a device word, zeroed here on the stream before the launch
-hipError_t launch_sha256(const ShaArgs &a, hipStream_t s) {
-    if (!a.n) return hipSuccess;
-    hipError_t e = hipMemsetAsync(a.counter, 0, sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
-    const uint64_t lanes = std::min<uint64_t>(a.n, 2048ull * 64);
-    sha256_kernel<<<(uint32_t)((lanes + 255) / 256), 256, 0, s>>>(a);
-    return hipGetLastError();
-}
-
-// ---- longest-first ordering ---------------------------------------------------
-constexpr uint32_t kLenBuckets = 4096;
-
-__device__ __forceinline__ uint32_t len_key(uint64_t i, const uint64_t *starts,
-                                            const uint64_t *ends, const uint32_t *lens) {
-    const uint64_t len = ends ? ((ends[i] & kPosMask) - starts[i] + 1) : lens[i];
-    const uint64_t b = len >> 16;
-    return kLenBuckets - 1 - (uint32_t)(b < kLenBuckets ? b : kLenBuckets - 1);
-}
-
-__global__ void len_hist_kernel(uint64_t n, const uint64_t *starts, const uint64_t *ends,
-                                const uint32_t *lens, uint32_t *hist) {
+// ---- engine bookkeeping kernels ------------------------------------------------
+__global__ void sha_append_chunks_kernel(ShaChain *list, const uint32_t *n_cur, const uint8_t *data,
+                                         const uint64_t *starts, const uint64_t *ends, uint64_t n,
+                                         uint8_t *ids) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) atomicAdd(&hist[len_key(i, starts, ends, lens)], 1u);
+    if (i >= n) return;
+    const uint64_t s = starts[i];
+    const uint64_t e = (ends[i] & kPosMask) + 1;
+    ShaChain c;
+    c.ptr = (uint64_t)(uintptr_t)(data + s);
+    c.end = (uint64_t)(uintptr_t)(data + e);
+    c.len = e - s;
+    c.out = ids + 32 * i;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c.st[k] = kIV[k];
+    list[*n_cur + i] = c;
 }
 
-__global__ void len_scatter_kernel(uint64_t n, const uint64_t *starts, const uint64_t *ends,
-                                   const uint32_t *lens, uint32_t *cursor, uint32_t *order) {
+__global__ void sha_append_blobs_kernel(ShaChain *list, const uint32_t *n_cur, const uint8_t *data,
+                                        const uint64_t *off, const uint32_t *lens, uint64_t n,
+                                        uint8_t *ids) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) order[atomicAdd(&cursor[len_key(i, starts, ends, lens)], 1u)] = (uint32_t)i;
+    if (i >= n) return;
+    ShaChain c;
+    c.ptr = (uint64_t)(uintptr_t)(data + off[i]);
+    c.end = c.ptr + lens[i];
+    c.len = lens[i];
+    c.out = ids + 32 * i;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c.st[k] = kIV[k];
+    list[*n_cur + i] = c;
 }
 
-// hist: scratch of >= 2*kLenBuckets + 8 u32
-hipError_t launch_length_order(uint64_t n, const uint64_t *starts, const uint64_t *ends,
-                               const uint32_t *lens, uint32_t *hist, uint32_t *order,
-                               hipStream_t s) {
-    if (!n) return hipSuccess;
-    uint32_t *cursor = hist + kLenBuckets;
-    uint32_t *partials = cursor + kLenBuckets + 1;
-    hipError_t e = hipMemsetAsync(hist, 0, kLenBuckets * sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
-    const uint32_t blocks = (uint32_t)((n + 255) / 256);
-    len_hist_kernel<<<blocks, 256, 0, s>>>(n, starts, ends, lens, hist);
-    e = launch_scan_u32(hist, cursor, kLenBuckets, partials, 0xffffffffu, s);
-    if (e != hipSuccess) return e;
-    len_scatter_kernel<<<blocks, 256, 0, s>>>(n, starts, ends, lens, cursor, order);
-    return hipGetLastError();
+__global__ void sha_count_add_kernel(uint32_t *n_cur, uint32_t add) { *n_cur += add; }
+
+// longest-first order of the active list: bucket = 4095 - f(blocks this slice),
+// f monotone, exact below 1024 blocks, 1/64 relative precision above
+constexpr uint32_t kShaBuckets = 4096;
+__device__ __forceinline__ uint32_t sha_key(const ShaChain &c, uint32_t budget) {
+    const uint32_t b = min(blocks_left(c.ptr, c.end), budget);
+    uint32_t f;
+    if (b < 1024) {
+        f = b;
+    } else {
+        const uint32_t l = 31 - __clz(b);  // >= 10
+        f = 1024 + ((l - 10) << 6) + ((b >> (l - 6)) & 63);
+    }
+    return kShaBuckets - 1 - min(f, kShaBuckets - 1);
+}
+
+__global__ void sha_hist_kernel(const ShaChain *list, const uint32_t *n_cur, uint32_t budget,
+                                uint32_t *hist) {
+    const uint32_t n = *n_cur;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        atomicAdd(&hist[sha_key(list[i], budget)], 1u);
+}
+
+__global__ void sha_scatter_kernel(const ShaChain *list, const uint32_t *n_cur, uint32_t budget,
+                                   uint32_t *cursor, uint32_t *order) {
+    const uint32_t n = *n_cur;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        order[atomicAdd(&cursor[sha_key(list[i], budget)], 1u)] = i;
+}
+
+// ---- ShaEngine (host) ------------------------------------------------------------
+int ShaEngine::init(int dev) {
+    device = dev;
+    VS_TRY(ctl.ensure(64));
+    VS_TRY(hist.ensure((2 * kShaBuckets + 16) * 4));
+    VS_HIP(hipMemset(ctl.p, 0, 64));
+    VS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    return 0;
+}
+
+void ShaEngine::release() {
+    for (DevBuf *b : {&list[0], &list[1], &order, &hist, &ctl}) b->release();
+    groups.clear();
+    ub = 0;
+    cap = 0;
+}
+
+uint32_t *ShaEngine::count(int which) { return ctl.as<uint32_t>() + which; }
+
+// capacity for n_new more chains on top of every chain that may still be active
+int ShaEngine::reserve(uint64_t n_new, hipStream_t s) {
+    const uint64_t need = ub + n_new;
+    if (need > 0xffffffffull) return fail(VS_ERR_ARG, "too many active SHA-256 chains");
+    if (need <= cap) return 0;
+    uint64_t ncap = std::max<uint64_t>(need + need / 2, 4096);
+    // growing: wait for queued slices, carry the current list over
+    VS_HIP(hipStreamSynchronize(s));
+    DevBuf nl[2], no;
+    VS_TRY(nl[0].ensure(ncap * sizeof(ShaChain)));
+    VS_TRY(nl[1].ensure(ncap * sizeof(ShaChain)));
+    VS_TRY(no.ensure(ncap * 4));
+    if (cap) VS_HIP(hipMemcpy(nl[cur].p, list[cur].p, cap * sizeof(ShaChain), hipMemcpyDeviceToDevice));
+    list[0].release();
+    list[1].release();
+    order.release();
+    list[0] = nl[0];
+    list[1] = nl[1];
+    order = no;
+    cap = ncap;
+    return 0;
+}
+
+int ShaEngine::append_chunks(const uint8_t *data, const uint64_t *starts, const uint64_t *ends,
+                             uint64_t n, uint8_t *ids, uint32_t max_blocks, hipStream_t s) {
+    if (!n) return 0;
+    VS_TRY(reserve(n, s));
+    sha_append_chunks_kernel<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(
+        list[cur].as<ShaChain>(), count(cur), data, starts, ends, n, ids);
+    sha_count_add_kernel<<<1, 1, 0, s>>>(count(cur), (uint32_t)n);
+    VS_HIP(hipGetLastError());
+    ub += n;
+    groups.push_back({n, max_blocks});
+    return 0;
+}
+
+int ShaEngine::append_blobs(const uint8_t *data, const uint64_t *off, const uint32_t *lens,
+                            uint64_t n, uint8_t *ids, hipStream_t s) {
+    if (!n) return 0;
+    VS_TRY(reserve(n, s));
+    sha_append_blobs_kernel<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(
+        list[cur].as<ShaChain>(), count(cur), data, off, lens, n, ids);
+    sha_count_add_kernel<<<1, 1, 0, s>>>(count(cur), (uint32_t)n);
+    VS_HIP(hipGetLastError());
+    ub += n;
+    groups.push_back({n, 0xffffffffu});
+    return 0;
+}
+
+// advance every active chain by up to `budget` blocks (0xffffffff: to the end)
+int ShaEngine::slice(uint32_t budget, hipStream_t s) {
+    if (ub == 0) return 0;
+    const int nxt = cur ^ 1;
+    uint32_t *cursor = hist.as<uint32_t>() + kShaBuckets;
+    uint32_t *partials = cursor + kShaBuckets + 1;
+    VS_HIP(hipMemsetAsync(hist.p, 0, kShaBuckets * 4, s));
+    const uint32_t sb = (uint32_t)std::min<uint64_t>((ub + 255) / 256, 4096);
+    sha_hist_kernel<<<sb, 256, 0, s>>>(list[cur].as<ShaChain>(), count(cur), budget,
+                                       hist.as<uint32_t>());
+    VS_HIP(launch_scan_u32(hist.as<uint32_t>(), cursor, kShaBuckets, partials, 0xffffffffu, s));
+    sha_scatter_kernel<<<sb, 256, 0, s>>>(list[cur].as<ShaChain>(), count(cur), budget, cursor,
+                                          order.as<uint32_t>());
+    // zero the next list's count and the tile counter
+    VS_HIP(hipMemsetAsync(count(nxt), 0, 4, s));
+    VS_HIP(hipMemsetAsync(count(2), 0, 4, s));
+    ShaSliceArgs a{};
+    a.cur = list[cur].as<ShaChain>();
+    a.next = list[nxt].as<ShaChain>();
+    a.order = order.as<uint32_t>();
+    a.n_cur = count(cur);
+    a.n_next = count(nxt);
+    a.tile_ctr = count(2);
+    a.budget = budget;
+    // persistent grid: LDS (32 KiB per workgroup) admits 5 workgroups per CU
+    const uint64_t tiles = (ub + 63) / 64;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)std::max(cus, 1) * 5);
+    sha_slice_kernel<<<grid, 128, 0, s>>>(a);
+    VS_HIP(hipGetLastError());
+    cur = nxt;
+    // chains of a group finish within ceil(max_blocks / budget) slices
+    uint64_t nub = 0;
+    std::vector<Group> keep;
+    for (Group g : groups) {
+        if (budget == 0xffffffffu || g.max_blocks <= budget) continue;
+        g.max_blocks -= budget;
+        nub += g.n;
+        keep.push_back(g);
+    }
+    groups.swap(keep);
+    ub = nub;
+    return 0;
 }
 
 // ---- synthetic volume bytes -------------------------------------
