@@ -75,6 +75,9 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=int, default=4)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hash-stream", choices=["own", "main"], default="own",
+                    help="SHA-256 slices on the handle's own hash stream (overlapping the next "
+                         "fingerprint pass) or serialised on the main stream")
     ap.add_argument("--hash-slice", type=int, default=8192,
                     help="SHA-256 blocks per chunk per step (time-sliced engine; 0 = unbounded)")
     args = ap.parse_args()
@@ -103,6 +106,11 @@ def main():
 
     dc = DeviceChunker(TestPol, MinSize, MaxSize, 20, device=local)
     dc.set_hash_slice(args.hash_slice)
+    if args.hash_stream == "main":
+        # hash slices queue behind the fingerprint pass on one stream
+        one = torch.cuda.Stream(dev)
+        dc.set_stream(one.cuda_stream)
+        dc.set_hash_stream(one.cuda_stream)
     coll = torch_collectives(dev) if world > 1 else None
 
     def step():
@@ -202,6 +210,7 @@ def main():
             "stages_ms_per_step": {k: round(v, 3) for k, v in per_step.items()},
             "kernels": roof,
             "hash_slice_blocks": args.hash_slice,
+            "hash_stream": args.hash_stream,
             "sha_slices": launches[2],
             "single_volume": {"ms": round(lat * 1e3, 2),
                               "GBps": round(total / lat / 1e9, 2),

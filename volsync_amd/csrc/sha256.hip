@@ -74,9 +74,14 @@ __device__ __forceinline__ uint32_t blocks_left(uint64_t ptr, uint64_t end) {
 // Raw little-endian words of the block at ptr: 16 words (+1 when ptr is not
 // 4-byte aligned) of a data block; only the words holding tail bytes of the
 // first padding block (never reading past the blob); none for the second.
+// (global address space: the loads count only in vmcnt, so the producer's
+// prefetch stays in flight across the LDS barrier; flat loads would also count
+// in lgkmcnt and be drained by the barrier's lgkmcnt(0))
+typedef __attribute__((address_space(1))) const uint32_t gu32;
+
 __device__ __forceinline__ void load_raw(uint32_t (&d)[17], uint64_t ptr, uint64_t end) {
     const uint32_t r = (uint32_t)(ptr & 3);
-    const uint32_t *wp = (const uint32_t *)(uintptr_t)(ptr - r);
+    gu32 *wp = (gu32 *)(uintptr_t)(ptr - r);
     const int64_t left = (int64_t)(end - ptr);
     if (left >= 64) {
 #pragma unroll
@@ -188,7 +193,7 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
     __shared__ uint4 wk[2][16 * 64];  // 2 x 16 KiB: W+K of one block of 64 chains
     __shared__ uint32_t tile_sh;
     const uint32_t lane = threadIdx.x & 63;
-    const bool producer = threadIdx.x < 64;
+    const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;  // wave-uniform
     const uint32_t n = *a.n_cur;
     const uint32_t ntiles = (n + 63) / 64;
     if (!producer) __builtin_amdgcn_s_setprio(2);  // the rounds are the critical path
