@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libvsgpu.so")
+# VSGPU_LIB: an alternative build of the same library (kernel A/B experiments)
+LIB_PATH = os.environ.get("VSGPU_LIB") or os.path.join(_HERE, "lib", "libvsgpu.so")
 
 VS_OK = 0
 VS_EOF = 1

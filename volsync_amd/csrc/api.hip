@@ -26,7 +26,8 @@ int fail(int code, const std::string &msg) {
     return code;
 }
 
-// strip = 64 * G with G % 3 == 0 (fingerprint.hip rotates three group buffers)
+// strip = 64 * G with G % 3 == 0 and G < 256 (fingerprint.hip rotates three
+// 64-byte group buffers and notes groups by 8-bit index)
 constexpr uint32_t kStrip = 12288;
 
 enum Stage { kStFp = 0, kStSel = 1, kStSha = 2, kStOther = 3 };
@@ -37,6 +38,7 @@ using namespace vsgpu;
 
 struct vs_cdc {
     int device = 0;
+    int cus = 256;  // compute units (persistent fingerprint grid)
     hipStream_t stream = nullptr;
     hipStream_t own = nullptr;
     // parameters
@@ -328,27 +330,18 @@ static int run_scan_kernels(vs_cdc *h) {
         StageTimer t(h, kStFp);
         FpArgs a = fp_args(h);
         const bool wide = h->avg_bits > 32;
-        // strips whose reads stay inside [0, dlen) need no bounds checks
+        // strips whose reads stay inside [0, dlen) need no bounds checks; the
+        // rest (at most a few) run bounds-checked inside the same launch
         uint64_t k_lo = (h->base >= 64) ? 0 : 1;
         uint64_t k_hi = (h->dlen >= h->base) ? (h->dlen - h->base) / kStrip : 0;
         k_hi = std::min(k_hi, h->nstrips);
         k_lo = std::min(k_lo, h->nstrips);
         if (k_hi < k_lo) k_hi = k_lo;
-        if (k_hi > k_lo) {
-            a.k_first = k_lo;
-            a.k_count = k_hi - k_lo;
-            VS_HIP(launch_fingerprint(a, false, wide, h->stream));
-        }
-        if (k_lo > 0) {
-            a.k_first = 0;
-            a.k_count = k_lo;
-            VS_HIP(launch_fingerprint(a, true, wide, h->stream));
-        }
-        if (h->nstrips > k_hi) {
-            a.k_first = k_hi;
-            a.k_count = h->nstrips - k_hi;
-            VS_HIP(launch_fingerprint(a, true, wide, h->stream));
-        }
+        a.k_lo = k_lo;
+        a.k_hi = k_hi;
+        a.n_edge = k_lo + (h->nstrips - k_hi);
+        a.work = h->flags.as<uint32_t>() + 3;  // zeroed with the flags above
+        VS_HIP(launch_fingerprint(a, wide, h->cus, h->stream));
     }
     {
         StageTimer t(h, kStSel);
@@ -669,6 +662,8 @@ VS_API int vs_cdc_open(int device, uint64_t pol, uint32_t min_size, uint32_t max
     }
     h->stream = h->own;
     h->hstream = h->own_h;
+    if (hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+        h->cus = 256;
     if (h->sha.init(device) < 0) {
         std::string msg = g_err;
         vs_cdc_close(h);

@@ -14,6 +14,18 @@
 // lane group always hit 32 distinct bank pairs, whatever the indices.
 // 8.5 VALU + 2 ds_read_b64 per byte; the OUT8 lookup is off the digest's
 // dependency chain.
+//
+// The digest chain costs one LDS round trip per byte, so each lane carries
+// two strips ("chains") interleaved byte by byte.  The grid is persistent
+// (one 12-wave workgroup per CU, tables loaded once); waves take 128 strips
+// at a time from a work counter, and the few strips whose reads need bounds
+// checks (the first one when it has no 64-byte warm-up before it, the last
+// ones) are done by wave 0 of workgroup 0 beside the others.  Each lane
+// reads whole 64-byte groups (four back-to-back dwordx4 loads, one cache-line
+// pair), three per chain: the group 64 bytes back (the evicted bytes), the
+// current group and the next.  The hot loop only notes which groups hold a
+// candidate; their exact offsets are found after the strip by re-rolling each
+// noted group from a 64-byte warm-up (the window property again).
 #include "internal.hpp"
 
 namespace vsgpu {
@@ -21,6 +33,7 @@ namespace vsgpu {
 constexpr uint32_t kTabEntries = 256 * kFpCopies;  // u64 entries per table
 constexpr uint32_t kOut8Byte = kTabEntries * 8;    // byte offset of OUT8 in LDS (0x10000)
 static_assert(kOut8Byte == 0x10000, "roll() builds OUT8 addresses with v_perm");
+constexpr uint32_t kUnit = 128;                    // strips per work unit: 2 per lane
 
 typedef uint32_t G16[16];  // one 64-byte group as 16 little-endian words
 
@@ -41,7 +54,7 @@ __device__ __forceinline__ void load_group(G16 &g, const uint8_t *data, int64_t 
                                            uint64_t dlen) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        uint4 v = load16<GUARD>(data, off + 16 * q, dlen);
+        const uint4 v = load16<GUARD>(data, off + 16 * q, dlen);
         g[4 * q + 0] = v.x;
         g[4 * q + 1] = v.y;
         g[4 * q + 2] = v.z;
@@ -54,11 +67,10 @@ __device__ __forceinline__ uint64_t lds_u64(const char *lds, uint32_t byte_addr)
 }
 
 // One byte of the rolling window.  oldw/neww hold the evicted / incoming byte
-// in byte lane J.  Returns the new low digest word (for the cut test).
+// in byte lane J.
 template <int J>
-__device__ __forceinline__ uint32_t roll(uint32_t &hi, uint32_t &lo, uint32_t oldw,
-                                         uint32_t neww, uint32_t lane8, uint32_t sh,
-                                         const char *lds) {
+__device__ __forceinline__ void roll(uint32_t &hi, uint32_t &lo, uint32_t oldw, uint32_t neww,
+                                     uint32_t lane8, uint32_t sh, const char *lds) {
     const uint32_t lane8o = lane8 | kOut8Byte;
     // lane8o = lane*8 | 0x10000 (OUT8 base): one v_perm builds
     // [lane*8, b_old, 0x01, 0x00] = 0x10000 + b_old*256 + lane*8
@@ -71,7 +83,6 @@ __device__ __forceinline__ uint32_t roll(uint32_t &hi, uint32_t &lo, uint32_t ol
     const uint32_t nlo = __builtin_amdgcn_perm(lo, neww, 0x06050400u | J);  // lo<<8 | b_new
     hi = __builtin_amdgcn_bitop3_b32(nhi, (uint32_t)(mv >> 32), (uint32_t)(ov >> 32), 0x96);
     lo = __builtin_amdgcn_bitop3_b32(nlo, (uint32_t)mv, (uint32_t)ov, 0x96);
-    return lo;
 }
 
 // warm-up roll: the window still holds virtual zeros, OUT8[0] == 0
@@ -104,27 +115,25 @@ __device__ __forceinline__ void process_group(uint32_t (&hi)[CH], uint32_t (&lo)
     for (int c = 0; c < CH; ++c) m[c] = 0xffffffffu;
 #pragma unroll
     for (int w = 0; w < 16; ++w) {
-#define VS_ROLL2(J0, J1)                                                                 \
-    {                                                                                    \
-        uint32_t a_[CH], b_[CH];                                                         \
-        _Pragma("unroll") for (int c = 0; c < CH; ++c) a_[c] =                           \
-            (roll<J0>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds),                \
-             cut_bits<WIDE>(hi[c], lo[c], mlo, mhi));                                    \
-        _Pragma("unroll") for (int c = 0; c < CH; ++c) b_[c] =                           \
-            (roll<J1>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds),                \
-             cut_bits<WIDE>(hi[c], lo[c], mlo, mhi));                                    \
-        _Pragma("unroll") for (int c = 0; c < CH; ++c) m[c] =                            \
-            __builtin_elementwise_min(__builtin_elementwise_min(m[c], a_[c]), b_[c]);    \
-    }
-        VS_ROLL2(0, 1)
-        VS_ROLL2(2, 3)
-#undef VS_ROLL2
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                switch (j) {
+                    case 0: roll<0>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
+                    case 1: roll<1>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
+                    case 2: roll<2>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
+                    default: roll<3>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
+                }
+                m[c] = __builtin_elementwise_min(m[c], cut_bits<WIDE>(hi[c], lo[c], mlo, mhi));
+            }
+        }
     }
 }
 
-// ---- rare path: a group holds at least one candidate -------------------------
+// ---- candidate offsets: re-roll the noted groups ---------------------------------
 template <bool GUARD>
-__device__ __forceinline__ uint8_t byte_at(const uint8_t *data, int64_t p, uint64_t dlen) {
+__device__ __forceinline__ uint32_t byte_at(const uint8_t *data, int64_t p, uint64_t dlen) {
     if (GUARD && (p < 0 || (uint64_t)p >= dlen)) return 0;
     return data[p];
 }
@@ -133,7 +142,6 @@ struct StripRec {
     uint64_t k;      // strip index
     uint32_t cnt;    // candidates so far
     uint32_t slot;   // dense pool slot
-    bool valid;      // chain maps to a real strip
 };
 
 __device__ void rec_dense_alloc(const FpArgs &a, StripRec &r) {
@@ -154,86 +162,82 @@ __device__ void rec_dense_alloc(const FpArgs &a, StripRec &r) {
     }
 }
 
+// Every candidate in [from, to) of strip r (from - strip_base and to - from
+// multiples of 64): the digest entering `from` is rebuilt from the 64 bytes
+// before it, then the window rolls byte by byte.
 template <bool GUARD, bool WIDE>
-__device__ void rare_group(const FpArgs &a, StripRec &r, int64_t gpos, uint32_t hi,
-                           uint32_t lo, uint32_t sh, uint32_t lane8, const char *lds,
-                           uint64_t strip_base) {
-    // gpos: data offset of the group's first byte; (hi,lo): digest before it
-    uint64_t bits = 0;
-    for (int j = 0; j < 64; ++j) {
-        const int64_t p = gpos + j;
-        const uint32_t bo = byte_at<GUARD>(a.data, p - 64, a.dlen);
-        const uint32_t bn = byte_at<GUARD>(a.data, p, a.dlen);
+__device__ void rescan(const FpArgs &a, StripRec &r, int64_t from, int64_t to, uint32_t lane8,
+                       const char *lds, uint64_t strip_base) {
+    const uint32_t sh = a.idx_shift;
+    uint32_t hi = 0, lo = 0;
+    for (int64_t p = from - 64; p < from; ++p) {
         const uint32_t idx = __builtin_amdgcn_ubfe(hi, sh, 8);
         const uint64_t mv = lds_u64(lds, (idx << 8) | lane8);
-        const uint64_t ov = lds_u64(lds, kOut8Byte + (bo << 8) + lane8);
-        const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 24);
-        const uint32_t nlo = (lo << 8) | bn;
-        hi = nhi ^ (uint32_t)(mv >> 32) ^ (uint32_t)(ov >> 32);
-        lo = nlo ^ (uint32_t)mv ^ (uint32_t)ov;
-        if (cut_bits<WIDE>(hi, lo, a.mask_lo, a.mask_hi) == 0 && (uint64_t)p < a.scan_end &&
-            r.valid) {
-            const uint32_t off = (uint32_t)((uint64_t)p - strip_base);
-            if (r.cnt < (uint32_t)kSlots) {
-                a.offs[r.k * kSlots + r.cnt] = off;
-            } else {
-                if (r.cnt == (uint32_t)kSlots) rec_dense_alloc(a, r);
-                bits |= 1ull << j;
-            }
-            r.cnt++;
-        }
+        hi = __builtin_amdgcn_alignbit(hi, lo, 24) ^ (uint32_t)(mv >> 32);
+        lo = ((lo << 8) | byte_at<GUARD>(a.data, p, a.dlen)) ^ (uint32_t)mv;
     }
-    if (bits && r.slot != kNoSlot) {
-        const uint32_t words = a.strip / 32;
-        uint32_t *bw = a.pool + (uint64_t)r.slot * words;
-        const uint32_t w0 = (uint32_t)(((uint64_t)gpos - strip_base) >> 5);
-        bw[w0] |= (uint32_t)bits;
-        bw[w0 + 1] |= (uint32_t)(bits >> 32);
+    for (int64_t g = from; g < to; g += 64) {
+        uint64_t bits = 0;
+        for (int j = 0; j < 64; ++j) {
+            const int64_t p = g + j;
+            const uint32_t bo = byte_at<GUARD>(a.data, p - 64, a.dlen);
+            const uint32_t bn = byte_at<GUARD>(a.data, p, a.dlen);
+            const uint32_t idx = __builtin_amdgcn_ubfe(hi, sh, 8);
+            const uint64_t mv = lds_u64(lds, (idx << 8) | lane8);
+            const uint64_t ov = lds_u64(lds, kOut8Byte + (bo << 8) + lane8);
+            const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 24);
+            const uint32_t nlo = (lo << 8) | bn;
+            hi = nhi ^ (uint32_t)(mv >> 32) ^ (uint32_t)(ov >> 32);
+            lo = nlo ^ (uint32_t)mv ^ (uint32_t)ov;
+            if (cut_bits<WIDE>(hi, lo, a.mask_lo, a.mask_hi) == 0 && (uint64_t)p < a.scan_end) {
+                const uint32_t off = (uint32_t)((uint64_t)p - strip_base);
+                if (r.cnt < (uint32_t)kSlots) {
+                    a.offs[r.k * kSlots + r.cnt] = off;
+                } else {
+                    if (r.cnt == (uint32_t)kSlots) rec_dense_alloc(a, r);
+                    bits |= 1ull << j;
+                }
+                r.cnt++;
+            }
+        }
+        if (bits && r.slot != kNoSlot) {
+            uint32_t *bw = a.pool + (uint64_t)r.slot * (a.strip / 32);
+            const uint32_t w0 = (uint32_t)(((uint64_t)g - strip_base) >> 5);
+            bw[w0] |= (uint32_t)bits;
+            bw[w0 + 1] |= (uint32_t)(bits >> 32);
+        }
     }
 }
 
+// noted groups of one chain: up to three 8-bit group indices and a count in
+// the top byte; kNoteAll = more than three (the whole strip is re-rolled)
+constexpr uint32_t kNoteAll = 0xff000000u;
+__device__ __forceinline__ uint32_t note_group(uint32_t notes, uint32_t g) {
+    const uint32_t n = notes >> 24;
+    if (n >= 3) return kNoteAll;
+    return (notes | (g << (8 * n))) + (1u << 24);
+}
+
+// CH strips per lane, byte-interleaved.  kk[c]: strip indices; valid[c] false
+// for a padding chain (it computes but records nothing).
 template <int CH, bool GUARD, bool WIDE>
-__global__ __launch_bounds__(kFpThreads) void fp_kernel(FpArgs a) {
-    __shared__ __attribute__((aligned(16))) uint64_t tabs[2 * kTabEntries];  // 128 KiB
-    for (uint32_t i = threadIdx.x; i < kTabEntries; i += blockDim.x) {
-        const uint32_t e = i / kFpCopies;
-        tabs[i] = a.mod_tab[e];
-        tabs[kTabEntries + i] = a.out8_tab[e];
-    }
-    __syncthreads();
-    const char *lds = (const char *)tabs;
-    const uint32_t lane8 = (threadIdx.x & 31) * 8;
+__device__ __forceinline__ void run_strips(const FpArgs &a, const char *lds, uint32_t lane8,
+                                           const uint64_t (&kk)[CH], const bool (&valid)[CH]) {
     const uint32_t sh = a.idx_shift;
-    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t G = a.strip / 64;  // checked groups per strip (multiple of 3)
-
-    StripRec rec[CH];
+    const uint32_t G = a.strip / 64;  // groups per strip, a multiple of 3 (and < 256)
     int64_t sb[CH];  // strip base (data offset)
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-        uint64_t k = tid + (uint64_t)c * T;
-        rec[c].valid = k < a.k_count;
-        if (!rec[c].valid) k = a.k_count - 1;
-        rec[c].k = a.k_first + k;
-        rec[c].cnt = 0;
-        rec[c].slot = kNoSlot;
-        sb[c] = (int64_t)(a.base + rec[c].k * a.strip);
-    }
-
-    uint32_t hi[CH], lo[CH], m[CH];
+    uint32_t hi[CH], lo[CH], m[CH], notes[CH];
     G16 X[CH], Y[CH], Z[CH];
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
+        sb[c] = (int64_t)(a.base + kk[c] * a.strip);
         load_group<GUARD>(X[c], a.data, sb[c] - 64, a.dlen);  // warm-up bytes
-        load_group<GUARD>(Y[c], a.data, sb[c], a.dlen);       // group 1
-    }
-    // warm-up: the window starts as 64 virtual zero bytes, digest 0
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
+        load_group<GUARD>(Y[c], a.data, sb[c], a.dlen);       // group 0
         hi[c] = 0;
         lo[c] = 0;
+        notes[c] = 0;
     }
+    // warm-up: the window starts as 64 virtual zero bytes, digest 0
 #pragma unroll
     for (int w = 0; w < 16; ++w) {
 #pragma unroll
@@ -245,26 +249,21 @@ __global__ __launch_bounds__(kFpThreads) void fp_kernel(FpArgs a) {
         }
     }
 
+    // group GI: evicted bytes in OLD (group GI-1), incoming in NEW; NEXT <- GI+1
 #define VS_GROUP(OLD, NEW, NEXT, GI)                                                      \
     {                                                                                     \
-        if ((GI) + 1 <= G) {                                                              \
+        {   /* unconditional (the last group reloads itself): no phi copies */          \
+            const int64_t gn_ = 64 * (int64_t)min((GI) + 1, G - 1);                        \
             _Pragma("unroll") for (int c = 0; c < CH; ++c)                                \
-                load_group<GUARD>(NEXT[c], a.data, sb[c] + 64 * (int64_t)(GI), a.dlen);   \
-        }                                                                                 \
-        uint32_t h0[CH], l0[CH];                                                          \
-        _Pragma("unroll") for (int c = 0; c < CH; ++c) {                                  \
-            h0[c] = hi[c];                                                                \
-            l0[c] = lo[c];                                                                \
+                load_group<GUARD>(NEXT[c], a.data, sb[c] + gn_, a.dlen);                  \
         }                                                                                 \
         process_group<CH, WIDE>(hi, lo, OLD, NEW, m, lane8, sh, lds, a.mask_lo, a.mask_hi); \
         _Pragma("unroll") for (int c = 0; c < CH; ++c) {                                  \
-            if (m[c] == 0)                                                                \
-                rare_group<GUARD, WIDE>(a, rec[c], sb[c] + 64 * (int64_t)((GI) - 1), h0[c], \
-                                        l0[c], sh, lane8, lds, (uint64_t)sb[c]);          \
+            if (m[c] == 0) notes[c] = note_group(notes[c], (GI));                         \
         }                                                                                 \
     }
 
-    for (uint32_t g = 1; g <= G; g += 3) {
+    for (uint32_t g = 0; g < G; g += 3) {
         VS_GROUP(X, Y, Z, g)
         VS_GROUP(Y, Z, X, g + 1)
         VS_GROUP(Z, X, Y, g + 2)
@@ -273,33 +272,69 @@ __global__ __launch_bounds__(kFpThreads) void fp_kernel(FpArgs a) {
 
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
-        if (rec[c].valid) {
-            a.counts[rec[c].k] = rec[c].cnt;
-            a.dense_slot[rec[c].k] = rec[c].slot;
+        if (!valid[c]) continue;
+        StripRec r{kk[c], 0, kNoSlot};
+        const uint32_t n = notes[c] >> 24;
+        if (notes[c] == kNoteAll) {
+            rescan<GUARD, WIDE>(a, r, sb[c], sb[c] + a.strip, lane8, lds, (uint64_t)sb[c]);
+        } else {
+            for (uint32_t i = 0; i < n; ++i) {
+                const int64_t g0 = sb[c] + 64 * (int64_t)((notes[c] >> (8 * i)) & 0xff);
+                rescan<GUARD, WIDE>(a, r, g0, g0 + 64, lane8, lds, (uint64_t)sb[c]);
+            }
         }
+        a.counts[r.k] = r.cnt;
+        a.dense_slot[r.k] = r.slot;
     }
 }
 
-#ifndef VS_FP_CHAINS
-#define VS_FP_CHAINS 1
-#endif
-
-hipError_t launch_fingerprint(const FpArgs &a, bool guard, bool wide, hipStream_t s) {
-    if (a.k_count == 0) return hipSuccess;
-    constexpr int CH = VS_FP_CHAINS;
-    const uint64_t threads = (a.k_count + CH - 1) / CH;
-    const uint32_t blocks = (uint32_t)((threads + kFpThreads - 1) / kFpThreads);
-    if (guard) {
-        if (wide)
-            fp_kernel<CH, true, true><<<blocks, kFpThreads, 0, s>>>(a);
-        else
-            fp_kernel<CH, true, false><<<blocks, kFpThreads, 0, s>>>(a);
-    } else {
-        if (wide)
-            fp_kernel<CH, false, true><<<blocks, kFpThreads, 0, s>>>(a);
-        else
-            fp_kernel<CH, false, false><<<blocks, kFpThreads, 0, s>>>(a);
+template <bool WIDE>
+__global__ __launch_bounds__(kFpThreads) void fp_kernel(FpArgs a) {
+    __shared__ __attribute__((aligned(16))) uint64_t tabs[2 * kTabEntries];  // 128 KiB
+    for (uint32_t i = threadIdx.x; i < kTabEntries; i += blockDim.x) {
+        const uint32_t e = i / kFpCopies;
+        tabs[i] = a.mod_tab[e];
+        tabs[kTabEntries + i] = a.out8_tab[e];
     }
+    __syncthreads();
+    const char *lds = (const char *)tabs;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lane8 = (threadIdx.x & 31) * 8;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // bounds-checked strips: one per lane on wave 0 of workgroup 0
+    if (blockIdx.x == 0 && wave == 0) {
+        for (uint64_t e0 = 0; e0 < a.n_edge; e0 += 64) {
+            const uint64_t e = e0 + lane;
+            const bool v = e < a.n_edge;
+            const uint64_t ee = v ? e : 0;
+            const uint64_t kk[1] = {ee < a.k_lo ? ee : a.k_hi + (ee - a.k_lo)};
+            const bool vv[1] = {v};
+            run_strips<1, true, WIDE>(a, lds, lane8, kk, vv);
+        }
+    }
+    // interior strips: units of 128 strips, two chains per lane
+    for (;;) {
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(a.work, 1u);
+        u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
+        const uint64_t k0 = a.k_lo + (uint64_t)u * kUnit;
+        if (k0 >= a.k_hi) break;
+        const uint64_t kA = k0 + lane, kB = k0 + 64 + lane;
+        const uint64_t kk[2] = {kA < a.k_hi ? kA : k0, kB < a.k_hi ? kB : k0};
+        const bool vv[2] = {kA < a.k_hi, kB < a.k_hi};
+        run_strips<2, false, WIDE>(a, lds, lane8, kk, vv);
+    }
+}
+
+hipError_t launch_fingerprint(const FpArgs &a, bool wide, int cus, hipStream_t s) {
+    const uint64_t units = (a.k_hi - a.k_lo + kUnit - 1) / kUnit;
+    if (units == 0 && a.n_edge == 0) return hipSuccess;
+    const uint64_t grid =
+        std::max<uint64_t>(1, std::min<uint64_t>(units, (uint64_t)std::max(cus, 1)));
+    if (wide)
+        fp_kernel<true><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
+    else
+        fp_kernel<false><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 

@@ -66,7 +66,7 @@ void pol_tables(uint64_t pol, uint64_t out_tab[256], uint64_t mod_tab[256]);
 void pol_out8(uint64_t pol, const uint64_t out_tab[256], uint64_t out8[256]);
 
 // ---- fingerprint pass ------------------------------------------------------
-constexpr int kFpThreads = 1024;   // one 16-wave workgroup per CU (LDS: 128 KiB tables)
+constexpr int kFpThreads = 768;    // one 12-wave workgroup per CU (LDS: 128 KiB tables; 168 VGPRs)
 constexpr int kFpCopies = 32;      // lane-private table copies: conflict-free ds_read_b64
 constexpr int kSlots = 3;          // candidate offsets kept per strip (dense strips: bitmask)
 constexpr uint32_t kNoSlot = 0xffffffffu;
@@ -81,8 +81,9 @@ struct FpArgs {
     uint64_t dlen;         // readable bytes at data
     uint64_t base;         // data offset of strip 0 (multiple of 64)
     uint64_t scan_end;     // candidates are recorded for positions < scan_end
-    uint64_t k_first;      // first strip of this launch
-    uint64_t k_count;      // strips in this launch
+    uint64_t k_lo, k_hi;   // interior strips [k_lo, k_hi): reads need no bounds checks
+    uint64_t n_edge;       // the other strips ([0, k_lo), [k_hi, nstrips)): bounds-checked
+    uint32_t *work;        // interior work-unit counter (zeroed before the launch)
     uint32_t strip;        // bytes per strip (multiple of 64)
     uint32_t idx_shift;    // digest bit of the table index, minus 32 (deg - 40)
     uint32_t mask_lo, mask_hi;
@@ -96,7 +97,7 @@ struct FpArgs {
     const uint64_t *mod_tab;   // [256]
     const uint64_t *out8_tab;  // [256]
 };
-hipError_t launch_fingerprint(const FpArgs &a, bool guard, bool wide_mask, hipStream_t s);
+hipError_t launch_fingerprint(const FpArgs &a, bool wide_mask, int cus, hipStream_t s);
 
 // ---- selection -------------------------------------------------------------
 constexpr uint64_t kPosMask = (1ull << 62) - 1;

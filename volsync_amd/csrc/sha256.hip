@@ -71,30 +71,43 @@ __device__ __forceinline__ uint32_t blocks_left(uint64_t ptr, uint64_t end) {
     return b > 0xffffffffull ? 0xffffffffu : (uint32_t)b;
 }
 
-// Raw little-endian words of the block at ptr: 16 words (+1 when ptr is not
-// 4-byte aligned) of a data block; only the words holding tail bytes of the
-// first padding block (never reading past the blob); none for the second.
-// (global address space: the loads count only in vmcnt, so the producer's
-// prefetch stays in flight across the LDS barrier; flat loads would also count
-// in lgkmcnt and be drained by the barrier's lgkmcnt(0))
-typedef __attribute__((address_space(1))) const uint32_t gu32;
+// Block data reaches the producer by cooperative, coalesced loads.  A chain's
+// bytes are read as aligned 16-byte segments: block j of a slice starting at
+// ptr covers the segments at A + 64 j + 16 s, s = 0..4, with A = ptr & ~15
+// (ptr & 15 is the same for every block of a chain); segment 4 of block j is
+// segment 0 of block j+1, so a block needs segments 1..4.  For those, lane m
+// of load instruction i (i = 0..3) fetches segment 1 + m % 4 of chain
+// 16 i + m / 4: one instruction touches 16 chains (16 pages) instead of 64,
+// which is what the address-translation path can sustain.  The segments are
+// staged in the free LDS slot and each lane reads back its own chain's four.
+// A segment with no byte of the blob is read from `safe` (the blob's last
+// segment, or the digest slot of an empty blob): every load is
+// unconditional and in mapped memory; message() masks bytes past the end.
+// Global address space: the loads count only in vmcnt, so the prefetch stays
+// in flight across the LDS barrier.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 
-__device__ __forceinline__ void load_raw(uint32_t (&d)[17], uint64_t ptr, uint64_t end) {
-    const uint32_t r = (uint32_t)(ptr & 3);
-    gu32 *wp = (gu32 *)(uintptr_t)(ptr - r);
-    const int64_t left = (int64_t)(end - ptr);
-    if (left >= 64) {
+__device__ __forceinline__ uint4 load_seg(uint64_t a, uint64_t end, uint64_t safe) {
+    const u32x4 v = *(gu32x4 *)(uintptr_t)(a < end ? a : safe);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Raw little-endian words d[0..16] of a block from its five segments s0 and
+// s[0..3]: d[k] = word k + q of that 80-byte window, q = (ptr & 15) >> 2.
+__device__ __forceinline__ void window_words(uint32_t (&d)[17], const uint4 &s0,
+                                             const uint4 (&s)[4], uint32_t q) {
+    const uint32_t win[20] = {s0.x,   s0.y,   s0.z,   s0.w,   s[0].x, s[0].y, s[0].z,
+                              s[0].w, s[1].x, s[1].y, s[1].z, s[1].w, s[2].x, s[2].y,
+                              s[2].z, s[2].w, s[3].x, s[3].y, s[3].z, s[3].w};
+    // bit selects (v_bitop3), not a ternary on q: the compiler turns that into
+    // a dynamically indexed private array, i.e. scratch memory
+    const uint32_t m1 = 0u - (q & 1u), m2 = 0u - ((q >> 1) & 1u);
+    uint32_t t[19];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) d[k] = wp[k];
-        d[16] = r ? wp[16] : 0u;
-    } else if (left > 0) {
-        const uint32_t lim = r + (uint32_t)left;  // bytes of wp[] that belong to the blob
+    for (int i = 0; i < 19; ++i) t[i] = ch(m1, win[i + 1], win[i]);
 #pragma unroll
-        for (int k = 0; k < 17; ++k) d[k] = (4u * k < lim) ? wp[k] : 0u;
-    } else {
-#pragma unroll
-        for (int k = 0; k < 17; ++k) d[k] = 0u;
-    }
+    for (int k = 0; k < 17; ++k) d[k] = ch(m2, t[k + 2], t[k]);
 }
 
 // Big-endian message words W[0..15] of the block at ptr from its raw words.
@@ -216,25 +229,58 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
         steps = __builtin_amdgcn_readfirstlane(steps);
         if (steps == 0) continue;
         if (producer) {
-            uint32_t dr[17], w[16];
-            uint64_t p = ch0.ptr;
-            if (mine > 0) load_raw(dr, p, ch0.end);
-            uint32_t dn[17];
-            if (mine > 1) load_raw(dn, p + 64, ch0.end);
+            const uint64_t p = ch0.ptr, e = ch0.end, L = ch0.len;
+            const uint64_t A = p & ~15ull;
+            const uint64_t safe =
+                L ? ((e - 1) & ~15ull) : ((uint64_t)(uintptr_t)ch0.out & ~15ull);
+            const uint32_t q = (uint32_t)(p & 15) >> 2;
+            // the chain this lane loads for in instruction i, and its segment offset
+            uint64_t LA[4], LE[4], LS[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int src = 16 * i + (int)(lane >> 2);
+                LA[i] = (uint64_t)__shfl((long long)A, src, 64);
+                LE[i] = (uint64_t)__shfl((long long)e, src, 64);
+                LS[i] = (uint64_t)__shfl((long long)safe, src, 64);
+            }
+            const uint64_t so = 16 + 16 * (lane & 3);
+            // staged segments: chain c, segment t at uint4 index 5 c + t (80-byte
+            // stride: conflict-free ds_write_b128 / ds_read_b128)
+            const uint32_t wr = 5 * (lane >> 2) + (lane & 3);
+            uint4 R[4], c = load_seg(A, e, safe), S[4];
+            uint32_t d[17], w[16];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + so, LE[i], LS[i]);
+            // block 0 -> slot 0
+#pragma unroll
+            for (int i = 0; i < 4; ++i) wk[0][80 * i + wr] = R[i];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) S[t] = wk[0][5 * lane + t];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + 64 + so, LE[i], LS[i]);
+            window_words(d, c, S, q);
+            c = S[3];
             if (mine > 0) {
-                message(w, dr, p, ch0.end, ch0.len);
+                message(w, d, p, e, L);
                 schedule_to_lds(w, wk[0], lane);
             }
             __syncthreads();
             for (uint32_t j = 0; j < steps; ++j) {
-                // produce block j+1 while the consumer runs block j
-                if (j + 1 < mine) {
-                    const uint64_t pj = p + 64ull * (j + 1);
+                // produce block j+1 while the consumer runs block j; its segments
+                // arrived during step j-1, block j+2's are fetched now
+                uint4 *slot = wk[(j + 1) & 1];
+                const uint64_t nb = 64ull * (j + 2) + so;
 #pragma unroll
-                    for (int k = 0; k < 17; ++k) dr[k] = dn[k];
-                    if (j + 2 < mine) load_raw(dn, pj + 64, ch0.end);  // prefetch j+2
-                    message(w, dr, pj, ch0.end, ch0.len);
-                    schedule_to_lds(w, wk[(j + 1) & 1], lane);
+                for (int i = 0; i < 4; ++i) slot[80 * i + wr] = R[i];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + nb, LE[i], LS[i]);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) S[t] = slot[5 * lane + t];
+                window_words(d, c, S, q);
+                c = S[3];
+                if (j + 1 < mine) {
+                    message(w, d, p + 64ull * (j + 1), e, L);
+                    schedule_to_lds(w, slot, lane);
                 }
                 __syncthreads();
             }
