@@ -78,7 +78,7 @@ def main():
     ap.add_argument("--hash-stream", choices=["own", "main"], default="own",
                     help="SHA-256 slices on the handle's own hash stream (overlapping the next "
                          "fingerprint pass) or serialised on the main stream")
-    ap.add_argument("--hash-slice", type=int, default=8192,
+    ap.add_argument("--hash-slice", type=int, default=1024,
                     help="SHA-256 blocks per chunk per step (time-sliced engine; 0 = unbounded)")
     args = ap.parse_args()
 
@@ -182,6 +182,17 @@ def main():
                    "unit": "GB/s", "frac": round(sha_gbs / HBM_PEAK_GBS, 4), "traffic": None,
                    "valu_frac": round(sha_gbs * SHA_OPS_PER_BYTE / 1e3 / VALU_PEAK_TOPS, 4)},
     }
+    # roofline.traffic: HBM bytes per step from the committed rocprofv3
+    # FETCH_SIZE/WRITE_SIZE passes (profiles/traffic.json, tools/traffic.py),
+    # scaled to this run's volume; null when no profile matches
+    try:
+        tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+        for k in roof:
+            if k in tj:
+                roof[k]["traffic"] = round(tj[k]["bytes_per_volume"] * own_bytes / tj["volume_bytes"])
+                roof[k]["traffic_source"] = tj["source"]
+    except (OSError, ValueError, KeyError):
+        pass
     dom_name = "sha256" if per_step["sha256"] >= per_step["fingerprint"] else "fingerprint"
     roofline = dict(roof[dom_name])
     roofline["kernel"] = dom_name

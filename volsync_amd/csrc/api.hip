@@ -78,10 +78,10 @@ struct vs_cdc {
     DevBuf n_out;
     // SHA-256: time-sliced engine on its own stream (hstream)
     ShaEngine sha;
-    uint32_t hash_budget = 8192;  // blocks per chain per slice (0xffffffff: unbounded)
+    uint32_t hash_budget = 1024;  // blocks per chain per slice (0xffffffff: unbounded)
     uint32_t chain_slices = 1;    // slices that finish any chain: ceil(max blocks / budget)
     uint64_t slices = 0;          // slices launched
-    static constexpr int kSliceEv = 32;
+    static constexpr int kSliceEv = 64;
     hipEvent_t slice_ev[kSliceEv] = {};  // event after slice i at [i % kSliceEv]
     hipStream_t hstream = nullptr;
     hipStream_t own_h = nullptr;
@@ -222,7 +222,9 @@ static int size_ring(vs_cdc *h) {
     const uint64_t mb = sha_blocks(h->max_size);
     const uint64_t L = (h->hash_budget == 0xffffffffu) ? 1 : (mb + h->hash_budget - 1) / h->hash_budget;
     h->chain_slices = (uint32_t)std::min<uint64_t>(L, 1u << 30);
-    const size_t want = (size_t)std::min<uint64_t>(L + 2, 24);
+    // one slot per batch still hashing: a chain of max_size finishes L slices
+    // (= batches) after its own, so L + 2 slots never make the host wait
+    const size_t want = (size_t)std::min<uint64_t>(L + 2, 256);
     if (h->slots.size() != want) {
         VS_TRY(sync_stream(h, true));
         for (auto &s : h->slots) {
