@@ -113,7 +113,7 @@ int vs_cdc_set_hash_stream(vs_cdc *h, void *hip_stream);
  * advances every queued chunk by at most `blocks` 64-byte blocks and carries
  * the midstate of unfinished chunks to the next batch's launch; vs_cdc_wait
  * hashes the rest.  0 = unbounded (every batch hashed to the end in one
- * launch).  Default 8192 (512 KiB per chunk per batch). */
+ * launch).  Default 1024 (64 KiB per chunk per batch). */
 int vs_cdc_set_hash_slice(vs_cdc *h, uint32_t blocks);
 /* Pipelined batches: batch numbers count vs_cdc_finish calls from 0; the ring
  * keeps the last *ring batches' chunk lists.  Data passed to vs_cdc_scan must
