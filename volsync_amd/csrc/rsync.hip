@@ -47,6 +47,15 @@ __device__ __forceinline__ void load16(const uint8_t *p, uint64_t pos, uint64_t 
     }
 }
 
+// 16 bytes at p (global address space, any alignment): the load counts only in
+// vmcnt, so a prefetch stays in flight past LDS traffic
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gload16(const uint8_t *p) {
+    typedef __attribute__((address_space(1))) const u32x4 g4;
+    const u32x4 v = *(g4 *)(uintptr_t)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // (sum b, sum u*b) over bytes [pos, pos+n) with u = position - pos (local weights)
 __device__ void weak_parts(const uint8_t *p, uint64_t pos, uint64_t n, uint64_t lim,
                            uint32_t &sx, uint32_t &sux) {
@@ -169,17 +178,30 @@ size_t rs_sort_tmp_bytes(uint64_t n_keys, bool pairs) {
 }
 
 // ---- R6 coarse prefix sums of the source ------------------------------------------
-// per kRsG-byte block j: px[j] = sum x, pt[j] = sum t*x (t absolute, mod 2^32)
-__global__ void rs_block_sums_kernel(const uint8_t *data, uint64_t len, uint64_t nblk,
-                                     uint32_t *px, uint32_t *pt) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// per kRsG-byte block j: px[j] = sum x, pt[j] = sum t*x (t absolute, mod 2^32).
+// One wave per block: lane l sums bytes [64 l, 64 l + 64) with local weights,
+// then sux = sum_l (sux_l + 64 l * sx_l) across the wave (coalesced reads).
+__global__ __launch_bounds__(256) void rs_block_sums_kernel(const uint8_t *data, uint64_t len,
+                                                            uint64_t nblk, uint32_t *px,
+                                                            uint32_t *pt) {
+    const uint64_t j = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
     if (j >= nblk) return;
     const uint64_t pos = j * kRsG;
     const uint64_t n = min((uint64_t)kRsG, len - pos);
-    uint32_t sx, sux;
-    weak_parts(data, pos, n, len, sx, sux);
-    px[j] = sx;
-    pt[j] = (uint32_t)pos * sx + sux;
+    const uint64_t lo = min((uint64_t)lane * 64, n), hi = min(lo + 64, n);
+    uint32_t sx = 0, sux = 0;
+    if (hi > lo) weak_parts(data, pos + lo, hi - lo, len, sx, sux);
+    sux += (uint32_t)lo * sx;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        sx += (uint32_t)__shfl_xor((int)sx, o, 64);
+        sux += (uint32_t)__shfl_xor((int)sux, o, 64);
+    }
+    if (lane == 0) {
+        px[j] = sx;
+        pt[j] = (uint32_t)pos * sx + sux;
+    }
 }
 
 hipError_t launch_rs_prefix(const uint8_t *data, uint64_t len, uint32_t *px, uint32_t *pt,
@@ -187,8 +209,7 @@ hipError_t launch_rs_prefix(const uint8_t *data, uint64_t len, uint32_t *px, uin
                             hipStream_t s) {
     const uint64_t nblk = (len + kRsG - 1) / kRsG;
     if (nblk) {
-        rs_block_sums_kernel<<<(uint32_t)((nblk + 255) / 256), 256, 0, s>>>(data, len, nblk, px,
-                                                                            pt);
+        rs_block_sums_kernel<<<(uint32_t)((nblk + 3) / 4), 256, 0, s>>>(data, len, nblk, px, pt);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -240,45 +261,121 @@ __device__ __forceinline__ void emit(const RsScanArgs &a, uint64_t o, uint32_t s
     }
 }
 
+// Candidates are collected per workgroup in LDS and appended to the global
+// list with one atomic per workgroup: a single global counter bumped once per
+// candidate serialises millions of same-address atomics.
+constexpr uint32_t kScanThreads = 128;
+constexpr uint32_t kLocCand = 1024;
+
 // lane per strip of kRsStrip offsets in [0, nfull): full windows of blength bytes
-__global__ void rs_scan_kernel(RsScanArgs a) {
+__global__ __launch_bounds__(kScanThreads) void rs_scan_kernel(RsScanArgs a) {
+    __shared__ uint64_t loc_off[kLocCand];
+    __shared__ uint32_t loc_sum[kLocCand];
+    __shared__ uint32_t loc_n;
+    __shared__ unsigned long long loc_base;
+    if (threadIdx.x == 0) loc_n = 0;
+    __syncthreads();
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t o0 = k * kRsStrip;
-    if (o0 >= a.nfull) return;
-    const uint64_t o1 = min(o0 + kRsStrip, a.nfull);
-    const uint64_t n = a.blength;
-    // window sum at o0 from the coarse prefixes (o0 is a multiple of kRsG)
-    uint32_t xa, ta, xb, tb;
-    prefix_at(a, o0, xa, ta);
-    prefix_at(a, o0 + n, xb, tb);
-    uint32_t s1 = xb - xa;
-    uint32_t s2 = (uint32_t)(n + o0) * s1 - (tb - ta);
-    const uint8_t *d = a.data;
-    const uint32_t nn = (uint32_t)n;
-    for (uint64_t o = o0; o < o1; o += 16) {
-        uint32_t wo[4], wi[4];
-        load16(d, o, a.len, wo);       // bytes leaving: o .. o+15
-        load16(d, o + n, a.len, wi);   // bytes entering: o+n .. o+n+15
-        uint32_t sums[16];
+    if (o0 < a.nfull) {
+        const uint64_t o1 = min(o0 + kRsStrip, a.nfull);
+        const uint64_t n = a.blength;
+        // window sum at o0 from the coarse prefixes (o0 is a multiple of kRsG)
+        uint32_t xa, ta, xb, tb;
+        prefix_at(a, o0, xa, ta);
+        prefix_at(a, o0 + n, xb, tb);
+        uint32_t s1 = xb - xa;
+        uint32_t s2 = (uint32_t)(n + o0) * s1 - (tb - ta);
+        const uint8_t *d = a.data;
+        const uint32_t nn = (uint32_t)n;
+        uint64_t o = o0;
+        if (o1 + n + 32 <= a.len) {
+            // interior strip: unconditional 32-byte loads, the next group's
+            // prefetched while this one's 32 filter gathers are in flight
+            uint4 po0 = gload16(d + o), po1 = gload16(d + o + 16);
+            uint4 pi0 = gload16(d + o + n), pi1 = gload16(d + o + n + 16);
+            for (; o < o1; o += 32) {
+                const uint32_t wo[8] = {po0.x, po0.y, po0.z, po0.w, po1.x, po1.y, po1.z, po1.w};
+                const uint32_t wi[8] = {pi0.x, pi0.y, pi0.z, pi0.w, pi1.x, pi1.y, pi1.z, pi1.w};
+                po0 = gload16(d + o + 32);
+                po1 = gload16(d + o + 48);
+                pi0 = gload16(d + o + n + 32);
+                pi1 = gload16(d + o + n + 48);
+                uint32_t sums[32];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            sums[j] = (s1 & 0xffffu) | (s2 << 16);
-            const uint32_t xo = (uint32_t)__builtin_amdgcn_sbfe(wo[j >> 2], 8 * (j & 3), 8);
-            const uint32_t xi = (uint32_t)__builtin_amdgcn_sbfe(wi[j >> 2], 8 * (j & 3), 8);
-            // hash_search's roll: s1 -= out; s2 -= k*out; s1 += in; s2 += s1
-            s1 = s1 - xo + xi;
-            s2 = s2 - nn * xo + s1;
-        }
-        uint32_t hit = 0;
+                for (int j = 0; j < 32; ++j) {
+                    sums[j] = (s1 & 0xffffu) | (s2 << 16);
+                    const uint32_t xo = (uint32_t)__builtin_amdgcn_sbfe(wo[j >> 2], 8 * (j & 3), 8);
+                    const uint32_t xi = (uint32_t)__builtin_amdgcn_sbfe(wi[j >> 2], 8 * (j & 3), 8);
+                    s1 = s1 - xo + xi;
+                    s2 = s2 - nn * xo + s1;
+                }
+                uint32_t hit = 0;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const uint32_t f = sums[j] >> (32 - a.fbits);
-            hit |= ((a.filt[f >> 5] >> (f & 31)) & 1u) << j;
+                for (int j = 0; j < 32; ++j) {
+                    const uint32_t f = sums[j] >> (32 - a.fbits);
+                    hit |= ((a.filt[f >> 5] >> (f & 31)) & 1u) << j;
+                }
+                while (hit) {
+                    const int j = __builtin_ctz(hit);
+                    hit &= hit - 1;
+                    if (o + j < o1 && probe(a, sums[j], true)) {
+                        const uint32_t slot = atomicAdd(&loc_n, 1u);
+                        if (slot < kLocCand) {
+                            loc_off[slot] = o + j;
+                            loc_sum[slot] = sums[j];
+                        } else {
+                            emit(a, o + j, sums[j]);
+                        }
+                    }
+                }
+            }
         }
-        while (hit) {
-            const int j = __builtin_ctz(hit);
-            hit &= hit - 1;
-            if (o + j < o1 && probe(a, sums[j], true)) emit(a, o + j, sums[j]);
+        for (; o < o1; o += 16) {
+            uint32_t wo[4], wi[4];
+            load16(d, o, a.len, wo);       // bytes leaving: o .. o+15
+            load16(d, o + n, a.len, wi);   // bytes entering: o+n .. o+n+15
+            uint32_t sums[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                sums[j] = (s1 & 0xffffu) | (s2 << 16);
+                const uint32_t xo = (uint32_t)__builtin_amdgcn_sbfe(wo[j >> 2], 8 * (j & 3), 8);
+                const uint32_t xi = (uint32_t)__builtin_amdgcn_sbfe(wi[j >> 2], 8 * (j & 3), 8);
+                // hash_search's roll: s1 -= out; s2 -= k*out; s1 += in; s2 += s1
+                s1 = s1 - xo + xi;
+                s2 = s2 - nn * xo + s1;
+            }
+            uint32_t hit = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t f = sums[j] >> (32 - a.fbits);
+                hit |= ((a.filt[f >> 5] >> (f & 31)) & 1u) << j;
+            }
+            while (hit) {
+                const int j = __builtin_ctz(hit);
+                hit &= hit - 1;
+                if (o + j < o1 && probe(a, sums[j], true)) {
+                    const uint32_t slot = atomicAdd(&loc_n, 1u);
+                    if (slot < kLocCand) {
+                        loc_off[slot] = o + j;
+                        loc_sum[slot] = sums[j];
+                    } else {
+                        emit(a, o + j, sums[j]);  // local buffer full
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t m = min(loc_n, kLocCand);
+    if (m == 0) return;
+    if (threadIdx.x == 0) loc_base = atomicAdd((unsigned long long *)a.n_cand, (unsigned long long)m);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+        const unsigned long long slot = loc_base + i;
+        if (slot < a.cap) {
+            a.cand_off[slot] = loc_off[i];
+            a.cand_sum[slot] = loc_sum[i];
         }
     }
 }
@@ -291,7 +388,9 @@ __global__ void rs_scan_tail_kernel(RsScanArgs a, uint64_t o) {
 
 hipError_t launch_rs_scan(const RsScanArgs &a, hipStream_t s) {
     const uint64_t strips = (a.nfull + kRsStrip - 1) / kRsStrip;
-    if (strips) rs_scan_kernel<<<(uint32_t)((strips + 127) / 128), 128, 0, s>>>(a);
+    if (strips)
+        rs_scan_kernel<<<(uint32_t)((strips + kScanThreads - 1) / kScanThreads), kScanThreads, 0,
+                         s>>>(a);
     if (a.remainder && a.count && a.len >= a.remainder)
         rs_scan_tail_kernel<<<1, 1, 0, s>>>(a, a.len - a.remainder);
     return hipGetLastError();

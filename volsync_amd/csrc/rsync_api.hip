@@ -19,6 +19,9 @@
 #include <cstring>
 #include <vector>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "internal.hpp"
 
 #define VS_API extern "C" __attribute__((visibility("default")))
@@ -123,7 +126,7 @@ int build_table(vs_rsync *h) {
     const uint32_t count = (uint32_t)h->count;
     h->dbits = std::min<uint32_t>(std::max<uint32_t>(ceil_log2(std::max<uint32_t>(count, 1)) + 1, 4),
                                   26);
-    h->fbits = std::min<uint32_t>(std::max<uint32_t>(ceil_log2(std::max<uint32_t>(count, 1)) + 3, 10),
+    h->fbits = std::min<uint32_t>(std::max<uint32_t>(ceil_log2(std::max<uint32_t>(count, 1)) + 5, 10),
                                   28);
     const size_t n = std::max<uint32_t>(count, 1);
     VS_TRY(h->d_keys.ensure(n * 8));
@@ -286,6 +289,11 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
     VS_HIP(launch_rs_prefix((const uint8_t *)dev_src, (uint64_t)len, h->px.as<uint32_t>(),
                             h->pt.as<uint32_t>(), h->pxs.as<uint32_t>(), h->pts.as<uint32_t>(),
                             h->partials.as<uint32_t>(), h->stream));
+    static const bool trace = getenv("VSGPU_RS_TRACE") != nullptr;
+    if (trace) {
+        VS_HIP(hipStreamSynchronize(h->stream));
+        fprintf(stderr, "rs: prefix %.1f ms\n", now_ms() - t0);
+    }
     // 2. weak scan (re-run once with an exact capacity on overflow)
     RsScanArgs a{};
     a.data = (const uint8_t *)dev_src;
@@ -317,6 +325,8 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
         VS_HIP(hipMemcpyAsync(h->pinned, h->n_cand.p, 8, hipMemcpyDeviceToHost, h->stream));
         VS_HIP(hipStreamSynchronize(h->stream));
         nc = h->pinned[0];
+        if (trace) fprintf(stderr, "rs: scan done %.1f ms (%llu candidates)\n", now_ms() - t0,
+                           (unsigned long long)nc);
         if (nc <= cap) break;
         cap = nc;
         if (attempt == 1) return fail(VS_ERR_STATE, "candidate buffer overflow");
@@ -338,6 +348,7 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
     }
     h->st_cand = (int64_t)nc;
     const double t1 = now_ms();
+    if (trace) fprintf(stderr, "rs: sorted + copied %.1f ms\n", t1 - t0);
     h->ms[2] = t1 - t0;
     // 4. round 0: chained candidates (another candidate one block length away)
     std::vector<uint8_t> known(nc, 0), strong(nc * (size_t)h->s2length);
