@@ -26,7 +26,7 @@ int fail(int code, const std::string &msg) {
     return code;
 }
 
-// strip = 64 * G with G % 3 == 0 and G < 256 (fingerprint.hip rotates three
+// strip = 64 * G with G even and G < 256 (fingerprint.hip alternates two
 // 64-byte group buffers and notes groups by 8-bit index)
 constexpr uint32_t kStrip = 12288;
 

@@ -33,9 +33,19 @@ namespace vsgpu {
 constexpr uint32_t kTabEntries = 256 * kFpCopies;  // u64 entries per table
 constexpr uint32_t kOut8Byte = kTabEntries * 8;    // byte offset of OUT8 in LDS (0x10000)
 static_assert(kOut8Byte == 0x10000, "roll() builds OUT8 addresses with v_perm");
-constexpr uint32_t kUnit = 128;                    // strips per work unit: 2 per lane
+#ifndef VS_FP_CHAINS
+#define VS_FP_CHAINS 2
+#endif
+constexpr int kChains = VS_FP_CHAINS;             // strips per lane
+constexpr uint32_t kUnit = 64 * kChains;          // strips per work unit
 
-typedef uint32_t G16[16];  // one 64-byte group as 16 little-endian words
+#ifndef VS_FP_GROUP
+#define VS_FP_GROUP 16
+#endif
+constexpr int kGW = VS_FP_GROUP;      // words per group buffer (16: 64 B, 32: 128 B = one line)
+constexpr int kGB = 4 * kGW;          // bytes per group
+typedef uint32_t G16[16];  // one 64-byte group as 16 little-endian words (warm-up, process_group)
+typedef uint32_t GBuf[kGW];
 
 template <bool GUARD>
 __device__ __forceinline__ uint4 load16(const uint8_t *data, int64_t off, uint64_t dlen) {
@@ -128,6 +138,62 @@ __device__ __forceinline__ void process_group(uint32_t (&hi)[CH], uint32_t (&lo)
                 m[c] = __builtin_elementwise_min(m[c], cut_bits<WIDE>(hi[c], lo[c], mlo, mhi));
             }
         }
+    }
+}
+
+// process_group with the next group streamed into `old` as it is consumed:
+// once quarter q of the evicted bytes has been rolled past, its four words are
+// refilled with quarter q of the group after `nw` (at byte offset nxt[c]).
+// Two 64-byte buffers per strip then hold the evicted bytes, the incoming
+// bytes and the prefetch.
+template <int CH, bool GUARD, bool WIDE>
+__device__ __forceinline__ void process_group_pf(uint32_t (&hi)[CH], uint32_t (&lo)[CH],
+                                                 GBuf (&old)[CH], const GBuf (&nw)[CH],
+                                                 uint32_t (&m)[CH], uint32_t lane8, uint32_t sh,
+                                                 const char *lds, const FpArgs &a,
+                                                 const int64_t (&nxt)[CH]) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) m[c] = 0xffffffffu;
+#pragma unroll
+    for (int q = 0; q < kGW / 4; ++q) {
+#pragma unroll
+        for (int w = 4 * q; w < 4 * q + 4; ++w) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int c = 0; c < CH; ++c) {
+                    switch (j) {
+                        case 0: roll<0>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
+                        case 1: roll<1>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
+                        case 2: roll<2>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
+                        default: roll<3>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
+                    }
+                    m[c] = __builtin_elementwise_min(
+                        m[c], cut_bits<WIDE>(hi[c], lo[c], a.mask_lo, a.mask_hi));
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const uint4 v = load16<GUARD>(a.data, nxt[c] + 16 * q, a.dlen);
+            old[c][4 * q + 0] = v.x;
+            old[c][4 * q + 1] = v.y;
+            old[c][4 * q + 2] = v.z;
+            old[c][4 * q + 3] = v.w;
+        }
+    }
+}
+
+template <bool GUARD>
+__device__ __forceinline__ void load_buf(GBuf &g, const uint8_t *data, int64_t off,
+                                         uint64_t dlen) {
+#pragma unroll
+    for (int q = 0; q < kGW / 4; ++q) {
+        const uint4 v = load16<GUARD>(data, off + 16 * q, dlen);
+        g[4 * q + 0] = v.x;
+        g[4 * q + 1] = v.y;
+        g[4 * q + 2] = v.z;
+        g[4 * q + 3] = v.w;
     }
 }
 
@@ -224,49 +290,49 @@ template <int CH, bool GUARD, bool WIDE>
 __device__ __forceinline__ void run_strips(const FpArgs &a, const char *lds, uint32_t lane8,
                                            const uint64_t (&kk)[CH], const bool (&valid)[CH]) {
     const uint32_t sh = a.idx_shift;
-    const uint32_t G = a.strip / 64;  // groups per strip, a multiple of 3 (and < 256)
+    const uint32_t G = a.strip / kGB;  // groups per strip, even (and < 256)
     int64_t sb[CH];  // strip base (data offset)
     uint32_t hi[CH], lo[CH], m[CH], notes[CH];
-    G16 X[CH], Y[CH], Z[CH];
+    GBuf A[CH], B[CH];  // evicted / incoming bytes; the evicted buffer refills with the next group
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
         sb[c] = (int64_t)(a.base + kk[c] * a.strip);
-        load_group<GUARD>(X[c], a.data, sb[c] - 64, a.dlen);  // warm-up bytes
-        load_group<GUARD>(Y[c], a.data, sb[c], a.dlen);       // group 0
+        load_buf<GUARD>(A[c], a.data, sb[c] - kGB, a.dlen);  // warm-up bytes (last 64 used)
+        load_buf<GUARD>(B[c], a.data, sb[c], a.dlen);        // group 0
         hi[c] = 0;
         lo[c] = 0;
         notes[c] = 0;
     }
-    // warm-up: the window starts as 64 virtual zero bytes, digest 0
+    // warm-up over the 64 bytes before the strip: the window starts as 64
+    // virtual zero bytes, digest 0 (with 128-byte groups the first 64 bytes of
+    // A are never used)
 #pragma unroll
-    for (int w = 0; w < 16; ++w) {
+    for (int w = kGW - 16; w < kGW; ++w) {
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
-            roll_warm<0>(hi[c], lo[c], X[c][w], lane8, sh, lds);
-            roll_warm<1>(hi[c], lo[c], X[c][w], lane8, sh, lds);
-            roll_warm<2>(hi[c], lo[c], X[c][w], lane8, sh, lds);
-            roll_warm<3>(hi[c], lo[c], X[c][w], lane8, sh, lds);
+            roll_warm<0>(hi[c], lo[c], A[c][w], lane8, sh, lds);
+            roll_warm<1>(hi[c], lo[c], A[c][w], lane8, sh, lds);
+            roll_warm<2>(hi[c], lo[c], A[c][w], lane8, sh, lds);
+            roll_warm<3>(hi[c], lo[c], A[c][w], lane8, sh, lds);
         }
     }
 
-    // group GI: evicted bytes in OLD (group GI-1), incoming in NEW; NEXT <- GI+1
-#define VS_GROUP(OLD, NEW, NEXT, GI)                                                      \
+    // group GI: evicted bytes in OLD (group GI-1, refilled with GI+1 as it is
+    // consumed; the last group reloads itself), incoming in NEW
+#define VS_GROUP(OLD, NEW, GI)                                                            \
     {                                                                                     \
-        {   /* unconditional (the last group reloads itself): no phi copies */          \
-            const int64_t gn_ = 64 * (int64_t)min((GI) + 1, G - 1);                        \
-            _Pragma("unroll") for (int c = 0; c < CH; ++c)                                \
-                load_group<GUARD>(NEXT[c], a.data, sb[c] + gn_, a.dlen);                  \
-        }                                                                                 \
-        process_group<CH, WIDE>(hi, lo, OLD, NEW, m, lane8, sh, lds, a.mask_lo, a.mask_hi); \
+        int64_t nx_[CH];                                                                  \
+        _Pragma("unroll") for (int c = 0; c < CH; ++c)                                    \
+            nx_[c] = sb[c] + kGB * (int64_t)min((GI) + 1, G - 1);                          \
+        process_group_pf<CH, GUARD, WIDE>(hi, lo, OLD, NEW, m, lane8, sh, lds, a, nx_);   \
         _Pragma("unroll") for (int c = 0; c < CH; ++c) {                                  \
             if (m[c] == 0) notes[c] = note_group(notes[c], (GI));                         \
         }                                                                                 \
     }
 
-    for (uint32_t g = 0; g < G; g += 3) {
-        VS_GROUP(X, Y, Z, g)
-        VS_GROUP(Y, Z, X, g + 1)
-        VS_GROUP(Z, X, Y, g + 2)
+    for (uint32_t g = 0; g < G; g += 2) {
+        VS_GROUP(A, B, g)
+        VS_GROUP(B, A, g + 1)
     }
 #undef VS_GROUP
 
@@ -279,8 +345,8 @@ __device__ __forceinline__ void run_strips(const FpArgs &a, const char *lds, uin
             rescan<GUARD, WIDE>(a, r, sb[c], sb[c] + a.strip, lane8, lds, (uint64_t)sb[c]);
         } else {
             for (uint32_t i = 0; i < n; ++i) {
-                const int64_t g0 = sb[c] + 64 * (int64_t)((notes[c] >> (8 * i)) & 0xff);
-                rescan<GUARD, WIDE>(a, r, g0, g0 + 64, lane8, lds, (uint64_t)sb[c]);
+                const int64_t g0 = sb[c] + kGB * (int64_t)((notes[c] >> (8 * i)) & 0xff);
+                rescan<GUARD, WIDE>(a, r, g0, g0 + kGB, lane8, lds, (uint64_t)sb[c]);
             }
         }
         a.counts[r.k] = r.cnt;
@@ -312,17 +378,22 @@ __global__ __launch_bounds__(kFpThreads) void fp_kernel(FpArgs a) {
             run_strips<1, true, WIDE>(a, lds, lane8, kk, vv);
         }
     }
-    // interior strips: units of 128 strips, two chains per lane
+    // interior strips: units of 64 * kChains strips, kChains per lane
     for (;;) {
         uint32_t u = 0;
         if (lane == 0) u = atomicAdd(a.work, 1u);
         u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
         const uint64_t k0 = a.k_lo + (uint64_t)u * kUnit;
         if (k0 >= a.k_hi) break;
-        const uint64_t kA = k0 + lane, kB = k0 + 64 + lane;
-        const uint64_t kk[2] = {kA < a.k_hi ? kA : k0, kB < a.k_hi ? kB : k0};
-        const bool vv[2] = {kA < a.k_hi, kB < a.k_hi};
-        run_strips<2, false, WIDE>(a, lds, lane8, kk, vv);
+        uint64_t kk[kChains];
+        bool vv[kChains];
+#pragma unroll
+        for (int c = 0; c < kChains; ++c) {
+            const uint64_t k = k0 + 64 * c + lane;
+            vv[c] = k < a.k_hi;
+            kk[c] = vv[c] ? k : k0;
+        }
+        run_strips<kChains, false, WIDE>(a, lds, lane8, kk, vv);
     }
 }
 

@@ -66,7 +66,10 @@ void pol_tables(uint64_t pol, uint64_t out_tab[256], uint64_t mod_tab[256]);
 void pol_out8(uint64_t pol, const uint64_t out_tab[256], uint64_t out8[256]);
 
 // ---- fingerprint pass ------------------------------------------------------
-constexpr int kFpThreads = 768;    // one 12-wave workgroup per CU (LDS: 128 KiB tables; 168 VGPRs)
+#ifndef VS_FP_THREADS
+#define VS_FP_THREADS 768
+#endif
+constexpr int kFpThreads = VS_FP_THREADS;  // one workgroup per CU (LDS: 128 KiB tables)
 constexpr int kFpCopies = 32;      // lane-private table copies: conflict-free ds_read_b64
 constexpr int kSlots = 3;          // candidate offsets kept per strip (dense strips: bitmask)
 constexpr uint32_t kNoSlot = 0xffffffffu;
