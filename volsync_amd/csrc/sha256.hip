@@ -137,7 +137,7 @@ __device__ __forceinline__ void message(uint32_t (&w)[16], const uint32_t (&d)[1
     }
 }
 
-// Producer: W[t] + K[t] for t = 0..63 into the LDS slot (word group q of
+// Producer: W[t] for t = 0..63 into the LDS slot (word group q of
 // lane l at uint4 index q*64 + l: conflict-free ds_write_b128 / ds_read_b128).
 __device__ __forceinline__ void schedule_to_lds(uint32_t (&w)[16], uint4 *slot, uint32_t lane) {
 #pragma unroll
@@ -155,7 +155,7 @@ __device__ __forceinline__ void schedule_to_lds(uint32_t (&w)[16], uint4 *slot, 
                 const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
                 wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
             }
-            o[i] = wt + kK256[t];
+            o[i] = wt;
         }
         slot[q * 64 + lane] = make_uint4(o[0], o[1], o[2], o[3]);
     }
@@ -178,14 +178,16 @@ __device__ __forceinline__ void compress_lds(uint32_t (&st)[8], const uint4 *slo
     for (int q = 0; q < 16; q += 2) {
         const uint4 v = slot[q * 64 + lane];
         const uint4 u = slot[(q + 1) * 64 + lane];
-        VS_SHA_ROUND(a, b, c, d, e, f, g, h, v.x)
-        VS_SHA_ROUND(h, a, b, c, d, e, f, g, v.y)
-        VS_SHA_ROUND(g, h, a, b, c, d, e, f, v.z)
-        VS_SHA_ROUND(f, g, h, a, b, c, d, e, v.w)
-        VS_SHA_ROUND(e, f, g, h, a, b, c, d, u.x)
-        VS_SHA_ROUND(d, e, f, g, h, a, b, c, u.y)
-        VS_SHA_ROUND(c, d, e, f, g, h, a, b, u.z)
-        VS_SHA_ROUND(b, c, d, e, f, g, h, a, u.w)
+        // + K[t] here rather than in the producer: a scalar operand of the
+        // v_add3 the round needs anyway
+        VS_SHA_ROUND(a, b, c, d, e, f, g, h, v.x + kK256[4 * q + 0])
+        VS_SHA_ROUND(h, a, b, c, d, e, f, g, v.y + kK256[4 * q + 1])
+        VS_SHA_ROUND(g, h, a, b, c, d, e, f, v.z + kK256[4 * q + 2])
+        VS_SHA_ROUND(f, g, h, a, b, c, d, e, v.w + kK256[4 * q + 3])
+        VS_SHA_ROUND(e, f, g, h, a, b, c, d, u.x + kK256[4 * q + 4])
+        VS_SHA_ROUND(d, e, f, g, h, a, b, c, u.y + kK256[4 * q + 5])
+        VS_SHA_ROUND(c, d, e, f, g, h, a, b, u.z + kK256[4 * q + 6])
+        VS_SHA_ROUND(b, c, d, e, f, g, h, a, u.w + kK256[4 * q + 7])
     }
     st[0] += a;
     st[1] += b;
@@ -203,7 +205,7 @@ __device__ __forceinline__ void compress_lds(uint32_t (&st)[8], const uint4 *slo
 // each wave = chain l of the tile) and step through the same block loop, one
 // workgroup barrier per block.
 __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
-    __shared__ uint4 wk[2][16 * 64];  // 2 x 16 KiB: W+K of one block of 64 chains
+    __shared__ uint4 wk[2][16 * 64];  // 2 x 16 KiB: W of one block of 64 chains
     __shared__ uint32_t tile_sh;
     const uint32_t lane = threadIdx.x & 63;
     const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;  // wave-uniform
