@@ -195,6 +195,147 @@ def rsync_main(args):
         dist.destroy_process_group()
 
 
+def smallfiles_cpu_baseline(sizes, sample_files: int, threads: int):
+    """Go crypto/sha256 stand-in: OpenSSL SHA-256 via hashlib (which releases
+    the GIL), one blob per file over `threads` threads, on the first
+    `sample_files` files of the same size distribution (synthetic bytes)."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
+    sz = sizes[:sample_files]
+    raw = np.random.default_rng(7).integers(0, 256, int(sz.max()), dtype=np.uint8).tobytes()
+    mv = memoryview(raw)
+
+    def work(lo_hi):
+        lo, hi = lo_hi
+        for k in range(lo, hi):
+            hashlib.sha256(mv[: int(sz[k])]).digest()
+    parts = [(i * len(sz) // threads, (i + 1) * len(sz) // threads) for i in range(threads)]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(work, parts))
+    dt = time.perf_counter() - t0
+    return {"value": round(float(sz.sum()) / dt / 1e9, 3), "unit": "GB/s", "cores": threads,
+            "kind": "port", "sample": f"{len(sz)} files ({float(sz.sum()) / 2**30:.2f} GiB) of the "
+            f"C5 size distribution, hashlib/OpenSSL SHA-256 on {threads} threads",
+            "cpu": _cpu_model()}
+
+
+def smallfiles_main(args):
+    """C5: 1 M files of 4-64 KiB (seed 6) drawn from 500 K distinct payloads
+    (dedup-heavy), packed contiguously in HBM with an offsets array.  Every file
+    is below MinSize, so restic makes exactly one chunk per file and its blob ID
+    is SHA-256 of the whole file.  A step = the blob IDs
+    of all files (vs_sha256_run_device) + the SaveBlob dedup count (unique IDs).
+    value = file bytes hashed per second.  Files are split evenly over ranks
+    (replicas of the same shape; no collective)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from volsync_amd import DeviceSha256, synth_fill_device
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    nf, npay = args.files, max(1, args.files // 2)
+    rng = np.random.default_rng(6 + rank)
+    psize = rng.integers(4096, 65537, npay)
+    pick = rng.integers(0, npay, nf)
+    sizes = psize[pick]
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    total = int(sizes.sum())
+    # payload j = synthetic stream (seed 6) at j * 64 KiB; files gathered into
+    # one packed buffer in 1 GiB pieces
+    pool = torch.empty(npay << 16, dtype=torch.uint8, device=dev)
+    synth_fill_device(pool.data_ptr(), 6, 0, npay << 16, device=local)
+    packed = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    src = torch.from_numpy((pick.astype(np.int64) << 16)).to(dev)
+    szd = torch.from_numpy(sizes.astype(np.int64)).to(dev)
+    ofd = torch.from_numpy(offs).to(dev)
+    f0 = 0
+    while f0 < nf:
+        f1 = int(np.searchsorted(offs, offs[f0] + (1 << 30), side="left"))
+        f1 = max(f1, f0 + 1)
+        s_, z_, o_ = src[f0:f1], szd[f0:f1], ofd[f0:f1]
+        nbytes = int(z_.sum().item())
+        rel = torch.arange(nbytes, device=dev) - torch.repeat_interleave(o_ - o_[0], z_, output_size=nbytes)
+        idx = torch.repeat_interleave(s_, z_, output_size=nbytes) + rel
+        packed[int(offs[f0]):int(offs[f0]) + nbytes] = pool[idx]
+        del rel, idx
+        f0 = f1
+    del pool, src, szd
+    torch.cuda.empty_cache()
+    lens = torch.from_numpy(sizes.astype(np.int32)).to(dev)
+    ids = torch.zeros((nf, 32), dtype=torch.uint8, device=dev)
+    sh = DeviceSha256(local)
+    sh.set_wide(args.hash_wide, args.wide_drain)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        sh.run(packed.data_ptr(), ofd.data_ptr(), lens.data_ptr(), nf, ids.data_ptr(), stream)
+        return torch.unique(ids[:, :8].contiguous().view(torch.int64)).numel()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    # spot check against hashlib (first files of every distinct size class)
+    import hashlib
+    host = ids[:64].cpu().numpy()
+    for i in range(64):
+        o, n = int(offs[i]), int(sizes[i])
+        assert bytes(host[i]) == hashlib.sha256(packed[o:o + n].cpu().numpy().tobytes()).digest()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    uniq = 0
+    for _ in range(args.steps):
+        uniq = step()
+    ev1.record()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    # kernel time: the hash launches ran on `stream` between the two events
+    # (unique() included: an upper bound on the hash time)
+    k_ms = ev0.elapsed_time(ev1) / args.steps
+    gbs = total / k_ms / 1e6
+    if rank == 0:
+        out = {
+            "metric": "GB/s SHA-256 blob IDs (restic, C5 small files)",
+            "value": round(total * world * args.steps / dt / 1e9, 2), "unit": "GB/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (splitmix64 payloads, device-resident, packed)",
+            "config": {"workload": f"C5: {nf} files of 4-64 KiB from {npay} payloads"
+                                   f"{' per rank' if world > 1 else ''}",
+                       "bytes": total, "unique_ids": uniq,
+                       "parallelism": f"replicas x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "valu_frac": round(gbs * SHA_OPS_PER_BYTE / 1e3 / VALU_PEAK_TOPS, 4),
+                         "kernel": "sha256 (hash engine, unbounded slice)"},
+            "hash_wide": args.hash_wide,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = smallfiles_cpu_baseline(sizes, 200000, args.cpu_threads)
+        print(json.dumps(out), flush=True)
+    sh.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -209,11 +350,20 @@ def main():
                          "fingerprint pass) or serialised on the main stream")
     ap.add_argument("--hash-slice", type=int, default=1024,
                     help="SHA-256 blocks per chunk per step (time-sliced engine; 0 = unbounded)")
-    ap.add_argument("--mode", choices=["cdc", "rsync"], default="cdc",
-                    help="cdc: C2/C3 chunk+hash (the BASELINE metric); rsync: C4-shape delta match")
+    ap.add_argument("--hash-wide", type=lambda x: int(x, 0), default=0,
+                    help="active chains from which the SHA-256 engine runs whole-SHA "
+                         "wavefronts (0 = library default, 0xffffffff = never)")
+    ap.add_argument("--wide-drain", type=int, default=0,
+                    help="blocks per throughput-mode drain launch (0 = library default)")
+    ap.add_argument("--mode", choices=["cdc", "rsync", "smallfiles"], default="cdc",
+                    help="cdc: C2/C3 chunk+hash (the BASELINE metric); rsync: C4-shape delta "
+                         "match; smallfiles: C5 per-file blob IDs")
+    ap.add_argument("--files", type=int, default=1_000_000, help="smallfiles: files per GPU")
     args = ap.parse_args()
     if args.mode == "rsync":
         return rsync_main(args)
+    if args.mode == "smallfiles":
+        return smallfiles_main(args)
 
     import torch
     import torch.distributed as dist
@@ -239,6 +389,7 @@ def main():
 
     dc = DeviceChunker(TestPol, MinSize, MaxSize, 20, device=local)
     dc.set_hash_slice(args.hash_slice)
+    dc.set_hash_wide(args.hash_wide, args.wide_drain)
     if args.hash_stream == "main":
         # hash slices queue behind the fingerprint pass on one stream
         one = torch.cuda.Stream(dev)
@@ -355,6 +506,7 @@ def main():
             "kernels": roof,
             "hash_slice_blocks": args.hash_slice,
             "hash_stream": args.hash_stream,
+            "hash_wide": args.hash_wide, "wide_drain": args.wide_drain,
             "sha_slices": launches[2],
             "single_volume": {"ms": round(lat * 1e3, 2),
                               "GBps": round(total / lat / 1e9, 2),

@@ -115,6 +115,14 @@ int vs_cdc_set_hash_stream(vs_cdc *h, void *hip_stream);
  * hashes the rest.  0 = unbounded (every batch hashed to the end in one
  * launch).  Default 1024 (64 KiB per chunk per batch). */
 int vs_cdc_set_hash_slice(vs_cdc *h, uint32_t blocks);
+/* Throughput mode of the SHA-256 engine: once at least
+ * min_chains chunks are being hashed, each wavefront hashes 64 chunks whole
+ * instead of the producer/consumer split, and a drain advances them by
+ * drain_blocks per launch until fewer than min_chains remain.  Results are
+ * identical in both modes.  min_chains 0 = the handle's default (never for
+ * vs_cdc, whose long chunks make the tail; 384 per CU for vs_sha), 0xffffffff
+ * = never; drain_blocks 0 = default (4096). */
+int vs_cdc_set_hash_wide(vs_cdc *h, uint32_t min_chains, uint32_t drain_blocks);
 /* Pipelined batches: batch numbers count vs_cdc_finish calls from 0; the ring
  * keeps the last *ring batches' chunk lists.  Data passed to vs_cdc_scan must
  * stay valid until its batch's blob IDs are final (vs_cdc_wait). */
@@ -153,6 +161,8 @@ typedef struct vs_sha vs_sha;
 int vs_sha256_open(int device, vs_sha **h);
 int vs_sha256_run_device(vs_sha *h, const void *dev_buf, const uint64_t *dev_off,
                          const uint32_t *dev_len, size_t n, uint8_t *dev_out, void *hip_stream);
+/* Same knob as vs_cdc_set_hash_wide for a vs_sha handle. */
+int vs_sha256_set_wide(vs_sha *h, uint32_t min_chains, uint32_t drain_blocks);
 void vs_sha256_close(vs_sha *h);
 /* Host-memory convenience form (copies in and out). */
 int vs_sha256_batch(int device, const void *buf, size_t buf_len, const uint64_t *off,

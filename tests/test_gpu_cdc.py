@@ -284,3 +284,57 @@ def test_pipelined_batches(gpu, budget):
                for c in dc.batch_chunks(first + i, 0, counts[i])]
         assert got == O.cdc_hash(datas[i], P.TEST_POL, mn, mx, ab)
     dc.close()
+
+
+@pytest.mark.parametrize("min_chains,drain", [(1, 3), (1, 0), (40, 2)])
+def test_wide_mode_pipelined(gpu, min_chains, drain):
+    """Throughput mode of the SHA-256 engine (whole-SHA wavefronts): forced on
+    from `min_chains` active chunks, with drains of `drain` blocks per launch
+    and a split-mode finish below the threshold; pipelined batches under
+    budgeted slices of 5 blocks.  Blob IDs must equal the oracle's."""
+    from volsync_amd import DeviceChunker
+    mn, mx, ab = 16384, 1 << 18, 15
+    dc = DeviceChunker(P.TEST_POL, mn, mx, ab)
+    dc.set_hash_slice(5)
+    dc.set_hash_wide(min_chains, drain)
+    datas, bufs, counts = [], [], []
+    first, ring = dc.batches()
+    for i in range(5):
+        data = O.synth(190 + i, 0, (3 << 20) + 1213 * i)
+        t = to_dev(data)
+        n, consumed = dc.process(t.data_ptr(), len(data), 0, True)
+        datas.append(data)
+        bufs.append(t)
+        counts.append(n)
+    dc.wait()
+    done, ring = dc.batches()
+    for i in range(max(0, 5 - ring), 5):
+        got = [(c.Start, c.Length, c.Cut, c.ID.hex())
+               for c in dc.batch_chunks(first + i, 0, counts[i])]
+        assert got == O.cdc_hash(datas[i], P.TEST_POL, mn, mx, ab)
+    dc.close()
+
+
+@pytest.mark.parametrize("drain", [1, 2, 4096])
+def test_wide_mode_blobs_vs_hashlib(gpu, drain):
+    """Throughput mode over blobs of every length 0..200 at every alignment
+    (padding in one or two blocks, misaligned starts) plus 4-64 KiB files."""
+    import torch
+    from volsync_amd import DeviceSha256
+    rng = np.random.default_rng(11)
+    buf = O.synth(71, 0, 2 << 20)
+    lens = list(range(0, 201)) + [int(x) for x in rng.integers(4096, 65537, 300)]
+    offs = [int(rng.integers(0, len(buf) - n)) for n in lens]
+    d = to_dev(buf)
+    do = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    dl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    out = torch.zeros((len(lens), 32), dtype=torch.uint8, device="cuda")
+    sh = DeviceSha256()
+    sh.set_wide(1, drain)
+    sh.run(d.data_ptr(), do.data_ptr(), dl.data_ptr(), len(lens), out.data_ptr())
+    torch.cuda.synchronize()
+    sh.close()
+    got = out.cpu().numpy()
+    raw = buf.tobytes()
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        assert bytes(got[i]) == hashlib.sha256(raw[o:o + n]).digest(), (i, o, n)

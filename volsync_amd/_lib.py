@@ -92,6 +92,7 @@ def _load() -> ctypes.CDLL:
         "vs_cdc_set_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_slice": (c_int, [vp, c_u32]),
+        "vs_cdc_set_hash_wide": (c_int, [vp, c_u32, c_u32]),
         "vs_cdc_batches": (c_int, [vp, u64p, u64p]),
         "vs_cdc_get_batch_chunks": (c_int, [vp, c_u64, c_u64, c_u64, ctypes.POINTER(VsChunk)]),
         "vs_cdc_scan": (c_int, [vp, vp, c_u64, c_u64, c_u64, c_u64, c_int]),
@@ -104,6 +105,7 @@ def _load() -> ctypes.CDLL:
         "vs_sha256_open": (c_int, [c_int, ctypes.POINTER(vp)]),
         "vs_sha256_run_device": (c_int, [vp, vp, vp, vp, c_size, vp, vp]),
         "vs_sha256_close": (None, [vp]),
+        "vs_sha256_set_wide": (c_int, [vp, c_u32, c_u32]),
         "vs_sha256_batch": (c_int, [c_int, vp, c_size, vp, vp, c_size, vp]),
         "vs_synth_fill_device": (c_int, [c_int, c_u64, c_u64, c_u64, vp, vp]),
         "vs_rsync_sizes": (c_int, [i64, i32, i32p, i32p, i32p, i32p]),

@@ -206,6 +206,11 @@ class DeviceChunker:
         """Blocks per chunk per batch of the time-sliced SHA-256 engine (0 = unbounded)."""
         check(lib.vs_cdc_set_hash_slice(self._h, int(blocks)))
 
+    def set_hash_wide(self, min_chains: int = 0, drain_blocks: int = 0) -> None:
+        """Throughput mode of the SHA-256 engine from min_chains active chunks
+        (0 = default, 0xffffffff = never); drain_blocks per drain launch."""
+        check(lib.vs_cdc_set_hash_wide(self._h, int(min_chains), int(drain_blocks)))
+
     def batches(self):
         """(batches finished so far, batches the ring keeps)."""
         f = ctypes.c_uint64(0)
@@ -303,6 +308,10 @@ class DeviceSha256:
         check(lib.vs_sha256_run_device(self._h, ctypes.c_void_p(dev_buf), ctypes.c_void_p(dev_off),
                                        ctypes.c_void_p(dev_len), n, ctypes.c_void_p(dev_out),
                                        ctypes.c_void_p(stream or None)))
+
+    def set_wide(self, min_chains: int = 0, drain_blocks: int = 0) -> None:
+        """Throughput mode from min_chains active blobs (0 = default, 0xffffffff = never)."""
+        check(lib.vs_sha256_set_wide(self._h, int(min_chains), int(drain_blocks)))
 
     def close(self) -> None:
         if self._h:

@@ -810,6 +810,18 @@ VS_API int vs_cdc_set_hash_slice(vs_cdc *h, uint32_t blocks) {
     return size_ring(h);
 }
 
+static void set_wide(ShaEngine &e, uint32_t min_chains, uint32_t drain_blocks) {
+    e.wide_min = min_chains ? min_chains : e.wide_default;
+    e.wide_budget = drain_blocks ? drain_blocks : 4096;
+}
+
+VS_API int vs_cdc_set_hash_wide(vs_cdc *h, uint32_t min_chains, uint32_t drain_blocks) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    VS_TRY(cdc_wait(h));
+    set_wide(h->sha, min_chains, drain_blocks);
+    return 0;
+}
+
 VS_API int vs_cdc_get_batch_chunks(vs_cdc *h, uint64_t batch, uint64_t first, uint64_t n,
                                    vs_chunk *out) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
@@ -877,7 +889,13 @@ VS_API int vs_sha256_open(int device, vs_sha **out) {
     VS_HIP(hipSetDevice(device));
     vs_sha *h = new vs_sha();
     h->device = device;
-    if (h->eng.init(device) < 0 ||
+    // many independent blobs (C5): throughput mode from 384 active blobs per
+    // CU (split mode saturates at 5 x 64 per CU).  vs_cdc
+    // handles keep split mode: their long chunks' latency is the tail.
+    const bool ok = h->eng.init(device) == 0;
+    h->eng.wide_default = (uint32_t)std::max(h->eng.cus, 1) * 384;
+    h->eng.wide_min = h->eng.wide_default;
+    if (!ok ||
         hipEventCreateWithFlags(&h->done, hipEventDisableTiming) != hipSuccess) {
         std::string msg = g_err;
         vs_sha256_close(h);
@@ -909,6 +927,13 @@ VS_API int vs_sha256_run_device(vs_sha *h, const void *dev_buf, const uint64_t *
     VS_HIP(hipSetDevice(h->device));
     return sha_run(h, (const uint8_t *)dev_buf, dev_off, dev_len, n, dev_out,
                    (hipStream_t)hip_stream);
+}
+
+VS_API int vs_sha256_set_wide(vs_sha *h, uint32_t min_chains, uint32_t drain_blocks) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    if (h->ran) VS_HIP(hipEventSynchronize(h->done));
+    set_wide(h->eng, min_chains, drain_blocks);
+    return 0;
 }
 
 VS_API void vs_sha256_close(vs_sha *h) {

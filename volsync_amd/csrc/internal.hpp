@@ -179,7 +179,14 @@ struct ShaEngine {
     uint64_t cap = 0;  // chains per list
     uint64_t ub = 0;   // upper bound on the active chains
     std::vector<Group> groups;
+    // throughput mode (sha_slice_wide_kernel) once this many chains are active;
+    // a drain advances them by wide_budget blocks per slice until fewer remain
+    uint32_t wide_min = 0xffffffffu;  // never, unless the handle sets it
+    uint32_t wide_default = 0xffffffffu;
+    uint32_t wide_budget = 4096;
+    uint32_t *live_h = nullptr;  // pinned: active-chain count read back during a drain
     int init(int dev);
+    int launch(uint32_t budget, bool wide, hipStream_t s);
     void release();
     uint32_t *count(int which);
     int reserve(uint64_t n_new, hipStream_t s);

@@ -200,6 +200,37 @@ __device__ __forceinline__ void compress_lds(uint32_t (&st)[8], const uint4 *slo
 }
 #undef VS_SHA_ROUND
 
+// End of a chain's turn in a slice: write the digest of a finished chain, or
+// append the midstate of an unfinished one to the next active list
+// (wave-aggregated: one atomic per wave).
+__device__ __forceinline__ void retire(const ShaSliceArgs &a, const ShaChain &ch0,
+                                       const uint32_t (&st)[8], bool valid, uint32_t mine,
+                                       uint32_t left, uint32_t lane) {
+    const bool finished = valid && mine == left;
+    const bool survive = valid && !finished;
+    if (finished) {
+        uint4 *out = (uint4 *)ch0.out;
+        out[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]),
+                            __builtin_bswap32(st[2]), __builtin_bswap32(st[3]));
+        out[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]),
+                            __builtin_bswap32(st[6]), __builtin_bswap32(st[7]));
+    }
+    const uint64_t bal = __ballot(survive);
+    if (bal) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(a.n_next, (uint32_t)__popcll(bal));
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (survive) {
+            const uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+            ShaChain nc = ch0;
+            nc.ptr = ch0.ptr + 64ull * mine;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) nc.st[i] = st[i];
+            a.next[pos] = nc;
+        }
+    }
+}
+
 // One slice over the active chains.  Workgroup = 2 waves:
 // wave 0 produces, wave 1 consumes; both hold the same 64 chains (lane l of
 // each wave = chain l of the tile) and step through the same block loop, one
@@ -295,31 +326,131 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
                 if (j < mine) compress_lds(st, wk[j & 1], lane);
                 __syncthreads();
             }
-            const bool finished = valid && mine == left;
-            const bool survive = valid && !finished;
-            if (finished) {
-                uint4 *out = (uint4 *)ch0.out;
-                out[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]),
-                                    __builtin_bswap32(st[2]), __builtin_bswap32(st[3]));
-                out[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]),
-                                    __builtin_bswap32(st[6]), __builtin_bswap32(st[7]));
-            }
-            // survivors: wave-aggregated append to the next active list
-            const uint64_t bal = __ballot(survive);
-            if (bal) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(a.n_next, (uint32_t)__popcll(bal));
-                base = __builtin_amdgcn_readfirstlane(base);
-                if (survive) {
-                    const uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
-                    ShaChain nc = ch0;
-                    nc.ptr = ch0.ptr + 64ull * mine;
+            retire(a, ch0, st, valid, mine, left, lane);
+        }
+    }
+}
+
+// Throughput mode: with enough active chains to give every
+// SIMD several waves, a chain's latency no longer matters and the split's
+// LDS round trip and barrier only cost throughput.  Each wave then owns a tile
+// of 64 chains and does everything itself: the same cooperative segment loads
+// as the producer (staged through a wave-private LDS area), message expansion
+// in a rolling 16-word register window, and the 64 rounds.
+__device__ __forceinline__ void compress_regs(uint32_t (&st)[8], uint32_t (&w)[16]) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+    uint32_t e = st[4], f = st[5], g = st[6], h = st[7];
+#define VS_SHA_ROUND(a, b, c, d, e, f, g, h, wk)                                   \
+    {                                                                              \
+        const uint32_t t1_ = h + xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)) +       \
+                             ch(e, f, g) + (wk);                                   \
+        const uint32_t t2_ = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)) + maj(a, b, c); \
+        d += t1_;                                                                  \
+        h = t1_ + t2_;                                                             \
+    }
+#define VS_W(t)                                                                              \
+    ((t) < 16 ? w[(t)&15]                                                                    \
+              : (w[(t)&15] = w[(t)&15] +                                                     \
+                             xor3(rotr(w[((t)-15) & 15], 7), rotr(w[((t)-15) & 15], 18),    \
+                                  w[((t)-15) & 15] >> 3) +                                   \
+                             w[((t)-7) & 15] +                                               \
+                             xor3(rotr(w[((t)-2) & 15], 17), rotr(w[((t)-2) & 15], 19),     \
+                                  w[((t)-2) & 15] >> 10)))
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) nc.st[i] = st[i];
-                    a.next[pos] = nc;
-                }
+    for (int t = 0; t < 64; t += 8) {
+        VS_SHA_ROUND(a, b, c, d, e, f, g, h, VS_W(t + 0) + kK256[t + 0])
+        VS_SHA_ROUND(h, a, b, c, d, e, f, g, VS_W(t + 1) + kK256[t + 1])
+        VS_SHA_ROUND(g, h, a, b, c, d, e, f, VS_W(t + 2) + kK256[t + 2])
+        VS_SHA_ROUND(f, g, h, a, b, c, d, e, VS_W(t + 3) + kK256[t + 3])
+        VS_SHA_ROUND(e, f, g, h, a, b, c, d, VS_W(t + 4) + kK256[t + 4])
+        VS_SHA_ROUND(d, e, f, g, h, a, b, c, VS_W(t + 5) + kK256[t + 5])
+        VS_SHA_ROUND(c, d, e, f, g, h, a, b, VS_W(t + 6) + kK256[t + 6])
+        VS_SHA_ROUND(b, c, d, e, f, g, h, a, VS_W(t + 7) + kK256[t + 7])
+    }
+#undef VS_W
+#undef VS_SHA_ROUND
+    st[0] += a;
+    st[1] += b;
+    st[2] += c;
+    st[3] += d;
+    st[4] += e;
+    st[5] += f;
+    st[6] += g;
+    st[7] += h;
+}
+
+// Cross-lane exchange through a wave-private LDS area: the LDS unit executes
+// one wave's ds_write / ds_read in issue order, so only compiler reordering
+// must be prevented.  (A wave-scope fence would also wait for the in-flight
+// prefetch loads -- vmcnt(0) -- and serialise every block on HBM latency.)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+constexpr int kWideWaves = 4;  // waves per workgroup, each independent
+__global__ __launch_bounds__(64 * kWideWaves, 3) void sha_slice_wide_kernel(ShaSliceArgs a) {
+    __shared__ uint4 stage_all[kWideWaves][5 * 64];  // 5 KiB per wave
+    const uint32_t lane = threadIdx.x & 63;
+    uint4 *stage = stage_all[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+    const uint32_t n = *a.n_cur;
+    const uint32_t ntiles = (n + 63) / 64;
+    for (;;) {
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(a.tile_ctr, 1u);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (t >= ntiles) break;
+        const uint32_t idx = t * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t ci = valid ? (a.order ? a.order[idx] : idx) : 0u;
+        const ShaChain ch0 = a.cur[ci];
+        const uint32_t left = valid ? blocks_left(ch0.ptr, ch0.end) : 0u;
+        const uint32_t mine = min(left, a.budget);
+        uint32_t steps = mine;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, o, 64));
+        steps = __builtin_amdgcn_readfirstlane(steps);
+        if (steps == 0) continue;
+        const uint64_t p = ch0.ptr, e = ch0.end, L = ch0.len;
+        const uint64_t A = p & ~15ull;
+        const uint64_t safe = L ? ((e - 1) & ~15ull) : ((uint64_t)(uintptr_t)ch0.out & ~15ull);
+        const uint32_t q = (uint32_t)(p & 15) >> 2;
+        uint64_t LA[4], LE[4], LS[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int src = 16 * i + (int)(lane >> 2);
+            LA[i] = (uint64_t)__shfl((long long)A, src, 64);
+            LE[i] = (uint64_t)__shfl((long long)e, src, 64);
+            LS[i] = (uint64_t)__shfl((long long)safe, src, 64);
+        }
+        const uint64_t so = 16 + 16 * (lane & 3);
+        const uint32_t wr = 5 * (lane >> 2) + (lane & 3);
+        uint32_t st[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st[i] = ch0.st[i];
+        uint4 R[4], c = load_seg(A, e, safe), S[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + so, LE[i], LS[i]);
+        for (uint32_t j = 0; j < steps; ++j) {
+            // block j's segments arrived during block j-1; fetch block j+1's now
+#pragma unroll
+            for (int i = 0; i < 4; ++i) stage[80 * i + wr] = R[i];
+            const uint64_t nb = 64ull * (j + 1) + so;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + nb, LE[i], LS[i]);
+            wave_lds_sync();
+#pragma unroll
+            for (int k = 0; k < 4; ++k) S[k] = stage[5 * lane + k];
+            wave_lds_sync();
+            uint32_t d[17], w[16];
+            window_words(d, c, S, q);
+            c = S[3];
+            if (j < mine) {
+                message(w, d, p + 64ull * j, e, L);
+                compress_regs(st, w);
             }
         }
+        retire(a, ch0, st, valid, mine, left, lane);
     }
 }
 
@@ -373,18 +504,45 @@ __device__ __forceinline__ uint32_t sha_key(const ShaChain &c, uint32_t budget) 
     return kShaBuckets - 1 - min(f, kShaBuckets - 1);
 }
 
-__global__ void sha_hist_kernel(const ShaChain *list, const uint32_t *n_cur, uint32_t budget,
-                                uint32_t *hist) {
+// Budgeted slices put most chains in one bucket (remaining >= budget), so both
+// kernels aggregate their atomics: the histogram in LDS per workgroup, the
+// scatter per run of equal keys within a wave (one atomic per distinct key).
+__global__ __launch_bounds__(256) void sha_hist_kernel(const ShaChain *list, const uint32_t *n_cur,
+                                                       uint32_t budget, uint32_t *hist) {
+    __shared__ uint32_t h[kShaBuckets];
+    for (uint32_t i = threadIdx.x; i < kShaBuckets; i += blockDim.x) h[i] = 0;
+    __syncthreads();
     const uint32_t n = *n_cur;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        atomicAdd(&hist[sha_key(list[i], budget)], 1u);
+        atomicAdd(&h[sha_key(list[i], budget)], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kShaBuckets; i += blockDim.x)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
-__global__ void sha_scatter_kernel(const ShaChain *list, const uint32_t *n_cur, uint32_t budget,
-                                   uint32_t *cursor, uint32_t *order) {
+__global__ __launch_bounds__(256) void sha_scatter_kernel(const ShaChain *list,
+                                                          const uint32_t *n_cur, uint32_t budget,
+                                                          uint32_t *cursor, uint32_t *order) {
     const uint32_t n = *n_cur;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        order[atomicAdd(&cursor[sha_key(list[i], budget)], 1u)] = i;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    // whole waves iterate together (ballots below)
+    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += stride) {
+        const uint32_t i = base + lane;
+        const bool valid = i < n;
+        const uint32_t key = valid ? sha_key(list[i], budget) : 0xffffffffu;
+        uint64_t todo = __ballot(valid);
+        while (todo) {
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)todo) - 1;
+            const uint32_t k = (uint32_t)__shfl((int)key, (int)leader, 64);
+            const uint64_t grp = __ballot(valid && key == k);
+            uint32_t pos = 0;
+            if (lane == leader) pos = atomicAdd(&cursor[k], (uint32_t)__popcll(grp));
+            pos = (uint32_t)__shfl((int)pos, (int)leader, 64);
+            if (valid && key == k) order[pos + (uint32_t)__popcll(grp & ((1ull << lane) - 1))] = i;
+            todo &= ~grp;
+        }
+    }
 }
 
 // ---- ShaEngine (host) ------------------------------------------------------------
@@ -394,6 +552,7 @@ int ShaEngine::init(int dev) {
     VS_TRY(hist.ensure((2 * kShaBuckets + 16) * 4));
     VS_HIP(hipMemset(ctl.p, 0, 64));
     VS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (!live_h) VS_HIP(hipHostMalloc((void **)&live_h, 4, hipHostMallocDefault));
     return 0;
 }
 
@@ -402,6 +561,8 @@ void ShaEngine::release() {
     groups.clear();
     ub = 0;
     cap = 0;
+    if (live_h) (void)hipHostFree(live_h);
+    live_h = nullptr;
 }
 
 uint32_t *ShaEngine::count(int which) { return ctl.as<uint32_t>() + which; }
@@ -455,15 +616,39 @@ int ShaEngine::append_blobs(const uint8_t *data, const uint64_t *off, const uint
     return 0;
 }
 
-// advance every active chain by up to `budget` blocks (0xffffffff: to the end)
+// advance every active chain by up to `budget` blocks (0xffffffff: to the end).
+// A drain reads the exact count back between throughput-mode
+// slices and finishes the last wide_min chains in split (latency) mode, so the
+// longest chains' tail runs at the split's per-chain speed.
 int ShaEngine::slice(uint32_t budget, hipStream_t s) {
     if (ub == 0) return 0;
+    // budgeted slices run beside the next volume's fingerprint pass: split
+    // mode leaves that pass room (throughput mode measured slower there)
+    if (budget != 0xffffffffu) return launch(budget, false, s);
+    while (ub >= wide_min) {
+        VS_HIP(hipMemcpyAsync(live_h, count(cur), 4, hipMemcpyDeviceToHost, s));
+        VS_HIP(hipStreamSynchronize(s));
+        const uint32_t live = *live_h;
+        if (live == 0) {
+            groups.clear();
+            ub = 0;
+            return 0;
+        }
+        if (live < wide_min) break;
+        VS_TRY(launch(std::max(wide_budget, 1u), true, s));
+    }
+    return launch(budget, false, s);
+}
+
+int ShaEngine::launch(uint32_t budget, bool wide, hipStream_t s) {
+    if (ub == 0) return 0;  // every chain finished within the previous budgets
     const int nxt = cur ^ 1;
     uint32_t *cursor = hist.as<uint32_t>() + kShaBuckets;
     uint32_t *partials = cursor + kShaBuckets + 1;
     VS_HIP(hipMemsetAsync(hist.p, 0, kShaBuckets * 4, s));
     const uint32_t sb = (uint32_t)std::min<uint64_t>((ub + 255) / 256, 4096);
-    sha_hist_kernel<<<sb, 256, 0, s>>>(list[cur].as<ShaChain>(), count(cur), budget,
+    const uint32_t hb = std::min<uint32_t>(sb, (uint32_t)std::max(cus, 1) * 2);
+    sha_hist_kernel<<<hb, 256, 0, s>>>(list[cur].as<ShaChain>(), count(cur), budget,
                                        hist.as<uint32_t>());
     VS_HIP(launch_scan_u32(hist.as<uint32_t>(), cursor, kShaBuckets, partials, 0xffffffffu, s));
     sha_scatter_kernel<<<sb, 256, 0, s>>>(list[cur].as<ShaChain>(), count(cur), budget, cursor,
@@ -479,10 +664,17 @@ int ShaEngine::slice(uint32_t budget, hipStream_t s) {
     a.n_next = count(nxt);
     a.tile_ctr = count(2);
     a.budget = budget;
-    // persistent grid: LDS (32 KiB per workgroup) admits 5 workgroups per CU
     const uint64_t tiles = (ub + 63) / 64;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)std::max(cus, 1) * 5);
-    sha_slice_kernel<<<grid, 128, 0, s>>>(a);
+    if (wide) {
+        // persistent grid: 3 waves per SIMD (launch bounds: <= 168 VGPRs)
+        const uint64_t slots = (uint64_t)std::max(cus, 1) * 4 * 3 / kWideWaves;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWideWaves - 1) / kWideWaves, slots);
+        sha_slice_wide_kernel<<<grid, 64 * kWideWaves, 0, s>>>(a);
+    } else {
+        // persistent grid: LDS (32 KiB per workgroup) admits 5 workgroups per CU
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)std::max(cus, 1) * 5);
+        sha_slice_kernel<<<grid, 128, 0, s>>>(a);
+    }
     VS_HIP(hipGetLastError());
     cur = nxt;
     // chains of a group finish within ceil(max_blocks / budget) slices
