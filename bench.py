@@ -26,9 +26,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
-VALU_PEAK_TOPS = 78.6        # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 ops/s
-SHA_OPS_PER_BYTE = 1384 / 64  # DESIGN.md 3.3 (per 64-byte block)
-FP_OPS_PER_BYTE = 8.5
+# Integer VALU issue peak, measured (tools/valu/valu_peak.hip ->
+# profiles/r01_valu_peak): the three-operand VOP3 instructions SHA-256 and the
+# fingerprint are made of (v_alignbit, v_bitop3, v_add3, v_perm, v_lshl_or)
+# issue once per ~4.2 cycles per SIMD however many waves share it (two-operand
+# VOP2 such as v_xor: ~2.8).  256 CU x 4 SIMD x 64 lanes x 2.4 GHz / 4.2:
+VALU_PEAK_TOPS = 256 * 4 * 64 * 2.4e9 / 4.2 / 1e12   # 37.4 T lane-ops/s
+# VALU lane-instructions per input byte, from SQ_INSTS_VALU (wave-instructions)
+# x 64 / bytes in profiles/r01_final: SHA-256 ~1490 per 64-byte block, the
+# fingerprint ~8.8 per byte
+SHA_OPS_PER_BYTE = 1490 / 64
+FP_OPS_PER_BYTE = 8.8
 
 
 def cpu_baseline(sample_bytes: int, threads: int):
@@ -348,7 +356,7 @@ def main():
     ap.add_argument("--hash-stream", choices=["own", "main"], default="own",
                     help="SHA-256 slices on the handle's own hash stream (overlapping the next "
                          "fingerprint pass) or serialised on the main stream")
-    ap.add_argument("--hash-slice", type=int, default=1024,
+    ap.add_argument("--hash-slice", type=int, default=512,
                     help="SHA-256 blocks per chunk per step (time-sliced engine; 0 = unbounded)")
     ap.add_argument("--hash-wide", type=lambda x: int(x, 0), default=0,
                     help="active chains from which the SHA-256 engine runs whole-SHA "
@@ -457,6 +465,10 @@ def main():
     fp_gbs = own_bytes / fp_ms / 1e6 if fp_ms else 0.0
     sha_gbs = own_bytes / sha_ms / 1e6 if sha_ms else 0.0
     iso = {s: round(iso_ms[i], 3) for i, s in enumerate(stages)}
+    # per-launch averages over the timed region, comparable with the
+    # rocprofv3 kernel trace of the same command (profiles/r01_final)
+    avg_launch = {s: round(ms[i] / launches[i], 3) if launches[i] else None
+                  for i, s in enumerate(stages)}
     roof = {
         "fingerprint": {"bound": "hbm", "achieved": round(fp_gbs, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(fp_gbs / HBM_PEAK_GBS, 4),
@@ -477,6 +489,10 @@ def main():
                 roof[k]["traffic_source"] = tj["source"]
     except (OSError, ValueError, KeyError):
         pass
+    roof["fingerprint"]["avg_launch_ms"] = avg_launch["fingerprint"]
+    roof["fingerprint"]["launches"] = launches[0]
+    roof["sha256"]["avg_launch_ms"] = avg_launch["sha256"]
+    roof["sha256"]["launches"] = launches[2]
     dom_name = "sha256" if per_step["sha256"] >= per_step["fingerprint"] else "fingerprint"
     roofline = dict(roof[dom_name])
     roofline["kernel"] = dom_name
@@ -504,6 +520,10 @@ def main():
             "roofline": roofline,
             "stages_ms_per_step": {k: round(v, 3) for k, v in per_step.items()},
             "kernels": roof,
+            # the whole step shares one resource: VALU issue (fingerprint +
+            # SHA-256 lane-ops over the step time, against the measured peak)
+            "pipeline_valu_frac": round(total * args.steps / dt * (SHA_OPS_PER_BYTE + FP_OPS_PER_BYTE)
+                                        / world / 1e12 / VALU_PEAK_TOPS, 4),
             "hash_slice_blocks": args.hash_slice,
             "hash_stream": args.hash_stream,
             "hash_wide": args.hash_wide, "wide_drain": args.wide_drain,

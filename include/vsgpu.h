@@ -113,7 +113,7 @@ int vs_cdc_set_hash_stream(vs_cdc *h, void *hip_stream);
  * advances every queued chunk by at most `blocks` 64-byte blocks and carries
  * the midstate of unfinished chunks to the next batch's launch; vs_cdc_wait
  * hashes the rest.  0 = unbounded (every batch hashed to the end in one
- * launch).  Default 1024 (64 KiB per chunk per batch). */
+ * launch).  Default 512 (32 KiB per chunk per batch). */
 int vs_cdc_set_hash_slice(vs_cdc *h, uint32_t blocks);
 /* Throughput mode of the SHA-256 engine: once at least
  * min_chains chunks are being hashed, each wavefront hashes 64 chunks whole
@@ -148,7 +148,8 @@ int vs_cdc_process(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t origi
 int vs_cdc_get_chunks(vs_cdc *h, uint64_t first, uint64_t n, vs_chunk *out);
 /* Accumulated device time (ms) per pipeline stage since the last reset of the
  * timers, measured with HIP events on the handle's stream when enabled.
- * stage: 0 fingerprint, 1 select, 2 sha256, 3 other. */
+ * stage: 0 fingerprint, 1 select, 2 sha256 (the hash kernels alone; their
+ * histogram / scan / scatter bookkeeping launches are not timed), 3 other. */
 int vs_cdc_timing(vs_cdc *h, int enable, double ms_out[4], uint64_t launches_out[4]);
 
 /* ---- batched SHA-256 (restic.Hash over many blobs; C5 small files) ----

@@ -10,7 +10,7 @@ import argparse
 import json
 import os
 
-KERNELS = {"fingerprint": "fp_kernel<false>", "sha256": "sha_slice_kernel"}
+KERNELS = {"fingerprint": "fp_kernel<2>", "sha256": "sha_slice_kernel"}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("prof")

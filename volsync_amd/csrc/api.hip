@@ -78,7 +78,7 @@ struct vs_cdc {
     DevBuf n_out;
     // SHA-256: time-sliced engine on its own stream (hstream)
     ShaEngine sha;
-    uint32_t hash_budget = 1024;  // blocks per chain per slice (0xffffffff: unbounded)
+    uint32_t hash_budget = 512;   // blocks per chain per slice (0xffffffff: unbounded)
     uint32_t chain_slices = 1;    // slices that finish any chain: ceil(max blocks / budget)
     uint64_t slices = 0;          // slices launched
     static constexpr int kSliceEv = 64;
@@ -179,6 +179,16 @@ static int sync_stream(vs_cdc *h, bool all = false) {
     return 0;
 }
 
+// VSGPU_FP_FAST=0 selects the generic fingerprint variant even where the
+// FAST one applies (A/B measurements; results are identical)
+static bool fast_fp_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("VSGPU_FP_FAST");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // one slice of the hash engine on the hash stream, followed by its event.
 // Flow control: before slice i reuses event slot i % kSliceEv the host waits
 // for slice i - kSliceEv, so "c + kSliceEv <= slices" implies slice c is done.
@@ -191,10 +201,15 @@ static int run_slice(vs_cdc *h, uint32_t budget) {
     } else if (i > (uint64_t)vs_cdc::kSliceEv) {
         VS_HIP(hipEventSynchronize(e));
     }
-    {
-        StageTimer t(h, kStSha, h->hstream);
-        VS_TRY(h->sha.slice(budget, h->hstream));
-    }
+    // stage "sha256" = the hash kernels alone, bracketed inside the engine
+    // (comparable with a rocprofv3 kernel trace); its bookkeeping launches
+    // (histogram, scan, scatter) are not timed
+    if (h->timing) h->sha.ev_get = [h] { return get_event(h); };
+    const int rc = h->sha.slice(budget, h->hstream);
+    h->sha.ev_get = nullptr;
+    for (auto &p : h->sha.kernel_pairs) h->pend.push_back({kStSha, p.first, p.second});
+    h->sha.kernel_pairs.clear();
+    VS_TRY(rc);
     VS_HIP(hipEventRecord(e, h->hstream));
     h->slices = i;
     if (budget == 0xffffffffu)
@@ -343,7 +358,8 @@ static int run_scan_kernels(vs_cdc *h) {
         a.k_hi = k_hi;
         a.n_edge = k_lo + (h->nstrips - k_hi);
         a.work = h->flags.as<uint32_t>() + 3;  // zeroed with the flags above
-        VS_HIP(launch_fingerprint(a, wide, h->cus, h->stream));
+        const bool fast = !wide && h->idx_shift >= 8 && fast_fp_enabled();
+        VS_HIP(launch_fingerprint(a, wide, fast, h->cus, h->stream));
     }
     {
         StageTimer t(h, kStSel);

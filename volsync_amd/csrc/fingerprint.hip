@@ -78,15 +78,18 @@ __device__ __forceinline__ uint64_t lds_u64(const char *lds, uint32_t byte_addr)
 
 // One byte of the rolling window.  oldw/neww hold the evicted / incoming byte
 // in byte lane J.
-template <int J>
+template <int J, bool FAST = false>
 __device__ __forceinline__ void roll(uint32_t &hi, uint32_t &lo, uint32_t oldw, uint32_t neww,
                                      uint32_t lane8, uint32_t sh, const char *lds) {
     const uint32_t lane8o = lane8 | kOut8Byte;
     // lane8o = lane*8 | 0x10000 (OUT8 base): one v_perm builds
     // [lane*8, b_old, 0x01, 0x00] = 0x10000 + b_old*256 + lane*8
     const uint32_t oaddr = __builtin_amdgcn_perm(lane8o, oldw, 0x0c060004u | (J << 8));
-    const uint32_t idx = __builtin_amdgcn_ubfe(hi, sh, 8);
-    const uint32_t maddr = (idx << 8) | lane8;
+    // MOD address idx*256 + lane*8.  FAST (deg >= 48, sh >= 8): a two-operand
+    // shift (half the issue cost of a three-operand VOP3) and one v_and_or
+    // instead of v_bfe + v_lshl_or
+    const uint32_t maddr = FAST ? (((hi >> (sh - 8)) & 0xff00u) | lane8)
+                                : ((__builtin_amdgcn_ubfe(hi, sh, 8) << 8) | lane8);
     const uint64_t ov = lds_u64(lds, oaddr);
     const uint64_t mv = lds_u64(lds, maddr);
     const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 24);            // hi<<8 | lo>>24
@@ -106,6 +109,10 @@ __device__ __forceinline__ void roll_warm(uint32_t &hi, uint32_t &lo, uint32_t n
     hi = nhi ^ (uint32_t)(mv >> 32);
     lo = nlo ^ (uint32_t)mv;
 }
+
+// kernel variants: mask within the low digest word / wider than 32 bits /
+// FAST = low word and deg >= 48 (the restic default): cheaper MOD address
+constexpr int kFpNarrow = 0, kFpWide = 1, kFpFast = 2;
 
 template <bool WIDE>
 __device__ __forceinline__ uint32_t cut_bits(uint32_t hi, uint32_t lo, uint32_t mlo,
@@ -146,7 +153,7 @@ __device__ __forceinline__ void process_group(uint32_t (&hi)[CH], uint32_t (&lo)
 // refilled with quarter q of the group after `nw` (at byte offset nxt[c]).
 // Two 64-byte buffers per strip then hold the evicted bytes, the incoming
 // bytes and the prefetch.
-template <int CH, bool GUARD, bool WIDE>
+template <int CH, bool GUARD, int MODE>
 __device__ __forceinline__ void process_group_pf(uint32_t (&hi)[CH], uint32_t (&lo)[CH],
                                                  GBuf (&old)[CH], const GBuf (&nw)[CH],
                                                  uint32_t (&m)[CH], uint32_t lane8, uint32_t sh,
@@ -162,14 +169,17 @@ __device__ __forceinline__ void process_group_pf(uint32_t (&hi)[CH], uint32_t (&
             for (int j = 0; j < 4; ++j) {
 #pragma unroll
                 for (int c = 0; c < CH; ++c) {
+                    constexpr bool F = MODE == kFpFast;
                     switch (j) {
-                        case 0: roll<0>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
-                        case 1: roll<1>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
-                        case 2: roll<2>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
-                        default: roll<3>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
+                        case 0: roll<0, F>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
+                        case 1: roll<1, F>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
+                        case 2: roll<2, F>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
+                        default: roll<3, F>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
                     }
+                    // (a v_min_u16 prefilter on the low 16 digest bits measured
+                    // slower: 27.8 vs 22.8 ms per 64 GiB)
                     m[c] = __builtin_elementwise_min(
-                        m[c], cut_bits<WIDE>(hi[c], lo[c], a.mask_lo, a.mask_hi));
+                        m[c], cut_bits<MODE == kFpWide>(hi[c], lo[c], a.mask_lo, a.mask_hi));
                 }
             }
         }
@@ -286,7 +296,7 @@ __device__ __forceinline__ uint32_t note_group(uint32_t notes, uint32_t g) {
 
 // CH strips per lane, byte-interleaved.  kk[c]: strip indices; valid[c] false
 // for a padding chain (it computes but records nothing).
-template <int CH, bool GUARD, bool WIDE>
+template <int CH, bool GUARD, int MODE>
 __device__ __forceinline__ void run_strips(const FpArgs &a, const char *lds, uint32_t lane8,
                                            const uint64_t (&kk)[CH], const bool (&valid)[CH]) {
     const uint32_t sh = a.idx_shift;
@@ -324,7 +334,7 @@ __device__ __forceinline__ void run_strips(const FpArgs &a, const char *lds, uin
         int64_t nx_[CH];                                                                  \
         _Pragma("unroll") for (int c = 0; c < CH; ++c)                                    \
             nx_[c] = sb[c] + kGB * (int64_t)min((GI) + 1, G - 1);                          \
-        process_group_pf<CH, GUARD, WIDE>(hi, lo, OLD, NEW, m, lane8, sh, lds, a, nx_);   \
+        process_group_pf<CH, GUARD, MODE>(hi, lo, OLD, NEW, m, lane8, sh, lds, a, nx_);     \
         _Pragma("unroll") for (int c = 0; c < CH; ++c) {                                  \
             if (m[c] == 0) notes[c] = note_group(notes[c], (GI));                         \
         }                                                                                 \
@@ -342,11 +352,11 @@ __device__ __forceinline__ void run_strips(const FpArgs &a, const char *lds, uin
         StripRec r{kk[c], 0, kNoSlot};
         const uint32_t n = notes[c] >> 24;
         if (notes[c] == kNoteAll) {
-            rescan<GUARD, WIDE>(a, r, sb[c], sb[c] + a.strip, lane8, lds, (uint64_t)sb[c]);
+            rescan<GUARD, MODE == kFpWide>(a, r, sb[c], sb[c] + a.strip, lane8, lds, (uint64_t)sb[c]);
         } else {
             for (uint32_t i = 0; i < n; ++i) {
                 const int64_t g0 = sb[c] + kGB * (int64_t)((notes[c] >> (8 * i)) & 0xff);
-                rescan<GUARD, WIDE>(a, r, g0, g0 + kGB, lane8, lds, (uint64_t)sb[c]);
+                rescan<GUARD, MODE == kFpWide>(a, r, g0, g0 + kGB, lane8, lds, (uint64_t)sb[c]);
             }
         }
         a.counts[r.k] = r.cnt;
@@ -354,7 +364,7 @@ __device__ __forceinline__ void run_strips(const FpArgs &a, const char *lds, uin
     }
 }
 
-template <bool WIDE>
+template <int MODE>
 __global__ __launch_bounds__(kFpThreads) void fp_kernel(FpArgs a) {
     __shared__ __attribute__((aligned(16))) uint64_t tabs[2 * kTabEntries];  // 128 KiB
     for (uint32_t i = threadIdx.x; i < kTabEntries; i += blockDim.x) {
@@ -375,7 +385,7 @@ __global__ __launch_bounds__(kFpThreads) void fp_kernel(FpArgs a) {
             const uint64_t ee = v ? e : 0;
             const uint64_t kk[1] = {ee < a.k_lo ? ee : a.k_hi + (ee - a.k_lo)};
             const bool vv[1] = {v};
-            run_strips<1, true, WIDE>(a, lds, lane8, kk, vv);
+            run_strips<1, true, MODE>(a, lds, lane8, kk, vv);
         }
     }
     // interior strips: units of 64 * kChains strips, kChains per lane
@@ -393,19 +403,21 @@ __global__ __launch_bounds__(kFpThreads) void fp_kernel(FpArgs a) {
             vv[c] = k < a.k_hi;
             kk[c] = vv[c] ? k : k0;
         }
-        run_strips<kChains, false, WIDE>(a, lds, lane8, kk, vv);
+        run_strips<kChains, false, MODE>(a, lds, lane8, kk, vv);
     }
 }
 
-hipError_t launch_fingerprint(const FpArgs &a, bool wide, int cus, hipStream_t s) {
+hipError_t launch_fingerprint(const FpArgs &a, bool wide, bool fast, int cus, hipStream_t s) {
     const uint64_t units = (a.k_hi - a.k_lo + kUnit - 1) / kUnit;
     if (units == 0 && a.n_edge == 0) return hipSuccess;
     const uint64_t grid =
         std::max<uint64_t>(1, std::min<uint64_t>(units, (uint64_t)std::max(cus, 1)));
     if (wide)
-        fp_kernel<true><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
+        fp_kernel<kFpWide><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
+    else if (fast)
+        fp_kernel<kFpFast><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
     else
-        fp_kernel<false><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
+        fp_kernel<kFpNarrow><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 

@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <algorithm>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/vsgpu.h"
@@ -100,7 +101,8 @@ struct FpArgs {
     const uint64_t *mod_tab;   // [256]
     const uint64_t *out8_tab;  // [256]
 };
-hipError_t launch_fingerprint(const FpArgs &a, bool wide_mask, int cus, hipStream_t s);
+// fast: the FAST variant (idx_shift >= 8, i.e. deg >= 48)
+hipError_t launch_fingerprint(const FpArgs &a, bool wide_mask, bool fast, int cus, hipStream_t s);
 
 // ---- selection -------------------------------------------------------------
 constexpr uint64_t kPosMask = (1ull << 62) - 1;
@@ -185,6 +187,10 @@ struct ShaEngine {
     uint32_t wide_default = 0xffffffffu;
     uint32_t wide_budget = 4096;
     uint32_t *live_h = nullptr;  // pinned: active-chain count read back during a drain
+    // optional timing of the hash kernels alone (no bookkeeping launches):
+    // when ev_get is set, launch() brackets each slice kernel with two events
+    std::function<hipEvent_t()> ev_get;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> kernel_pairs;
     int init(int dev);
     int launch(uint32_t budget, bool wide, hipStream_t s);
     void release();

@@ -665,6 +665,8 @@ int ShaEngine::launch(uint32_t budget, bool wide, hipStream_t s) {
     a.tile_ctr = count(2);
     a.budget = budget;
     const uint64_t tiles = (ub + 63) / 64;
+    hipEvent_t ka = ev_get ? ev_get() : nullptr, kb = ka ? ev_get() : nullptr;
+    if (kb) VS_HIP(hipEventRecord(ka, s));
     if (wide) {
         // persistent grid: 3 waves per SIMD (launch bounds: <= 168 VGPRs)
         const uint64_t slots = (uint64_t)std::max(cus, 1) * 4 * 3 / kWideWaves;
@@ -674,6 +676,10 @@ int ShaEngine::launch(uint32_t budget, bool wide, hipStream_t s) {
         // persistent grid: LDS (32 KiB per workgroup) admits 5 workgroups per CU
         const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)std::max(cus, 1) * 5);
         sha_slice_kernel<<<grid, 128, 0, s>>>(a);
+    }
+    if (kb) {
+        VS_HIP(hipEventRecord(kb, s));
+        kernel_pairs.push_back({ka, kb});
     }
     VS_HIP(hipGetLastError());
     cur = nxt;
