@@ -103,13 +103,18 @@ def rsync_main(args):
     edited (seed 5: 4 KiB overwrite / 1-64 B insert / 1-64 B delete), both
     device-resident.  A step = generate_and_send_sums over D (weak + XXH3-128
     per block) + build_hash_table + match_sums over S (weak scan, strong
-    verification rounds, greedy walk).  value = (|D| + |S|) per second.  The
-    greedy walk is sequential, so N GPUs run N independent replicas."""
+    verification rounds, greedy walk).  value = (|D| + |S|) per second.
+    N GPUs: D is ONE file of N x per-GPU bytes, sharded by block range; each
+    rank computes the sums of its blocks and an RCCL all-gather assembles the
+    full table on every rank (volsync_amd/rsync_shard.py) -- the path's only
+    collective.  Each rank then matches its own piece of S (the edited copy of
+    its D range, walked from the piece's start) against the full table."""
     import numpy as np
     import torch
     import torch.distributed as dist
     from volsync_amd import Matcher, sum_sizes_sqroot, synth_fill_device
     from volsync_amd.rsync import CSUM_XXH3_128
+    from volsync_amd.rsync_shard import BlockShard, gather_sums
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -118,12 +123,15 @@ def rsync_main(args):
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    n = int(args.per_gpu_gib * (1 << 30))
-    hdr = sum_sizes_sqroot(n)
+    per = int(args.per_gpu_gib * (1 << 30))
+    hdr = sum_sizes_sqroot(per * world)
+    shard = BlockShard.for_rank(per * world, hdr.blength, world, rank)
+    n = shard.byte_hi - shard.byte_lo
     db = torch.empty(n, dtype=torch.uint8, device=dev)
-    synth_fill_device(db.data_ptr(), 4, 0, n, device=local)
-    rng = np.random.default_rng(5)
-    edits = np.sort(rng.choice(hdr.count, hdr.count // 10, replace=False))
+    synth_fill_device(db.data_ptr(), 4, shard.byte_lo, n, device=local)
+    rng = np.random.default_rng(5 + rank)
+    full_blocks = n // hdr.blength
+    edits = np.sort(rng.choice(full_blocks, full_blocks // 10, replace=False))
     pieces, pos = [], 0
     for b in edits.tolist():
         at = b * hdr.blength + int(rng.integers(0, hdr.blength - 4096))
@@ -141,17 +149,21 @@ def rsync_main(args):
     pieces.append(db[pos:])
     ds = torch.cat(pieces)
     del pieces
-    s1 = torch.zeros(hdr.count, dtype=torch.int32, device=dev)
-    s2 = torch.zeros(hdr.count * hdr.s2length, dtype=torch.uint8, device=dev)
+    s1 = torch.zeros(max(shard.blocks, 1), dtype=torch.int32, device=dev)
+    s2 = torch.zeros(max(shard.blocks, 1) * hdr.s2length, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize(dev)
     m = Matcher(local)
+    m.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     seed = 0x5EED5EED
 
     def step():
         m.signatures_device(db.data_ptr(), n, hdr.blength, hdr.s2length, CSUM_XXH3_128, seed,
                             s1.data_ptr(), s2.data_ptr())
-        m.load_sums_device(hdr.count, hdr.blength, hdr.s2length, hdr.remainder, s1.data_ptr(),
-                           s2.data_ptr(), CSUM_XXH3_128, seed)
+        f1, f2 = s1, s2
+        if world > 1:
+            f1, f2 = gather_sums(s1, s2, shard, hdr.s2length, dist.all_gather)
+        m.load_sums_device(hdr.count, hdr.blength, hdr.s2length, hdr.remainder, f1.data_ptr(),
+                           f2.data_ptr(), CSUM_XXH3_128, seed)
         return m.match_device(ds.data_ptr(), ds.numel())
 
     for _ in range(args.warmup):
@@ -175,7 +187,11 @@ def rsync_main(args):
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    tot = (n + ds.numel()) * world
+    tot = n + ds.numel()
+    if world > 1:
+        t = torch.tensor([tot], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        tot = int(t.item())
     value = tot * args.steps / dt / 1e9
     sig_gbs = n / (stages["signatures"] / args.steps) / 1e6 if stages["signatures"] else 0.0
     if rank == 0:
@@ -185,8 +201,8 @@ def rsync_main(args):
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (splitmix64 destination + C4 edits, device-resident)",
-            "config": {"workload": f"C4-shape: {n >> 30} GiB destination vs 10%-edited source, "
-                                   f"{'replicas x' + str(world) if world > 1 else '1 GPU'}",
+            "config": {"workload": f"C4-shape: {(per * world) >> 30} GiB destination vs 10%-edited "
+                                   f"source, {'block-range shards x' + str(world) + ' (sums all-gathered over RCCL)' if world > 1 else '1 GPU'}",
                        "blength": hdr.blength, "s2length": hdr.s2length, "count": hdr.count,
                        "csum": "xxh128", "checksum_seed": hex(seed), "matches": nm},
             "roofline": {"bound": "hbm", "achieved": round(sig_gbs, 1), "peak": HBM_PEAK_GBS,

@@ -194,3 +194,51 @@ def test_c4_shape_properties(gpu):
     from volsync_amd import SumStruct, match_sums
     s = SumStruct(0, hw.count, hw.blength, hw.s2length, hw.remainder, c1, c2)
     assert match_sums(sw, s, R.CSUM_XXH3_128, 0x5EED5EED) == want
+
+
+@pytest.mark.parametrize("world,n,block_size", [
+    (2, (5 << 20) + 777, 0),      # short last block on the last shard
+    (3, 8 << 20, 1000),           # odd block size: shard byte ranges unaligned
+    (8, 3 << 20, 0),
+])
+def test_block_sharded_signatures_on_device(gpu, world, n, block_size):
+    """The device side of the sharded signature pass: each "rank" runs
+    vs_rsync_signatures_device over ONLY its block range's bytes (a separate
+    device buffer), gather_sums assembles the pieces (identity all-gather on
+    one device), and the table and the match list equal the whole-file ones."""
+    import torch
+    from volsync_amd import Matcher, sum_sizes_sqroot
+    from volsync_amd.rsync_shard import BlockShard, gather_sums
+    csum, seed = R.CSUM_XXH3_128, 0x5EED5EED
+    basis = O.synth(300 + world, 0, n)
+    hdr = sum_sizes_sqroot(n, block_size)
+    m = Matcher()
+    pieces = []
+    for sh in BlockShard.split(n, hdr.blength, world):
+        db = to_dev(basis[sh.byte_lo:sh.byte_hi])
+        s1 = torch.zeros(max(sh.blocks, 1), dtype=torch.int32, device="cuda")
+        s2 = torch.zeros(max(sh.blocks, 1) * hdr.s2length, dtype=torch.uint8, device="cuda")
+        m.signatures_device(db.data_ptr(), sh.byte_hi - sh.byte_lo, hdr.blength, hdr.s2length,
+                            csum, seed, s1.data_ptr(), s2.data_ptr())
+        pieces.append((sh, s1, s2))
+    torch.cuda.synchronize()
+    contrib = {}
+    for sh, s1, s2 in pieces:
+        def fake_gather(out, t, sh=sh):
+            # stands in for dist.all_gather: every rank's padded contribution
+            kind = "s1" if t.dtype == torch.int32 else "s2"
+            contrib.setdefault(kind, {})[sh.rank] = t.clone()
+            if len(contrib[kind]) == world:
+                for r in range(world):
+                    out[r].copy_(contrib[kind][r])
+        f1, f2 = gather_sums(s1, s2, sh, hdr.s2length, fake_gather)
+    c1, c2 = O.rsync_signatures(basis, hdr.blength, hdr.s2length, csum, seed)
+    assert (f1.cpu().numpy().view(np.uint32) == c1).all()
+    assert (f2.cpu().numpy().reshape(-1, hdr.s2length) == c2).all()
+    src = R.mutate(basis, hdr.blength, seed=11)
+    ds = to_dev(src)
+    m.load_sums_device(hdr.count, hdr.blength, hdr.s2length, hdr.remainder, f1.data_ptr(),
+                       f2.data_ptr(), csum, seed)
+    got = m.match_sums(ds.data_ptr(), len(src))
+    m.close()
+    assert got == O.rsync_match(src, c1, c2, hdr.blength, hdr.remainder, csum, seed)[0]

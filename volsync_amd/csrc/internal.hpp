@@ -254,12 +254,23 @@ struct RsScanArgs {
     const uint32_t *dir;
     const uint32_t *filt;
     uint32_t dbits, fbits;
+    // LDS prefilter: bit (sum >> (32 - lbits)) set iff some block's sum1 has
+    // those top bits; lives right after filt in the same allocation
+    const uint32_t *filt_l;
+    uint32_t lbits;
     unsigned long long *n_cand;
     uint64_t cap;
     uint64_t *cand_off;    // [cap]
     uint32_t *cand_sum;    // [cap]
 };
-hipError_t launch_rs_scan(const RsScanArgs &a, hipStream_t s);
+// bits of the LDS-resident prefilter (2^20 bits = 128 KiB) for an fbits filter
+__host__ __device__ inline uint32_t rs_lds_filter_bits(uint32_t fbits) {
+    return fbits < 20 ? fbits : 20;
+}
+inline size_t rs_filter_bytes(uint32_t fbits) {
+    return ((size_t)1 << fbits) / 8 + (((size_t)1 << rs_lds_filter_bits(fbits)) / 8);
+}
+hipError_t launch_rs_scan(const RsScanArgs &a, int cus, hipStream_t s);
 hipError_t launch_rs_sort_cands(void *tmp, size_t tmp_bytes, const uint64_t *off_in,
                                 uint64_t *off_out, const uint32_t *sum_in, uint32_t *sum_out,
                                 uint64_t n, int end_bit, hipStream_t s);

@@ -148,6 +148,10 @@ __global__ void rs_dir_kernel(const uint64_t *tkey, uint32_t count, uint32_t dbi
     if (p < count) {
         const uint32_t f = (uint32_t)(tkey[p] >> (64 - fbits));
         atomicOr(&filt[f >> 5], 1u << (f & 31));
+        // LDS prefilter, stored after the filter
+        uint32_t *filt_l = filt + ((1ull << fbits) / 32);
+        const uint32_t fl = (uint32_t)(tkey[p] >> (64 - rs_lds_filter_bits(fbits)));
+        atomicOr(&filt_l[fl >> 5], 1u << (fl & 31));
     }
 }
 
@@ -159,7 +163,7 @@ hipError_t launch_rs_table(const uint32_t *sum1, uint32_t count, uint64_t *keys,
     hipError_t e = hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, keys, tkey, (int)count, 0, 64,
                                                      s);
     if (e != hipSuccess) return e;
-    e = hipMemsetAsync(filt, 0, ((1ull << fbits) / 32) * 4, s);
+    e = hipMemsetAsync(filt, 0, rs_filter_bytes(fbits), s);
     if (e != hipSuccess) return e;
     rs_dir_kernel<<<(count + 1 + 255) / 256, 256, 0, s>>>(tkey, count, dbits, dir, fbits, filt);
     return hipGetLastError();
@@ -235,10 +239,22 @@ __device__ __forceinline__ void prefix_at(const RsScanArgs &a, uint64_t q, uint3
     stx = t;
 }
 
-// does a block with sum1 == sum and length k exist?
-__device__ __forceinline__ bool probe(const RsScanArgs &a, uint32_t sum, bool full) {
-    const uint32_t f = sum >> (32 - a.fbits);
-    if (!((a.filt[f >> 5] >> (f & 31)) & 1u)) return false;
+// both filter levels for one weak sum: the LDS prefilter, then -- only in the
+// lanes it passes, so the others issue no memory request -- the HBM/L2 filter
+__device__ __forceinline__ uint32_t filter2(const RsScanArgs &a, const uint32_t *lfilt,
+                                            uint32_t sum) {
+    const uint32_t fl = sum >> (32 - a.lbits);
+    uint32_t pass = (lfilt[fl >> 5] >> (fl & 31)) & 1u;
+    if (pass) {
+        const uint32_t f = sum >> (32 - a.fbits);
+        pass = (a.filt[f >> 5] >> (f & 31)) & 1u;
+    }
+    return pass;
+}
+
+// does a block with sum1 == sum and length k exist? (directory walk; the
+// filters were applied by the caller)
+__device__ __forceinline__ bool probe_dir(const RsScanArgs &a, uint32_t sum, bool full) {
     const uint32_t b = sum >> (32 - a.dbits);
     const uint32_t p0 = a.dir[b], p1 = a.dir[b + 1];
     for (uint32_t p = p0; p < p1; ++p) {
@@ -262,20 +278,26 @@ __device__ __forceinline__ void emit(const RsScanArgs &a, uint64_t o, uint32_t s
 }
 
 // Candidates are collected per workgroup in LDS and appended to the global
-// list with one atomic per workgroup: a single global counter bumped once per
-// candidate serialises millions of same-address atomics.
-constexpr uint32_t kScanThreads = 128;
-constexpr uint32_t kLocCand = 1024;
+// list with one atomic per workgroup and round: a single global counter bumped
+// once per candidate serialises millions of same-address atomics.
+//
+// Filter in two levels: every offset's weak sum is first tested against a
+// 2^20-bit prefilter held in LDS (the top 20 bits of the table's sums, built
+// with the table), and only the offsets that pass gather from the 2^fbits-bit
+// filter in HBM/L2 (filter2()).  With one random 4-byte gather per offset the
+// L2-resident filter alone bound the scan (~186 GB/s at C4 shape).  The grid is
+// persistent -- one workgroup per CU loads the prefilter once -- and each round
+// of strips flushes the workgroup's candidates.
+// 16 waves per CU: the gathers need the occupancy (512 threads: 332 ms, 1024:
+// 235 ms at C4 shape, despite 80 B/lane of scratch in the rare probe path)
+constexpr uint32_t kScanThreads = 1024;
+constexpr uint32_t kLocCand = 2048;
+constexpr uint32_t kLdsFiltWords = 1u << 15;  // 2^20 bits
 
-// lane per strip of kRsStrip offsets in [0, nfull): full windows of blength bytes
-__global__ __launch_bounds__(kScanThreads) void rs_scan_kernel(RsScanArgs a) {
-    __shared__ uint64_t loc_off[kLocCand];
-    __shared__ uint32_t loc_sum[kLocCand];
-    __shared__ uint32_t loc_n;
-    __shared__ unsigned long long loc_base;
-    if (threadIdx.x == 0) loc_n = 0;
-    __syncthreads();
-    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void scan_strip(const RsScanArgs &a, uint64_t k, const uint32_t *lfilt,
+                                           uint64_t *loc_off, uint32_t *loc_sum,
+                                           uint32_t *loc_n_p) {
+    uint32_t &loc_n = *loc_n_p;
     const uint64_t o0 = k * kRsStrip;
     if (o0 < a.nfull) {
         const uint64_t o1 = min(o0 + kRsStrip, a.nfull);
@@ -312,14 +334,11 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_kernel(RsScanArgs a) {
                 }
                 uint32_t hit = 0;
 #pragma unroll
-                for (int j = 0; j < 32; ++j) {
-                    const uint32_t f = sums[j] >> (32 - a.fbits);
-                    hit |= ((a.filt[f >> 5] >> (f & 31)) & 1u) << j;
-                }
+                for (int j = 0; j < 32; ++j) hit |= filter2(a, lfilt, sums[j]) << j;
                 while (hit) {
                     const int j = __builtin_ctz(hit);
                     hit &= hit - 1;
-                    if (o + j < o1 && probe(a, sums[j], true)) {
+                    if (o + j < o1 && probe_dir(a, sums[j], true)) {
                         const uint32_t slot = atomicAdd(&loc_n, 1u);
                         if (slot < kLocCand) {
                             loc_off[slot] = o + j;
@@ -347,14 +366,11 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_kernel(RsScanArgs a) {
             }
             uint32_t hit = 0;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const uint32_t f = sums[j] >> (32 - a.fbits);
-                hit |= ((a.filt[f >> 5] >> (f & 31)) & 1u) << j;
-            }
+            for (int j = 0; j < 16; ++j) hit |= filter2(a, lfilt, sums[j]) << j;
             while (hit) {
                 const int j = __builtin_ctz(hit);
                 hit &= hit - 1;
-                if (o + j < o1 && probe(a, sums[j], true)) {
+                if (o + j < o1 && probe_dir(a, sums[j], true)) {
                     const uint32_t slot = atomicAdd(&loc_n, 1u);
                     if (slot < kLocCand) {
                         loc_off[slot] = o + j;
@@ -366,31 +382,58 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_kernel(RsScanArgs a) {
             }
         }
     }
+}
+
+__global__ __launch_bounds__(kScanThreads) void rs_scan_kernel(RsScanArgs a) {
+    __shared__ uint32_t lfilt[kLdsFiltWords];
+    __shared__ uint64_t loc_off[kLocCand];
+    __shared__ uint32_t loc_sum[kLocCand];
+    __shared__ uint32_t loc_n;
+    __shared__ unsigned long long loc_base;
+    const uint32_t lw = (1u << a.lbits) / 32;
+    for (uint32_t i = threadIdx.x; i < lw; i += blockDim.x) lfilt[i] = a.filt_l[i];
+    if (threadIdx.x == 0) loc_n = 0;
     __syncthreads();
-    const uint32_t m = min(loc_n, kLocCand);
-    if (m == 0) return;
-    if (threadIdx.x == 0) loc_base = atomicAdd((unsigned long long *)a.n_cand, (unsigned long long)m);
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-        const unsigned long long slot = loc_base + i;
-        if (slot < a.cap) {
-            a.cand_off[slot] = loc_off[i];
-            a.cand_sum[slot] = loc_sum[i];
+    const uint64_t strips = (a.nfull + kRsStrip - 1) / kRsStrip;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < strips; base += stride) {
+        const uint64_t k = base + threadIdx.x;
+        if (k < strips) scan_strip(a, k, lfilt, loc_off, loc_sum, &loc_n);
+        __syncthreads();
+        const uint32_t m = min(loc_n, kLocCand);
+        if (m) {
+            if (threadIdx.x == 0)
+                loc_base = atomicAdd((unsigned long long *)a.n_cand, (unsigned long long)m);
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+                const unsigned long long slot = loc_base + i;
+                if (slot < a.cap) {
+                    a.cand_off[slot] = loc_off[i];
+                    a.cand_sum[slot] = loc_sum[i];
+                }
+            }
         }
+        __syncthreads();
+        if (threadIdx.x == 0) loc_n = 0;
+        __syncthreads();
     }
 }
 
 // the one shrunk-window offset that can match (the short last block), on one lane
 __global__ void rs_scan_tail_kernel(RsScanArgs a, uint64_t o) {
     const uint32_t sum = weak_sum(a.data, o, a.len - o, a.len);
-    if (probe(a, sum, false)) emit(a, o, sum);
+    if (probe_dir(a, sum, false)) emit(a, o, sum);
 }
 
-hipError_t launch_rs_scan(const RsScanArgs &a, hipStream_t s) {
+hipError_t launch_rs_scan(const RsScanArgs &a, int cus, hipStream_t s) {
     const uint64_t strips = (a.nfull + kRsStrip - 1) / kRsStrip;
-    if (strips)
-        rs_scan_kernel<<<(uint32_t)((strips + kScanThreads - 1) / kScanThreads), kScanThreads, 0,
-                         s>>>(a);
+    if (a.lbits > 20) return hipErrorInvalidValue;  // prefilter larger than its LDS array
+    if (strips) {
+        // persistent: one workgroup per CU (the 152 KiB of LDS admit one)
+        const uint64_t grid = std::min<uint64_t>((strips + kScanThreads - 1) / kScanThreads,
+                                                 (uint64_t)std::max(cus, 1));
+        rs_scan_kernel<<<(uint32_t)grid, kScanThreads, 0, s>>>(a);
+    }
     if (a.remainder && a.count && a.len >= a.remainder)
         rs_scan_tail_kernel<<<1, 1, 0, s>>>(a, a.len - a.remainder);
     return hipGetLastError();

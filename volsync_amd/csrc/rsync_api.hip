@@ -30,6 +30,7 @@ using namespace vsgpu;
 
 struct vs_rsync {
     int device = 0;
+    int cus = 256;
     hipStream_t own = nullptr, stream = nullptr;
     // signature table
     bool loaded = false;
@@ -132,7 +133,7 @@ int build_table(vs_rsync *h) {
     VS_TRY(h->d_keys.ensure(n * 8));
     VS_TRY(h->d_tkey.ensure(n * 8));
     VS_TRY(h->d_dir.ensure(((1ull << h->dbits) + 1) * 4));
-    VS_TRY(h->d_filt.ensure((1ull << h->fbits) / 8));
+    VS_TRY(h->d_filt.ensure(rs_filter_bytes(h->fbits)));
     const size_t tb = rs_sort_tmp_bytes(n, false);
     VS_TRY(h->d_tmp.ensure(tb));
     VS_HIP(launch_rs_table(h->d_sum1.as<uint32_t>(), count, h->d_keys.as<uint64_t>(),
@@ -309,6 +310,8 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
     a.filt = h->d_filt.as<uint32_t>();
     a.dbits = h->dbits;
     a.fbits = h->fbits;
+    a.lbits = rs_lds_filter_bits(h->fbits);
+    a.filt_l = h->d_filt.as<uint32_t>() + ((1ull << h->fbits) / 32);
     a.n_cand = (unsigned long long *)h->n_cand.p;
     // expected: weak collisions (count / 2^32 per offset) + one per matching block
     uint64_t cap = (uint64_t)((double)a.nfull * h->count / 4294967296.0 * 2.0) +
@@ -321,7 +324,7 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
         a.cand_off = h->c_off.as<uint64_t>();
         a.cand_sum = h->c_sum.as<uint32_t>();
         VS_HIP(hipMemsetAsync(h->n_cand.p, 0, 8, h->stream));
-        VS_HIP(launch_rs_scan(a, h->stream));
+        VS_HIP(launch_rs_scan(a, h->cus, h->stream));
         VS_HIP(hipMemcpyAsync(h->pinned, h->n_cand.p, 8, hipMemcpyDeviceToHost, h->stream));
         VS_HIP(hipStreamSynchronize(h->stream));
         nc = h->pinned[0];
@@ -404,6 +407,7 @@ VS_API int vs_rsync_open(int device, vs_rsync **out) {
     if (device < 0 || device >= ndev) return fail(VS_ERR_ARG, "device index out of range");
     vs_rsync *h = new vs_rsync();
     h->device = device;
+    (void)hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (rs_dev(h) < 0 || hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void **)&h->pinned, 64, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
