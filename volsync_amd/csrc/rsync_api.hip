@@ -184,22 +184,47 @@ inline int64_t group_start(const vs_rsync *h, uint32_t sum) {
     return -1;
 }
 
-// match.c hash_search over the sorted candidates.  A candidate whose strong
-// sum is unknown is treated as a non-match and reported in `need`.
-void walk(vs_rsync *h, int64_t len, const std::vector<uint64_t> &off,
-          const std::vector<uint32_t> &sum, const std::vector<uint8_t> &known,
-          const std::vector<uint8_t> &strong, std::vector<uint64_t> &need,
-          std::vector<vs_match> &out, int64_t &false_alarms) {
-    const size_t nc = off.size();
-    const uint32_t s2 = (uint32_t)h->s2length;
-    const int64_t end = len + 1 - blen(h, h->count - 1);
+// Where a walk resumes: the walk is deterministic, and a verification round
+// only adds strong sums, so everything before the first candidate whose sum
+// was unknown replays identically -- the next round starts there.
+struct WalkState {
     int64_t offset = 0;
     int32_t want_i = 0;
     size_t c = 0;
-    false_alarms = 0;
+    size_t nout = 0;
+    int64_t false_alarms = 0;
+};
+
+// match.c hash_search over the sorted candidates, from state `st`.  A
+// candidate whose strong sum is unknown is treated as a non-match and
+// reported in `need`; st then holds the state just before the first of them
+// (else the final state).
+void walk(vs_rsync *h, int64_t len, const std::vector<uint64_t> &off,
+          const std::vector<uint32_t> &sum, const std::vector<uint8_t> &known,
+          const std::vector<uint8_t> &strong, std::vector<uint64_t> &need,
+          std::vector<vs_match> &out, WalkState &st) {
+    const size_t nc = off.size();
+    const uint32_t s2 = (uint32_t)h->s2length;
+    const int64_t end = len + 1 - blen(h, h->count - 1);
+    int64_t offset = st.offset;
+    int32_t want_i = st.want_i;
+    size_t c = st.c;
+    int64_t false_alarms = st.false_alarms;
+    out.resize(st.nout);
+    bool resume_set = false;
+    WalkState resume;
     while (c < nc) {
         if ((int64_t)off[c] < offset) {
-            c = std::lower_bound(off.begin() + c, off.end(), (uint64_t)offset) - off.begin();
+            // after a match the walk jumps one block ahead, past the ~count /
+            // 2^32 * blength weak collisions inside it: gallop from c (a few
+            // nearby probes) instead of a binary search over the whole rest
+            size_t step = 1, lo = c, hi = c + 1;
+            while (hi < nc && off[hi] < (uint64_t)offset) {
+                lo = hi;
+                step <<= 1;
+                hi = std::min(nc, hi + step);
+            }
+            c = std::lower_bound(off.begin() + lo, off.begin() + hi, (uint64_t)offset) - off.begin();
             continue;
         }
         const int64_t o = (int64_t)off[c];
@@ -212,6 +237,10 @@ void walk(vs_rsync *h, int64_t len, const std::vector<uint64_t> &off,
             int32_t i = (int32_t)~(uint32_t)h->tkey_h[q];
             if (blen(h, i) != k) continue;
             if (!known[c]) {
+                if (!resume_set) {
+                    resume = {offset, want_i, c, out.size(), false_alarms};
+                    resume_set = true;
+                }
                 need.push_back(c);
                 break;
             }
@@ -234,6 +263,7 @@ void walk(vs_rsync *h, int64_t len, const std::vector<uint64_t> &off,
             ++c;
         }
     }
+    st = resume_set ? resume : WalkState{offset, want_i, c, out.size(), false_alarms};
 }
 
 // strong sums of candidate windows idx[] on the device -> strong/known
@@ -370,22 +400,21 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
     }
     double t_ver = 0, t_walk = 0;
     std::vector<vs_match> out;
-    int64_t fa = 0;
+    WalkState ws;
     for (;;) {
         double tv = now_ms();
         VS_TRY(verify(h, dev_src, len, off, batch, known, strong));
         t_ver += now_ms() - tv;
         ++h->st_rounds;
         batch.clear();
-        out.clear();
         double tw = now_ms();
-        walk(h, len, off, sum, known, strong, batch, out, fa);
+        walk(h, len, off, sum, known, strong, batch, out, ws);
         t_walk += now_ms() - tw;
         if (batch.empty()) break;
     }
     h->ms[3] = t_ver;
     h->ms[4] = t_walk;
-    h->st_fa = fa;
+    h->st_fa = ws.false_alarms;
     h->matches.swap(out);
     if (n_matches) *n_matches = (int64_t)h->matches.size();
     return 0;
