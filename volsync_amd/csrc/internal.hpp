@@ -231,7 +231,7 @@ struct RsSigArgs {
 hipError_t launch_rs_signatures(const RsSigArgs &a, hipStream_t s);
 hipError_t launch_rs_strong(const uint8_t *data, const uint64_t *offs, const uint32_t *lens,
                             uint64_t n, int csum_type, uint32_t seed, uint32_t s2length,
-                            uint8_t *out, hipStream_t s);
+                            uint8_t *out, uint32_t min_len, hipStream_t s);
 // sort keys (sum1 << 32 | ~index) -> tkey, directory over the top dbits of sum1
 // (2^dbits + 1 entries) and a 2^fbits-bit filter over the top fbits
 hipError_t launch_rs_table(const uint32_t *sum1, uint32_t count, uint64_t *keys, uint64_t *tkey,

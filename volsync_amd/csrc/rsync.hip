@@ -104,9 +104,154 @@ __global__ void rs_sig_kernel(RsSigArgs a) {
     for (uint32_t j = 0; j < a.s2length; ++j) a.sum2[i * a.s2length + j] = s[j];
 }
 
+// ---- cooperative XXH3 for long windows: 8 lanes per window ----------------------
+// One lane per 128 KiB window streams 64 windows 128 KiB apart through every
+// load instruction (64 pages per access).  XXH3's long-input state is 8
+// independent 64-bit accumulators over 64-byte stripes, so lane i of an
+// 8-lane group owns accumulator i and reads word i of every stripe: the
+// group's 8 loads form one contiguous 64-byte access.  acc[i ^ 1] += d[i]
+// (xxh3_long in strong.hpp) becomes acc[i] += d[i ^ 1] through a lane swap;
+// the scramble is per accumulator.  The same loads feed get_checksum1 (signed
+// byte sums via v_dot4), reduced over the group at the end.  Bit-identical to
+// vsstrong::checksum2 / weak_sum (tests/test_gpu_rsync.py).
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// signed-byte sum and position-weighted sum of the 8 bytes of d at byte pos
+__device__ __forceinline__ void weak8(uint64_t d, uint32_t pos, uint32_t &sx, uint32_t &sux) {
+    const uint32_t lo = (uint32_t)d, hi = (uint32_t)(d >> 32);
+    const uint32_t a = (uint32_t)dot4(lo, 0x01010101u, 0), b = (uint32_t)dot4(hi, 0x01010101u, 0);
+    sx += a + b;
+    sux += pos * a + (uint32_t)dot4(lo, 0x03020100u, 0) + (pos + 4) * b +
+           (uint32_t)dot4(hi, 0x03020100u, 0);
+}
+
+__device__ __forceinline__ void coop_stripe(uint64_t &acc, uint64_t d, uint32_t sb, uint32_t i,
+                                            uint64_t seed) {
+    const uint64_t k = d ^ vsstrong::csec_at(sb + 8 * i, seed);
+    acc += (uint64_t)(uint32_t)k * (k >> 32);
+    acc += shfl_xor64(d, 1);
+}
+
+// window p[0, len), len > 240; i = lane within the 8-lane group.  Returns
+// accumulator i; sx/sux = this lane's share of the weak-sum parts.
+__device__ __forceinline__ uint64_t coop_long(const uint8_t *p, uint64_t len, uint64_t seed,
+                                              uint32_t i, uint32_t &sx, uint32_t &sux) {
+    using namespace vsstrong;
+    const uint64_t init[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+    uint64_t acc = init[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) acc = (i == (uint32_t)j) ? init[j] : acc;
+    sx = 0;
+    sux = 0;
+    const uint64_t nb = (len - 1) / 1024;
+    const uint64_t sec_scr = sec64(16 + i, seed);
+    for (uint64_t b = 0; b < nb; ++b) {
+        const uint8_t *q = p + b * 1024 + 8 * i;
+#pragma unroll 4
+        for (uint32_t s = 0; s < 16; ++s) {
+            const uint64_t d = rd64(q + 64 * s);
+            weak8(d, (uint32_t)(b * 1024 + 64 * s + 8 * i), sx, sux);
+            coop_stripe(acc, d, 8 * s, i, seed);
+        }
+        acc ^= acc >> 47;
+        acc ^= sec_scr;
+        acc *= P32_1;
+    }
+    const uint32_t ns = (uint32_t)(((len - 1) - nb * 1024) / 64);
+    for (uint32_t s = 0; s < ns; ++s) {
+        const uint64_t off = nb * 1024 + 64 * s + 8 * i;
+        const uint64_t d = rd64(p + off);
+        weak8(d, (uint32_t)off, sx, sux);
+        coop_stripe(acc, d, 8 * s, i, seed);
+    }
+    // last stripe (overlaps): hashed whole, weak-summed from the first byte no
+    // earlier stripe covered
+    const uint64_t covered = (nb * 16 + ns) * 64;
+    const uint64_t off = len - 64 + 8 * i;
+    const uint64_t d = rd64(p + off);
+    coop_stripe(acc, d, 192 - 64 - 7, i, seed);
+    const uint64_t skip = covered > off ? min<uint64_t>(covered - off, 8) : 0;
+    weak8(skip >= 8 ? 0 : d & (~0ull << (8 * skip)), (uint32_t)off, sx, sux);
+    return acc;
+}
+
+// group-wide finish: weak sum and strong sum of the window (every lane returns them)
+__device__ __forceinline__ void coop_finish(uint64_t acc, uint32_t sx, uint32_t sux, uint64_t len,
+                                            int csum_type, uint64_t seed, uint32_t gbase,
+                                            uint32_t &weak, uint64_t &lo, uint64_t &hi) {
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+        sx += (uint32_t)__shfl_xor((int)sx, m, 64);
+        sux += (uint32_t)__shfl_xor((int)sux, m, 64);
+    }
+    const uint32_t s2 = (uint32_t)len * sx - sux;
+    weak = (sx & 0xffffu) | (s2 << 16);
+    vsstrong::Xxh3Long st;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) st.acc[j] = shfl64(acc, (int)gbase + j);
+    lo = st.merge(11, len * vsstrong::P64_1, seed);
+    hi = (csum_type == vsstrong::kXxh3_128) ? st.merge(192 - 64 - 11, ~(len * vsstrong::P64_2), seed)
+                                            : 0;
+}
+
+__device__ __forceinline__ void put_strong(uint8_t *out, uint32_t s2length, uint64_t lo, uint64_t hi) {
+    for (uint32_t j = 0; j < s2length; ++j)
+        out[j] = (uint8_t)(j < 8 ? lo >> (8 * j) : hi >> (8 * (j - 8)));
+}
+
+// signatures: 8 lanes per block (XXH3, every block > 240 bytes)
+__global__ __launch_bounds__(256) void rs_sig_coop_kernel(RsSigArgs a) {
+    const uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+    const uint32_t i = threadIdx.x & 7, gbase = (threadIdx.x & 63) & ~7u;
+    const uint64_t b = g < a.count ? g : a.count - 1;  // whole groups stay active (shuffles)
+    const uint64_t pos = b * a.blength;
+    const uint64_t n = (b == a.count - 1 && a.remainder) ? a.remainder : a.blength;
+    uint32_t sx, sux, weak;
+    uint64_t lo, hi;
+    const uint64_t acc = coop_long(a.data + pos, n, a.seed, i, sx, sux);
+    coop_finish(acc, sx, sux, n, a.csum_type, a.seed, gbase, weak, lo, hi);
+    if (g < a.count && i == 0) {
+        a.sum1[g] = weak;
+        put_strong(a.sum2 + g * a.s2length, a.s2length, lo, hi);
+    }
+}
+
+// candidate verification: 8 lanes per window (XXH3, every window > 240 bytes)
+__global__ __launch_bounds__(256) void rs_strong_coop_kernel(const uint8_t *data,
+                                                             const uint64_t *offs,
+                                                             const uint32_t *lens, uint64_t n,
+                                                             int csum_type, uint32_t seed,
+                                                             uint32_t s2length, uint8_t *out) {
+    const uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+    const uint32_t i = threadIdx.x & 7, gbase = (threadIdx.x & 63) & ~7u;
+    const uint64_t w = g < n ? g : n - 1;
+    const uint64_t len = lens[w];
+    uint32_t sx, sux, weak;
+    uint64_t lo, hi;
+    const uint64_t acc = coop_long(data + offs[w], len, seed, i, sx, sux);
+    coop_finish(acc, sx, sux, len, csum_type, seed, gbase, weak, lo, hi);
+    if (g < n && i == 0) put_strong(out + g * s2length, s2length, lo, hi);
+}
+
+static bool coop_ok(int csum_type) {
+    return csum_type == vsstrong::kXxh3_128 || csum_type == vsstrong::kXxh3_64;
+}
+
 hipError_t launch_rs_signatures(const RsSigArgs &a, hipStream_t s) {
     if (!a.count) return hipSuccess;
-    rs_sig_kernel<<<(uint32_t)((a.count + 127) / 128), 128, 0, s>>>(a);
+    if (coop_ok(a.csum_type) && a.blength > 240 && (a.remainder == 0 || a.remainder > 240))
+        rs_sig_coop_kernel<<<(uint32_t)((a.count * 8 + 255) / 256), 256, 0, s>>>(a);
+    else
+        rs_sig_kernel<<<(uint32_t)((a.count + 127) / 128), 128, 0, s>>>(a);
     return hipGetLastError();
 }
 
@@ -123,10 +268,14 @@ __global__ void rs_strong_kernel(const uint8_t *data, const uint64_t *offs, cons
 
 hipError_t launch_rs_strong(const uint8_t *data, const uint64_t *offs, const uint32_t *lens,
                             uint64_t n, int csum_type, uint32_t seed, uint32_t s2length,
-                            uint8_t *out, hipStream_t s) {
+                            uint8_t *out, uint32_t min_len, hipStream_t s) {
     if (!n) return hipSuccess;
-    rs_strong_kernel<<<(uint32_t)((n + 127) / 128), 128, 0, s>>>(data, offs, lens, n, csum_type,
-                                                                 seed, s2length, out);
+    if (coop_ok(csum_type) && min_len > 240)
+        rs_strong_coop_kernel<<<(uint32_t)((n * 8 + 255) / 256), 256, 0, s>>>(
+            data, offs, lens, n, csum_type, seed, s2length, out);
+    else
+        rs_strong_kernel<<<(uint32_t)((n + 127) / 128), 128, 0, s>>>(data, offs, lens, n,
+                                                                     csum_type, seed, s2length, out);
     return hipGetLastError();
 }
 

@@ -275,9 +275,11 @@ int verify(vs_rsync *h, const void *dev_src, int64_t len, const std::vector<uint
     const uint32_t s2 = (uint32_t)h->s2length;
     std::vector<uint64_t> vo(n);
     std::vector<uint32_t> vl(n);
+    uint32_t min_len = 0xffffffffu;
     for (size_t j = 0; j < n; ++j) {
         vo[j] = off[idx[j]];
         vl[j] = (uint32_t)std::min<int64_t>(h->blength, len - (int64_t)vo[j]);
+        min_len = std::min(min_len, vl[j]);
     }
     VS_TRY(h->v_off.ensure(n * 8));
     VS_TRY(h->v_len.ensure(n * 4));
@@ -286,7 +288,7 @@ int verify(vs_rsync *h, const void *dev_src, int64_t len, const std::vector<uint
     VS_HIP(hipMemcpyAsync(h->v_len.p, vl.data(), n * 4, hipMemcpyHostToDevice, h->stream));
     VS_HIP(launch_rs_strong((const uint8_t *)dev_src, h->v_off.as<uint64_t>(),
                             h->v_len.as<uint32_t>(), n, h->csum_type, h->seed, s2,
-                            h->v_out.as<uint8_t>(), h->stream));
+                            h->v_out.as<uint8_t>(), min_len, h->stream));
     std::vector<uint8_t> res(n * s2);
     VS_HIP(hipMemcpyAsync(res.data(), h->v_out.p, n * s2, hipMemcpyDeviceToHost, h->stream));
     VS_HIP(hipStreamSynchronize(h->stream));
