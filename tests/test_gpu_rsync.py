@@ -220,10 +220,12 @@ def test_block_sharded_signatures_on_device(gpu, world, n, block_size):
         s2 = torch.zeros(max(sh.blocks, 1) * hdr.s2length, dtype=torch.uint8, device="cuda")
         m.signatures_device(db.data_ptr(), sh.byte_hi - sh.byte_lo, hdr.blength, hdr.s2length,
                             csum, seed, s1.data_ptr(), s2.data_ptr())
-        pieces.append((sh, s1, s2))
+        # db stays referenced until the synchronize below: the kernel runs on
+        # the matcher's stream, which torch's allocator does not track
+        pieces.append((sh, s1, s2, db))
     torch.cuda.synchronize()
     contrib = {}
-    for sh, s1, s2 in pieces:
+    for sh, s1, s2, _ in pieces:
         def fake_gather(out, t, sh=sh):
             # stands in for dist.all_gather: every rank's padded contribution
             kind = "s1" if t.dtype == torch.int32 else "s2"
