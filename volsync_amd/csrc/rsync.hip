@@ -588,6 +588,30 @@ hipError_t launch_rs_scan(const RsScanArgs &a, int cus, hipStream_t s) {
     return hipGetLastError();
 }
 
+__device__ __forceinline__ bool sorted_has(const uint64_t *off, uint64_t n, uint64_t v) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (off[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < n && off[lo] == v;
+}
+
+__global__ void rs_chained_kernel(const uint64_t *off, uint64_t n, uint64_t bl, uint8_t *flag) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const uint64_t o = off[c];
+    flag[c] = (uint8_t)((o >= bl && sorted_has(off, n, o - bl)) || sorted_has(off, n, o + bl));
+}
+
+hipError_t launch_rs_chained(const uint64_t *off, uint64_t n, uint64_t blength, uint8_t *flag,
+                             hipStream_t s) {
+    if (!n) return hipSuccess;
+    rs_chained_kernel<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(off, n, blength, flag);
+    return hipGetLastError();
+}
+
 hipError_t launch_rs_sort_cands(void *tmp, size_t tmp_bytes, const uint64_t *off_in,
                                 uint64_t *off_out, const uint32_t *sum_in, uint32_t *sum_out,
                                 uint64_t n, int end_bit, hipStream_t s) {

@@ -49,6 +49,12 @@ struct vs_rsync {
     DevBuf v_off, v_len, v_out;
     // results
     std::vector<vs_match> matches;
+    // host scratch of match_device, reused across calls
+    std::vector<uint64_t> h_off, h_batch;
+    std::vector<uint32_t> h_sum;
+    std::vector<uint8_t> h_known, h_strong, h_flag;
+    DevBuf d_flag;
+    std::vector<vs_match> h_out;
     int64_t st_cand = 0, st_fa = 0, st_hashed = 0;
     int32_t st_rounds = 0;
     double ms[5] = {0, 0, 0, 0, 0};
@@ -367,8 +373,12 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
         if (attempt == 1) return fail(VS_ERR_STATE, "candidate buffer overflow");
     }
     // 3. sort candidates by offset
-    std::vector<uint64_t> off(nc);
-    std::vector<uint32_t> sum(nc);
+    // host scratch kept in the handle: first-touch page faults on ~160 MB of
+    // fresh vectors per call (C4 shape) cost ~100 ms
+    std::vector<uint64_t> &off = h->h_off;
+    std::vector<uint32_t> &sum = h->h_sum;
+    off.resize(nc);
+    sum.resize(nc);
     if (nc) {
         VS_TRY(h->c_off2.ensure(nc * 8));
         VS_TRY(h->c_sum2.ensure(nc * 4));
@@ -386,22 +396,29 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
     if (trace) fprintf(stderr, "rs: sorted + copied %.1f ms\n", t1 - t0);
     h->ms[2] = t1 - t0;
     // 4. round 0: chained candidates (another candidate one block length away)
-    std::vector<uint8_t> known(nc, 0), strong(nc * (size_t)h->s2length);
-    std::vector<uint64_t> batch;
-    {
-        const uint64_t bl = (uint64_t)h->blength;
-        size_t lo = 0, hi = 0;
-        for (size_t c = 0; c < nc; ++c) {
-            const uint64_t o = off[c];
-            while (lo < nc && off[lo] + bl < o) ++lo;
-            while (hi < nc && off[hi] < o + bl) ++hi;
-            const bool prev = lo < nc && off[lo] + bl == o;
-            const bool next = hi < nc && off[hi] == o + bl;
-            if (prev || next) batch.push_back(c);
-        }
+    std::vector<uint8_t> &known = h->h_known, &strong = h->h_strong;
+    known.assign(nc, 0);
+    strong.resize(nc * (size_t)h->s2length);
+    std::vector<uint64_t> &batch = h->h_batch;
+    batch.clear();
+    if (nc) {
+        // flags computed on the device over the sorted offsets (binary
+        // searches for o - blength and o + blength); the host loop over
+        // 8.9 M candidates took ~100 ms at C4 shape
+        VS_TRY(h->d_flag.ensure(nc));
+        VS_HIP(launch_rs_chained(h->c_off2.as<uint64_t>(), nc, (uint64_t)h->blength,
+                                 h->d_flag.as<uint8_t>(), h->stream));
+        h->h_flag.resize(nc);
+        VS_HIP(hipMemcpyAsync(h->h_flag.data(), h->d_flag.p, nc, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipStreamSynchronize(h->stream));
+        const uint8_t *fl = h->h_flag.data();
+        for (size_t c = 0; c < nc; ++c)
+            if (fl[c]) batch.push_back(c);
     }
+    if (trace) fprintf(stderr, "rs: chained batch %.1f ms (%zu)\n", now_ms() - t0, batch.size());
     double t_ver = 0, t_walk = 0;
-    std::vector<vs_match> out;
+    std::vector<vs_match> &out = h->h_out;
+    out.clear();
     WalkState ws;
     for (;;) {
         double tv = now_ms();
@@ -416,8 +433,10 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
     }
     h->ms[3] = t_ver;
     h->ms[4] = t_walk;
+    if (trace) fprintf(stderr, "rs: match done %.1f ms (verify %.1f, walk %.1f)\n", now_ms() - t0,
+                       t_ver, t_walk);
     h->st_fa = ws.false_alarms;
-    h->matches.swap(out);
+    h->matches.assign(out.begin(), out.end());
     if (n_matches) *n_matches = (int64_t)h->matches.size();
     return 0;
 }
@@ -462,7 +481,8 @@ VS_API void vs_rsync_close(vs_rsync *h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (DevBuf *b : {&h->d_sum1, &h->d_keys, &h->d_tkey, &h->d_dir, &h->d_filt, &h->d_tmp, &h->px,
                       &h->pt, &h->pxs, &h->pts, &h->partials, &h->c_off, &h->c_sum, &h->c_off2,
-                      &h->c_sum2, &h->n_cand, &h->sort_tmp, &h->v_off, &h->v_len, &h->v_out})
+                      &h->c_sum2, &h->n_cand, &h->sort_tmp, &h->v_off, &h->v_len, &h->v_out,
+                      &h->d_flag})
         b->release();
     if (h->pinned) (void)hipHostFree(h->pinned);
     if (h->own) (void)hipStreamDestroy(h->own);
