@@ -388,17 +388,29 @@ __device__ __forceinline__ void prefix_at(const RsScanArgs &a, uint64_t q, uint3
     stx = t;
 }
 
-// both filter levels for one weak sum: the LDS prefilter, then -- only in the
-// lanes it passes, so the others issue no memory request -- the HBM/L2 filter
-__device__ __forceinline__ uint32_t filter2(const RsScanArgs &a, const uint32_t *lfilt,
-                                            uint32_t sum) {
-    const uint32_t fl = sum >> (32 - a.lbits);
-    uint32_t pass = (lfilt[fl >> 5] >> (fl & 31)) & 1u;
-    if (pass) {
-        const uint32_t f = sum >> (32 - a.fbits);
-        pass = (a.filt[f >> 5] >> (f & 31)) & 1u;
+// Both filter levels for 8 weak sums: the LDS prefilter tests first, then 8 unconditional
+// HBM/L2 loads issued back to back (lanes that failed the prefilter read word
+// 0, one shared address), so a lane waits for one round trip per 8 offsets
+// instead of one per passing offset.  Bits j0..j0+7 of the result.
+template <int J0, int N>
+__device__ __forceinline__ uint32_t filter8(const RsScanArgs &a, const uint32_t *lfilt,
+                                            const uint32_t (&sums)[N]) {
+    uint32_t lp = 0, w[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t fl = sums[J0 + j] >> (32 - a.lbits);
+        lp |= ((lfilt[fl >> 5] >> (fl & 31)) & 1u) << j;
     }
-    return pass;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t f = sums[J0 + j] >> (32 - a.fbits);
+        sh[j] = f & 31;
+        w[j] = *(((lp >> j) & 1u) ? a.filt + (f >> 5) : a.filt);
+    }
+    uint32_t hit = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hit |= (((w[j] >> sh[j]) & (lp >> j)) & 1u) << (J0 + j);
+    return hit;
 }
 
 // does a block with sum1 == sum and length k exist? (directory walk; the
@@ -433,7 +445,7 @@ __device__ __forceinline__ void emit(const RsScanArgs &a, uint64_t o, uint32_t s
 // Filter in two levels: every offset's weak sum is first tested against a
 // 2^20-bit prefilter held in LDS (the top 20 bits of the table's sums, built
 // with the table), and only the offsets that pass gather from the 2^fbits-bit
-// filter in HBM/L2 (filter2()).  With one random 4-byte gather per offset the
+// filter in HBM/L2 (filter8()).  With one random 4-byte gather per offset the
 // L2-resident filter alone bound the scan (~186 GB/s at C4 shape).  The grid is
 // persistent -- one workgroup per CU loads the prefilter once -- and each round
 // of strips flushes the workgroup's candidates.
@@ -482,8 +494,8 @@ __device__ __forceinline__ void scan_strip(const RsScanArgs &a, uint64_t k, cons
                     s2 = s2 - nn * xo + s1;
                 }
                 uint32_t hit = 0;
-#pragma unroll
-                for (int j = 0; j < 32; ++j) hit |= filter2(a, lfilt, sums[j]) << j;
+                hit = filter8<0>(a, lfilt, sums) | filter8<8>(a, lfilt, sums) |
+                      filter8<16>(a, lfilt, sums) | filter8<24>(a, lfilt, sums);
                 while (hit) {
                     const int j = __builtin_ctz(hit);
                     hit &= hit - 1;
@@ -514,8 +526,7 @@ __device__ __forceinline__ void scan_strip(const RsScanArgs &a, uint64_t k, cons
                 s2 = s2 - nn * xo + s1;
             }
             uint32_t hit = 0;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) hit |= filter2(a, lfilt, sums[j]) << j;
+            hit = filter8<0>(a, lfilt, sums) | filter8<8>(a, lfilt, sums);
             while (hit) {
                 const int j = __builtin_ctz(hit);
                 hit &= hit - 1;
