@@ -271,8 +271,10 @@ inline size_t rs_filter_bytes(uint32_t fbits) {
     return ((size_t)1 << fbits) / 8 + (((size_t)1 << rs_lds_filter_bits(fbits)) / 8);
 }
 hipError_t launch_rs_scan(const RsScanArgs &a, int cus, hipStream_t s);
-// flag[c] = some candidate sits exactly one block before or after off[c]
-// (off sorted ascending): the walk's likely strong-sum needs
+// flag[0, n): some candidate sits exactly one block before or after off[c]
+// (off sorted ascending); flag[n, 2n): chained, or not covered by a chained
+// candidate in the block window before it -- the walk's likely strong-sum
+// needs.  flag holds 2n bytes.
 hipError_t launch_rs_chained(const uint64_t *off, uint64_t n, uint64_t blength, uint8_t *flag,
                              hipStream_t s);
 hipError_t launch_rs_sort_cands(void *tmp, size_t tmp_bytes, const uint64_t *off_in,

@@ -616,10 +616,39 @@ __global__ void rs_chained_kernel(const uint64_t *off, uint64_t n, uint64_t bl, 
     flag[c] = (uint8_t)((o >= bl && sorted_has(off, n, o - bl)) || sorted_has(off, n, o + bl));
 }
 
+// Round-0 prediction of the candidates the walk will visit: a chained
+// candidate, or one that no chained candidate in the block window before it
+// covers (the walk, having matched that one, would jump past it).  Isolated
+// weak collisions in edited regions are the second kind; hashing them up
+// front saves a verification round and a second walk.  Only a prediction:
+// the round loop in rsync_api.hip still guarantees rsync's decisions.
+__global__ void rs_visit_kernel(const uint64_t *off, uint64_t n, uint64_t bl,
+                                const uint8_t *chained, uint8_t *visit) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    uint8_t v = chained[c];
+    if (!v) {
+        const uint64_t o = off[c];
+        bool covered = false;
+        // ~count / 2^32 * blength weak collisions per window: a short scan;
+        // past the cap assume covered (a missed prediction costs a round)
+        for (uint64_t p = c, k = 0; p > 0 && off[p - 1] + bl > o; --p, ++k) {
+            if (k == 256 || chained[p - 1]) {
+                covered = true;
+                break;
+            }
+        }
+        v = !covered;
+    }
+    visit[c] = v;
+}
+
 hipError_t launch_rs_chained(const uint64_t *off, uint64_t n, uint64_t blength, uint8_t *flag,
                              hipStream_t s) {
     if (!n) return hipSuccess;
-    rs_chained_kernel<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(off, n, blength, flag);
+    const uint32_t grid = (uint32_t)((n + 255) / 256);
+    rs_chained_kernel<<<grid, 256, 0, s>>>(off, n, blength, flag);
+    rs_visit_kernel<<<grid, 256, 0, s>>>(off, n, blength, flag, flag + n);
     return hipGetLastError();
 }
 

@@ -10,7 +10,9 @@
 //      device computed for that window;
 //   3. verification rounds: the walk needs strong sums only for candidates it
 //      visits.  Round 0 hashes "chained" candidates (another candidate one
-//      block length away, the shape of runs of matching blocks); each walk
+//      block length away, the shape of runs of matching blocks) and those no
+//      chained candidate in the block window before them covers (isolated
+//      weak collisions in edited regions, which the walk visits); each walk
 //      then treats a candidate without a strong sum as a non-match and
 //      records it; the recorded windows are hashed on the device and the
 //      walk repeats.  The final walk found every strong sum it needed, so it
@@ -395,7 +397,8 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
     const double t1 = now_ms();
     if (trace) fprintf(stderr, "rs: sorted + copied %.1f ms\n", t1 - t0);
     h->ms[2] = t1 - t0;
-    // 4. round 0: chained candidates (another candidate one block length away)
+    // 4. round 0: chained candidates (another candidate one block length
+    // away) plus the uncovered ones (see rs_visit_kernel)
     std::vector<uint8_t> &known = h->h_known, &strong = h->h_strong;
     known.assign(nc, 0);
     strong.resize(nc * (size_t)h->s2length);
@@ -405,11 +408,12 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
         // flags computed on the device over the sorted offsets (binary
         // searches for o - blength and o + blength); the host loop over
         // 8.9 M candidates took ~100 ms at C4 shape
-        VS_TRY(h->d_flag.ensure(nc));
+        VS_TRY(h->d_flag.ensure(2 * nc));
         VS_HIP(launch_rs_chained(h->c_off2.as<uint64_t>(), nc, (uint64_t)h->blength,
                                  h->d_flag.as<uint8_t>(), h->stream));
         h->h_flag.resize(nc);
-        VS_HIP(hipMemcpyAsync(h->h_flag.data(), h->d_flag.p, nc, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync(h->h_flag.data(), h->d_flag.as<uint8_t>() + nc, nc,
+                              hipMemcpyDeviceToHost, h->stream));
         VS_HIP(hipStreamSynchronize(h->stream));
         const uint8_t *fl = h->h_flag.data();
         for (size_t c = 0; c < nc; ++c)
