@@ -201,7 +201,32 @@ struct WalkState {
     size_t c = 0;
     size_t nout = 0;
     int64_t false_alarms = 0;
+    int64_t end_false_alarms = 0;  // at the end of the (optimistic) walk
 };
+
+// After the walk's needs were hashed: did any of them strong-match a table
+// entry the walk would have compared it with?  If none did, treating each as
+// a non-match was exactly rsync's decision, so the walk's output stands and
+// only its false-alarm count lacks their compares (`extra_fa`).
+bool needs_match(vs_rsync *h, int64_t len, const std::vector<uint64_t> &off,
+                 const std::vector<uint32_t> &sum, const std::vector<uint8_t> &strong,
+                 const std::vector<uint64_t> &need, int64_t *extra_fa) {
+    const uint32_t s2 = (uint32_t)h->s2length;
+    int64_t fa = 0;
+    for (const uint64_t c : need) {
+        const int64_t k = std::min<int64_t>(h->blength, len - (int64_t)off[c]);
+        const uint32_t s = sum[c];
+        for (int64_t q = group_start(h, s); q >= 0 && q < h->count && (uint32_t)(h->tkey_h[q] >> 32) == s;
+             ++q) {
+            const int32_t i = (int32_t)~(uint32_t)h->tkey_h[q];
+            if (blen(h, i) != k) continue;
+            if (memcmp(strong.data() + c * s2, h->sum2.data() + (size_t)i * s2, s2) == 0) return true;
+            ++fa;
+        }
+    }
+    *extra_fa = fa;
+    return false;
+}
 
 // match.c hash_search over the sorted candidates, from state `st`.  A
 // candidate whose strong sum is unknown is treated as a non-match and
@@ -272,6 +297,7 @@ void walk(vs_rsync *h, int64_t len, const std::vector<uint64_t> &off,
         }
     }
     st = resume_set ? resume : WalkState{offset, want_i, c, out.size(), false_alarms};
+    st.end_false_alarms = false_alarms;
 }
 
 // strong sums of candidate windows idx[] on the device -> strong/known
@@ -429,10 +455,26 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
         VS_TRY(verify(h, dev_src, len, off, batch, known, strong));
         t_ver += now_ms() - tv;
         ++h->st_rounds;
-        batch.clear();
         double tw = now_ms();
+        int64_t extra_fa = 0;
+        if (h->st_rounds > 1 && !needs_match(h, len, off, sum, strong, batch, &extra_fa)) {
+            // every need was a false alarm: no replay (out holds the whole walk)
+            ws.false_alarms = ws.end_false_alarms + extra_fa;
+            t_walk += now_ms() - tw;
+            break;
+        }
+        batch.clear();
         walk(h, len, off, sum, known, strong, batch, out, ws);
         t_walk += now_ms() - tw;
+        if (trace && !batch.empty()) {
+            const uint64_t b0 = batch[0];
+            fprintf(stderr,
+                    "rs: round %d needs %zu (resume c=%zu of %llu, offset %lld; first need "
+                    "c=%llu off=%llu chained=%d)\n",
+                    h->st_rounds, batch.size(), ws.c, (unsigned long long)nc,
+                    (long long)ws.offset, (unsigned long long)b0,
+                    (unsigned long long)off[b0], (int)h->h_flag[b0]);
+        }
         if (batch.empty()) break;
     }
     h->ms[3] = t_ver;
