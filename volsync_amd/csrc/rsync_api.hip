@@ -30,6 +30,38 @@
 
 using namespace vsgpu;
 
+// Page-locks a host vector's storage for the candidate read-backs (≈ 115 MB
+// at C4 shape; a pageable copy goes through staging buffers at a fraction of
+// the link rate).  Re-registered only when the vector's storage moves.
+struct HostReg {
+    void *p = nullptr;
+    size_t n = 0;
+    template <typename T>
+    hipError_t cover(std::vector<T> &v) {
+        const size_t bytes = v.capacity() * sizeof(T);
+        if (!bytes || (v.data() == p && bytes <= n)) return hipSuccess;
+        release();
+        if (hipHostRegister(v.data(), bytes, hipHostRegisterDefault) == hipSuccess) {
+            p = v.data();
+            n = bytes;
+        } else {
+            (void)hipGetLastError();  // not fatal: the copy stays pageable
+        }
+        return hipSuccess;
+    }
+    // before the vector may reallocate (its old pages must not stay registered)
+    template <typename T>
+    void grow(std::vector<T> &v, size_t count) {
+        if (count > v.capacity()) release();
+        v.resize(count);
+    }
+    void release() {
+        if (p) (void)hipHostUnregister(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
 struct vs_rsync {
     int device = 0;
     int cus = 256;
@@ -56,6 +88,7 @@ struct vs_rsync {
     std::vector<uint32_t> h_sum;
     std::vector<uint8_t> h_known, h_strong, h_flag;
     DevBuf d_flag;
+    HostReg reg_off, reg_sum, reg_flag;
     std::vector<vs_match> h_out;
     int64_t st_cand = 0, st_fa = 0, st_hashed = 0;
     int32_t st_rounds = 0;
@@ -405,8 +438,8 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
     // fresh vectors per call (C4 shape) cost ~100 ms
     std::vector<uint64_t> &off = h->h_off;
     std::vector<uint32_t> &sum = h->h_sum;
-    off.resize(nc);
-    sum.resize(nc);
+    h->reg_off.grow(off, nc);
+    h->reg_sum.grow(sum, nc);
     if (nc) {
         VS_TRY(h->c_off2.ensure(nc * 8));
         VS_TRY(h->c_sum2.ensure(nc * 4));
@@ -415,6 +448,8 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
         VS_HIP(launch_rs_sort_cands(h->sort_tmp.p, h->sort_tmp.cap, h->c_off.as<uint64_t>(),
                                     h->c_off2.as<uint64_t>(), h->c_sum.as<uint32_t>(),
                                     h->c_sum2.as<uint32_t>(), nc, end_bit, h->stream));
+        VS_HIP(h->reg_off.cover(off));
+        VS_HIP(h->reg_sum.cover(sum));
         VS_HIP(hipMemcpyAsync(off.data(), h->c_off2.p, nc * 8, hipMemcpyDeviceToHost, h->stream));
         VS_HIP(hipMemcpyAsync(sum.data(), h->c_sum2.p, nc * 4, hipMemcpyDeviceToHost, h->stream));
         VS_HIP(hipStreamSynchronize(h->stream));
@@ -437,7 +472,8 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
         VS_TRY(h->d_flag.ensure(2 * nc));
         VS_HIP(launch_rs_chained(h->c_off2.as<uint64_t>(), nc, (uint64_t)h->blength,
                                  h->d_flag.as<uint8_t>(), h->stream));
-        h->h_flag.resize(nc);
+        h->reg_flag.grow(h->h_flag, nc);
+        VS_HIP(h->reg_flag.cover(h->h_flag));
         VS_HIP(hipMemcpyAsync(h->h_flag.data(), h->d_flag.as<uint8_t>() + nc, nc,
                               hipMemcpyDeviceToHost, h->stream));
         VS_HIP(hipStreamSynchronize(h->stream));
@@ -531,6 +567,7 @@ VS_API void vs_rsync_close(vs_rsync *h) {
                       &h->d_flag})
         b->release();
     if (h->pinned) (void)hipHostFree(h->pinned);
+    for (HostReg *r : {&h->reg_off, &h->reg_sum, &h->reg_flag}) r->release();
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
 }
