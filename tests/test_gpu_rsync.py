@@ -111,6 +111,17 @@ def test_weak_collisions_and_false_alarms(gpu):
         want, fa = O.rsync_match(src, c1, c2, bl, rem, csum_type, seed)
         s = SumStruct(0, cnt, bl, s2l, rem, c1, c2)
         assert match_sums(src, s, csum_type, seed) == want
+        # device-resident source through a Matcher: the false-alarm count too
+        # (the no-replay branch completes it from the round-1 needs' compares)
+        import torch
+        from volsync_amd import Matcher
+        ds = torch.from_numpy(src.copy()).to("cuda")
+        m = Matcher()
+        m.load_sums(s, csum_type, seed)
+        assert m.match_sums(ds.data_ptr(), len(src)) == want
+        st = m.stats()
+        m.close()
+        assert st["false_alarms"] == fa
 
 
 def test_repeated_blocks_prefer_adjacent(gpu):
