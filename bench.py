@@ -360,6 +360,125 @@ def smallfiles_main(args):
         dist.destroy_process_group()
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """--gpus N > 1 without a torch.distributed launcher around us: start
+    `torch.distributed.run --nproc-per-node N` on this same command line as a
+    CHILD process (before anything here touches the GPU), wait for it and
+    return its exit code.  Rank 0 of the child prints the JSON line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+class DryChunker:
+    """--dry: a stand-in for the device chunker with the same scan / stitch /
+    finish surface, so the REAL multi-rank protocol (volsync_amd/shard.py) and
+    its collectives run over gloo on CPU.  Candidate cut positions are a
+    position-independent pseudo-random function of the byte offset (one per
+    ~avg bytes, like the fingerprint's), and the min/max rule of Chunker.Next
+    selects among them.  It computes no fingerprints and no hashes: it
+    rehearses the launcher, the rendezvous and the exit exchange, nothing
+    else (value is reported as null)."""
+
+    def __init__(self, mn: int, mx: int, avg: int):
+        self.mn, self.mx, self.avg = mn, mx, avg
+
+    def _cands(self, lo: int, hi: int):
+        import numpy as np
+        blk = 1 << 20
+        out = []
+        for b in range(lo // blk, (hi + blk - 1) // blk):
+            rng = np.random.default_rng([77, b])
+            k = rng.poisson(blk / self.avg)
+            pos = np.sort(rng.integers(0, blk, k)) + b * blk
+            out.append(pos[(pos >= lo) & (pos < hi)])
+        return np.concatenate(out) if out else np.zeros(0, np.int64)
+
+    def scan(self, ptr, length, origin, own_lo, own_hi, final):
+        self.own_lo, self.own_hi, self.end = own_lo, own_hi, origin + length
+        self.final = final
+        self.scan_end = min(own_hi + self.mx - 1, self.end)
+        self.c = self._cands(own_lo, self.scan_end)
+
+    def stitch(self, entry):
+        import numpy as np
+        self.cuts, s = [], entry
+        while s < self.own_hi and s < self.end:
+            k = int(np.searchsorted(self.c, s + self.mn - 1))
+            if k < len(self.c) and self.c[k] <= s + self.mx - 1:
+                cut = int(self.c[k])
+            elif s + self.mx - 1 < self.scan_end:
+                cut = s + self.mx - 1
+            else:
+                cut = self.end - 1
+            self.cuts.append((s, cut))
+            s = cut + 1
+        return s, True
+
+    def finish(self):
+        return len(self.cuts)
+
+
+def dry_main(args):
+    """Multi-rank rehearsal on CPU (gloo): shard specs of the C3 shape at
+    --per-gpu-gib per rank, the scan / exit all-gather / re-stitch protocol
+    with DryChunker, and the same chunk list checked against one rank doing
+    the whole volume.  Prints the bench JSON shape with value null."""
+    import torch.distributed as dist
+    from volsync_amd.shard import ShardSpec, run_shard, torch_collectives
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    per = int(args.per_gpu_gib * (1 << 30))
+    total = per * world
+    mn, mx = 512 << 10, 8 << 20
+    spec = ShardSpec.for_rank(total, world, rank, mx)
+    h = DryChunker(mn, mx, 1 << 20)
+    st = {}
+    t0 = time.perf_counter()
+    if world > 1:
+        run_shard(h, spec, 0, *torch_collectives(None), stats=st)
+        parts = [None] * world
+        dist.all_gather_object(parts, h.cuts)
+        mine = [c for p in parts for c in p]
+    else:
+        h.scan(0, spec.data_hi - spec.data_lo, spec.data_lo, spec.own_lo, spec.own_hi, True)
+        h.stitch(spec.own_lo)
+        mine = h.cuts
+    dt = time.perf_counter() - t0
+    if rank == 0:
+        ref = DryChunker(mn, mx, 1 << 20)
+        ref.scan(0, total, 0, 0, total, True)
+        ref.stitch(0)
+        out = {"metric": "GB/s chunked+SHA-256 (restic CDC)", "value": None, "unit": "GB/s",
+               "n_gpus": world, "steps": 0, "warmup": 0, "ms_per_step": round(dt * 1e3, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+               "data": "dry run: no GPU, no fingerprints or hashes (protocol rehearsal)",
+               "dry": True,
+               "config": {"workload": f"C3-shape: {total >> 30} GiB volume byte-range sharded "
+                                      f"over {world} ranks ({per >> 30} GiB per rank)",
+                          "per_gpu_bytes": per, "parallelism": f"byte-range shards x{world}"},
+               "world_size": dist.get_world_size() if world > 1 else 1,
+               "backend": "gloo" if world > 1 else None,
+               "exchange_rounds": st.get("exchange_rounds", 0),
+               "chunks": len(mine), "protocol_matches_single_rank": mine == ref.cuts}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -383,7 +502,15 @@ def main():
                     help="cdc: C2/C3 chunk+hash (the BASELINE metric); rsync: C4-shape delta "
                          "match; smallfiles: C5 per-file blob IDs")
     ap.add_argument("--files", type=int, default=1_000_000, help="smallfiles: files per GPU")
+    ap.add_argument("--dry", action="store_true",
+                    help="CPU/gloo rehearsal of the multi-rank protocol (no GPU; value null)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # not under a launcher: become one (a child process, started before
+        # this process has touched the GPU)
+        sys.exit(launch_ranks(args.gpus))
+    if args.dry:
+        return dry_main(args)
     if args.mode == "rsync":
         return rsync_main(args)
     if args.mode == "smallfiles":
@@ -420,6 +547,7 @@ def main():
         dc.set_stream(one.cuda_stream)
         dc.set_hash_stream(one.cuda_stream)
     coll = torch_collectives(dev) if world > 1 else None
+    xst = {}
 
     def step():
         # one volume pass: fingerprint + cut selection + Cut values on the main
@@ -429,7 +557,7 @@ def main():
         if world == 1:
             n, _ = dc.process(buf.data_ptr(), dlen, 0, True)
         else:
-            n = run_shard(dc, spec, buf.data_ptr(), *coll)
+            n = run_shard(dc, spec, buf.data_ptr(), *coll, stats=xst)
         return n
 
     for _ in range(args.warmup):
@@ -529,7 +657,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic (splitmix64 volume image, device-resident)",
             "config": {"workload": "C2: 64 GiB volume, restic CDC + SHA-256, 1 GPU" if world == 1
-                       else f"C3-shape: {total >> 30} GiB volume byte-range sharded over {world} GPUs",
+                       else f"C3-shape: {total >> 30} GiB volume byte-range sharded over {world} "
+                            f"GPUs ({per >> 30} GiB per GPU)",
                        "volume_bytes": total, "per_gpu_bytes": per, "chunks": nch,
                        "pol": "0x3DA3358B4DC173", "min": MinSize, "max": MaxSize, "avg_bits": 20,
                        "parallelism": f"byte-range shards x{world}"},
@@ -544,6 +673,8 @@ def main():
             "hash_stream": args.hash_stream,
             "hash_wide": args.hash_wide, "wide_drain": args.wide_drain,
             "sha_slices": launches[2],
+            "rccl_world_size": dist.get_world_size() if world > 1 else 1,
+            "exchange_rounds_last_step": xst.get("exchange_rounds", 0),
             "single_volume": {"ms": round(lat * 1e3, 2),
                               "GBps": round(total / lat / 1e9, 2),
                               "stages_ms": iso},

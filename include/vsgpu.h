@@ -194,6 +194,11 @@ int vs_rsync_sizes(int64_t len, int32_t block_size, int32_t *blength, int32_t *s
 
 typedef struct vs_rsync vs_rsync;
 int vs_rsync_open(int device, vs_rsync **h);
+/* Ordering: with the handle's own stream (default) every call that reads or
+ * writes caller device memory first waits for work already queued on the null
+ * stream (e.g. the fill of dev_sum1 or the kernel that wrote the source); with
+ * vs_rsync_set_stream the caller's stream must already order those producers
+ * before the call. */
 int vs_rsync_set_stream(vs_rsync *h, void *hip_stream); /* NULL = handle's own stream */
 void vs_rsync_close(vs_rsync *h);
 /* Replaces generator.c generate_and_send_sums (get_checksum1 + get_checksum2

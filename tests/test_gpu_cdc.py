@@ -338,3 +338,24 @@ def test_wide_mode_blobs_vs_hashlib(gpu, drain):
     raw = buf.tobytes()
     for i, (o, n) in enumerate(zip(offs, lens)):
         assert bytes(got[i]) == hashlib.sha256(raw[o:o + n]).digest(), (i, o, n)
+
+
+def test_reset_drains_queued_chains(gpu):
+    """ADVICE r1: vs_cdc_reset to a different max_size changes the ring length;
+    chains that an earlier batch left queued in the time-sliced engine (budget
+    3 blocks, no wait) must be hashed to the end before the slots are released,
+    else their next slice writes blob IDs into freed memory.  The batch after
+    the reset must equal the oracle."""
+    from volsync_amd import DeviceChunker
+    mn, ab = 8192, 13
+    dc = DeviceChunker(P.TEST_POL, mn, 1 << 17, ab)
+    dc.set_hash_slice(3)
+    a = O.synth(401, 0, (6 << 20) + 31)
+    ta = to_dev(a)
+    dc.process(ta.data_ptr(), len(a), 0, True)     # no wait: chains stay queued
+    dc.reset(P.TEST_POL, mn, 1 << 19, ab)          # ring length changes with max_size
+    b = O.synth(402, 0, (5 << 20) + 77)
+    assert dev_chunks(b, P.TEST_POL, mn, 1 << 19, ab, dc=dc) == \
+        O.cdc_hash(b, P.TEST_POL, mn, 1 << 19, ab)
+    dc.close()
+    del ta

@@ -239,11 +239,11 @@ def test_block_sharded_signatures_on_device(gpu, world, n, block_size):
     for sh, s1, s2, _ in pieces:
         def fake_gather(out, t, sh=sh):
             # stands in for dist.all_gather: every rank's padded contribution
-            kind = "s1" if t.dtype == torch.int32 else "s2"
-            contrib.setdefault(kind, {})[sh.rank] = t.clone()
-            if len(contrib[kind]) == world:
+            # (one packed record per rank); the last rank sees them all
+            contrib[sh.rank] = t.clone()
+            if len(contrib) == world:
                 for r in range(world):
-                    out[r].copy_(contrib[kind][r])
+                    out[r].copy_(contrib[r])
         f1, f2 = gather_sums(s1, s2, sh, hdr.s2length, fake_gather)
     c1, c2 = O.rsync_signatures(basis, hdr.blength, hdr.s2length, csum, seed)
     assert (f1.cpu().numpy().view(np.uint32) == c1).all()

@@ -195,6 +195,12 @@ class DeviceChunker:
     def handle(self):
         return self._h
 
+    def reset(self, pol: int = TestPol, min_size: int = MinSize, max_size: int = MaxSize,
+              avg_bits: int = AverageBits) -> None:
+        """Chunker.ResetWithBoundaries + SetAverageBits on the same device buffers
+        (finishes hashing every queued batch first)."""
+        check(lib.vs_cdc_reset(self._h, int(pol), int(min_size), int(max_size), int(avg_bits)))
+
     def set_stream(self, hip_stream: int) -> None:
         check(lib.vs_cdc_set_stream(self._h, ctypes.c_void_p(hip_stream or None)))
 

@@ -241,6 +241,9 @@ static int size_ring(vs_cdc *h) {
     // (= batches) after its own, so L + 2 slots never make the host wait
     const size_t want = (size_t)std::min<uint64_t>(L + 2, 256);
     if (h->slots.size() != want) {
+        // budgeted chains of earlier batches still point into the old slots'
+        // id arrays: hash them to the end before the slots are released
+        VS_TRY(drain_hash(h));
         VS_TRY(sync_stream(h, true));
         for (auto &s : h->slots) {
             s.start.release();
@@ -703,6 +706,10 @@ VS_API int vs_cdc_reset(vs_cdc *h, uint64_t pol, uint32_t min_size, uint32_t max
                         uint32_t avg_bits) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
     VS_TRY(set_dev(h));
+    // drain the hash engine first: chains queued by earlier batches still
+    // write blob IDs into their ring slots, which size_ring() releases when
+    // the new max_size changes the ring length
+    VS_TRY(cdc_wait(h));
     VS_TRY(set_params(h, pol, min_size, max_size, avg_bits));
     h->state = 0;
     h->ready.clear();

@@ -32,20 +32,25 @@ using namespace vsgpu;
 
 // Page-locks a host vector's storage for the candidate read-backs (≈ 115 MB
 // at C4 shape; a pageable copy goes through staging buffers at a fraction of
-// the link rate).  Re-registered only when the vector's storage moves.
+// the link rate).  Re-registered only when the vector's storage moves.  A
+// failed registration (e.g. hipErrorHostMemoryAlreadyRegistered when a small
+// vector shares a page with a registered one) is remembered for that storage,
+// so it is not retried on every call: the copy just stays pageable.
 struct HostReg {
     void *p = nullptr;
     size_t n = 0;
+    bool registered = false;
     template <typename T>
     hipError_t cover(std::vector<T> &v) {
         const size_t bytes = v.capacity() * sizeof(T);
         if (!bytes || (v.data() == p && bytes <= n)) return hipSuccess;
         release();
+        p = v.data();
+        n = bytes;
         if (hipHostRegister(v.data(), bytes, hipHostRegisterDefault) == hipSuccess) {
-            p = v.data();
-            n = bytes;
+            registered = true;
         } else {
-            (void)hipGetLastError();  // not fatal: the copy stays pageable
+            (void)hipGetLastError();  // not fatal; remembered until the storage moves
         }
         return hipSuccess;
     }
@@ -56,7 +61,8 @@ struct HostReg {
         v.resize(count);
     }
     void release() {
-        if (p) (void)hipHostUnregister(p);
+        if (registered) (void)hipHostUnregister(p);
+        registered = false;
         p = nullptr;
         n = 0;
     }
@@ -66,6 +72,7 @@ struct vs_rsync {
     int device = 0;
     int cus = 256;
     hipStream_t own = nullptr, stream = nullptr;
+    hipEvent_t ev_null = nullptr;   // orders own-stream work after null-stream work
     // signature table
     bool loaded = false;
     int32_t count = 0, blength = 0, s2length = 0, remainder = 0;
@@ -103,6 +110,17 @@ int rs_dev(vs_rsync *h) {
         (void)hipGetLastError();
         return fail(VS_ERR_NO_DEVICE, "hipSetDevice failed");
     }
+    return 0;
+}
+
+// The handle's own stream is non-blocking: an entry point that reads or
+// writes caller device memory first waits for work the caller queued on the
+// null stream (e.g. torch's zero-fill of the output, or the cat that built the
+// table).  With vs_rsync_set_stream the caller's stream carries that order.
+int order_after_null(vs_rsync *h) {
+    if (h->stream != h->own) return 0;
+    VS_HIP(hipEventRecord(h->ev_null, nullptr));
+    VS_HIP(hipStreamWaitEvent(h->stream, h->ev_null, 0));
     return 0;
 }
 
@@ -378,6 +396,7 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
     if (n_matches) *n_matches = 0;
     if (len == 0 || h->count == 0) return 0;  // match_sums: no sums -> all literal
     const double t0 = now_ms();
+    VS_TRY(order_after_null(h));
     // 1. coarse prefixes
     const uint64_t nblk = ((uint64_t)len + kRsG - 1) / kRsG;
     VS_TRY(h->px.ensure(nblk * 4));
@@ -541,6 +560,7 @@ VS_API int vs_rsync_open(int device, vs_rsync **out) {
     h->device = device;
     (void)hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (rs_dev(h) < 0 || hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_null, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void **)&h->pinned, 64, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         vs_rsync_close(h);
@@ -568,6 +588,7 @@ VS_API void vs_rsync_close(vs_rsync *h) {
         b->release();
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (HostReg *r : {&h->reg_off, &h->reg_sum, &h->reg_flag}) r->release();
+    if (h->ev_null) (void)hipEventDestroy(h->ev_null);
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
 }
@@ -594,6 +615,7 @@ VS_API int vs_rsync_signatures_device(vs_rsync *h, const void *dev_basis, int64_
     a.sum1 = dev_sum1;
     a.sum2 = dev_sum2;
     const double t0 = now_ms();
+    VS_TRY(order_after_null(h));
     VS_HIP(launch_rs_signatures(a, h->stream));
     VS_HIP(hipStreamSynchronize(h->stream));
     h->ms[0] = now_ms() - t0;
@@ -631,6 +653,7 @@ VS_API int vs_rsync_load_sums_device(vs_rsync *h, int32_t count, int32_t blength
     h->sum1.resize(count);
     h->sum2.resize((size_t)count * s2length);
     VS_TRY(h->d_sum1.ensure((size_t)std::max(count, 1) * 4));
+    VS_TRY(order_after_null(h));
     if (count) {
         VS_HIP(hipMemcpyAsync(h->d_sum1.p, dev_sum1, (size_t)count * 4, hipMemcpyDeviceToDevice,
                               h->stream));

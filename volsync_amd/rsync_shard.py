@@ -61,17 +61,16 @@ def gather_sums(sum1, sum2, shard: BlockShard, s2length: int,
     Ranks own unequal block counts, so each contribution is padded to the
     largest; the padding is dropped when the pieces are concatenated."""
     import torch
-    m = shard.max_blocks()
+    m = max(shard.max_blocks(), 1)
     dev = sum1.device
-    p1 = torch.zeros(max(m, 1), dtype=sum1.dtype, device=dev)
-    p2 = torch.zeros(max(m, 1) * s2length, dtype=sum2.dtype, device=dev)
-    p1[: shard.blocks] = sum1[: shard.blocks]
-    p2[: shard.blocks * s2length] = sum2[: shard.blocks * s2length]
-    g1 = [torch.empty_like(p1) for _ in range(shard.world)]
-    g2 = [torch.empty_like(p2) for _ in range(shard.world)]
-    all_gather(g1, p1)
-    all_gather(g2, p2)
+    # one packed byte record per rank -- [m x sum1 (4 B LE)] [m x s2length] --
+    # so the table travels in ONE collective
+    rec = torch.zeros(m * (4 + s2length), dtype=torch.uint8, device=dev)
+    rec[: shard.blocks * 4] = sum1[: shard.blocks].contiguous().view(torch.uint8)
+    rec[m * 4: m * 4 + shard.blocks * s2length] = sum2[: shard.blocks * s2length]
+    g = [torch.empty_like(rec) for _ in range(shard.world)]
+    all_gather(g, rec)
     parts = BlockShard.split(shard.length, shard.blength, shard.world)
-    full1 = torch.cat([g1[r][: s.blocks] for r, s in enumerate(parts)])
-    full2 = torch.cat([g2[r][: s.blocks * s2length] for r, s in enumerate(parts)])
+    full1 = torch.cat([g[r][: s.blocks * 4] for r, s in enumerate(parts)]).view(sum1.dtype)
+    full2 = torch.cat([g[r][m * 4: m * 4 + s.blocks * s2length] for r, s in enumerate(parts)])
     return full1, full2

@@ -83,23 +83,31 @@ def run_shards_local(handles: Sequence, specs: Sequence[ShardSpec], ptrs: Sequen
     return out
 
 
-def run_shard(h, spec: ShardSpec, ptr: int, allgather_u64, allreduce_sum) -> int:
+def run_shard(h, spec: ShardSpec, ptr: int, allgather_u64, allreduce_sum,
+              stats: dict = None) -> int:
     """Distributed version: this rank's part.  allgather_u64(x) -> list of all
     ranks' x; allreduce_sum(x) -> sum.  Returns this rank's chunk count (read
-    them with h.chunks(0, n))."""
+    them with h.chunks(0, n)); stats (optional) receives the exchange rounds
+    and this rank's re-stitches."""
     _scan(h, spec, ptr)
     entry = spec.own_lo
     ex = h.stitch(entry)[0]
+    rounds = restitches = 0
     for _ in range(spec.world + 2):
         gathered = allgather_u64(ex)
+        rounds += 1
         want = spec.own_lo if spec.rank == 0 else int(gathered[spec.rank - 1])
         moved = 0
         if want != entry:
             entry = want
             ex = h.stitch(entry)[0]
             moved = 1
+            restitches += 1
         if allreduce_sum(moved) == 0:
             break
+    if stats is not None:
+        stats["exchange_rounds"] = rounds
+        stats["restitches"] = restitches
     return h.finish()
 
 
