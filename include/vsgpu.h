@@ -222,6 +222,27 @@ int vs_rsync_load_sums_device(vs_rsync *h, int32_t count, int32_t blength, int32
  * including chain order, the want_i preference and false-alarm handling).
  * Blocks until done; *n_matches = number of matches. */
 int vs_rsync_match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_matches);
+/* Sharded match_sums: one hash_search over a source file of
+ * file_len bytes, split by byte range across devices/handles.  This handle
+ * owns the walk's visits to offsets [own_lo, own_hi); dev_src points at file
+ * offset `origin` (<= own_lo) and holds len bytes covering
+ * [own_lo, min(own_hi + blength - 1, file_len)).  match_scan finds the
+ * candidates and walks the range speculatively from own_lo (want_i 0 when
+ * own_lo == 0, as hash_search starts; otherwise "no preference"), returning
+ * that walk's exit state: the first offset >= own_hi it would visit, and
+ * want_i there.  match_stitch re-walks from the true entry (the previous
+ * range's exit) until it rejoins the speculative walk and returns the new
+ * exit; it may be called again with another entry.  match_finish makes the
+ * walk from the last entry given (the speculative one if none) the result:
+ * matches with offsets in [entry, own_hi), file offsets, in order.  The
+ * ranges' results concatenated equal one vs_rsync_match_device over the
+ * whole file, false-alarm counts included (vs_rsync_stats). */
+int vs_rsync_match_scan(vs_rsync *h, const void *dev_src, int64_t len, int64_t origin,
+                        int64_t file_len, int64_t own_lo, int64_t own_hi, int64_t *exit_off,
+                        int32_t *exit_want);
+int vs_rsync_match_stitch(vs_rsync *h, int64_t entry, int32_t want_i, int64_t *exit_off,
+                          int32_t *exit_want);
+int vs_rsync_match_finish(vs_rsync *h, int64_t *n_matches);
 /* Copy matches [first, first+n) of the last match run to host. */
 int vs_rsync_get_matches(vs_rsync *h, int64_t first, int64_t n, vs_match *out);
 /* Counters of the last match run: weak candidates found by the scan,

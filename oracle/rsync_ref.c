@@ -327,3 +327,114 @@ int64_t ref_rsync_match(const uint8_t *src, int64_t len, int32_t count, int32_t 
     if (false_alarms) *false_alarms = fa;
     return nm;
 }
+
+/* ------------------------------------------------------------------ */
+/* hash_search restricted to one shard of the source (multi-GPU walk  */
+/* stitch).  TEST INFRASTRUCTURE: the checker of the     */
+/* sharded device walk, and the test double of the gloo protocol.     */
+/* ------------------------------------------------------------------ */
+/* The greedy walk of hash_search (above), started from the state (entry,
+ * want_i) instead of (0, 0), over the offsets of [entry, hi): it visits
+ * offset o iff o < hi and (o < end or o == 0) -- the do-while visits offset 0
+ * unconditionally -- and stops at the first offset >= hi.  *exit_off /
+ * *exit_want = that state (exit_off = hi when the walk ran out at `end`), which
+ * is the next shard's entry.  win points at file offset win_lo and must cover
+ * [entry, min(hi + blength - 1, len)).  Offsets are file offsets; len is the
+ * whole source file's length.  Matches with offset in [entry, hi) are
+ * emitted in order; returns #matches or -1.  Walking [0, len) from (0, 0)
+ * reproduces ref_rsync_match exactly. */
+int64_t ref_rsync_walk(const uint8_t *win, int64_t win_lo, int64_t len, int64_t hi, int64_t entry,
+                       int32_t entry_want, int32_t count, int32_t blength, int32_t remainder,
+                       int32_t s2length, const uint32_t *sum1, const uint8_t *sum2, int csum_type,
+                       uint32_t seed, int64_t *m_off, int32_t *m_idx, int64_t cap,
+                       int64_t *false_alarms, int64_t *exit_off, int32_t *exit_want) {
+    int64_t nm = 0, fa = 0;
+    *exit_off = entry > hi ? entry : hi;
+    *exit_want = entry_want;
+    if (false_alarms) *false_alarms = 0;
+    if (len <= 0 || count <= 0 || entry >= hi) return 0;
+#define BLEN(i) (((i) == count - 1 && remainder) ? remainder : blength)
+    const int64_t end = len + 1 - BLEN(count - 1);
+    if (!(entry < end || entry == 0)) return 0;
+    uint32_t tablesize = (uint32_t)(count / 8) * 10 + 11;
+    const int trad = tablesize < (1u << 16);
+    if (trad) tablesize = 1u << 16;
+    int32_t *table = (int32_t *)malloc(sizeof(int32_t) * tablesize);
+    int32_t *chain = (int32_t *)malloc(sizeof(int32_t) * (size_t)count);
+    if (!table || !chain) { free(table); free(chain); return -1; }
+    memset(table, 0xff, sizeof(int32_t) * tablesize);
+    for (int32_t i = 0; i < count; ++i) {
+        uint32_t t = trad ? (((sum1[i] & 0xffff) + (sum1[i] >> 16)) & 0xffff) : sum1[i] % tablesize;
+        chain[i] = table[t];
+        table[t] = i;
+    }
+    const int8_t *map = (const int8_t *)(win - win_lo);   /* indexed by file offset */
+    int32_t want_i = entry_want;
+    int64_t offset = entry;
+    int64_t k = (len - offset < blength) ? len - offset : blength;
+    uint32_t sum = ref_rsync_checksum1((const uint8_t *)map + offset, (int32_t)k);
+    uint32_t s1 = sum & 0xffff, s2 = sum >> 16;
+    uint8_t sum2buf[16];
+    for (;;) {
+        int done_csum2 = 0;
+        int32_t i;
+        sum = (s1 & 0xffff) | (s2 << 16);
+        uint32_t hash_entry = trad ? ((s1 + s2) & 0xffff) : sum % tablesize;
+        if ((i = table[hash_entry]) < 0) goto null_hash;
+        do {
+            if (sum != sum1[i]) continue;
+            int32_t l = (int32_t)((len - offset < blength) ? len - offset : blength);
+            if (l != BLEN(i)) continue;
+            if (!done_csum2) {
+                if (ref_rsync_checksum2((const uint8_t *)map + offset, l, csum_type, seed,
+                                        sum2buf) < 0) {
+                    free(table); free(chain); return -1;
+                }
+                done_csum2 = 1;
+            }
+            if (memcmp(sum2buf, sum2 + (int64_t)i * s2length, (size_t)s2length) != 0) {
+                fa++;
+                continue;
+            }
+            if (i != want_i && want_i < count && sum == sum1[want_i] &&
+                memcmp(sum2buf, sum2 + (int64_t)want_i * s2length, (size_t)s2length) == 0)
+                i = want_i;
+            want_i = i + 1;
+            if (nm < cap) { m_off[nm] = offset; m_idx[nm] = i; }
+            nm++;
+            offset += BLEN(i) - 1;
+            if (offset + 1 >= hi || offset + 1 >= end) {   /* next visit is past the shard */
+                ++offset;
+                goto done;
+            }
+            k = (len - offset < blength) ? len - offset : blength;
+            sum = ref_rsync_checksum1((const uint8_t *)map + offset, (int32_t)k);
+            s1 = sum & 0xffff;
+            s2 = sum >> 16;
+            break;
+        } while ((i = chain[i]) >= 0);
+    null_hash:;
+        if (offset + 1 >= hi || offset + 1 >= end) {
+            ++offset;
+            goto done;
+        }
+        int more = offset + k < len;
+        s1 -= (uint32_t)(int32_t)map[offset];
+        s2 -= (uint32_t)k * (uint32_t)(int32_t)map[offset];
+        if (more) {
+            s1 += (uint32_t)(int32_t)map[offset + k];
+            s2 += s1;
+        } else {
+            --k;
+        }
+        ++offset;
+    }
+done:
+#undef BLEN
+    free(table);
+    free(chain);
+    *exit_off = offset >= hi ? offset : hi;
+    *exit_want = want_i;
+    if (false_alarms) *false_alarms = fa;
+    return nm;
+}

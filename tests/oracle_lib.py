@@ -141,3 +141,37 @@ def rsync_match(src: np.ndarray, sum1: np.ndarray, sum2: np.ndarray, blength: in
     if n < 0:
         raise RuntimeError("match restatement failed")
     return [(int(mo[i]), int(mi[i])) for i in range(n)], int(fa.value)
+
+
+def rsync_walk(win: np.ndarray, win_lo: int, length: int, hi: int, entry: int, want: int,
+               sum1: np.ndarray, sum2: np.ndarray, blength: int, remainder: int, csum_type: int,
+               seed: int):
+    """hash_search over the shard [entry, hi) of a source of `length` bytes
+    (oracle/rsync_ref.c ref_rsync_walk): (matches, false_alarms, exit_off,
+    exit_want).  win holds file bytes from win_lo."""
+    L = _rs()
+    if not getattr(L, "_walk_ready", False):
+        i64, i32, vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
+        L.ref_rsync_walk.restype = i64
+        L.ref_rsync_walk.argtypes = [vp, i64, i64, i64, i64, i32, i32, i32, i32, i32, vp, vp,
+                                     ctypes.c_int, ctypes.c_uint32, vp, vp, i64,
+                                     ctypes.POINTER(i64), ctypes.POINTER(i64),
+                                     ctypes.POINTER(i32)]
+        L._walk_ready = True
+    count = len(sum1)
+    s2length = sum2.shape[1] if count else 2
+    cap = max(0, hi - entry) // max(1, min(blength, remainder or blength)) + 8
+    mo = np.zeros(cap, np.int64)
+    mi = np.zeros(cap, np.int32)
+    fa, eo, ew = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int32(0)
+    w = np.ascontiguousarray(win, np.uint8)
+    s1 = np.ascontiguousarray(sum1, np.uint32)
+    s2 = np.ascontiguousarray(sum2, np.uint8)
+    n = L.ref_rsync_walk(w.ctypes.data if len(w) else None, win_lo, length, hi, entry, want,
+                         count, blength, remainder, s2length, s1.ctypes.data if count else None,
+                         s2.ctypes.data if count else None, csum_type, seed, mo.ctypes.data,
+                         mi.ctypes.data, cap, ctypes.byref(fa), ctypes.byref(eo),
+                         ctypes.byref(ew))
+    if n < 0:
+        raise RuntimeError("walk restatement failed")
+    return [(int(mo[i]), int(mi[i])) for i in range(n)], int(fa.value), int(eo.value), int(ew.value)

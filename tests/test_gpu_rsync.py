@@ -255,3 +255,113 @@ def test_block_sharded_signatures_on_device(gpu, world, n, block_size):
     got = m.match_sums(ds.data_ptr(), len(src))
     m.close()
     assert got == O.rsync_match(src, c1, c2, hdr.blength, hdr.remainder, csum, seed)[0]
+
+
+def _sharded_device_match(src, hdr_or_sums, world, csum, seed, dev_sums=None):
+    """One Matcher per "rank", each holding ONLY its source window (own range
+    + blength - 1 bytes of right halo) in its own device buffer; the walk
+    stitch runs in one process (run_walk_shards_local, the same Jacobi rounds
+    as the distributed protocol).  Returns (matches, false-alarm total)."""
+    from volsync_amd import Matcher, SumStruct
+    from volsync_amd.rsync_shard import SourceShard, run_walk_shards_local
+    s = hdr_or_sums
+    specs = SourceShard.split(len(src), s.blength, world)
+    hs, bufs = [], []
+    for sp in specs:
+        m = Matcher()
+        m.load_sums(s, csum, seed)
+        bufs.append(to_dev(src[sp.data_lo:sp.data_hi]))
+        hs.append(m)
+    got = run_walk_shards_local(hs, specs, [b.data_ptr() for b in bufs])
+    fa = sum(m.stats()["false_alarms"] for m in hs)
+    for m in hs:
+        m.close()
+    return got, fa
+
+
+@pytest.mark.parametrize("world,n,block_size,csum,seed,frac", [
+    (2, (5 << 20) + 777, 0, R.CSUM_XXH3_128, 0x5EED5EED, 0.10),   # short last block
+    (3, 8 << 20, 1000, R.CSUM_XXH3_128, 1, 0.20),                 # unaligned blocks
+    (5, 6 << 20, 0, R.CSUM_MD5, 0x5EED5EED, 0.10),
+    (8, 3 << 20, 0, R.CSUM_XXH64, 0, 0.30),
+    (7, 2 << 20, 65536, R.CSUM_XXH3_64, 9, 0.05),                 # ranges of ~4.5 blocks
+])
+def test_sharded_walk_on_device(gpu, world, n, block_size, csum, seed, frac):
+    """Byte-range sharded hash_search on the device: matches and false alarms
+    of the concatenated ranges == ONE hash_search over the file (C oracle)."""
+    from volsync_amd import SumStruct
+    basis = O.synth(500 + world, 0, n)
+    bl, s2l, cnt, rem = O.rsync_sizes(n, block_size)
+    c1, c2 = O.rsync_signatures(basis, bl, s2l, csum, seed)
+    src = R.mutate(basis, bl, seed=world, frac=frac)
+    s = SumStruct(n, cnt, bl, s2l, rem, c1, c2)
+    want, fa = O.rsync_match(src, c1, c2, bl, rem, csum, seed)
+    got, gfa = _sharded_device_match(src, s, world, csum, seed)
+    assert got == want
+    assert gfa == fa
+
+
+def test_sharded_walk_boundaries_in_edits_and_duplicates(gpu):
+    """Shard boundaries placed ON edited regions and inside runs of identical
+    blocks (want_i decides), for every boundary offset within one block."""
+    from volsync_amd import SumStruct
+    from volsync_amd import Matcher
+    from volsync_amd.rsync_shard import SourceShard, run_walk_shards_local
+    unit = O.synth(5, 0, 700)
+    basis = np.concatenate([np.tile(unit, 40), O.synth(7, 0, 30_000)])
+    bl, s2l, cnt, rem = O.rsync_sizes(len(basis))
+    c1, c2 = O.rsync_signatures(basis, bl, s2l, R.CSUM_XXH3_128, 77)
+    src = np.concatenate([basis[:7000], O.synth(6, 0, 333), basis[:14000], basis[350:40_000]])
+    want, fa = O.rsync_match(src, c1, c2, bl, rem, R.CSUM_XXH3_128, 77)
+    s = SumStruct(len(basis), cnt, bl, s2l, rem, c1, c2)
+    d = to_dev(src)
+    for cut in list(range(6900, 7400, 37)) + [7000, 7333, 7334, 21_333, 21_334, 22_000]:
+        specs = [SourceShard(0, 2, len(src), bl, 0, cut, 0, min(cut + bl - 1, len(src))),
+                 SourceShard(1, 2, len(src), bl, cut, len(src), cut & ~15, len(src))]
+        hs = []
+        for _ in specs:
+            m = Matcher()
+            m.load_sums(s, R.CSUM_XXH3_128, 77)
+            hs.append(m)
+        got = run_walk_shards_local(hs, specs, [d.data_ptr() + sp.data_lo for sp in specs])
+        gfa = sum(m.stats()["false_alarms"] for m in hs)
+        for m in hs:
+            m.close()
+        assert got == want, cut
+        assert gfa == fa, cut
+
+
+def test_c4_params_exact_1g(gpu):
+    """C4's own matcher parameters -- blength 131072, s2length 5, xxh128,
+    checksum_seed 0x5EED5EED -- on a 1 GiB basis with C4 edits (10 % of the
+    blocks: 4 KiB overwrites, 1-64 B inserts/deletes): the device match list
+    and false-alarm count equal the C hash_search exactly, on one device and
+    byte-range sharded 4 ways."""
+    import torch
+    from volsync_amd import Matcher, SumStruct
+    n, bl, s2l, csum, seed = 1 << 30, 131072, 5, R.CSUM_XXH3_128, 0x5EED5EED
+    basis = O.synth(4, 0, n)
+    src = R.mutate(basis, bl, seed=5, frac=0.10)
+    db = to_dev(basis)
+    cnt, rem = n // bl, 0
+    s1 = torch.zeros(cnt, dtype=torch.int32, device="cuda")
+    s2 = torch.zeros(cnt * s2l, dtype=torch.uint8, device="cuda")
+    m = Matcher()
+    m.signatures_device(db.data_ptr(), n, bl, s2l, csum, seed, s1.data_ptr(), s2.data_ptr())
+    torch.cuda.synchronize()
+    del db
+    c1, c2 = O.rsync_signatures(basis, bl, s2l, csum, seed)
+    assert (s1.cpu().numpy().view(np.uint32) == c1).all()
+    assert (s2.cpu().numpy().reshape(-1, s2l) == c2).all()
+    want, fa = O.rsync_match(src, c1, c2, bl, rem, csum, seed)
+    m.load_sums_device(cnt, bl, s2l, rem, s1.data_ptr(), s2.data_ptr(), csum, seed)
+    ds = to_dev(src)
+    got = m.match_sums(ds.data_ptr(), len(src))
+    st = m.stats()
+    m.close()
+    assert got == want
+    assert st["false_alarms"] == fa
+    del ds
+    s = SumStruct(n, cnt, bl, s2l, rem, c1, c2)
+    got4, fa4 = _sharded_device_match(src, s, 4, csum, seed)
+    assert got4 == want and fa4 == fa

@@ -1,0 +1,126 @@
+"""Multi-rank CPU tests (gloo) of the byte-range sharded hash_search
+(volsync_amd/rsync_shard.py run_walk_shard): speculative walk per rank ->
+all-gather of exit states -> re-walk from the true entry -> finish.
+
+Each rank runs a test double of the device matcher built on the C oracle
+(oracle/rsync_ref.c ref_rsync_walk, test infrastructure) that sees ONLY its
+own byte window (own range + blength - 1 bytes of right halo), so the test
+checks the exchange logic, the want_i hand-over and that the halo suffices.
+The concatenated match list and false-alarm total must equal ONE hash_search
+over the whole file (ref_rsync_match)."""
+import json
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+from oracle import rsync_ref as R
+from tests import oracle_lib as O
+
+
+class OracleWalkRank:
+    """match_scan / match_stitch / match_finish / matches, as volsync_amd.Matcher."""
+
+    def __init__(self, window, sums, blength, remainder, csum, seed):
+        self.w = window
+        self.c1, self.c2 = sums
+        self.bl, self.rem, self.csum, self.seed = blength, remainder, csum, seed
+
+    def _walk(self, entry, want):
+        m, fa, eo, ew = O.rsync_walk(self.w, self.origin, self.length, self.own_hi, entry, want,
+                                     self.c1, self.c2, self.bl, self.rem, self.csum, self.seed)
+        self.m, self.fa = m, fa
+        return eo, ew
+
+    def match_scan(self, ptr, dlen, origin, length, own_lo, own_hi):
+        assert dlen == len(self.w)
+        self.origin, self.length, self.own_lo, self.own_hi = origin, length, own_lo, own_hi
+        # speculative entry: rank 0 starts as hash_search does; the others
+        # with want_i = count ("no preference": want_i < count fails)
+        return self._walk(own_lo, 0 if own_lo == 0 else len(self.c1))
+
+    def match_stitch(self, entry, want):
+        assert entry >= self.own_lo
+        return self._walk(entry, want)
+
+    def match_finish(self):
+        return len(self.m)
+
+    def matches(self, first, n):
+        return self.m[first:first + n]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _case(n, block_size, csum, seed, frac):
+    basis = O.synth(57, 0, n)
+    bl, s2, cnt, rem = O.rsync_sizes(n, block_size)
+    c1, c2 = O.rsync_signatures(basis, bl, s2, csum, seed)
+    src = R.mutate(basis, bl, seed=9, frac=frac)
+    return src, (c1, c2), bl, rem
+
+
+def _worker(rank, world, port, args, outdir):
+    import torch.distributed as dist
+    from volsync_amd.rsync_shard import SourceShard, run_walk_shard, torch_pair_collectives
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, block_size, csum, seed, frac = args
+    src, sums, bl, rem = _case(n, block_size, csum, seed, frac)
+    spec = SourceShard.for_rank(len(src), bl, world, rank)
+    h = OracleWalkRank(src[spec.data_lo:spec.data_hi].copy(), sums, bl, rem, csum, seed)
+    st = {}
+    cnt = run_walk_shard(h, spec, 0, *torch_pair_collectives(None), stats=st)
+    mine = {"m": h.matches(0, cnt), "fa": h.fa, "rounds": st["exchange_rounds"]}
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    if rank == 0:
+        with open(os.path.join(outdir, "result.json"), "w") as f:
+            json.dump(allr, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,args", [
+    (2, ((3 << 20) + 777, 0, R.CSUM_XXH3_128, 0x5EED5EED, 0.10)),   # short last block
+    (3, (1 << 20, 4096, R.CSUM_MD5, 0x5EED5EED, 0.20)),
+    (5, (700 << 10, 8192, R.CSUM_XXH64, 0, 0.10)),                   # ranks of ~17 blocks
+    (4, (300_000, 100_000, R.CSUM_XXH3_128, 3, 0.30)),               # own range < blength
+])
+def test_sharded_walk_gloo(world, args):
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, _free_port(), args, d), nprocs=world, join=True,
+                           start_method="spawn")
+        res = json.load(open(os.path.join(d, "result.json")))
+    got = [tuple(x) for r in res for x in r["m"]]
+    src, (c1, c2), bl, rem = _case(*args)
+    want, fa = O.rsync_match(src, c1, c2, bl, rem, args[2], args[3])
+    assert got == want
+    assert sum(r["fa"] for r in res) == fa
+
+
+@pytest.mark.parametrize("world", [2, 3, 6, 11])
+def test_sharded_walk_local_dup_blocks(world):
+    """Repeated blocks (want_i decides between identical blocks) with the
+    shard boundaries inside runs of duplicates: the want_i hand-over across
+    ranks must reproduce hash_search's choices."""
+    from volsync_amd.rsync_shard import SourceShard, run_walk_shards_local
+    unit = O.synth(5, 0, 700)
+    basis = np.tile(unit, 64)
+    src = np.concatenate([basis[:7000], O.synth(6, 0, 333), basis[:14000], basis[350:9000]])
+    bl, s2, cnt, rem = O.rsync_sizes(len(basis))
+    c1, c2 = O.rsync_signatures(basis, bl, s2, R.CSUM_XXH3_128, 77)
+    specs = SourceShard.split(len(src), bl, world)
+    hs = [OracleWalkRank(src[s.data_lo:s.data_hi].copy(), (c1, c2), bl, rem, R.CSUM_XXH3_128, 77)
+          for s in specs]
+    got = run_walk_shards_local(hs, specs, [0] * world)
+    want, fa = O.rsync_match(src, c1, c2, bl, rem, R.CSUM_XXH3_128, 77)
+    assert got == want
+    assert sum(h.fa for h in hs) == fa

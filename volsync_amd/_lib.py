@@ -116,6 +116,9 @@ def _load() -> ctypes.CDLL:
         "vs_rsync_load_sums": (c_int, [vp, i32, i32, i32, i32, vp, vp, c_int, c_u32]),
         "vs_rsync_load_sums_device": (c_int, [vp, i32, i32, i32, i32, vp, vp, c_int, c_u32]),
         "vs_rsync_match_device": (c_int, [vp, vp, i64, i64p]),
+        "vs_rsync_match_scan": (c_int, [vp, vp, i64, i64, i64, i64, i64, i64p, i32p]),
+        "vs_rsync_match_stitch": (c_int, [vp, i64, i32, i64p, i32p]),
+        "vs_rsync_match_finish": (c_int, [vp, i64p]),
         "vs_rsync_get_matches": (c_int, [vp, i64, i64, ctypes.POINTER(VsMatch)]),
         "vs_rsync_stats": (c_int, [vp, i64p, i64p, i64p, i32p]),
         "vs_rsync_timing": (c_int, [vp, ctypes.POINTER(ctypes.c_double)]),

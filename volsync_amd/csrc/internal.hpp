@@ -244,9 +244,11 @@ hipError_t launch_rs_prefix(const uint8_t *data, uint64_t len, uint32_t *px, uin
                             hipStream_t s);
 
 struct RsScanArgs {
-    const uint8_t *data;   // source bytes
-    uint64_t len;
-    uint64_t nfull;        // offsets with a full blength window: len - blength + 1 (or 0)
+    const uint8_t *data;   // source bytes (data-relative offsets below)
+    uint64_t len;          // readable bytes at data
+    uint64_t lo;           // first offset reported (offsets below lo are skipped)
+    uint64_t nfull;        // end (exclusive) of the full-window offsets reported (<= len - blength + 1)
+    int64_t tail;          // the one shrunk-window offset that can match the short last block, or -1
     uint64_t blength;
     uint32_t count, remainder;
     const uint32_t *px_scan, *pt_scan;

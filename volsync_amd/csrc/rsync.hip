@@ -499,7 +499,7 @@ __device__ __forceinline__ void scan_strip(const RsScanArgs &a, uint64_t k, cons
                 while (hit) {
                     const int j = __builtin_ctz(hit);
                     hit &= hit - 1;
-                    if (o + j < o1 && probe_dir(a, sums[j], true)) {
+                    if (o + j < o1 && o + j >= a.lo && probe_dir(a, sums[j], true)) {
                         const uint32_t slot = atomicAdd(&loc_n, 1u);
                         if (slot < kLocCand) {
                             loc_off[slot] = o + j;
@@ -530,7 +530,7 @@ __device__ __forceinline__ void scan_strip(const RsScanArgs &a, uint64_t k, cons
             while (hit) {
                 const int j = __builtin_ctz(hit);
                 hit &= hit - 1;
-                if (o + j < o1 && probe_dir(a, sums[j], true)) {
+                if (o + j < o1 && o + j >= a.lo && probe_dir(a, sums[j], true)) {
                     const uint32_t slot = atomicAdd(&loc_n, 1u);
                     if (slot < kLocCand) {
                         loc_off[slot] = o + j;
@@ -554,11 +554,12 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_kernel(RsScanArgs a) {
     for (uint32_t i = threadIdx.x; i < lw; i += blockDim.x) lfilt[i] = a.filt_l[i];
     if (threadIdx.x == 0) loc_n = 0;
     __syncthreads();
-    const uint64_t strips = (a.nfull + kRsStrip - 1) / kRsStrip;
+    const uint64_t k0 = a.lo / kRsStrip;
+    const uint64_t strips = (a.nfull + kRsStrip - 1) / kRsStrip - k0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < strips; base += stride) {
         const uint64_t k = base + threadIdx.x;
-        if (k < strips) scan_strip(a, k, lfilt, loc_off, loc_sum, &loc_n);
+        if (k < strips) scan_strip(a, k0 + k, lfilt, loc_off, loc_sum, &loc_n);
         __syncthreads();
         const uint32_t m = min(loc_n, kLocCand);
         if (m) {
@@ -581,12 +582,14 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_kernel(RsScanArgs a) {
 
 // the one shrunk-window offset that can match (the short last block), on one lane
 __global__ void rs_scan_tail_kernel(RsScanArgs a, uint64_t o) {
-    const uint32_t sum = weak_sum(a.data, o, a.len - o, a.len);
+    const uint32_t sum = weak_sum(a.data, o, a.remainder, a.len);
     if (probe_dir(a, sum, false)) emit(a, o, sum);
 }
 
 hipError_t launch_rs_scan(const RsScanArgs &a, int cus, hipStream_t s) {
-    const uint64_t strips = (a.nfull + kRsStrip - 1) / kRsStrip;
+    const uint64_t k0 = a.lo / kRsStrip;
+    const uint64_t kend = (a.nfull + kRsStrip - 1) / kRsStrip;
+    const uint64_t strips = (a.nfull > a.lo) ? kend - k0 : 0;
     if (a.lbits > 20) return hipErrorInvalidValue;  // prefilter larger than its LDS array
     if (strips) {
         // persistent: one workgroup per CU (the 152 KiB of LDS admit one)
@@ -594,8 +597,8 @@ hipError_t launch_rs_scan(const RsScanArgs &a, int cus, hipStream_t s) {
                                                  (uint64_t)std::max(cus, 1));
         rs_scan_kernel<<<(uint32_t)grid, kScanThreads, 0, s>>>(a);
     }
-    if (a.remainder && a.count && a.len >= a.remainder)
-        rs_scan_tail_kernel<<<1, 1, 0, s>>>(a, a.len - a.remainder);
+    if (a.tail >= 0 && a.remainder && a.count && (uint64_t)a.tail + a.remainder <= a.len)
+        rs_scan_tail_kernel<<<1, 1, 0, s>>>(a, (uint64_t)a.tail);
     return hipGetLastError();
 }
 

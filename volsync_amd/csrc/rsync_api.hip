@@ -68,6 +68,24 @@ struct HostReg {
     }
 };
 
+// One sharded match run (vs_rsync_match_scan .. _finish).  Offsets in spec /
+// fin are data-relative (file offset - origin).
+struct RsRun {
+    const uint8_t *dev = nullptr;  // device bytes at file offset `origin`
+    int64_t dlen = 0, origin = 0, flen = 0, own_lo = 0, own_hi = 0;
+    int64_t spec_entry = 0;
+    int32_t spec_want = 0;
+    std::vector<vs_match> spec;          // the speculative walk's matches
+    std::vector<int64_t> spec_fa_before; // false alarms before each match's offset
+    int64_t spec_fa = 0, spec_exit = 0;
+    int32_t spec_exit_want = 0;
+    std::vector<vs_match> fin;           // the walk from the true entry (use_spec: = spec)
+    bool use_spec = true;
+    int64_t fin_fa = 0, fin_exit = 0;
+    int32_t fin_exit_want = 0;
+    int state = 0;                       // 0 none, 1 scanned, 2 stitched, 3 finished
+};
+
 struct vs_rsync {
     int device = 0;
     int cus = 256;
@@ -97,6 +115,7 @@ struct vs_rsync {
     DevBuf d_flag;
     HostReg reg_off, reg_sum, reg_flag;
     std::vector<vs_match> h_out;
+    RsRun run;
     int64_t st_cand = 0, st_fa = 0, st_hashed = 0;
     int32_t st_rounds = 0;
     double ms[5] = {0, 0, 0, 0, 0};
@@ -253,19 +272,29 @@ struct WalkState {
     size_t nout = 0;
     int64_t false_alarms = 0;
     int64_t end_false_alarms = 0;  // at the end of the (optimistic) walk
+    int64_t exit_off = 0;          // first visited offset >= stop (final state)
+    int32_t exit_want = 0;
+};
+
+// Offsets inside a walk are relative to the device data (file offset
+// `origin`); F = file length - origin, so k = min(blength, F - o) and
+// hash_search's end = F + 1 - len(last block), exactly as for a whole file.
+struct WalkGeom {
+    int64_t F = 0;      // file end, data-relative
+    int64_t stop = 0;   // own_hi, data-relative: the walk stops at the first offset >= stop
 };
 
 // After the walk's needs were hashed: did any of them strong-match a table
 // entry the walk would have compared it with?  If none did, treating each as
 // a non-match was exactly rsync's decision, so the walk's output stands and
 // only its false-alarm count lacks their compares (`extra_fa`).
-bool needs_match(vs_rsync *h, int64_t len, const std::vector<uint64_t> &off,
+bool needs_match(vs_rsync *h, int64_t F, const std::vector<uint64_t> &off,
                  const std::vector<uint32_t> &sum, const std::vector<uint8_t> &strong,
                  const std::vector<uint64_t> &need, int64_t *extra_fa) {
     const uint32_t s2 = (uint32_t)h->s2length;
     int64_t fa = 0;
     for (const uint64_t c : need) {
-        const int64_t k = std::min<int64_t>(h->blength, len - (int64_t)off[c]);
+        const int64_t k = std::min<int64_t>(h->blength, F - (int64_t)off[c]);
         const uint32_t s = sum[c];
         for (int64_t q = group_start(h, s); q >= 0 && q < h->count && (uint32_t)(h->tkey_h[q] >> 32) == s;
              ++q) {
@@ -279,23 +308,38 @@ bool needs_match(vs_rsync *h, int64_t len, const std::vector<uint64_t> &off,
     return false;
 }
 
-// match.c hash_search over the sorted candidates, from state `st`.  A
-// candidate whose strong sum is unknown is treated as a non-match and
-// reported in `need`; st then holds the state just before the first of them
-// (else the final state).
-void walk(vs_rsync *h, int64_t len, const std::vector<uint64_t> &off,
+// The speculative walk a re-walk may merge into: its matches
+// (data-relative offsets), the false alarms counted before each match's
+// offset was processed, its total and its exit state.
+struct SpecWalk {
+    const std::vector<vs_match> *m = nullptr;
+    const std::vector<int64_t> *fa_before = nullptr;
+    int64_t fa = 0, exit_off = 0;
+    int32_t exit_want = 0;
+};
+
+// match.c hash_search over the sorted candidates, from state `st`, until the
+// first offset >= g.stop.  A candidate whose strong sum is unknown is treated
+// as a non-match and reported in `need`; st then holds the state just before
+// the first of them (else the final state).  With `merge`, the walk ends at
+// its first match that the speculative walk also made (same offset, same
+// block): both walks continue identically from there, so the rest of the
+// output, the false alarms and the exit are the speculative walk's.
+void walk(vs_rsync *h, const WalkGeom &g, const std::vector<uint64_t> &off,
           const std::vector<uint32_t> &sum, const std::vector<uint8_t> &known,
           const std::vector<uint8_t> &strong, std::vector<uint64_t> &need,
-          std::vector<vs_match> &out, WalkState &st) {
+          std::vector<vs_match> &out, std::vector<int64_t> &out_fa, WalkState &st,
+          const SpecWalk *merge) {
     const size_t nc = off.size();
     const uint32_t s2 = (uint32_t)h->s2length;
-    const int64_t end = len + 1 - blen(h, h->count - 1);
+    const int64_t end = g.F + 1 - blen(h, h->count - 1);
     int64_t offset = st.offset;
     int32_t want_i = st.want_i;
     size_t c = st.c;
     int64_t false_alarms = st.false_alarms;
     out.resize(st.nout);
-    bool resume_set = false;
+    out_fa.resize(st.nout);
+    bool resume_set = false, merged = false;
     WalkState resume;
     while (c < nc) {
         if ((int64_t)off[c] < offset) {
@@ -312,10 +356,11 @@ void walk(vs_rsync *h, int64_t len, const std::vector<uint64_t> &off,
             continue;
         }
         const int64_t o = (int64_t)off[c];
-        if (o >= end) break;
-        const int64_t k = std::min<int64_t>(h->blength, len - o);
+        if (o >= end || o >= g.stop) break;
+        const int64_t k = std::min<int64_t>(h->blength, g.F - o);
         const uint32_t s = sum[c];
         const int64_t p0 = group_start(h, s);
+        const int64_t fa_visit = false_alarms;
         bool matched = false;
         for (int64_t q = p0; q >= 0 && q < h->count && (uint32_t)(h->tkey_h[q] >> 32) == s; ++q) {
             int32_t i = (int32_t)~(uint32_t)h->tkey_h[q];
@@ -328,42 +373,66 @@ void walk(vs_rsync *h, int64_t len, const std::vector<uint64_t> &off,
                 need.push_back(c);
                 break;
             }
-            const uint8_t *st = strong.data() + c * s2;
-            if (memcmp(st, h->sum2.data() + (size_t)i * s2, s2) != 0) {
+            const uint8_t *st2 = strong.data() + c * s2;
+            if (memcmp(st2, h->sum2.data() + (size_t)i * s2, s2) != 0) {
                 ++false_alarms;
                 continue;
             }
             if (i != want_i && want_i < h->count && s == h->sum1[want_i] &&
-                memcmp(st, h->sum2.data() + (size_t)want_i * s2, s2) == 0)
+                memcmp(st2, h->sum2.data() + (size_t)want_i * s2, s2) == 0)
                 i = want_i;
             out.push_back({o, i, 0});
+            out_fa.push_back(fa_visit);
             want_i = i + 1;
             offset = o + blen(h, i);
             matched = true;
+            if (merge) {
+                const std::vector<vs_match> &sm = *merge->m;
+                auto it = std::lower_bound(sm.begin(), sm.end(), o,
+                                           [](const vs_match &x, int64_t v) { return x.offset < v; });
+                if (it != sm.end() && it->offset == o && it->block_index == i) {
+                    const size_t j = (size_t)(it - sm.begin());
+                    out.insert(out.end(), it + 1, sm.end());
+                    for (size_t t = j + 1; t < sm.size(); ++t)
+                        out_fa.push_back(fa_visit + (*merge->fa_before)[t] - (*merge->fa_before)[j]);
+                    false_alarms = fa_visit + merge->fa - (*merge->fa_before)[j];
+                    offset = merge->exit_off;
+                    want_i = merge->exit_want;
+                    merged = true;
+                }
+            }
             break;
         }
+        if (merged) break;
         if (!matched) {
             offset = o + 1;
             ++c;
         }
     }
+    const int64_t ex = std::max(offset, g.stop);
     st = resume_set ? resume : WalkState{offset, want_i, c, out.size(), false_alarms};
     st.end_false_alarms = false_alarms;
+    st.exit_off = ex;
+    st.exit_want = want_i;
 }
 
 // strong sums of candidate windows idx[] on the device -> strong/known
-int verify(vs_rsync *h, const void *dev_src, int64_t len, const std::vector<uint64_t> &off,
+int verify(vs_rsync *h, const uint8_t *dev, int64_t F, const std::vector<uint64_t> &off,
            const std::vector<uint64_t> &idx, std::vector<uint8_t> &known,
            std::vector<uint8_t> &strong) {
-    const size_t n = idx.size();
+    std::vector<uint64_t> todo;
+    todo.reserve(idx.size());
+    for (const uint64_t c : idx)
+        if (!known[c]) todo.push_back(c);
+    const size_t n = todo.size();
     if (!n) return 0;
     const uint32_t s2 = (uint32_t)h->s2length;
     std::vector<uint64_t> vo(n);
     std::vector<uint32_t> vl(n);
     uint32_t min_len = 0xffffffffu;
     for (size_t j = 0; j < n; ++j) {
-        vo[j] = off[idx[j]];
-        vl[j] = (uint32_t)std::min<int64_t>(h->blength, len - (int64_t)vo[j]);
+        vo[j] = off[todo[j]];
+        vl[j] = (uint32_t)std::min<int64_t>(h->blength, F - (int64_t)vo[j]);
         min_len = std::min(min_len, vl[j]);
     }
     VS_TRY(h->v_off.ensure(n * 8));
@@ -371,54 +440,91 @@ int verify(vs_rsync *h, const void *dev_src, int64_t len, const std::vector<uint
     VS_TRY(h->v_out.ensure(n * s2));
     VS_HIP(hipMemcpyAsync(h->v_off.p, vo.data(), n * 8, hipMemcpyHostToDevice, h->stream));
     VS_HIP(hipMemcpyAsync(h->v_len.p, vl.data(), n * 4, hipMemcpyHostToDevice, h->stream));
-    VS_HIP(launch_rs_strong((const uint8_t *)dev_src, h->v_off.as<uint64_t>(),
-                            h->v_len.as<uint32_t>(), n, h->csum_type, h->seed, s2,
-                            h->v_out.as<uint8_t>(), min_len, h->stream));
+    VS_HIP(launch_rs_strong(dev, h->v_off.as<uint64_t>(), h->v_len.as<uint32_t>(), n,
+                            h->csum_type, h->seed, s2, h->v_out.as<uint8_t>(), min_len, h->stream));
     std::vector<uint8_t> res(n * s2);
     VS_HIP(hipMemcpyAsync(res.data(), h->v_out.p, n * s2, hipMemcpyDeviceToHost, h->stream));
     VS_HIP(hipStreamSynchronize(h->stream));
     for (size_t j = 0; j < n; ++j) {
-        memcpy(strong.data() + idx[j] * s2, res.data() + j * s2, s2);
-        known[idx[j]] = 1;
+        memcpy(strong.data() + todo[j] * s2, res.data() + j * s2, s2);
+        known[todo[j]] = 1;
     }
     h->st_hashed += (int64_t)n;
     return 0;
 }
 
-int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_matches) {
-    if (!h->loaded) return fail(VS_ERR_STATE, "vs_rsync_match_device before vs_rsync_load_sums");
-    if (len < 0 || (len && !dev_src)) return fail(VS_ERR_ARG, "bad source");
-    VS_TRY(rs_dev(h));
-    h->matches.clear();
-    h->st_cand = h->st_fa = h->st_hashed = 0;
-    h->st_rounds = 0;
-    for (int i = 2; i < 5; ++i) h->ms[i] = 0;
-    if (n_matches) *n_matches = 0;
-    if (len == 0 || h->count == 0) return 0;  // match_sums: no sums -> all literal
+// Walks from (entry, want) (data-relative) with verification rounds until
+// every strong sum the walk needed was known; the result is exactly
+// hash_search's over [entry, stop).  batch: round 0's windows to hash first.
+int run_walk(vs_rsync *h, int64_t entry, int32_t want, const SpecWalk *merge,
+             std::vector<uint64_t> &batch, std::vector<vs_match> &out,
+             std::vector<int64_t> &out_fa, WalkState &ws) {
+    RsRun &r = h->run;
+    const WalkGeom g{r.flen - r.origin, r.own_hi - r.origin};
+    const std::vector<uint64_t> &off = h->h_off;
+    ws = WalkState{};
+    ws.offset = entry;
+    ws.want_i = want;
+    ws.c = std::lower_bound(off.begin(), off.end(), (uint64_t)std::max<int64_t>(entry, 0)) - off.begin();
+    out.clear();
+    out_fa.clear();
+    double t_ver = 0, t_walk = 0;
+    for (int round = 0;; ++round) {
+        double tv = now_ms();
+        VS_TRY(verify(h, r.dev, g.F, off, batch, h->h_known, h->h_strong));
+        t_ver += now_ms() - tv;
+        ++h->st_rounds;
+        double tw = now_ms();
+        int64_t extra_fa = 0;
+        if (round > 0 && !needs_match(h, g.F, off, h->h_sum, h->h_strong, batch, &extra_fa)) {
+            // every need was a false alarm: no replay (out holds the whole walk)
+            ws.false_alarms = ws.end_false_alarms + extra_fa;
+            t_walk += now_ms() - tw;
+            break;
+        }
+        batch.clear();
+        walk(h, g, off, h->h_sum, h->h_known, h->h_strong, batch, out, out_fa, ws, merge);
+        t_walk += now_ms() - tw;
+        if (batch.empty()) {
+            ws.false_alarms = ws.end_false_alarms;
+            break;
+        }
+    }
+    h->ms[3] += t_ver;
+    h->ms[4] += t_walk;
+    return 0;
+}
+
+// Candidates of the owned offsets: coarse prefix sums, weak scan of every
+// full-window offset in [own_lo, min(own_hi, F - blength + 1)) plus the one
+// shrunk window that can match (the short last block), radix-sorted by
+// offset and read back; round 0's "visit" predictions (rs_visit_kernel).
+int scan_candidates(vs_rsync *h, std::vector<uint64_t> &batch) {
+    RsRun &r = h->run;
+    const int64_t dlen = r.dlen;
+    const int64_t F = r.flen - r.origin;
+    const int64_t lo = r.own_lo - r.origin, hi = r.own_hi - r.origin;
+    static const bool trace = getenv("VSGPU_RS_TRACE") != nullptr;
     const double t0 = now_ms();
-    VS_TRY(order_after_null(h));
-    // 1. coarse prefixes
-    const uint64_t nblk = ((uint64_t)len + kRsG - 1) / kRsG;
+    // 1. coarse prefixes of the data
+    const uint64_t nblk = ((uint64_t)dlen + kRsG - 1) / kRsG;
     VS_TRY(h->px.ensure(nblk * 4));
     VS_TRY(h->pt.ensure(nblk * 4));
     VS_TRY(h->pxs.ensure((nblk + 1) * 4));
     VS_TRY(h->pts.ensure((nblk + 1) * 4));
     VS_TRY(h->partials.ensure((nblk / 4096 + 2) * 4));
     VS_TRY(h->n_cand.ensure(16));
-    VS_HIP(launch_rs_prefix((const uint8_t *)dev_src, (uint64_t)len, h->px.as<uint32_t>(),
-                            h->pt.as<uint32_t>(), h->pxs.as<uint32_t>(), h->pts.as<uint32_t>(),
+    VS_HIP(launch_rs_prefix(r.dev, (uint64_t)dlen, h->px.as<uint32_t>(), h->pt.as<uint32_t>(),
+                            h->pxs.as<uint32_t>(), h->pts.as<uint32_t>(),
                             h->partials.as<uint32_t>(), h->stream));
-    static const bool trace = getenv("VSGPU_RS_TRACE") != nullptr;
-    if (trace) {
-        VS_HIP(hipStreamSynchronize(h->stream));
-        fprintf(stderr, "rs: prefix %.1f ms\n", now_ms() - t0);
-    }
     // 2. weak scan (re-run once with an exact capacity on overflow)
     RsScanArgs a{};
-    a.data = (const uint8_t *)dev_src;
-    a.len = (uint64_t)len;
+    a.data = r.dev;
+    a.len = (uint64_t)dlen;
     a.blength = (uint64_t)h->blength;
-    a.nfull = (a.len >= a.blength) ? a.len - a.blength + 1 : 0;
+    a.lo = (uint64_t)lo;
+    const int64_t nfull_end = std::min<int64_t>(hi, F - h->blength + 1);
+    a.nfull = nfull_end > lo ? (uint64_t)nfull_end : 0;
     a.count = (uint32_t)h->count;
     a.remainder = (uint32_t)h->remainder;
     a.px_scan = h->pxs.as<uint32_t>();
@@ -431,9 +537,12 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
     a.lbits = rs_lds_filter_bits(h->fbits);
     a.filt_l = h->d_filt.as<uint32_t>() + ((1ull << h->fbits) / 32);
     a.n_cand = (unsigned long long *)h->n_cand.p;
+    const int64_t tail = F - h->remainder;   // the short last block's only window
+    a.tail = (h->remainder && tail >= lo && tail < hi && tail >= 0) ? (int64_t)tail : -1;
     // expected: weak collisions (count / 2^32 per offset) + one per matching block
-    uint64_t cap = (uint64_t)((double)a.nfull * h->count / 4294967296.0 * 2.0) +
-                   (uint64_t)len / h->blength * 2 + 65536;
+    const uint64_t span = a.nfull > a.lo ? a.nfull - a.lo : 0;
+    uint64_t cap = (uint64_t)((double)span * h->count / 4294967296.0 * 2.0) +
+                   span / h->blength * 2 + 65536;
     uint64_t nc = 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
         VS_TRY(h->c_off.ensure(cap * 8));
@@ -452,9 +561,8 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
         cap = nc;
         if (attempt == 1) return fail(VS_ERR_STATE, "candidate buffer overflow");
     }
-    // 3. sort candidates by offset
-    // host scratch kept in the handle: first-touch page faults on ~160 MB of
-    // fresh vectors per call (C4 shape) cost ~100 ms
+    // 3. sort candidates by offset; host scratch kept in the handle (first-touch
+    // page faults on ~160 MB of fresh vectors per call cost ~100 ms at C4 shape)
     std::vector<uint64_t> &off = h->h_off;
     std::vector<uint32_t> &sum = h->h_sum;
     h->reg_off.grow(off, nc);
@@ -463,7 +571,7 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
         VS_TRY(h->c_off2.ensure(nc * 8));
         VS_TRY(h->c_sum2.ensure(nc * 4));
         VS_TRY(h->sort_tmp.ensure(rs_sort_tmp_bytes(nc, true)));
-        const int end_bit = (int)std::max<uint32_t>(ceil_log2((uint64_t)len + 1), 1);
+        const int end_bit = (int)std::max<uint32_t>(ceil_log2((uint64_t)dlen + 1), 1);
         VS_HIP(launch_rs_sort_cands(h->sort_tmp.p, h->sort_tmp.cap, h->c_off.as<uint64_t>(),
                                     h->c_off2.as<uint64_t>(), h->c_sum.as<uint32_t>(),
                                     h->c_sum2.as<uint32_t>(), nc, end_bit, h->stream));
@@ -474,20 +582,13 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
         VS_HIP(hipStreamSynchronize(h->stream));
     }
     h->st_cand = (int64_t)nc;
-    const double t1 = now_ms();
-    if (trace) fprintf(stderr, "rs: sorted + copied %.1f ms\n", t1 - t0);
-    h->ms[2] = t1 - t0;
+    h->h_known.assign(nc, 0);
+    h->h_strong.resize(nc * (size_t)h->s2length);
     // 4. round 0: chained candidates (another candidate one block length
-    // away) plus the uncovered ones (see rs_visit_kernel)
-    std::vector<uint8_t> &known = h->h_known, &strong = h->h_strong;
-    known.assign(nc, 0);
-    strong.resize(nc * (size_t)h->s2length);
-    std::vector<uint64_t> &batch = h->h_batch;
+    // away) plus the uncovered ones (see rs_visit_kernel), flagged on the
+    // device over the sorted offsets
     batch.clear();
     if (nc) {
-        // flags computed on the device over the sorted offsets (binary
-        // searches for o - blength and o + blength); the host loop over
-        // 8.9 M candidates took ~100 ms at C4 shape
         VS_TRY(h->d_flag.ensure(2 * nc));
         VS_HIP(launch_rs_chained(h->c_off2.as<uint64_t>(), nc, (uint64_t)h->blength,
                                  h->d_flag.as<uint8_t>(), h->stream));
@@ -500,46 +601,123 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
         for (size_t c = 0; c < nc; ++c)
             if (fl[c]) batch.push_back(c);
     }
-    if (trace) fprintf(stderr, "rs: chained batch %.1f ms (%zu)\n", now_ms() - t0, batch.size());
-    double t_ver = 0, t_walk = 0;
-    std::vector<vs_match> &out = h->h_out;
-    out.clear();
-    WalkState ws;
-    for (;;) {
-        double tv = now_ms();
-        VS_TRY(verify(h, dev_src, len, off, batch, known, strong));
-        t_ver += now_ms() - tv;
-        ++h->st_rounds;
-        double tw = now_ms();
-        int64_t extra_fa = 0;
-        if (h->st_rounds > 1 && !needs_match(h, len, off, sum, strong, batch, &extra_fa)) {
-            // every need was a false alarm: no replay (out holds the whole walk)
-            ws.false_alarms = ws.end_false_alarms + extra_fa;
-            t_walk += now_ms() - tw;
-            break;
-        }
-        batch.clear();
-        walk(h, len, off, sum, known, strong, batch, out, ws);
-        t_walk += now_ms() - tw;
-        if (trace && !batch.empty()) {
-            const uint64_t b0 = batch[0];
-            fprintf(stderr,
-                    "rs: round %d needs %zu (resume c=%zu of %llu, offset %lld; first need "
-                    "c=%llu off=%llu chained=%d)\n",
-                    h->st_rounds, batch.size(), ws.c, (unsigned long long)nc,
-                    (long long)ws.offset, (unsigned long long)b0,
-                    (unsigned long long)off[b0], (int)h->h_flag[b0]);
-        }
-        if (batch.empty()) break;
+    h->ms[2] += now_ms() - t0;
+    if (trace) fprintf(stderr, "rs: candidates + round-0 batch %.1f ms (%zu)\n", now_ms() - t0,
+                       batch.size());
+    return 0;
+}
+
+// ---- sharded match_sums: scan + speculative walk, stitch, finish
+int match_scan(vs_rsync *h, const void *dev_src, int64_t dlen, int64_t origin, int64_t flen,
+               int64_t own_lo, int64_t own_hi, int64_t *exit_off, int32_t *exit_want) {
+    if (!h->loaded) return fail(VS_ERR_STATE, "vs_rsync_match_scan before vs_rsync_load_sums");
+    if (dlen < 0 || (dlen && !dev_src) || origin < 0 || flen < origin + dlen || own_lo < origin ||
+        own_hi < own_lo || own_hi > flen)
+        return fail(VS_ERR_ARG, "bad source range (need origin <= own_lo <= own_hi <= file_len)");
+    const int64_t need_hi = std::min<int64_t>(own_hi + h->blength - 1, flen);
+    if (own_hi > own_lo && origin + dlen < need_hi)
+        return fail(VS_ERR_ARG, "source data must cover [own_lo, min(own_hi + blength - 1, file_len))");
+    VS_TRY(rs_dev(h));
+    RsRun &r = h->run;
+    r = RsRun{};
+    r.dev = (const uint8_t *)dev_src;
+    r.dlen = dlen;
+    r.origin = origin;
+    r.flen = flen;
+    r.own_lo = own_lo;
+    r.own_hi = own_hi;
+    h->st_cand = h->st_fa = h->st_hashed = 0;
+    h->st_rounds = 0;
+    for (int i = 2; i < 5; ++i) h->ms[i] = 0;
+    // the speculative entry: hash_search's own start at offset 0, else
+    // want_i = count ("no preference": want_i < count fails)
+    r.spec_entry = own_lo;
+    r.spec_want = own_lo == 0 ? 0 : h->count;
+    r.state = 1;
+    const int64_t rel_hi = own_hi - origin;
+    if (own_hi == own_lo || flen == 0 || h->count == 0) {
+        // match_sums: no sums (or no owned offsets) -> all literal
+        r.spec_exit = std::max(own_lo, own_hi);
+        r.spec_exit_want = r.spec_want;
+    } else {
+        VS_TRY(order_after_null(h));
+        std::vector<uint64_t> &batch = h->h_batch;
+        VS_TRY(scan_candidates(h, batch));
+        WalkState ws;
+        VS_TRY(run_walk(h, own_lo - origin, r.spec_want, nullptr, batch, r.spec, r.spec_fa_before,
+                        ws));
+        r.spec_fa = ws.false_alarms;
+        r.spec_exit = ws.exit_off + origin;
+        r.spec_exit_want = ws.exit_want;
+        (void)rel_hi;
     }
-    h->ms[3] = t_ver;
-    h->ms[4] = t_walk;
-    if (trace) fprintf(stderr, "rs: match done %.1f ms (verify %.1f, walk %.1f)\n", now_ms() - t0,
-                       t_ver, t_walk);
-    h->st_fa = ws.false_alarms;
-    h->matches.assign(out.begin(), out.end());
+    r.fin_exit = r.spec_exit;
+    r.fin_exit_want = r.spec_exit_want;
+    r.fin_fa = r.spec_fa;
+    r.use_spec = true;
+    h->st_fa = r.fin_fa;
+    if (exit_off) *exit_off = r.spec_exit;
+    if (exit_want) *exit_want = r.spec_exit_want;
+    return 0;
+}
+
+int match_stitch(vs_rsync *h, int64_t entry, int32_t want, int64_t *exit_off, int32_t *exit_want) {
+    RsRun &r = h->run;
+    if (r.state < 1) return fail(VS_ERR_STATE, "vs_rsync_match_stitch before vs_rsync_match_scan");
+    if (entry < r.own_lo) return fail(VS_ERR_ARG, "entry before the scanned own range");
+    if (want < 0) return fail(VS_ERR_ARG, "negative want_i");
+    VS_TRY(rs_dev(h));
+    if (entry == r.spec_entry && want == r.spec_want) {
+        r.use_spec = true;
+        r.fin_exit = r.spec_exit;
+        r.fin_exit_want = r.spec_exit_want;
+        r.fin_fa = r.spec_fa;
+    } else if (entry >= r.own_hi || h->count == 0 || r.flen == 0) {
+        // a match of the previous shard spans this whole range: nothing to visit
+        r.use_spec = false;
+        r.fin.clear();
+        r.fin_fa = 0;
+        r.fin_exit = std::max(entry, r.own_hi);
+        r.fin_exit_want = want;
+    } else {
+        SpecWalk sw{&r.spec, &r.spec_fa_before, r.spec_fa, r.spec_exit - r.origin, r.spec_exit_want};
+        std::vector<uint64_t> &batch = h->h_batch;
+        batch.clear();
+        WalkState ws;
+        std::vector<int64_t> fa_before;
+        VS_TRY(run_walk(h, entry - r.origin, want, &sw, batch, r.fin, fa_before, ws));
+        r.use_spec = false;
+        r.fin_fa = ws.false_alarms;
+        r.fin_exit = ws.exit_off + r.origin;
+        r.fin_exit_want = ws.exit_want;
+    }
+    r.state = 2;
+    h->st_fa = r.fin_fa;
+    if (exit_off) *exit_off = r.fin_exit;
+    if (exit_want) *exit_want = r.fin_exit_want;
+    return 0;
+}
+
+int match_finish(vs_rsync *h, int64_t *n_matches) {
+    RsRun &r = h->run;
+    if (r.state < 1) return fail(VS_ERR_STATE, "vs_rsync_match_finish before vs_rsync_match_scan");
+    const std::vector<vs_match> &src = r.use_spec ? r.spec : r.fin;
+    h->matches.resize(src.size());
+    for (size_t j = 0; j < src.size(); ++j)
+        h->matches[j] = {src[j].offset + r.origin, src[j].block_index, 0};
+    h->st_fa = r.fin_fa;
+    r.state = 3;
     if (n_matches) *n_matches = (int64_t)h->matches.size();
     return 0;
+}
+
+int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_matches) {
+    if (!h->loaded) return fail(VS_ERR_STATE, "vs_rsync_match_device before vs_rsync_load_sums");
+    if (len < 0 || (len && !dev_src)) return fail(VS_ERR_ARG, "bad source");
+    h->matches.clear();
+    if (n_matches) *n_matches = 0;
+    VS_TRY(match_scan(h, dev_src, len, 0, len, 0, len, nullptr, nullptr));
+    return match_finish(h, n_matches);
 }
 
 }  // namespace
@@ -671,6 +849,24 @@ VS_API int vs_rsync_match_device(vs_rsync *h, const void *dev_src, int64_t len,
                                  int64_t *n_matches) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
     return match_device(h, dev_src, len, n_matches);
+}
+
+VS_API int vs_rsync_match_scan(vs_rsync *h, const void *dev_src, int64_t len, int64_t origin,
+                               int64_t file_len, int64_t own_lo, int64_t own_hi,
+                               int64_t *exit_off, int32_t *exit_want) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    return match_scan(h, dev_src, len, origin, file_len, own_lo, own_hi, exit_off, exit_want);
+}
+
+VS_API int vs_rsync_match_stitch(vs_rsync *h, int64_t entry, int32_t want_i, int64_t *exit_off,
+                                 int32_t *exit_want) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    return match_stitch(h, entry, want_i, exit_off, exit_want);
+}
+
+VS_API int vs_rsync_match_finish(vs_rsync *h, int64_t *n_matches) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    return match_finish(h, n_matches);
 }
 
 VS_API int vs_rsync_get_matches(vs_rsync *h, int64_t first, int64_t n, vs_match *out) {

@@ -120,6 +120,29 @@ class Matcher:
         self._last_n = n.value
         return n.value
 
+    # ---- sharded hash_search (volsync_amd/rsync_shard.py run_walk_shard) ----
+    def match_scan(self, dev_src: int, length: int, origin: int, file_len: int, own_lo: int,
+                   own_hi: int) -> Tuple[int, int]:
+        """Candidates + speculative walk of file offsets [own_lo, own_hi);
+        returns the speculative exit state (offset, want_i)."""
+        eo, ew = ctypes.c_int64(0), ctypes.c_int32(0)
+        check(lib.vs_rsync_match_scan(self._h, ctypes.c_void_p(dev_src or None), length, origin,
+                                      file_len, own_lo, own_hi, ctypes.byref(eo), ctypes.byref(ew)))
+        return int(eo.value), int(ew.value)
+
+    def match_stitch(self, entry: int, want_i: int) -> Tuple[int, int]:
+        """Re-walk from the true entry state; returns the new exit state."""
+        eo, ew = ctypes.c_int64(0), ctypes.c_int32(0)
+        check(lib.vs_rsync_match_stitch(self._h, entry, want_i, ctypes.byref(eo),
+                                        ctypes.byref(ew)))
+        return int(eo.value), int(ew.value)
+
+    def match_finish(self) -> int:
+        n = ctypes.c_int64(0)
+        check(lib.vs_rsync_match_finish(self._h, ctypes.byref(n)))
+        self._last_n = n.value
+        return n.value
+
     def matches(self, first: int = 0, n: Optional[int] = None) -> List[Tuple[int, int]]:
         if n is None:
             n = self.stats()["matches"] - first

@@ -15,7 +15,7 @@ match_sums over its source.  That all-gather is the path's only collective.
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Callable, List, Tuple
+from typing import Callable, List, Sequence, Tuple
 
 
 @dataclass
@@ -74,3 +74,117 @@ def gather_sums(sum1, sum2, shard: BlockShard, s2length: int,
     full1 = torch.cat([g[r][: s.blocks * 4] for r, s in enumerate(parts)]).view(sum1.dtype)
     full2 = torch.cat([g[r][m * 4: m * 4 + s.blocks * s2length] for r, s in enumerate(parts)])
     return full1, full2
+
+
+# ---- sharded match_sums: byte-range walk with an exit stitch -----------------
+#
+# rsync's sender runs ONE hash_search over the whole source file
+# (/root/reference/mover-rsync/source.sh:54); its greedy walk is sequential:
+# the state at any offset is (offset, want_i).  The source is split by byte
+# range: rank r owns the walk's visits to offsets [own_lo, own_hi) and holds
+# the bytes [own_lo, own_hi + blength - 1) (a window starting below own_hi
+# reads up to blength - 1 bytes past it).  Protocol, the rsync twin of the CDC
+# exit stitch (volsync_amd/shard.py):
+#   1. match_scan: every rank finds its weak-sum candidates and walks its
+#      range speculatively from (own_lo, want_i = "no preference"; rank 0 from
+#      (0, 0) exactly as hash_search starts) -- no communication;
+#   2. all-gather the exit states (first offset >= own_hi, want_i); rank r's
+#      true entry is rank r-1's exit; a rank whose entry changed re-walks from
+#      it (match_stitch) until its walk reaches a match the speculative walk
+#      also made -- from there the two are identical -- and reports its new
+#      exit; repeat until no entry changes (sum all-reduce);
+#   3. match_finish: each rank's matches with offsets in its range, in order.
+# Concatenated in rank order they equal one hash_search over the whole file.
+@dataclass
+class SourceShard:
+    rank: int
+    world: int
+    length: int     # whole source file length
+    blength: int
+    own_lo: int
+    own_hi: int
+    data_lo: int
+    data_hi: int
+
+    @staticmethod
+    def for_rank(length: int, blength: int, world: int, rank: int) -> "SourceShard":
+        lo = length * rank // world
+        hi = length * (rank + 1) // world
+        return SourceShard(rank, world, length, blength, lo, hi, lo & ~15,
+                           min(hi + blength - 1, length))
+
+    @staticmethod
+    def split(length: int, blength: int, world: int) -> List["SourceShard"]:
+        return [SourceShard.for_rank(length, blength, world, r) for r in range(world)]
+
+
+def run_walk_shard(h, spec: SourceShard, ptr: int, allgather_pair, allreduce_sum,
+                   stats: dict = None) -> int:
+    """This rank's part of the sharded hash_search.  h: a Matcher with the
+    table loaded (or a test double with the same match_scan / match_stitch /
+    match_finish surface); ptr: device address of file offset spec.data_lo.
+    allgather_pair((off, want)) -> every rank's pair; allreduce_sum(x) -> sum.
+    Returns this rank's match count (h.matches(0, n))."""
+    ex = h.match_scan(ptr, spec.data_hi - spec.data_lo, spec.data_lo, spec.length, spec.own_lo,
+                      spec.own_hi)
+    entry = None   # the speculative entry
+    rounds = rewalks = 0
+    for _ in range(spec.world + 2):
+        gathered = allgather_pair(ex)
+        rounds += 1
+        want = (0, 0) if spec.rank == 0 else tuple(gathered[spec.rank - 1])
+        moved = 0
+        if spec.rank and want != entry:
+            entry = want
+            ex = h.match_stitch(*want)
+            moved = 1
+            rewalks += 1
+        if allreduce_sum(moved) == 0:
+            break
+    if stats is not None:
+        stats["exchange_rounds"] = rounds
+        stats["rewalks"] = rewalks
+    return h.match_finish()
+
+
+def torch_pair_collectives(device=None):
+    """(allgather_pair, allreduce_sum) over torch.distributed: RCCL on GPU
+    tensors with the nccl backend, gloo on CPU tensors."""
+    import torch
+    import torch.distributed as dist
+
+    def allgather_pair(p):
+        t = torch.tensor([int(p[0]), int(p[1])], dtype=torch.int64, device=device)
+        outs = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(outs, t)
+        return [(int(o[0].item()), int(o[1].item())) for o in outs]
+
+    def allreduce_sum(x: int):
+        t = torch.tensor([x], dtype=torch.int64, device=device)
+        dist.all_reduce(t)
+        return int(t.item())
+
+    return allgather_pair, allreduce_sum
+
+
+def run_walk_shards_local(handles: Sequence, specs: Sequence[SourceShard], ptrs: Sequence[int]):
+    """The same protocol with every rank in one process (Jacobi rounds, as the
+    distributed version runs them): the concatenated match list."""
+    world = len(specs)
+    exits = [h.match_scan(p, s.data_hi - s.data_lo, s.data_lo, s.length, s.own_lo, s.own_hi)
+             for h, s, p in zip(handles, specs, ptrs)]
+    entry = [None] * world
+    for _ in range(world + 2):
+        gathered = list(exits)
+        moved = 0
+        for r in range(1, world):
+            if gathered[r - 1] != entry[r]:
+                entry[r] = gathered[r - 1]
+                exits[r] = handles[r].match_stitch(*entry[r])
+                moved += 1
+        if moved == 0:
+            break
+    out = []
+    for h in handles:
+        out.extend(h.matches(0, h.match_finish()))
+    return out
