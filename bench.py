@@ -98,23 +98,88 @@ def rsync_cpu_baseline(sample_bytes: int):
             "cpu": _cpu_model()}
 
 
+class C4Plan:
+    """The C4 source file S as a function of the destination D: D (synthetic
+    stream, seed 4) with `frac` of its blocks edited (seed 5) -- a third each
+    overwrite a 4 KiB run inside the block, insert 1-64 bytes, delete 1-64
+    bytes (shifting everything after) -- as a list of segments of S, each a
+    copy of D or literal bytes (synthetic stream seed 6, 4 KiB apart per
+    edit).  Any byte range of S can be generated from it on any rank
+    (fill_device), so S is ONE file, sharded by byte range, with no rank
+    holding more than its own range plus halo."""
+
+    D_SEED, LIT_SEED = 4, 6
+
+    def __init__(self, dlen: int, blength: int, seed: int = 5, frac: float = 0.10,
+                 run: int = 4096):
+        import numpy as np
+        rng = np.random.default_rng(seed)
+        count = (dlen + blength - 1) // blength
+        full = dlen // blength
+        nedit = min(int(round(count * frac)), full)
+        blocks = np.sort(rng.choice(full, size=nedit, replace=False)).astype(np.int64)
+        kind = rng.integers(0, 3, nedit)
+        at = blocks * blength + rng.integers(0, max(1, blength - run), nedit)
+        ilen = rng.integers(1, 65, nedit)
+        dl = rng.integers(1, 65, nedit)
+        lit = np.where(kind == 0, run, np.where(kind == 1, ilen, 0)).astype(np.int64)
+        skip = np.where(kind == 0, run, np.where(kind == 2, dl, 0)).astype(np.int64)
+        resume = at + skip                        # D offset after edit e
+        dstart = np.concatenate([[0], resume])    # D pieces: [dstart[e], at[e]) then the tail
+        dend = np.concatenate([at, [dlen]])
+        dlenp = np.maximum(dend - dstart, 0)
+        # interleave: D piece e, literal e, ..., D tail
+        n = 2 * nedit + 1
+        length = np.zeros(n, np.int64)
+        kindv = np.zeros(n, np.int8)               # 0 = copy of D, 1 = literal
+        srcoff = np.zeros(n, np.int64)
+        length[0::2] = dlenp
+        srcoff[0::2] = dstart
+        length[1::2] = lit
+        kindv[1::2] = 1
+        srcoff[1::2] = np.arange(nedit, dtype=np.int64) * run
+        keep = length > 0
+        self.length, self.kind, self.srcoff = length[keep], kindv[keep], srcoff[keep]
+        self.start = np.concatenate([[0], np.cumsum(self.length)[:-1]]).astype(np.int64)
+        self.total = int(self.length.sum())
+        self.dlen, self.blength, self.edits = dlen, blength, nedit
+
+    def segments(self, lo: int, hi: int):
+        """(dest offset - lo, seed, stream offset, n) pieces covering S[lo, hi)."""
+        import numpy as np
+        i = max(0, int(np.searchsorted(self.start, lo, side="right")) - 1)
+        out = []
+        while i < len(self.start) and self.start[i] < hi:
+            s0, n0 = int(self.start[i]), int(self.length[i])
+            a, b = max(lo, s0), min(hi, s0 + n0)
+            if b > a:
+                seed = self.LIT_SEED if self.kind[i] else self.D_SEED
+                out.append((a - lo, seed, int(self.srcoff[i]) + (a - s0), b - a))
+            i += 1
+        return out
+
+    def fill_device(self, dev_ptr: int, lo: int, hi: int, device: int = 0, stream=None) -> None:
+        from volsync_amd import synth_fill_device
+        for d, seed, off, n in self.segments(lo, hi):
+            synth_fill_device(dev_ptr + d, seed, off, n, device=device, stream=stream)
+
+
 def rsync_main(args):
-    """C4 shape: destination D (seed 4) and source S = D with 10 % of its blocks
-    edited (seed 5: 4 KiB overwrite / 1-64 B insert / 1-64 B delete), both
-    device-resident.  A step = generate_and_send_sums over D (weak + XXH3-128
-    per block) + build_hash_table + match_sums over S (weak scan, strong
-    verification rounds, greedy walk).  value = (|D| + |S|) per second.
-    N GPUs: D is ONE file of N x per-GPU bytes, sharded by block range; each
-    rank computes the sums of its blocks and an RCCL all-gather assembles the
-    full table on every rank (volsync_amd/rsync_shard.py) -- the path's only
-    collective.  Each rank then matches its own piece of S (the edited copy of
-    its D range, walked from the piece's start) against the full table."""
-    import numpy as np
+    """C4: destination D (seed 4) and source S = D with 10 % of its blocks
+    edited (C4Plan), both device-resident, D and S each ONE file sharded
+    across the ranks.  A step = generate_and_send_sums over D (each rank its
+    block range: weak + XXH3-128 per block) + one RCCL all-gather of the sum
+    table (N > 1) + build_hash_table + match_sums over S: each rank scans its
+    byte range of S, walks it speculatively, and the walks are stitched by an
+    all-gather of exit states (volsync_amd/rsync_shard.py run_walk_shard), so
+    the concatenated match list is exactly ONE hash_search over S.
+    value = (|D| + |S|) per second over all ranks."""
     import torch
     import torch.distributed as dist
     from volsync_amd import Matcher, sum_sizes_sqroot, synth_fill_device
     from volsync_amd.rsync import CSUM_XXH3_128
-    from volsync_amd.rsync_shard import BlockShard, gather_sums
+    from volsync_amd.rsync_shard import (BlockShard, SourceShard, gather_sums, run_walk_shard,
+                                         torch_pair_collectives)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -124,37 +189,25 @@ def rsync_main(args):
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     per = int(args.per_gpu_gib * (1 << 30))
-    hdr = sum_sizes_sqroot(per * world)
-    shard = BlockShard.for_rank(per * world, hdr.blength, world, rank)
+    dtotal = per * world
+    hdr = sum_sizes_sqroot(dtotal)
+    shard = BlockShard.for_rank(dtotal, hdr.blength, world, rank)
     n = shard.byte_hi - shard.byte_lo
-    db = torch.empty(n, dtype=torch.uint8, device=dev)
-    synth_fill_device(db.data_ptr(), 4, shard.byte_lo, n, device=local)
-    rng = np.random.default_rng(5 + rank)
-    full_blocks = n // hdr.blength
-    edits = np.sort(rng.choice(full_blocks, full_blocks // 10, replace=False))
-    pieces, pos = [], 0
-    for b in edits.tolist():
-        at = b * hdr.blength + int(rng.integers(0, hdr.blength - 4096))
-        pieces.append(db[pos:at])
-        kind = int(rng.integers(0, 3))
-        if kind == 0:
-            pieces.append(torch.randint(0, 256, (4096,), dtype=torch.uint8, device=dev))
-            pos = at + 4096
-        elif kind == 1:
-            pieces.append(torch.randint(0, 256, (int(rng.integers(1, 65)),), dtype=torch.uint8,
-                                        device=dev))
-            pos = at
-        else:
-            pos = at + int(rng.integers(1, 65))
-    pieces.append(db[pos:])
-    ds = torch.cat(pieces)
-    del pieces
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    db = torch.empty(max(n, 16), dtype=torch.uint8, device=dev)
+    synth_fill_device(db.data_ptr(), C4Plan.D_SEED, shard.byte_lo, n, device=local, stream=stream)
+    plan = C4Plan(dtotal, hdr.blength)
+    sspec = SourceShard.for_rank(plan.total, hdr.blength, world, rank)
+    ds = torch.empty(max(sspec.data_hi - sspec.data_lo, 16), dtype=torch.uint8, device=dev)
+    plan.fill_device(ds.data_ptr(), sspec.data_lo, sspec.data_hi, device=local, stream=stream)
     s1 = torch.zeros(max(shard.blocks, 1), dtype=torch.int32, device=dev)
     s2 = torch.zeros(max(shard.blocks, 1) * hdr.s2length, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize(dev)
     m = Matcher(local)
-    m.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    m.set_stream(stream)
     seed = 0x5EED5EED
+    coll = torch_pair_collectives(dev) if world > 1 else (lambda p: [p], lambda x: x)
+    xst = {}
 
     def step():
         m.signatures_device(db.data_ptr(), n, hdr.blength, hdr.s2length, CSUM_XXH3_128, seed,
@@ -164,13 +217,14 @@ def rsync_main(args):
             f1, f2 = gather_sums(s1, s2, shard, hdr.s2length, dist.all_gather)
         m.load_sums_device(hdr.count, hdr.blength, hdr.s2length, hdr.remainder, f1.data_ptr(),
                            f2.data_ptr(), CSUM_XXH3_128, seed)
-        return m.match_device(ds.data_ptr(), ds.numel())
+        return run_walk_shard(m, sspec, ds.data_ptr(), *coll, stats=xst)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    m.kernel_time(reset=True)
     t0 = time.perf_counter()
     nm = 0
     stages = dict.fromkeys(["signatures", "table", "scan", "verify", "walk"], 0.0)
@@ -182,18 +236,21 @@ def rsync_main(args):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    kt = m.kernel_time()
     st = m.stats()
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    tot = n + ds.numel()
-    if world > 1:
-        t = torch.tensor([tot], dtype=torch.int64, device=dev)
-        dist.all_reduce(t)
-        tot = int(t.item())
-    value = tot * args.steps / dt / 1e9
-    sig_gbs = n / (stages["signatures"] / args.steps) / 1e6 if stages["signatures"] else 0.0
+        c = torch.tensor([nm], dtype=torch.int64, device=dev)
+        dist.all_reduce(c)
+        nm = int(c.item())
+    value = (dtotal + plan.total) * args.steps / dt / 1e9
+    own_src = sspec.own_hi - sspec.own_lo
+    scan_ms, scan_n = kt["scan"]
+    scan_gbs = own_src / (scan_ms / scan_n) / 1e6 if scan_n else 0.0
+    sig_ms, sig_n = kt["signatures"]
+    ver_ms, ver_n = kt["verify"]
     if rank == 0:
         out = {
             "metric": "GB/s rsync delta match (|D|+|S|)",
@@ -201,16 +258,38 @@ def rsync_main(args):
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (splitmix64 destination + C4 edits, device-resident)",
-            "config": {"workload": f"C4-shape: {(per * world) >> 30} GiB destination vs 10%-edited "
-                                   f"source, {'block-range shards x' + str(world) + ' (sums all-gathered over RCCL)' if world > 1 else '1 GPU'}",
+            "config": {"workload": f"C4-shape: {dtotal >> 30} GiB destination vs 10%-edited "
+                                   f"source ({plan.edits} edits), "
+                                   + (f"D block-range and S byte-range sharded x{world} "
+                                      f"({per >> 30} GiB of D per GPU; sums all-gathered, walks "
+                                      f"stitched over RCCL)" if world > 1 else "1 GPU"),
                        "blength": hdr.blength, "s2length": hdr.s2length, "count": hdr.count,
-                       "csum": "xxh128", "checksum_seed": hex(seed), "matches": nm},
-            "roofline": {"bound": "hbm", "achieved": round(sig_gbs, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(sig_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "signatures (weak + XXH3-128 per block)"},
+                       "source_bytes": plan.total, "csum": "xxh128", "checksum_seed": hex(seed),
+                       "matches": nm},
+            # dominant kernel: the weak scan over the rank's source range;
+            # algorithmic bytes per launch = the source bytes it covers (one
+            # read of each), over its HIP-event launch time
+            "roofline": {"bound": "hbm", "achieved": round(scan_gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(scan_gbs / HBM_PEAK_GBS, 4),
+                         "traffic": None, "kernel": "rs_scan_kernel (weak scan)",
+                         "avg_launch_ms": round(scan_ms / scan_n, 3) if scan_n else None,
+                         "launches": scan_n},
+            "kernels_ms_per_step": {"scan": round(scan_ms / args.steps, 3),
+                                    "verify": round(ver_ms / args.steps, 3),
+                                    "signatures": round(sig_ms / args.steps, 3)},
+            "signatures_GBps": round(n / (sig_ms / sig_n) / 1e6, 1) if sig_n else None,
             "stages_ms_per_step": {k: round(v / args.steps, 3) for k, v in stages.items()},
             "match_stats": st,
+            "rccl_world_size": dist.get_world_size() if world > 1 else 1,
+            "exchange_rounds_last_step": xst.get("exchange_rounds", 0),
         }
+        try:
+            tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+            r = tj["rs_scan"]
+            out["roofline"]["traffic"] = round(r["bytes_per_source_byte"] * own_src)
+            out["roofline"]["traffic_source"] = tj["rs_scan"]["source"]
+        except (OSError, ValueError, KeyError):
+            pass
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = rsync_cpu_baseline(args.cpu_sample_gib << 28)
         print(json.dumps(out), flush=True)

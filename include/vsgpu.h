@@ -253,6 +253,11 @@ int vs_rsync_stats(vs_rsync *h, int64_t *candidates, int64_t *false_alarms,
 /* Device time (ms) of the last run's stages: 0 signatures, 1 table, 2 scan
  * (prefix + weak scan + sort), 3 strong verification, 4 host walk. */
 int vs_rsync_timing(vs_rsync *h, double ms_out[5]);
+/* Device time of one kernel class summed over its launches since the handle
+ * was opened (or the last reset), from HIP events on the handle's stream:
+ * which 0 = weak scan / device walk, 1 = strong-sum verification,
+ * 2 = signatures.  reset != 0 zeroes the totals after reading them. */
+int vs_rsync_kernel_time(vs_rsync *h, int which, int reset, double *ms, int64_t *launches);
 
 /* Host-memory one-shot forms: copy in, run, copy out. */
 int vs_rsync_signatures(int device, const void *basis, int64_t len, int32_t blength,

@@ -365,3 +365,45 @@ def test_c4_params_exact_1g(gpu):
     s = SumStruct(n, cnt, bl, s2l, rem, c1, c2)
     got4, fa4 = _sharded_device_match(src, s, 4, csum, seed)
     assert got4 == want and fa4 == fa
+
+
+def _plan_host(plan, lo, hi):
+    out = np.zeros(hi - lo, np.uint8)
+    for d, seed, off, n in plan.segments(lo, hi):
+        out[d:d + n] = O.synth(seed, off, n)
+    return out
+
+
+def test_c4plan_source_sharded_exact(gpu):
+    """bench.py's C4 workload generator at 256 MiB (blength 16384): every
+    rank's device-generated source range equals the host-generated one, and
+    the sharded walk over them (3 ranks, the bench's run_walk_shard protocol)
+    equals ONE hash_search over the whole source (C oracle)."""
+    import bench
+    import torch
+    from volsync_amd import Matcher, SumStruct, sum_sizes_sqroot
+    from volsync_amd.rsync_shard import SourceShard, run_walk_shards_local
+    dlen = 256 << 20
+    hdr = sum_sizes_sqroot(dlen)
+    plan = bench.C4Plan(dlen, hdr.blength)
+    src = _plan_host(plan, 0, plan.total)
+    basis = O.synth(bench.C4Plan.D_SEED, 0, dlen)
+    c1, c2 = O.rsync_signatures(basis, hdr.blength, hdr.s2length, R.CSUM_XXH3_128, 0x5EED5EED)
+    want, fa = O.rsync_match(src, c1, c2, hdr.blength, hdr.remainder, R.CSUM_XXH3_128, 0x5EED5EED)
+    s = SumStruct(dlen, hdr.count, hdr.blength, hdr.s2length, hdr.remainder, c1, c2)
+    specs = SourceShard.split(plan.total, hdr.blength, 3)
+    hs, bufs = [], []
+    for sp in specs:
+        b = torch.empty(sp.data_hi - sp.data_lo + 16, dtype=torch.uint8, device="cuda")
+        plan.fill_device(b.data_ptr(), sp.data_lo, sp.data_hi)
+        torch.cuda.synchronize()
+        assert np.array_equal(b[: sp.data_hi - sp.data_lo].cpu().numpy(), src[sp.data_lo:sp.data_hi])
+        m = Matcher()
+        m.load_sums(s, R.CSUM_XXH3_128, 0x5EED5EED)
+        hs.append(m)
+        bufs.append(b)
+    got = run_walk_shards_local(hs, specs, [b.data_ptr() for b in bufs])
+    gfa = sum(m.stats()["false_alarms"] for m in hs)
+    for m in hs:
+        m.close()
+    assert got == want and gfa == fa

@@ -122,6 +122,7 @@ def _load() -> ctypes.CDLL:
         "vs_rsync_get_matches": (c_int, [vp, i64, i64, ctypes.POINTER(VsMatch)]),
         "vs_rsync_stats": (c_int, [vp, i64p, i64p, i64p, i32p]),
         "vs_rsync_timing": (c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
+        "vs_rsync_kernel_time": (c_int, [vp, c_int, c_int, ctypes.POINTER(ctypes.c_double), i64p]),
         "vs_rsync_signatures": (c_int, [c_int, vp, i64, i32, i32, c_int, c_u32, vp, vp]),
         "vs_rsync_match": (c_int, [c_int, vp, i64, ctypes.POINTER(VsSigTable), c_int, c_u32,
                                    ctypes.POINTER(VsMatch), c_size, ctypes.POINTER(c_size)]),

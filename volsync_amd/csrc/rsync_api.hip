@@ -91,6 +91,12 @@ struct vs_rsync {
     int cus = 256;
     hipStream_t own = nullptr, stream = nullptr;
     hipEvent_t ev_null = nullptr;   // orders own-stream work after null-stream work
+    // device time of the kernels themselves (HIP events on h->stream around
+    // each launch; every entry point synchronises right after): [0] weak scan
+    // / device walk, [1] strong verification, [2] signatures
+    hipEvent_t kev[2] = {nullptr, nullptr};
+    double kms[3] = {0, 0, 0};
+    int64_t kn[3] = {0, 0, 0};
     // signature table
     bool loaded = false;
     int32_t count = 0, blength = 0, s2length = 0, remainder = 0;
@@ -142,6 +148,28 @@ int order_after_null(vs_rsync *h) {
     VS_HIP(hipStreamWaitEvent(h->stream, h->ev_null, 0));
     return 0;
 }
+
+// brackets one kernel launch with the handle's two timing events; fold()
+// after the stream synchronised adds the elapsed time to kms[which]
+struct KernelTimer {
+    vs_rsync *h;
+    int which;
+    bool on = false;
+    KernelTimer(vs_rsync *h_, int w) : h(h_), which(w) {
+        on = h->kev[0] && hipEventRecord(h->kev[0], h->stream) == hipSuccess;
+    }
+    void stop() {
+        if (on) on = hipEventRecord(h->kev[1], h->stream) == hipSuccess;
+    }
+    void fold() {  // call after hipStreamSynchronize(h->stream)
+        float ms = 0;
+        if (on && hipEventElapsedTime(&ms, h->kev[0], h->kev[1]) == hipSuccess) {
+            h->kms[which] += ms;
+            h->kn[which] += 1;
+        }
+        on = false;
+    }
+};
 
 uint32_t ceil_log2(uint64_t x) {
     uint32_t b = 0;
@@ -440,11 +468,14 @@ int verify(vs_rsync *h, const uint8_t *dev, int64_t F, const std::vector<uint64_
     VS_TRY(h->v_out.ensure(n * s2));
     VS_HIP(hipMemcpyAsync(h->v_off.p, vo.data(), n * 8, hipMemcpyHostToDevice, h->stream));
     VS_HIP(hipMemcpyAsync(h->v_len.p, vl.data(), n * 4, hipMemcpyHostToDevice, h->stream));
+    KernelTimer kt(h, 1);
     VS_HIP(launch_rs_strong(dev, h->v_off.as<uint64_t>(), h->v_len.as<uint32_t>(), n,
                             h->csum_type, h->seed, s2, h->v_out.as<uint8_t>(), min_len, h->stream));
+    kt.stop();
     std::vector<uint8_t> res(n * s2);
     VS_HIP(hipMemcpyAsync(res.data(), h->v_out.p, n * s2, hipMemcpyDeviceToHost, h->stream));
     VS_HIP(hipStreamSynchronize(h->stream));
+    kt.fold();
     for (size_t j = 0; j < n; ++j) {
         memcpy(strong.data() + todo[j] * s2, res.data() + j * s2, s2);
         known[todo[j]] = 1;
@@ -551,9 +582,12 @@ int scan_candidates(vs_rsync *h, std::vector<uint64_t> &batch) {
         a.cand_off = h->c_off.as<uint64_t>();
         a.cand_sum = h->c_sum.as<uint32_t>();
         VS_HIP(hipMemsetAsync(h->n_cand.p, 0, 8, h->stream));
+        KernelTimer kt(h, 0);
         VS_HIP(launch_rs_scan(a, h->cus, h->stream));
+        kt.stop();
         VS_HIP(hipMemcpyAsync(h->pinned, h->n_cand.p, 8, hipMemcpyDeviceToHost, h->stream));
         VS_HIP(hipStreamSynchronize(h->stream));
+        kt.fold();
         nc = h->pinned[0];
         if (trace) fprintf(stderr, "rs: scan done %.1f ms (%llu candidates)\n", now_ms() - t0,
                            (unsigned long long)nc);
@@ -739,6 +773,7 @@ VS_API int vs_rsync_open(int device, vs_rsync **out) {
     (void)hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (rs_dev(h) < 0 || hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_null, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreate(&h->kev[0]) != hipSuccess || hipEventCreate(&h->kev[1]) != hipSuccess ||
         hipHostMalloc((void **)&h->pinned, 64, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         vs_rsync_close(h);
@@ -767,6 +802,8 @@ VS_API void vs_rsync_close(vs_rsync *h) {
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (HostReg *r : {&h->reg_off, &h->reg_sum, &h->reg_flag}) r->release();
     if (h->ev_null) (void)hipEventDestroy(h->ev_null);
+    for (hipEvent_t e : h->kev)
+        if (e) (void)hipEventDestroy(e);
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
 }
@@ -794,8 +831,11 @@ VS_API int vs_rsync_signatures_device(vs_rsync *h, const void *dev_basis, int64_
     a.sum2 = dev_sum2;
     const double t0 = now_ms();
     VS_TRY(order_after_null(h));
+    KernelTimer kt(h, 2);
     VS_HIP(launch_rs_signatures(a, h->stream));
+    kt.stop();
     VS_HIP(hipStreamSynchronize(h->stream));
+    kt.fold();
     h->ms[0] = now_ms() - t0;
     return 0;
 }
@@ -891,6 +931,18 @@ VS_API int vs_rsync_stats(vs_rsync *h, int64_t *candidates, int64_t *false_alarm
 VS_API int vs_rsync_timing(vs_rsync *h, double ms_out[5]) {
     if (!h || !ms_out) return fail(VS_ERR_ARG, "null argument");
     for (int i = 0; i < 5; ++i) ms_out[i] = h->ms[i];
+    return 0;
+}
+
+VS_API int vs_rsync_kernel_time(vs_rsync *h, int which, int reset, double *ms,
+                                int64_t *launches) {
+    if (!h || which < 0 || which > 2) return fail(VS_ERR_ARG, "bad handle or kernel index");
+    if (ms) *ms = h->kms[which];
+    if (launches) *launches = h->kn[which];
+    if (reset) {
+        h->kms[which] = 0;
+        h->kn[which] = 0;
+    }
     return 0;
 }
 

@@ -163,6 +163,18 @@ class Matcher:
         check(lib.vs_rsync_timing(self._h, ms))
         return dict(zip(["signatures", "table", "scan", "verify", "walk"], list(ms)))
 
+    KERNELS = ("scan", "verify", "signatures")
+
+    def kernel_time(self, reset: bool = False) -> dict:
+        """{kernel: (ms summed over launches, launches)} from HIP events."""
+        out = {}
+        for w, name in enumerate(self.KERNELS):
+            ms, n = ctypes.c_double(0), ctypes.c_int64(0)
+            check(lib.vs_rsync_kernel_time(self._h, w, 1 if reset else 0, ctypes.byref(ms),
+                                           ctypes.byref(n)))
+            out[name] = (ms.value, n.value)
+        return out
+
     def match_sums(self, dev_src: int, length: int) -> List[Tuple[int, int]]:
         return self.matches(0, self.match_device(dev_src, length))
 
