@@ -405,3 +405,171 @@ int64_t ref_cdc_hash(const uint8_t *src, uint64_t len, uint64_t pol, uint64_t mi
     ref_chunker_free(c);
     return rc ? rc : (int64_t)n;
 }
+
+/* ------------------------------------------------------------------ */
+/* Multi-threaded checker for the synthetic stream at full config      */
+/* sizes (C2: 64 GiB).  TEST INFRASTRUCTURE (checker only).            */
+/* ------------------------------------------------------------------ */
+/* The chunker's digest at every position where Next() tests the cut
+ * condition has slid >= 64 bytes since the last reset, so it equals the
+ * canonical fingerprint of the 64-byte window ending there (checked against
+ * ref_chunker_next by tests/test_oracle.py): candidate positions are a
+ * property of the bytes alone and are found in parallel over byte ranges
+ * (each warmed up on the 64 bytes before it).  The min/max rule then selects
+ * cuts sequentially over the sorted candidates; the final chunk (EOF) is
+ * re-chunked by ref_chunker_next from its start, which yields its Cut value
+ * exactly; chunks are hashed in parallel.  The stream bytes are generated
+ * on the fly (ref_synth_fill), so no thread holds more than a few MiB. */
+typedef struct {
+    uint64_t seed, lo, hi, mask;
+    unsigned shift;
+    const uint64_t *tab_out, *tab_mod;
+    uint64_t *pos;   /* found candidate positions */
+    uint64_t n, cap;
+} cand_job;
+
+static void *cand_worker(void *arg) {
+    cand_job *j = (cand_job *)arg;
+    enum { BLK = 1 << 20 };
+    uint8_t *buf = (uint8_t *)malloc(BLK + WINDOW);
+    uint8_t win[WINDOW];
+    memset(win, 0, sizeof win);
+    unsigned wpos = 0;
+    uint64_t digest = 0;
+    const uint64_t w0 = j->lo >= WINDOW ? j->lo - WINDOW : 0;
+    for (uint64_t b = w0; b < j->hi; b += BLK) {
+        const uint64_t n = (j->hi - b < BLK) ? j->hi - b : BLK;
+        ref_synth_fill(j->seed, b, n, buf);
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint8_t x = buf[i];
+            const uint8_t out = win[wpos];
+            win[wpos] = x;
+            wpos = (wpos + 1) % WINDOW;
+            digest ^= j->tab_out[out];
+            const uint64_t idx = digest >> j->shift;
+            digest = (digest << 8 | x) ^ j->tab_mod[idx & 0xff];
+            const uint64_t p = b + i;
+            if (p >= j->lo && p >= WINDOW - 1 && (digest & j->mask) == 0) {
+                if (j->n == j->cap) {
+                    j->cap = j->cap ? 2 * j->cap : 1024;
+                    j->pos = (uint64_t *)realloc(j->pos, j->cap * sizeof(uint64_t));
+                }
+                j->pos[j->n++] = p;
+            }
+        }
+    }
+    free(buf);
+    return NULL;
+}
+
+typedef struct {
+    uint64_t seed;
+    const uint64_t *starts, *lens;
+    uint8_t *ids;
+    int64_t n;
+    int64_t next;
+    pthread_mutex_t mu;
+} synth_hash_queue;
+
+static void *synth_hash_worker(void *arg) {
+    synth_hash_queue *q = (synth_hash_queue *)arg;
+    uint8_t *buf = NULL;
+    uint64_t bcap = 0;
+    for (;;) {
+        pthread_mutex_lock(&q->mu);
+        const int64_t i = q->next < q->n ? q->next++ : -1;
+        pthread_mutex_unlock(&q->mu);
+        if (i < 0) break;
+        if (q->lens[i] > bcap) {
+            bcap = q->lens[i];
+            buf = (uint8_t *)realloc(buf, bcap);
+        }
+        ref_synth_fill(q->seed, q->starts[i], q->lens[i], buf);
+        ref_sha256_fast(buf, q->lens[i], q->ids + 32 * i);
+    }
+    free(buf);
+    return NULL;
+}
+
+/* Chunk list + blob IDs of bytes [0, len) of the synthetic stream `seed`,
+ * with `threads` threads.  Returns #chunks (<= cap written) or < 0. */
+int64_t ref_cdc_synth_mt(uint64_t seed, uint64_t len, uint64_t pol, uint64_t min_size,
+                         uint64_t max_size, int avg_bits, int threads, uint64_t *starts,
+                         uint64_t *lens, uint64_t *cuts, uint8_t *ids, uint64_t cap) {
+    if (pol == 0 || min_size < WINDOW || max_size < min_size || threads < 1) return -1;
+    if (threads > 256) threads = 256;
+    uint64_t tab_out[256], tab_mod[256];
+    ref_tables(pol, tab_out, tab_mod);
+    const uint64_t mask = (avg_bits >= 64) ? ~0ull : ((1ull << avg_bits) - 1);
+    cand_job jobs[256];
+    pthread_t th[256];
+    for (int t = 0; t < threads; ++t) {
+        memset(&jobs[t], 0, sizeof jobs[t]);
+        jobs[t].seed = seed;
+        jobs[t].lo = len * (uint64_t)t / (uint64_t)threads;
+        jobs[t].hi = len * (uint64_t)(t + 1) / (uint64_t)threads;
+        jobs[t].mask = mask;
+        jobs[t].shift = (unsigned)(ref_pol_deg(pol) - 8);
+        jobs[t].tab_out = tab_out;
+        jobs[t].tab_mod = tab_mod;
+        pthread_create(&th[t], NULL, cand_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+    /* selection: Chunker.Next's min/max rule over the sorted candidates */
+    uint64_t n = 0, s = 0;
+    int jt = 0;
+    uint64_t ji = 0;
+    int64_t rc = 0;
+    while (s < len) {
+        const uint64_t lo = s + min_size - 1, lim = s + max_size - 1;
+        while (jt < threads && (ji >= jobs[jt].n || jobs[jt].pos[ji] < lo)) {
+            if (ji < jobs[jt].n) { ++ji; continue; }
+            ++jt;
+            ji = 0;
+        }
+        uint64_t cut;
+        int eof = 0;
+        if (jt < threads && jobs[jt].pos[ji] <= lim && jobs[jt].pos[ji] < len) {
+            cut = jobs[jt].pos[ji];
+        } else if (lim < len) {
+            cut = lim;   /* forced at MaxSize */
+        } else {
+            cut = len - 1;
+            eof = 1;
+        }
+        if (n >= cap) { rc = -2; break; }
+        starts[n] = s;
+        lens[n] = cut - s + 1;
+        if (!eof) {
+            uint8_t w[WINDOW];
+            ref_synth_fill(seed, cut - (WINDOW - 1), WINDOW, w);
+            cuts[n] = ref_window_fp(w, WINDOW - 1, pol);
+        } else {
+            /* the final chunk: Next() from its start gives its Cut value */
+            uint8_t *tail = (uint8_t *)malloc(lens[n] ? lens[n] : 1);
+            ref_synth_fill(seed, s, lens[n], tail);
+            ref_chunker *c = ref_chunker_new(tail, lens[n], pol, min_size, max_size, avg_bits);
+            uint64_t ts, tl, tk;
+            if (!c || !ref_chunker_next(c, &ts, &tl, &tk) || tl != lens[n]) rc = -3;
+            cuts[n] = tk;
+            if (c) ref_chunker_free(c);
+            free(tail);
+        }
+        ++n;
+        s = cut + 1;
+    }
+    for (int t = 0; t < threads; ++t) free(jobs[t].pos);
+    if (rc) return rc;
+    synth_hash_queue q;
+    memset(&q, 0, sizeof q);
+    q.seed = seed;
+    q.starts = starts;
+    q.lens = lens;
+    q.ids = ids;
+    q.n = (int64_t)n;
+    pthread_mutex_init(&q.mu, NULL);
+    for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, synth_hash_worker, &q);
+    for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+    pthread_mutex_destroy(&q.mu);
+    return (int64_t)n;
+}

@@ -175,3 +175,25 @@ def rsync_walk(win: np.ndarray, win_lo: int, length: int, hi: int, entry: int, w
     if n < 0:
         raise RuntimeError("walk restatement failed")
     return [(int(mo[i]), int(mi[i])) for i in range(n)], int(fa.value), int(eo.value), int(ew.value)
+
+
+def cdc_synth_mt(seed: int, length: int, pol: int, mn: int, mx: int, avg_bits: int,
+                 threads: int):
+    """Chunk list + blob IDs of the synthetic stream's first `length` bytes,
+    multi-threaded (oracle/cdc_ref.c ref_cdc_synth_mt): [(start, len, cut, id)]."""
+    L = lib()
+    if not getattr(L, "_mt_ready", False):
+        u64, vp, ci = ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int
+        L.ref_cdc_synth_mt.restype = ctypes.c_int64
+        L.ref_cdc_synth_mt.argtypes = [u64, u64, u64, u64, u64, ci, ci, vp, vp, vp, vp, u64]
+        L._mt_ready = True
+    cap = length // max(1, mn) + 8
+    s = np.zeros(cap, np.uint64)
+    ln = np.zeros(cap, np.uint64)
+    c = np.zeros(cap, np.uint64)
+    ids = np.zeros((cap, 32), np.uint8)
+    n = L.ref_cdc_synth_mt(seed, length, pol, mn, mx, avg_bits, threads, s.ctypes.data,
+                           ln.ctypes.data, c.ctypes.data, ids.ctypes.data, cap)
+    if n < 0:
+        raise RuntimeError(f"multi-threaded oracle failed ({n})")
+    return s[:n], ln[:n], c[:n], ids[:n]

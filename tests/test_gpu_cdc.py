@@ -203,8 +203,10 @@ def test_synth_device_matches_oracle(gpu):
         assert (t.cpu().numpy() == O.synth(seed, off, n)).all()
 
 
+@pytest.mark.timeout(900)
 def test_full_size_c2_properties(gpu):
-    """Config C2 size (64 GiB, seed 2, default parameters) through properties:
+    """Config C2 size (64 GiB, seed 2, default parameters) through properties
+    and then exactly:
     chunks tile the volume, lengths obey min/max, Cut & mask == 0 unless forced,
     and sampled chunks match the oracle (cut rule from the chunk start) and
     hashlib (blob ID)."""
@@ -241,6 +243,18 @@ def test_full_size_c2_properties(gpu):
         assert (c.Start + ref[0], ref[1], ref[2], ref[3]) == (c.Start, c.Length, c.Cut, c.ID.hex())
     del t
     torch.cuda.empty_cache()
+    # the whole 43.7 K-row list, exactly: (Start, Length, Cut, blob ID) of
+    # every chunk against the multi-threaded oracle over the same stream
+    # (candidates found in parallel byte ranges, sequential min/max selection,
+    # parallel SHA-256; oracle/cdc_ref.c ref_cdc_synth_mt, pinned against the
+    # sequential Chunker.Next restatement by tests/test_oracle.py)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    s, ln, cu, ids = O.cdc_synth_mt(2, n, P.TEST_POL, MIN, MAX, 20, threads)
+    assert nch == len(s)
+    assert [c.Start for c in ch] == s.tolist()
+    assert [c.Length for c in ch] == ln.tolist()
+    assert [c.Cut for c in ch] == cu.tolist()
+    assert [c.ID for c in ch] == [bytes(r) for r in ids]
 
 
 @pytest.mark.parametrize("budget", [1, 2, 3, 7, 100, 0])

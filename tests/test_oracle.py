@@ -138,3 +138,19 @@ def test_rsync_sum_sizes_c4():
     assert [v.value for v in vals] == [131072, 5, 2097152, 0]
     assert O.lib().ref_rsync_sum_sizes(1000, 0, *[ctypes.byref(v) for v in vals]) == 0
     assert [v.value for v in vals] == [700, 2, 2, 300]
+
+
+@pytest.mark.parametrize("seed,n,mn,mx,ab", [
+    (1, 1 << 30, 512 << 10, 8 << 20, 20),   # C1
+    (5, 40 << 20, 64 << 10, 1 << 20, 16),
+    (9, 3 << 20, 4096, 65536, 13),          # forced cuts
+    (11, 700 << 10, 512 << 10, 8 << 20, 20),  # one EOF chunk > MinSize
+    (12, 100, 512 << 10, 8 << 20, 20),      # one tiny EOF chunk
+])
+def test_multithreaded_synth_oracle_equals_sequential(seed, n, mn, mx, ab):
+    """The multi-threaded full-size checker (ref_cdc_synth_mt: parallel
+    candidate ranges + sequential selection + parallel SHA-256) equals the
+    sequential Chunker.Next restatement, Cut values and IDs included."""
+    s, ln, cu, ids = O.cdc_synth_mt(seed, n, P.TEST_POL, mn, mx, ab, 7)
+    got = [(int(a), int(b), int(c), bytes(i).hex()) for a, b, c, i in zip(s, ln, cu, ids)]
+    assert got == O.cdc_hash(O.synth(seed, 0, n), P.TEST_POL, mn, mx, ab, n_hash=4)

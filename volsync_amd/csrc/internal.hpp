@@ -279,6 +279,59 @@ hipError_t launch_rs_scan(const RsScanArgs &a, int cus, hipStream_t s);
 // needs.  flag holds 2n bytes.
 hipError_t launch_rs_chained(const uint64_t *off, uint64_t n, uint64_t blength, uint8_t *flag,
                              hipStream_t s);
+// ---- device-resident greedy walk (rsync_walk.hip, XXH3, blength > 240) -----
+// Offsets are data-relative.  The owned range [lo, hi) is cut into segments
+// of seg_len; each wave walks one segment (spec kernel: from its own start;
+// stitch kernel: from the previous segment's exit, merging into the spec).
+struct RsWalkArgs {
+    const uint8_t *data;   // source bytes, 16-byte aligned
+    uint64_t dlen;
+    int64_t full_end;      // offsets below it have a full window (F - blength + 1)
+    int64_t lo, hi;        // the owned range
+    int64_t seg_len;
+    uint32_t nseg, cap;    // segments, match capacity per segment
+    uint32_t blength, count, remainder;
+    int csum_type;
+    uint64_t seed;
+    uint64_t s2mask_lo, s2mask_hi;   // the first s2length bytes of (lo64, hi64)
+    const uint64_t *sum2p;           // [count][2] zero-padded strong sums
+    const uint32_t *sum1;            // [count]
+    const uint64_t *tkey;            // sorted (sum1 << 32 | ~index)
+    const uint32_t *dir;
+    const uint32_t *filt, *filt_l;
+    uint32_t dbits, fbits, lbits;
+    int64_t e0;                      // segment 0's entry (offset, want_i)
+    int32_t w0;
+    int32_t spec_w0;                 // want_i of segment 0's speculative walk
+    uint32_t *work;                  // segment work counter
+    uint32_t *flags;                 // 1: an exit changed, 2: capacity overflow
+    // speculative walks [nseg * cap] / [nseg]
+    int64_t *spec_off;
+    int32_t *spec_idx;
+    int64_t *spec_fab;               // false alarms before the match's offset
+    uint32_t *spec_n;
+    uint64_t *spec_fa;
+    int64_t *spec_exit;
+    int32_t *spec_exitw;
+    // final walks: fin_off[0, fin_n) then spec[fin_from, spec_n) (fin_from
+    // 0xffffffff: the final walk is the speculative one)
+    int64_t *fin_entry;
+    int32_t *fin_entryw;
+    uint32_t *fin_from, *fin_n;
+    uint64_t *fin_fa;
+    int64_t *fin_off;
+    int32_t *fin_idx;
+    int64_t *fin_fab;
+    // exits of the current final walks, double-buffered across stitch passes
+    const int64_t *exit_old;
+    const int32_t *exitw_old;
+    int64_t *exit_new;
+    int32_t *exitw_new;
+    uint64_t *dbg;                   // debug builds: per-wave progress records (host-mapped)
+};
+hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t s);
+hipError_t launch_rs_pad_sum2(const uint8_t *sum2, uint32_t count, uint32_t s2length,
+                              uint64_t *out, hipStream_t s);
 hipError_t launch_rs_sort_cands(void *tmp, size_t tmp_bytes, const uint64_t *off_in,
                                 uint64_t *off_out, const uint32_t *sum_in, uint32_t *sum_out,
                                 uint64_t n, int end_bit, hipStream_t s);

@@ -84,6 +84,14 @@ struct RsRun {
     int64_t fin_fa = 0, fin_exit = 0;
     int32_t fin_exit_want = 0;
     int state = 0;                       // 0 none, 1 scanned, 2 stitched, 3 finished
+    // device-walk path (rsync_walk.hip): segments of the owned range, the
+    // current stitched exit, and the walk's continuation past the last full
+    // window (the short last block's one window, checked on the host)
+    bool dev_walk = false;
+    RsWalkArgs wa{};
+    int xcur = 0;                        // which exit buffer holds the current exits
+    std::vector<vs_match> tail;          // at most one match
+    int64_t tail_fa = 0;
 };
 
 struct vs_rsync {
@@ -108,6 +116,12 @@ struct vs_rsync {
     std::vector<uint64_t> tkey_h;   // sorted (sum1 << 32 | ~i)
     std::vector<uint32_t> dir_h;
     DevBuf d_sum1, d_keys, d_tkey, d_dir, d_filt, d_tmp;
+    DevBuf d_sum2p, d_sum2tmp;      // zero-padded 16-byte strong sums (device walk)
+    // device walk: per-segment results and two exit buffers
+    DevBuf w_spec_off, w_spec_idx, w_spec_fab, w_spec_n, w_spec_fa, w_spec_exit, w_spec_exitw;
+    DevBuf w_fin_entry, w_fin_entryw, w_fin_from, w_fin_n, w_fin_fa, w_fin_off, w_fin_idx,
+        w_fin_fab;
+    DevBuf w_exit[2], w_exitw[2], w_ctl;
     // scan
     DevBuf px, pt, pxs, pts, partials, c_off, c_sum, c_off2, c_sum2, n_cand, sort_tmp;
     // verification
@@ -641,6 +655,295 @@ int scan_candidates(vs_rsync *h, std::vector<uint64_t> &batch) {
     return 0;
 }
 
+// ---- device-walk path (rsync_walk.hip) -----------------------------------------
+#ifdef VS_WALK_DEBUG
+// debug builds: per-wave progress records in host-mapped memory, dumped by a
+// watchdog thread if a walk launch has not finished after VSGPU_WALK_WATCH s
+}  // namespace
+#include <atomic>
+#include <thread>
+namespace {
+uint64_t *g_walk_dbg = nullptr;
+std::atomic<int> g_walk_gen{0};
+void walk_watch_arm(vs_rsync *h, RsWalkArgs &a) {
+    const char *e = getenv("VSGPU_WALK_WATCH");
+    if (!e) return;
+    if (!g_walk_dbg && hipHostMalloc((void **)&g_walk_dbg, 4096 * 32, hipHostMallocMapped) != hipSuccess)
+        return;
+    memset(g_walk_dbg, 0xff, 4096 * 32);
+    a.dbg = g_walk_dbg;
+    const int gen = ++g_walk_gen;
+    const double secs = atof(e);
+    std::thread([gen, secs]() {
+        std::this_thread::sleep_for(std::chrono::duration<double>(secs));
+        if (g_walk_gen.load() != gen) return;
+        fprintf(stderr, "walk watchdog: launch %d still running; per-wave phase/offset/extra:\n", gen);
+        for (int w = 0; w < 4096; ++w) {
+            const volatile uint64_t *r = g_walk_dbg + 4 * w;
+            if (r[0] == ~0ull) continue;
+            fprintf(stderr, "  wave %d phase %llu o %lld x %llx\n", w, (unsigned long long)r[0],
+                    (long long)r[1], (unsigned long long)r[2]);
+        }
+        fflush(stderr);
+    }).detach();
+    (void)h;
+}
+void walk_watch_done() { ++g_walk_gen; }
+#else
+inline void walk_watch_arm(vs_rsync *, RsWalkArgs &) {}
+inline void walk_watch_done() {}
+#endif
+bool walk_eligible(const vs_rsync *h) {
+    static const bool host_only = getenv("VSGPU_RS_HOSTWALK") != nullptr;
+    return !host_only && (h->csum_type == VS_CSUM_XXH3_128 || h->csum_type == VS_CSUM_XXH3_64) &&
+           h->blength > 240;
+}
+
+// get_checksum1 on the host
+uint32_t host_weak(const uint8_t *p, int64_t n) {
+    uint32_t s1 = 0, s2 = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        s1 += (uint32_t)(int32_t)(int8_t)p[i];
+        s2 += s1;
+    }
+    return (s1 & 0xffffu) | (s2 << 16);
+}
+
+// Stitch passes until no segment's exit changes (Jacobi: a changed exit
+// reaches the next segment in the next pass).  Returns the last segment's exit.
+int walk_converge(vs_rsync *h, int64_t *x, int32_t *xw) {
+    RsRun &r = h->run;
+    RsWalkArgs &a = r.wa;
+    for (uint32_t pass = 0;; ++pass) {
+        if (pass > a.nseg + 2) return fail(VS_ERR_STATE, "device walk stitch did not converge");
+        a.exit_old = h->w_exit[r.xcur].as<int64_t>();
+        a.exitw_old = h->w_exitw[r.xcur].as<int32_t>();
+        a.exit_new = h->w_exit[r.xcur ^ 1].as<int64_t>();
+        a.exitw_new = h->w_exitw[r.xcur ^ 1].as<int32_t>();
+        VS_HIP(hipMemsetAsync(a.flags, 0, 4, h->stream));
+        KernelTimer kt(h, 0);
+        walk_watch_arm(h, a);
+        VS_HIP(launch_rs_walk(a, true, h->cus, h->stream));
+        kt.stop();
+        VS_HIP(hipMemcpyAsync(h->pinned, a.flags, 4, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipStreamSynchronize(h->stream));
+        walk_watch_done();
+        kt.fold();
+        r.xcur ^= 1;
+        const uint32_t fl = (uint32_t)h->pinned[0];
+        if (fl & 2u) return fail(VS_ERR_STATE, "device walk: segment match capacity exceeded");
+        if (!(fl & 1u)) break;
+    }
+    VS_HIP(hipMemcpyAsync(h->pinned, h->w_exit[r.xcur].as<int64_t>() + (a.nseg - 1), 8,
+                          hipMemcpyDeviceToHost, h->stream));
+    VS_HIP(hipMemcpyAsync((int32_t *)(h->pinned + 1), h->w_exitw[r.xcur].as<int32_t>() + (a.nseg - 1),
+                          4, hipMemcpyDeviceToHost, h->stream));
+    VS_HIP(hipStreamSynchronize(h->stream));
+    *x = (int64_t)h->pinned[0];
+    *xw = *(const int32_t *)(h->pinned + 1);
+    return 0;
+}
+
+// The walk's continuation past the last full window: of the offsets in
+// [max(x, full_end), end) only F - remainder (the short last block's one
+// window) can match.  x / xw: the device walk's exit.  Sets the range exit.
+int walk_tail(vs_rsync *h, int64_t x, int32_t xw, int64_t *exit_off, int32_t *exit_want) {
+    RsRun &r = h->run;
+    const int64_t F = r.flen - r.origin, hi = r.own_hi - r.origin;
+    r.tail.clear();
+    r.tail_fa = 0;
+    int64_t o = x;
+    int32_t want = xw;
+    const int64_t t = F - h->remainder;
+    static const bool trace = getenv("VSGPU_RS_TRACE") != nullptr;
+    if (trace)
+        fprintf(stderr, "rs: walk tail: device exit %lld want %d, tail offset %lld, range end %lld\n",
+                (long long)x, xw, (long long)t, (long long)hi);
+    if (h->remainder && o <= t && t < hi && t >= 0) {
+        std::vector<uint8_t> buf((size_t)h->remainder);
+        VS_HIP(hipMemcpyAsync(buf.data(), r.dev + t, buf.size(), hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipStreamSynchronize(h->stream));
+        const uint32_t sum = host_weak(buf.data(), h->remainder);
+        const uint32_t s2 = (uint32_t)h->s2length;
+        // the strong sum on the device (the same kernel the walk's windows use)
+        uint8_t st[16] = {0};
+        {
+            const uint64_t vo = (uint64_t)t;
+            const uint32_t vl = (uint32_t)h->remainder;
+            VS_TRY(h->v_off.ensure(8));
+            VS_TRY(h->v_len.ensure(4));
+            VS_TRY(h->v_out.ensure(16));
+            VS_HIP(hipMemcpyAsync(h->v_off.p, &vo, 8, hipMemcpyHostToDevice, h->stream));
+            VS_HIP(hipMemcpyAsync(h->v_len.p, &vl, 4, hipMemcpyHostToDevice, h->stream));
+            VS_HIP(launch_rs_strong(r.dev, h->v_off.as<uint64_t>(), h->v_len.as<uint32_t>(), 1,
+                                    h->csum_type, h->seed, s2, h->v_out.as<uint8_t>(), vl,
+                                    h->stream));
+            VS_HIP(hipMemcpyAsync(st, h->v_out.p, s2, hipMemcpyDeviceToHost, h->stream));
+            VS_HIP(hipStreamSynchronize(h->stream));
+            h->st_hashed += 1;
+        }
+        o = t + 1;   // no match: hash_search's loop ends (end = F + 1 - remainder)
+        for (int64_t q = group_start(h, sum); q >= 0 && q < h->count &&
+                                             (uint32_t)(h->tkey_h[q] >> 32) == sum;
+             ++q) {
+            int32_t i = (int32_t)~(uint32_t)h->tkey_h[q];
+            if (blen(h, i) != h->remainder) continue;
+            if (memcmp(st, h->sum2.data() + (size_t)i * s2, s2) != 0) {
+                ++r.tail_fa;
+                continue;
+            }
+            if (i != want && want < h->count && sum == h->sum1[want] &&
+                memcmp(st, h->sum2.data() + (size_t)want * s2, s2) == 0)
+                i = want;
+            r.tail.push_back({t, i, 0});
+            want = i + 1;
+            o = t + blen(h, i);
+            break;
+        }
+    }
+    *exit_off = std::max(o, hi) + r.origin;
+    *exit_want = want;
+    return 0;
+}
+
+// match_scan on the device-walk path: segments, speculative walks, stitch
+// from the range's speculative entry
+int walk_scan(vs_rsync *h) {
+    RsRun &r = h->run;
+    RsWalkArgs &a = r.wa;
+    a = RsWalkArgs{};
+    const int64_t F = r.flen - r.origin;
+    a.data = r.dev;
+    a.dlen = (uint64_t)r.dlen;
+    a.full_end = F - h->blength + 1;
+    a.lo = r.own_lo - r.origin;
+    a.hi = r.own_hi - r.origin;
+    a.seg_len = std::max<int64_t>((int64_t)h->blength * 32, 1 << 20);
+    a.nseg = (uint32_t)((a.hi - a.lo + a.seg_len - 1) / a.seg_len);
+    a.cap = (uint32_t)(a.seg_len / h->blength + 2);
+    a.blength = (uint32_t)h->blength;
+    a.count = (uint32_t)h->count;
+    a.remainder = (uint32_t)h->remainder;
+    a.csum_type = h->csum_type;
+    a.seed = h->seed;
+    const uint32_t s2 = (uint32_t)h->s2length;
+    a.s2mask_lo = s2 >= 8 ? ~0ull : ((1ull << (8 * s2)) - 1);
+    a.s2mask_hi = s2 <= 8 ? 0ull : (s2 >= 16 ? ~0ull : ((1ull << (8 * (s2 - 8))) - 1));
+    a.sum2p = h->d_sum2p.as<uint64_t>();
+    a.sum1 = h->d_sum1.as<uint32_t>();
+    a.tkey = h->d_tkey.as<uint64_t>();
+    a.dir = h->d_dir.as<uint32_t>();
+    a.filt = h->d_filt.as<uint32_t>();
+    a.fbits = h->fbits;
+    a.dbits = h->dbits;
+    a.lbits = rs_lds_filter_bits(h->fbits);
+    a.filt_l = h->d_filt.as<uint32_t>() + ((1ull << h->fbits) / 32);
+    const size_t ns = std::max<uint32_t>(a.nseg, 1), nc = ns * a.cap;
+    VS_TRY(h->w_spec_off.ensure(nc * 8));
+    VS_TRY(h->w_spec_idx.ensure(nc * 4));
+    VS_TRY(h->w_spec_fab.ensure(nc * 8));
+    VS_TRY(h->w_fin_off.ensure(nc * 8));
+    VS_TRY(h->w_fin_idx.ensure(nc * 4));
+    VS_TRY(h->w_fin_fab.ensure(nc * 8));
+    VS_TRY(h->w_spec_n.ensure(ns * 4));
+    VS_TRY(h->w_spec_fa.ensure(ns * 8));
+    VS_TRY(h->w_spec_exit.ensure(ns * 8));
+    VS_TRY(h->w_spec_exitw.ensure(ns * 4));
+    VS_TRY(h->w_fin_entry.ensure(ns * 8));
+    VS_TRY(h->w_fin_entryw.ensure(ns * 4));
+    VS_TRY(h->w_fin_from.ensure(ns * 4));
+    VS_TRY(h->w_fin_n.ensure(ns * 4));
+    VS_TRY(h->w_fin_fa.ensure(ns * 8));
+    for (int i = 0; i < 2; ++i) {
+        VS_TRY(h->w_exit[i].ensure(ns * 8));
+        VS_TRY(h->w_exitw[i].ensure(ns * 4));
+    }
+    VS_TRY(h->w_ctl.ensure(64));
+    a.work = h->w_ctl.as<uint32_t>();
+    a.flags = h->w_ctl.as<uint32_t>() + 4;
+    a.spec_off = h->w_spec_off.as<int64_t>();
+    a.spec_idx = h->w_spec_idx.as<int32_t>();
+    a.spec_fab = h->w_spec_fab.as<int64_t>();
+    a.spec_n = h->w_spec_n.as<uint32_t>();
+    a.spec_fa = h->w_spec_fa.as<uint64_t>();
+    a.spec_exit = h->w_spec_exit.as<int64_t>();
+    a.spec_exitw = h->w_spec_exitw.as<int32_t>();
+    a.fin_entry = h->w_fin_entry.as<int64_t>();
+    a.fin_entryw = h->w_fin_entryw.as<int32_t>();
+    a.fin_from = h->w_fin_from.as<uint32_t>();
+    a.fin_n = h->w_fin_n.as<uint32_t>();
+    a.fin_fa = h->w_fin_fa.as<uint64_t>();
+    a.fin_off = h->w_fin_off.as<int64_t>();
+    a.fin_idx = h->w_fin_idx.as<int32_t>();
+    a.fin_fab = h->w_fin_fab.as<int64_t>();
+    a.e0 = r.spec_entry - r.origin;
+    a.w0 = r.spec_want;
+    a.spec_w0 = r.spec_want;
+    // speculative walks -> w_exit[0]
+    r.xcur = 0;
+    a.exit_old = h->w_exit[1].as<int64_t>();
+    a.exitw_old = h->w_exitw[1].as<int32_t>();
+    a.exit_new = h->w_exit[0].as<int64_t>();
+    a.exitw_new = h->w_exitw[0].as<int32_t>();
+    const double t0 = now_ms();
+    VS_HIP(hipMemsetAsync(a.flags, 0, 4, h->stream));
+    {
+        KernelTimer kt(h, 0);
+        walk_watch_arm(h, a);
+        VS_HIP(launch_rs_walk(a, false, h->cus, h->stream));
+        kt.stop();
+        VS_HIP(hipMemcpyAsync(h->pinned, a.flags, 4, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipStreamSynchronize(h->stream));
+        walk_watch_done();
+        kt.fold();
+        if ((uint32_t)h->pinned[0] & 2u)
+            return fail(VS_ERR_STATE, "device walk: segment match capacity exceeded");
+    }
+    int64_t x = 0;
+    int32_t xw = 0;
+    VS_TRY(walk_converge(h, &x, &xw));
+    VS_TRY(walk_tail(h, x, xw, &r.spec_exit, &r.spec_exit_want));
+    h->ms[2] += now_ms() - t0;
+    return 0;
+}
+
+// the device walk's result (matches data-relative, in order) and false alarms
+int walk_collect(vs_rsync *h, std::vector<vs_match> &out, int64_t *fa) {
+    RsRun &r = h->run;
+    const RsWalkArgs &a = r.wa;
+    const size_t ns = a.nseg, nc = ns * a.cap;
+    std::vector<uint32_t> sn(ns), fn(ns), ff(ns);
+    std::vector<uint64_t> ffa(ns);
+    out.clear();
+    int64_t total = 0;
+    if (ns) {
+        std::vector<int64_t> so(nc), fo(nc);
+        std::vector<int32_t> si(nc), fi(nc);
+        VS_HIP(hipMemcpyAsync(sn.data(), a.spec_n, ns * 4, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync(fn.data(), a.fin_n, ns * 4, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync(ff.data(), a.fin_from, ns * 4, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync(ffa.data(), a.fin_fa, ns * 8, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync(so.data(), a.spec_off, nc * 8, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync(si.data(), a.spec_idx, nc * 4, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync(fo.data(), a.fin_off, nc * 8, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync(fi.data(), a.fin_idx, nc * 4, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipStreamSynchronize(h->stream));
+        for (size_t k = 0; k < ns; ++k) {
+            const size_t b = k * a.cap;
+            uint32_t from = 0;
+            if (ff[k] != 0xffffffffu) {
+                for (uint32_t j = 0; j < fn[k]; ++j) out.push_back({fo[b + j], fi[b + j], 0});
+                from = ff[k];
+            }
+            for (uint32_t j = from; j < sn[k]; ++j) out.push_back({so[b + j], si[b + j], 0});
+            total += (int64_t)ffa[k];
+        }
+    }
+    for (const vs_match &m : r.tail) out.push_back(m);
+    *fa = total + r.tail_fa;
+    return 0;
+}
+
 // ---- sharded match_sums: scan + speculative walk, stitch, finish
 int match_scan(vs_rsync *h, const void *dev_src, int64_t dlen, int64_t origin, int64_t flen,
                int64_t own_lo, int64_t own_hi, int64_t *exit_off, int32_t *exit_want) {
@@ -673,6 +976,15 @@ int match_scan(vs_rsync *h, const void *dev_src, int64_t dlen, int64_t origin, i
         // match_sums: no sums (or no owned offsets) -> all literal
         r.spec_exit = std::max(own_lo, own_hi);
         r.spec_exit_want = r.spec_want;
+    } else if (walk_eligible(h)) {
+        if (((uintptr_t)dev_src & 15) != 0)
+            return fail(VS_ERR_ARG, "device source must be 16-byte aligned");
+        VS_TRY(order_after_null(h));
+        r.dev_walk = true;
+        VS_TRY(walk_scan(h));
+        int64_t fa = 0;
+        VS_TRY(walk_collect(h, r.spec, &fa));
+        r.spec_fa = fa;
     } else {
         VS_TRY(order_after_null(h));
         std::vector<uint64_t> &batch = h->h_batch;
@@ -713,6 +1025,19 @@ int match_stitch(vs_rsync *h, int64_t entry, int32_t want, int64_t *exit_off, in
         r.fin_fa = 0;
         r.fin_exit = std::max(entry, r.own_hi);
         r.fin_exit_want = want;
+    } else if (r.dev_walk) {
+        r.wa.e0 = entry - r.origin;
+        r.wa.w0 = want;
+        int64_t x = 0;
+        int32_t xw = 0;
+        const double t0 = now_ms();
+        VS_TRY(walk_converge(h, &x, &xw));
+        VS_TRY(walk_tail(h, x, xw, &r.fin_exit, &r.fin_exit_want));
+        int64_t fa = 0;
+        VS_TRY(walk_collect(h, r.fin, &fa));
+        h->ms[2] += now_ms() - t0;
+        r.use_spec = false;
+        r.fin_fa = fa;
     } else {
         SpecWalk sw{&r.spec, &r.spec_fa_before, r.spec_fa, r.spec_exit - r.origin, r.spec_exit_want};
         std::vector<uint64_t> &batch = h->h_batch;
@@ -797,7 +1122,11 @@ VS_API void vs_rsync_close(vs_rsync *h) {
     for (DevBuf *b : {&h->d_sum1, &h->d_keys, &h->d_tkey, &h->d_dir, &h->d_filt, &h->d_tmp, &h->px,
                       &h->pt, &h->pxs, &h->pts, &h->partials, &h->c_off, &h->c_sum, &h->c_off2,
                       &h->c_sum2, &h->n_cand, &h->sort_tmp, &h->v_off, &h->v_len, &h->v_out,
-                      &h->d_flag})
+                      &h->d_flag, &h->d_sum2p, &h->d_sum2tmp, &h->w_spec_off, &h->w_spec_idx,
+                      &h->w_spec_fab, &h->w_spec_n, &h->w_spec_fa, &h->w_spec_exit,
+                      &h->w_spec_exitw, &h->w_fin_entry, &h->w_fin_entryw, &h->w_fin_from,
+                      &h->w_fin_n, &h->w_fin_fa, &h->w_fin_off, &h->w_fin_idx, &h->w_fin_fab,
+                      &h->w_exit[0], &h->w_exit[1], &h->w_exitw[0], &h->w_exitw[1], &h->w_ctl})
         b->release();
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (HostReg *r : {&h->reg_off, &h->reg_sum, &h->reg_flag}) r->release();
@@ -851,9 +1180,16 @@ VS_API int vs_rsync_load_sums(vs_rsync *h, int32_t count, int32_t blength, int32
     h->sum1.assign(sum1, sum1 + count);
     h->sum2.assign(sum2, sum2 + (size_t)count * s2length);
     VS_TRY(h->d_sum1.ensure((size_t)std::max(count, 1) * 4));
-    if (count)
+    VS_TRY(h->d_sum2p.ensure((size_t)std::max(count, 1) * 16));
+    VS_TRY(h->d_sum2tmp.ensure((size_t)std::max(count, 1) * s2length));
+    if (count) {
         VS_HIP(hipMemcpyAsync(h->d_sum1.p, sum1, (size_t)count * 4, hipMemcpyHostToDevice,
                               h->stream));
+        VS_HIP(hipMemcpyAsync(h->d_sum2tmp.p, sum2, (size_t)count * s2length,
+                              hipMemcpyHostToDevice, h->stream));
+        VS_HIP(launch_rs_pad_sum2(h->d_sum2tmp.as<uint8_t>(), (uint32_t)count, (uint32_t)s2length,
+                                  h->d_sum2p.as<uint64_t>(), h->stream));
+    }
     VS_TRY(build_table(h));
     h->ms[1] = now_ms() - t0;
     return 0;
@@ -880,6 +1216,10 @@ VS_API int vs_rsync_load_sums_device(vs_rsync *h, int32_t count, int32_t blength
         VS_HIP(hipMemcpyAsync(h->sum2.data(), dev_sum2, h->sum2.size(), hipMemcpyDeviceToHost,
                               h->stream));
     }
+    VS_TRY(h->d_sum2p.ensure((size_t)std::max(count, 1) * 16));
+    if (count)
+        VS_HIP(launch_rs_pad_sum2(dev_sum2, (uint32_t)count, (uint32_t)s2length,
+                                  h->d_sum2p.as<uint64_t>(), h->stream));
     VS_TRY(build_table(h));
     h->ms[1] = now_ms() - t0;
     return 0;
