@@ -247,8 +247,13 @@ def rsync_main(args):
         nm = int(c.item())
     value = (dtotal + plan.total) * args.steps / dt / 1e9
     own_src = sspec.own_hi - sspec.own_lo
+    # the dominant kernel: rs_walk_spec_kernel, one launch per step over the
+    # rank's whole source range (algorithmic bytes = those source bytes, each
+    # read once by the walk: a window hash where it matches, the rolling scan
+    # elsewhere); the stitch passes are reported beside it
     scan_ms, scan_n = kt["scan"]
     scan_gbs = own_src / (scan_ms / scan_n) / 1e6 if scan_n else 0.0
+    sti_ms, sti_n = kt["stitch"]
     sig_ms, sig_n = kt["signatures"]
     ver_ms, ver_n = kt["verify"]
     if rank == 0:
@@ -266,15 +271,15 @@ def rsync_main(args):
                        "blength": hdr.blength, "s2length": hdr.s2length, "count": hdr.count,
                        "source_bytes": plan.total, "csum": "xxh128", "checksum_seed": hex(seed),
                        "matches": nm},
-            # dominant kernel: the weak scan over the rank's source range;
-            # algorithmic bytes per launch = the source bytes it covers (one
-            # read of each), over its HIP-event launch time
             "roofline": {"bound": "hbm", "achieved": round(scan_gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(scan_gbs / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel": "rs_scan_kernel (weak scan)",
+                         "traffic": None,
+                         "kernel": "rs_walk_spec_kernel (device hash_search, speculative pass)",
                          "avg_launch_ms": round(scan_ms / scan_n, 3) if scan_n else None,
                          "launches": scan_n},
-            "kernels_ms_per_step": {"scan": round(scan_ms / args.steps, 3),
+            "kernels_ms_per_step": {"walk_spec": round(scan_ms / args.steps, 3),
+                                    "walk_stitch": round(sti_ms / args.steps, 3),
+                                    "stitch_launches_per_step": round(sti_n / args.steps, 2),
                                     "verify": round(ver_ms / args.steps, 3),
                                     "signatures": round(sig_ms / args.steps, 3)},
             "signatures_GBps": round(n / (sig_ms / sig_n) / 1e6, 1) if sig_n else None,
@@ -285,9 +290,9 @@ def rsync_main(args):
         }
         try:
             tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
-            r = tj["rs_scan"]
+            r = tj["rs_walk_spec"]
             out["roofline"]["traffic"] = round(r["bytes_per_source_byte"] * own_src)
-            out["roofline"]["traffic_source"] = tj["rs_scan"]["source"]
+            out["roofline"]["traffic_source"] = r["source"]
         except (OSError, ValueError, KeyError):
             pass
         if world == 1 and not args.no_cpu_baseline:
@@ -374,13 +379,15 @@ def smallfiles_main(args):
     torch.cuda.empty_cache()
     lens = torch.from_numpy(sizes.astype(np.int32)).to(dev)
     ids = torch.zeros((nf, 32), dtype=torch.uint8, device=dev)
+    first = torch.zeros(nf, dtype=torch.int32, device=dev)
     sh = DeviceSha256(local)
     sh.set_wide(args.hash_wide, args.wide_drain)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def step():
         sh.run(packed.data_ptr(), ofd.data_ptr(), lens.data_ptr(), nf, ids.data_ptr(), stream)
-        return torch.unique(ids[:, :8].contiguous().view(torch.int64)).numel()
+        # SaveBlob's dedup on the device (vs_blob_dedup): first occurrence per ID
+        return sh.dedup(ids.data_ptr(), nf, first.data_ptr(), stream)
 
     for _ in range(args.warmup):
         step()
@@ -410,7 +417,7 @@ def smallfiles_main(args):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     # kernel time: the hash launches ran on `stream` between the two events
-    # (unique() included: an upper bound on the hash time)
+    # (the dedup included: an upper bound on the hash time)
     k_ms = ev0.elapsed_time(ev1) / args.steps
     gbs = total / k_ms / 1e6
     if rank == 0:
@@ -558,6 +565,98 @@ def dry_main(args):
         dist.destroy_process_group()
 
 
+def host_main(args):
+    """C2 fed from host memory through the streaming drop-in API, as
+    gpuchunker's Chunker.Next does: vs_cdc_feed of 64 MiB reads taken from a
+    pinned host image of the volume, vs_cdc_next for the chunks until EOF
+    ("host-pinned end-to-end").  A step = one whole
+    volume streamed, chunked and hashed, every chunk (with its blob ID)
+    returned to the host.  value = volume bytes / wall time, H2D included;
+    the H2D rate of the same pinned buffer is measured beside it."""
+    import ctypes
+    import torch
+    from volsync_amd import MaxSize, MinSize, TestPol, synth_fill_device
+    from volsync_amd._lib import VS_EOF, VsChunk, check, lib
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    n = int(args.per_gpu_gib * (1 << 30))
+    host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    piece = min(n, 4 << 30)
+    tmp = torch.empty(piece, dtype=torch.uint8, device=dev)
+    for off in range(0, n, piece):
+        k = min(piece, n - off)
+        synth_fill_device(tmp.data_ptr(), 2, off, k)
+        host[off:off + k].copy_(tmp[:k])
+    torch.cuda.synchronize(dev)
+    # H2D reference: the same pinned buffer, one 4 GiB copy
+    t = time.perf_counter()
+    tmp.copy_(host[:piece], non_blocking=True)
+    torch.cuda.synchronize(dev)
+    h2d = piece / (time.perf_counter() - t) / 1e9
+    del tmp
+    torch.cuda.empty_cache()
+    h = ctypes.c_void_p()
+    check(lib.vs_cdc_open(0, TestPol, MinSize, MaxSize, 20, ctypes.byref(h)))
+    read = 64 << 20
+    cap = 4096
+    out = (VsChunk * cap)()
+    got = ctypes.c_size_t(0)
+
+    def step():
+        nch = 0
+        last = None
+        base = host.data_ptr()
+        for off in range(0, n, read):
+            check(lib.vs_cdc_feed(h, ctypes.c_void_p(base + off), min(read, n - off), 0))
+            while True:
+                check(lib.vs_cdc_next(h, out, cap, ctypes.byref(got)))
+                if not got.value:
+                    break
+                nch += got.value
+                last = out[got.value - 1]
+        check(lib.vs_cdc_feed(h, None, 0, 1))
+        while True:
+            rc = lib.vs_cdc_next(h, out, cap, ctypes.byref(got))
+            if rc == VS_EOF:
+                break
+            check(rc)
+            nch += got.value
+            if got.value:
+                last = out[got.value - 1]
+        assert last is not None and last.start + last.length == n, "stream not fully chunked"
+        check(lib.vs_cdc_reset(h, TestPol, MinSize, MaxSize, 20))
+        return nch
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    nch = 0
+    for _ in range(args.steps):
+        nch = step()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    stats = (ctypes.c_double * 4)()
+    check(lib.vs_cdc_stream_stats(h, stats))
+    lib.vs_cdc_close(h)
+    value = n * args.steps / dt / 1e9
+    print(json.dumps({
+        "metric": "GB/s chunked+SHA-256 (restic CDC), host-pinned end-to-end via vs_cdc_feed/next",
+        "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (splitmix64 volume image in pinned host memory, fed in 64 MiB reads)",
+        "config": {"workload": f"C2 streamed: {n >> 30} GiB volume through the Chunker.Next "
+                               f"drop-in path (H2D included), 1 GPU",
+                   "volume_bytes": n, "read_bytes": read, "chunks": nch,
+                   "pol": "0x3DA3358B4DC173", "min": MinSize, "max": MaxSize, "avg_bits": 20},
+        "h2d_GBps": round(h2d, 2), "frac_of_h2d": round(value / h2d, 4),
+        "stream_stats": {"pinned_bytes": stats[0], "staged_bytes": stats[1],
+                         "collect_waits": stats[2], "batches": stats[3]},
+    }), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -577,9 +676,10 @@ def main():
                          "wavefronts (0 = library default, 0xffffffff = never)")
     ap.add_argument("--wide-drain", type=int, default=0,
                     help="blocks per throughput-mode drain launch (0 = library default)")
-    ap.add_argument("--mode", choices=["cdc", "rsync", "smallfiles"], default="cdc",
+    ap.add_argument("--mode", choices=["cdc", "rsync", "smallfiles", "host"], default="cdc",
                     help="cdc: C2/C3 chunk+hash (the BASELINE metric); rsync: C4-shape delta "
-                         "match; smallfiles: C5 per-file blob IDs")
+                         "match; smallfiles: C5 per-file blob IDs; host: C2 streamed from "
+                         "pinned host memory through vs_cdc_feed/next")
     ap.add_argument("--files", type=int, default=1_000_000, help="smallfiles: files per GPU")
     ap.add_argument("--dry", action="store_true",
                     help="CPU/gloo rehearsal of the multi-rank protocol (no GPU; value null)")
@@ -594,6 +694,8 @@ def main():
         return rsync_main(args)
     if args.mode == "smallfiles":
         return smallfiles_main(args)
+    if args.mode == "host":
+        return host_main(args)
 
     import torch
     import torch.distributed as dist

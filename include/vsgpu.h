@@ -92,8 +92,17 @@ int vs_cdc_feed(vs_cdc *h, const void *buf, size_t n, int final);
  * needed, or VS_EOF once the final chunk has been returned (io.EOF). */
 int vs_cdc_next(vs_cdc *h, vs_chunk *out, size_t cap, size_t *n_out);
 void vs_cdc_close(vs_cdc *h);
-/* Bytes staged on the device per pipeline batch (default 256 MiB). */
+/* Streaming pipeline: fed bytes are copied to the device on a
+ * copy stream (pinned caller memory by DMA, waited for before the call
+ * returns; pageable memory through two pinned 64 MiB staging buffers) and
+ * chunked in batches of batch_bytes (default 512 MiB); up to 24 batches are
+ * in flight while their blob IDs are computed, and vs_cdc_next returns chunks
+ * in stream order as soon as theirs are final (after the final feed it waits
+ * for them).  The batch size can only change between streams. */
 int vs_cdc_set_batch_bytes(vs_cdc *h, uint64_t bytes);
+/* Streaming counters: [0] bytes fed from pinned memory, [1] bytes fed through
+ * the staging buffers, [2] times a call waited for a batch's IDs, [3] batches. */
+int vs_cdc_stream_stats(vs_cdc *h, double out[4]);
 
 /* ---- device-resident batch API (data already in HBM) ------------------
  * Chunks a device byte range that begins at a chunk boundary.  dev_data
@@ -165,6 +174,14 @@ int vs_sha256_run_device(vs_sha *h, const void *dev_buf, const uint64_t *dev_off
 /* Same knob as vs_cdc_set_hash_wide for a vs_sha handle. */
 int vs_sha256_set_wide(vs_sha *h, uint32_t min_chains, uint32_t drain_blocks);
 void vs_sha256_close(vs_sha *h);
+/* The SaveBlob dedup seam (restic Repository.SaveBlob: idx.Has / AddPending):
+ * for n 32-byte blob IDs in stream order (device array dev_ids), dev_first[i]
+ * = the smallest index whose ID equals ID i (i itself for the first, stored
+ * blob; any other value marks a duplicate), and *n_unique (optional; waits
+ * for the result) = the number of distinct IDs.  Queued on hip_stream (NULL =
+ * default stream); scratch lives in the vs_sha handle. */
+int vs_blob_dedup(vs_sha *h, const uint8_t *dev_ids, size_t n, uint32_t *dev_first,
+                  uint64_t *n_unique, void *hip_stream);
 /* Host-memory convenience form (copies in and out). */
 int vs_sha256_batch(int device, const void *buf, size_t buf_len, const uint64_t *off,
                     const uint32_t *len, size_t n, uint8_t (*out)[32]);
@@ -255,8 +272,9 @@ int vs_rsync_stats(vs_rsync *h, int64_t *candidates, int64_t *false_alarms,
 int vs_rsync_timing(vs_rsync *h, double ms_out[5]);
 /* Device time of one kernel class summed over its launches since the handle
  * was opened (or the last reset), from HIP events on the handle's stream:
- * which 0 = weak scan / device walk, 1 = strong-sum verification,
- * 2 = signatures.  reset != 0 zeroes the totals after reading them. */
+ * which 0 = weak scan / speculative device walk, 1 = strong-sum verification,
+ * 2 = signatures, 3 = device walk stitch passes.  reset != 0 zeroes the
+ * totals after reading them. */
 int vs_rsync_kernel_time(vs_rsync *h, int which, int reset, double *ms, int64_t *launches);
 
 /* Host-memory one-shot forms: copy in, run, copy out. */

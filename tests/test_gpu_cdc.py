@@ -373,3 +373,149 @@ def test_reset_drains_queued_chains(gpu):
         O.cdc_hash(b, P.TEST_POL, mn, 1 << 19, ab)
     dc.close()
     del ta
+
+
+def _stream_pinned(data: np.ndarray, pol, mn, mx, ab, read, batch=None, reuse=None):
+    """Feed `data` from pinned host memory through vs_cdc_feed / vs_cdc_next
+    (the streaming drop-in path, as gpuchunker's Next drives it)."""
+    import ctypes
+    import torch
+    from volsync_amd._lib import VS_EOF, VsChunk, check, lib
+    host = torch.empty(max(len(data), 1), dtype=torch.uint8, pin_memory=True)
+    host[: len(data)].copy_(torch.from_numpy(np.ascontiguousarray(data)))
+    h = reuse or ctypes.c_void_p()
+    if reuse is None:
+        check(lib.vs_cdc_open(0, pol, mn, mx, ab, ctypes.byref(h)))
+    else:
+        check(lib.vs_cdc_reset(h, pol, mn, mx, ab))
+    if batch:
+        check(lib.vs_cdc_set_batch_bytes(h, batch))
+    out = (VsChunk * 64)()
+    got = ctypes.c_size_t(0)
+    res = []
+
+    def take():
+        while True:
+            rc = lib.vs_cdc_next(h, out, 64, ctypes.byref(got))
+            if rc == VS_EOF:
+                return True
+            check(rc)
+            if not got.value:
+                return False
+            res.extend((int(c.start), int(c.length), int(c.cut), bytes(c.id).hex())
+                       for c in out[: got.value])
+
+    for off in range(0, len(data), read):
+        check(lib.vs_cdc_feed(h, ctypes.c_void_p(host.data_ptr() + off),
+                              min(read, len(data) - off), 0))
+        take()
+    check(lib.vs_cdc_feed(h, None, 0, 1))
+    assert take()
+    st = (ctypes.c_double * 4)()
+    check(lib.vs_cdc_stream_stats(h, st))
+    return res, h, list(st)
+
+
+def test_stream_1g_golden_pageable(gpu):
+    """C1 (1 GiB, seed 1, default parameters) through the Chunker mirror with
+    64 MiB reads from pageable memory (staged through the pinned buffers) and
+    the default 512 MiB batches: the committed golden chunk list exactly."""
+    from volsync_amd import EOF, NewWithBoundaries
+    doc = G.load(os.path.join(G.GOLDEN, "cdc_synth1_1g.json"))
+    data = G.make_input(doc["input"])
+    pol, mn, mx, ab = G.params(doc)
+    ck = NewWithBoundaries(io.BytesIO(data.tobytes()), pol, mn, mx, read_size=64 << 20,
+                           batch_bytes=512 << 20)
+    ck.SetAverageBits(ab)
+    got = []
+    while True:
+        try:
+            c = ck.Next()
+        except EOF:
+            break
+        got.append((c.Start, c.Length, c.Cut, c.ID.hex()))
+    ck.close()
+    assert got == G.expected(doc)
+
+
+def test_stream_1g_golden_pinned(gpu):
+    """The same 1 GiB fixture fed from pinned host memory (direct DMA) in
+    64 MiB reads with 128 MiB batches."""
+    import ctypes
+    from volsync_amd._lib import lib
+    doc = G.load(os.path.join(G.GOLDEN, "cdc_synth1_1g.json"))
+    data = G.make_input(doc["input"])
+    pol, mn, mx, ab = G.params(doc)
+    got, h, st = _stream_pinned(data, pol, mn, mx, ab, 64 << 20, batch=128 << 20)
+    lib.vs_cdc_close(h)
+    assert got == G.expected(doc)
+    assert st[0] == len(data) and st[1] == 0 and st[3] >= 8
+
+
+def test_stream_ring_wraps_and_reuse(gpu):
+    """Small batches (2*MaxSize + 1 MiB) so the 24-slot ring wraps many times
+    (backpressure: a batch's slot is reused only after its chunks were
+    collected); then the handle is reset and reused for a second stream."""
+    import ctypes
+    from volsync_amd._lib import lib
+    mn, mx, ab = 4096, 1 << 20, 16
+    data = O.synth(41, 0, (100 << 20) + 12345)
+    want = O.cdc_hash(data, P.TEST_POL, mn, mx, ab)
+    got, h, st = _stream_pinned(data, P.TEST_POL, mn, mx, ab, 5 << 20, batch=1)
+    assert got == want and st[3] > 30
+    data2 = O.synth(42, 0, 7 << 20)
+    got2, h, _ = _stream_pinned(data2, P.TEST_POL, mn, mx, ab, 1 << 20, batch=1, reuse=h)
+    lib.vs_cdc_close(h)
+    assert got2 == O.cdc_hash(data2, P.TEST_POL, mn, mx, ab)
+
+
+def test_stream_empty_and_tiny(gpu):
+    import ctypes
+    from volsync_amd._lib import lib
+    for n in (0, 1, 63, 100):
+        data = O.synth(43, 0, n)
+        got, h, _ = _stream_pinned(data, P.TEST_POL, MIN, MAX, 20, 1 << 20)
+        lib.vs_cdc_close(h)
+        assert got == O.cdc_hash(data, P.TEST_POL, MIN, MAX, 20)
+
+
+def test_blob_dedup_vs_hashlib(gpu):
+    """SaveBlob's dedup seam (vs_blob_dedup) on the 20 K-file C5-shape batch:
+    the distinct-ID count and every blob's first occurrence, against hashlib
+    IDs deduplicated on the host; plus identical, empty and single inputs."""
+    import torch
+    from volsync_amd import DeviceSha256
+    rng = np.random.default_rng(7)
+    nfiles = 20000
+    sizes = rng.integers(4096, 65537, nfiles)
+    sizes[::97] = rng.integers(0, 3, len(sizes[::97]))      # empty / 1-2 byte files
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    pool = O.synth(8, 0, 4 << 20)
+    buf = np.empty(int(sizes.sum()), np.uint8)
+    for o, n in zip(offs.tolist(), sizes.tolist()):
+        src = int(rng.integers(0, 3000)) * 1024
+        buf[o:o + n] = pool[src:src + n]
+    want_ids = [hashlib.sha256(buf[o:o + n].tobytes()).digest()
+                for o, n in zip(offs.tolist(), sizes.tolist())]
+    seen, want_first = {}, []
+    for i, d in enumerate(want_ids):
+        want_first.append(seen.setdefault(d, i))
+    d = to_dev(buf)
+    do = torch.from_numpy(offs.astype(np.int64)).cuda()
+    dl = torch.from_numpy(sizes.astype(np.int32)).cuda()
+    ids = torch.zeros((nfiles, 32), dtype=torch.uint8, device="cuda")
+    first = torch.zeros(nfiles, dtype=torch.int32, device="cuda")
+    sh = DeviceSha256()
+    sh.run(d.data_ptr(), do.data_ptr(), dl.data_ptr(), nfiles, ids.data_ptr())
+    nu = sh.dedup(ids.data_ptr(), nfiles, first.data_ptr())
+    assert [bytes(r) for r in ids.cpu().numpy()] == want_ids
+    assert nu == len(seen)
+    assert first.cpu().numpy().tolist() == want_first
+    # one ID repeated 50 000 times, a single blob, no blobs
+    same = torch.tensor(list(want_ids[5]) * 50000, dtype=torch.uint8, device="cuda").view(-1, 32)
+    f2 = torch.full((50000,), -1, dtype=torch.int32, device="cuda")
+    assert sh.dedup(same.data_ptr(), 50000, f2.data_ptr()) == 1
+    assert int(f2.max()) == 0 and int(f2.min()) == 0
+    assert sh.dedup(ids.data_ptr(), 1, first.data_ptr()) == 1
+    assert sh.dedup(ids.data_ptr(), 0, first.data_ptr()) == 0
+    sh.close()

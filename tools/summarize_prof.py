@@ -22,7 +22,7 @@ import shutil
 
 
 def short(name: str) -> str:
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     return n.replace("void ", "").replace("vsgpu::", "")
 
 

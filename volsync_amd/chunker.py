@@ -319,6 +319,17 @@ class DeviceSha256:
         """Throughput mode from min_chains active blobs (0 = default, 0xffffffff = never)."""
         check(lib.vs_sha256_set_wide(self._h, int(min_chains), int(drain_blocks)))
 
+    def dedup(self, dev_ids: int, n: int, dev_first: int, stream: Optional[int] = None,
+              count: bool = True) -> Optional[int]:
+        """Repository.SaveBlob's dedup over n device blob IDs (vs_blob_dedup):
+        dev_first[i] = first index with the same ID; returns the distinct-ID
+        count (waits) when count is set."""
+        u = ctypes.c_uint64(0)
+        check(lib.vs_blob_dedup(self._h, ctypes.c_void_p(dev_ids), n, ctypes.c_void_p(dev_first),
+                                ctypes.byref(u) if count else None,
+                                ctypes.c_void_p(stream or None)))
+        return int(u.value) if count else None
+
     def close(self) -> None:
         if self._h:
             lib.vs_sha256_close(self._h)

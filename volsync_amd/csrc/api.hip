@@ -91,12 +91,27 @@ struct vs_cdc {
     int state = 0;  // 0 idle, 1 scanned, 2 stitched, 3 finished
     // host staging
     uint64_t *pinned = nullptr;  // 8 u64 of pinned host memory
-    // streaming
-    DevBuf sbuf[2];
-    int scur = 0;
-    uint64_t sfill = 0, sorigin = 0, batch_bytes = 256ull << 20;
+    // streaming (vs_cdc_feed / vs_cdc_next): one device batch
+    // buffer per ring slot -- the hash engine reads a batch's chunks from its
+    // buffer until their blob IDs are final -- filled by H2D copies on a copy
+    // stream; finished batches are collected in order once their IDs are final
+    static constexpr size_t kStreamSlots = 24;
+    std::vector<DevBuf> sbufs;
+    uint64_t sfill = 0, sorigin = 0, batch_bytes = 512ull << 20;
+    bool streaming = false;          // the handle is in streaming mode (first feed .. reset)
+    uint32_t pre_stream_budget = 0;  // hash_budget before streaming changed it
+    std::deque<uint64_t> spend;      // batches whose chunks are not yet collected
     std::deque<vs_chunk> ready;
     bool final_fed = false;
+    hipStream_t cstream = nullptr;   // H2D copies
+    hipEvent_t ev_copy = nullptr;    // after the last copy into the filling buffer
+    bool copy_pending = false;
+    uint8_t *stage[2] = {nullptr, nullptr};   // pinned staging for pageable input
+    size_t stage_cap = 0;
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    bool stage_busy[2] = {false, false};
+    int stage_i = 0;
+    double feed_stats[4] = {0, 0, 0, 0};  // bytes direct, bytes staged, collect waits, batches
     // timing
     bool timing = false;
     struct Pend {
@@ -608,29 +623,169 @@ static int cdc_process(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t o
     return 0;
 }
 
-// streaming: run the pipeline over the staged bytes
+// ---- streaming ------------------------------------------------------------
+// Batch s lives in ring slot / device buffer s % R.  A batch's chunks become
+// `ready` once the slice that finishes its longest chain has completed.
+static bool batch_done(vs_cdc *h, uint64_t s) {
+    const vs_cdc::Slot &sl = h->slots[s % h->slots.size()];
+    const uint64_t c = sl.done_slice;
+    if (sl.n == 0 || c == 0) return true;
+    if (c > h->slices) return false;
+    if (c + vs_cdc::kSliceEv <= h->slices) return true;
+    const hipError_t e = hipEventQuery(h->slice_ev[c % vs_cdc::kSliceEv]);
+    if (e == hipErrorNotReady) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return e == hipSuccess;
+}
+
+// move batch s (the oldest pending one) to `ready`; block = wait for its IDs
+static int collect_batch(vs_cdc *h, uint64_t s, bool block) {
+    vs_cdc::Slot &sl = h->slots[s % h->slots.size()];
+    if (sl.seq != s) return fail(VS_ERR_STATE, "streaming batch recycled before collection");
+    if (!batch_done(h, s)) {
+        if (!block) return 1;
+        h->feed_stats[2] += 1;
+        if (sl.done_slice > h->slices) VS_TRY(drain_hash(h));
+        VS_HIP(hipEventSynchronize(h->slice_ev[sl.done_slice % vs_cdc::kSliceEv]));
+    }
+    const uint64_t n = sl.n;
+    if (n) {
+        std::vector<uint64_t> st(n), en(n), cu(n);
+        std::vector<uint8_t> id(n * 32);
+        VS_HIP(hipMemcpy(st.data(), sl.start.p, n * 8, hipMemcpyDeviceToHost));
+        VS_HIP(hipMemcpy(en.data(), sl.end.p, n * 8, hipMemcpyDeviceToHost));
+        VS_HIP(hipMemcpy(cu.data(), sl.cut.p, n * 8, hipMemcpyDeviceToHost));
+        VS_HIP(hipMemcpy(id.data(), sl.id.p, n * 32, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < n; ++i) {
+            vs_chunk c;
+            c.start = sl.origin + st[i];
+            c.length = (en[i] & kPosMask) - st[i] + 1;
+            c.cut = cu[i];
+            memcpy(c.id, &id[i * 32], 32);
+            h->ready.push_back(c);
+        }
+    }
+    h->spend.pop_front();
+    return 0;
+}
+
+// collect finished batches in order (block: at least the oldest one)
+static int collect_ready(vs_cdc *h, bool block) {
+    while (!h->spend.empty()) {
+        const int r = collect_batch(h, h->spend.front(), block);
+        if (r < 0) return r;
+        if (r == 1) break;
+        block = false;
+    }
+    return 0;
+}
+
+// the buffer of the next batch (seq = h->seq) is free: its slot's previous
+// batch has been collected (backpressure: wait for it)
+static int stream_buffer(vs_cdc *h, DevBuf **out) {
+    const size_t R = h->slots.size();
+    const uint64_t s = h->seq;
+    while (!h->spend.empty() && h->spend.front() + R <= s) VS_TRY(collect_batch(h, h->spend.front(), true));
+    DevBuf &b = h->sbufs[s % R];
+    const uint64_t batch = std::max<uint64_t>(h->batch_bytes, 2ull * h->max_size + (1 << 20));
+    const uint64_t need = batch + 2ull * h->max_size + (2 << 20);
+    if (b.cap < need) VS_TRY(b.ensure(need));
+    *out = &b;
+    return 0;
+}
+
+// first feed of a stream: streaming mode (slice budget so that a MaxSize
+// chain finishes within the ring), copy stream, staging buffers
+static int stream_begin(vs_cdc *h) {
+    if (h->streaming) return 0;
+    if (!h->cstream) {
+        VS_HIP(hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
+        VS_HIP(hipEventCreateWithFlags(&h->ev_copy, hipEventDisableTiming));
+        for (int i = 0; i < 2; ++i) VS_HIP(hipEventCreateWithFlags(&h->stage_ev[i], hipEventDisableTiming));
+    }
+    VS_TRY(cdc_wait(h));
+    h->pre_stream_budget = h->hash_budget;
+    const uint64_t mb = sha_blocks(h->max_size);
+    const uint64_t budget = (mb + vs_cdc::kStreamSlots - 3) / (vs_cdc::kStreamSlots - 2);
+    h->hash_budget = (uint32_t)std::max<uint64_t>(budget, 1);
+    VS_TRY(size_ring(h));
+    h->sbufs.resize(h->slots.size());
+    h->streaming = true;
+    return 0;
+}
+
+// copy n caller bytes to device dst on the copy stream.  Pinned caller memory
+// is DMA'd directly (and waited for before the call returns: the caller owns
+// it); pageable memory goes through two pinned staging buffers.
+static int stream_copy(vs_cdc *h, uint8_t *dst, const uint8_t *src, size_t n) {
+    if (!n) return 0;
+    hipPointerAttribute_t at;
+    bool pinned = false;
+    if (hipPointerGetAttributes(&at, src) == hipSuccess) pinned = at.type == hipMemoryTypeHost;
+    else (void)hipGetLastError();
+    if (pinned) {
+        VS_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, h->cstream));
+        VS_HIP(hipEventRecord(h->ev_copy, h->cstream));
+        VS_HIP(hipEventSynchronize(h->ev_copy));
+        h->feed_stats[0] += (double)n;
+        h->copy_pending = true;
+        return 0;
+    }
+    const size_t piece = 64ull << 20;
+    if (!h->stage[0]) {
+        for (int i = 0; i < 2; ++i)
+            if (hipHostMalloc((void **)&h->stage[i], piece, hipHostMallocDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                return fail(VS_ERR_NOMEM, "pinned staging allocation failed");
+            }
+        h->stage_cap = piece;
+    }
+    for (size_t off = 0; off < n; off += piece) {
+        const size_t k = std::min(piece, n - off);
+        const int i = h->stage_i;
+        if (h->stage_busy[i]) VS_HIP(hipEventSynchronize(h->stage_ev[i]));
+        memcpy(h->stage[i], src + off, k);
+        VS_HIP(hipMemcpyAsync(dst + off, h->stage[i], k, hipMemcpyHostToDevice, h->cstream));
+        VS_HIP(hipEventRecord(h->stage_ev[i], h->cstream));
+        h->stage_busy[i] = true;
+        h->stage_i ^= 1;
+    }
+    VS_HIP(hipEventRecord(h->ev_copy, h->cstream));
+    h->feed_stats[1] += (double)n;
+    h->copy_pending = true;
+    return 0;
+}
+
+// run the pipeline over the filling buffer's sfill bytes, carry the bytes
+// after the last determined chunk over to the next batch's buffer
 static int stream_run(vs_cdc *h, bool final) {
-    DevBuf &cur = h->sbuf[h->scur];
+    const size_t R = h->slots.size();
+    DevBuf &cur = h->sbufs[h->seq % R];
+    if (h->copy_pending) {
+        VS_HIP(hipStreamWaitEvent(h->stream, h->ev_copy, 0));
+        h->copy_pending = false;
+    }
+    const uint64_t s = h->seq;
     uint64_t n = 0, consumed = 0;
     VS_TRY(cdc_process(h, cur.p ? cur.p : h->tabs.p, h->sfill, h->sorigin, final ? 1 : 0, &n,
                        &consumed));
-    if (n) {
-        std::vector<vs_chunk> tmp(n);
-        VS_TRY(cdc_get_chunks(h, 0, n, tmp.data()));
-        for (auto &c : tmp) h->ready.push_back(c);
-    }
+    h->spend.push_back(s);
+    h->feed_stats[3] += 1;
     const uint64_t rest = h->sfill - consumed;
     if (rest) {
-        DevBuf &nxt = h->sbuf[h->scur ^ 1];
-        VS_TRY(nxt.ensure(std::max<uint64_t>(rest, h->batch_bytes) + (1 << 20)));
-        VS_HIP(hipMemcpyAsync(nxt.p, (uint8_t *)cur.p + consumed, rest, hipMemcpyDeviceToDevice,
+        DevBuf *nxt = nullptr;
+        VS_TRY(stream_buffer(h, &nxt));
+        VS_HIP(hipMemcpyAsync(nxt->p, (uint8_t *)cur.p + consumed, rest, hipMemcpyDeviceToDevice,
                               h->stream));
-        VS_TRY(sync_stream(h));
-        h->scur ^= 1;
+        // later H2D copies into the same buffer land after the carried bytes
+        VS_HIP(hipEventRecord(h->ev_copy, h->stream));
+        VS_HIP(hipStreamWaitEvent(h->cstream, h->ev_copy, 0));
     }
     h->sorigin += consumed;
     h->sfill = rest;
-    return 0;
+    return collect_ready(h, false);
 }
 
 }  // namespace vsgpu
@@ -710,17 +865,23 @@ VS_API int vs_cdc_reset(vs_cdc *h, uint64_t pol, uint32_t min_size, uint32_t max
     // write blob IDs into their ring slots, which size_ring() releases when
     // the new max_size changes the ring length
     VS_TRY(cdc_wait(h));
+    if (h->streaming) h->hash_budget = h->pre_stream_budget;   // the device API's budget again
     VS_TRY(set_params(h, pol, min_size, max_size, avg_bits));
     h->state = 0;
     h->ready.clear();
+    h->spend.clear();
     h->sfill = 0;
     h->sorigin = 0;
     h->final_fed = false;
+    h->copy_pending = false;
+    if (h->cstream) VS_HIP(hipStreamSynchronize(h->cstream));
+    h->streaming = false;   // the next feed re-derives the streaming slice budget
     return 0;
 }
 
 VS_API int vs_cdc_set_batch_bytes(vs_cdc *h, uint64_t bytes) {
     if (!h || bytes < 1) return fail(VS_ERR_ARG, "bad batch size");
+    if (h->streaming) return fail(VS_ERR_STATE, "batch size is fixed while a stream is fed (vs_cdc_reset first)");
     h->batch_bytes = bytes;
     return 0;
 }
@@ -730,36 +891,22 @@ VS_API int vs_cdc_feed(vs_cdc *h, const void *buf, size_t n, int final) {
     if (h->final_fed) return fail(VS_ERR_STATE, "stream already finalised (call vs_cdc_reset)");
     if (n && !buf) return fail(VS_ERR_ARG, "null buffer");
     VS_TRY(set_dev(h));
+    VS_TRY(stream_begin(h));
     const uint8_t *src = (const uint8_t *)buf;
     size_t left = n;
-    for (;;) {
-        // top up the staging buffer to batch_bytes, run a batch when full
-        DevBuf &cur = h->sbuf[h->scur];
-        // a batch of at least 2*MaxSize always determines its first chunk's cut,
-        // so every non-final run makes progress
-        const uint64_t batch = std::max<uint64_t>(h->batch_bytes, 2ull * h->max_size + (1 << 20));
+    // a batch of at least 2*MaxSize always determines its first chunk's cut,
+    // so every non-final run makes progress
+    const uint64_t batch = std::max<uint64_t>(h->batch_bytes, 2ull * h->max_size + (1 << 20));
+    while (left) {
+        DevBuf *cur = nullptr;
+        VS_TRY(stream_buffer(h, &cur));
         const uint64_t room = (h->sfill < batch) ? batch - h->sfill : 0;
         const uint64_t take = std::min<uint64_t>(room, left);
-        if (take) {
-            if (cur.cap < h->sfill + take) {
-                DevBuf bigger;
-                VS_TRY(bigger.ensure(std::max<uint64_t>(h->sfill + take, batch) + (1 << 20)));
-                if (h->sfill)
-                    VS_HIP(hipMemcpyAsync(bigger.p, cur.p, h->sfill, hipMemcpyDeviceToDevice,
-                                          h->stream));
-                VS_TRY(sync_stream(h));
-                cur.release();
-                cur = bigger;
-            }
-            VS_HIP(hipMemcpyAsync((uint8_t *)cur.p + h->sfill, src, take, hipMemcpyHostToDevice,
-                                  h->stream));
-            VS_TRY(sync_stream(h));
-            h->sfill += take;
-            src += take;
-            left -= take;
-        }
-        if (left == 0) break;
-        VS_TRY(stream_run(h, false));  // staging full, more input pending
+        VS_TRY(stream_copy(h, (uint8_t *)cur->p + h->sfill, src, take));
+        h->sfill += take;
+        src += take;
+        left -= take;
+        if (h->sfill >= batch) VS_TRY(stream_run(h, false));
     }
     if (final) {
         VS_TRY(stream_run(h, true));
@@ -770,13 +917,25 @@ VS_API int vs_cdc_feed(vs_cdc *h, const void *buf, size_t n, int final) {
 
 VS_API int vs_cdc_next(vs_cdc *h, vs_chunk *out, size_t cap, size_t *n_out) {
     if (!h || (!out && cap)) return fail(VS_ERR_ARG, "bad arguments");
+    if (n_out) *n_out = 0;
+    if (h->streaming) {
+        VS_TRY(set_dev(h));
+        // after the final feed nothing else will advance the stream: wait
+        VS_TRY(collect_ready(h, h->ready.empty() && h->final_fed));
+    }
     size_t k = 0;
     while (k < cap && !h->ready.empty()) {
         out[k++] = h->ready.front();
         h->ready.pop_front();
     }
     if (n_out) *n_out = k;
-    if (k == 0 && h->final_fed) return VS_EOF;
+    if (k == 0 && h->final_fed && h->spend.empty()) return VS_EOF;
+    return 0;
+}
+
+VS_API int vs_cdc_stream_stats(vs_cdc *h, double out[4]) {
+    if (!h || !out) return fail(VS_ERR_ARG, "bad arguments");
+    for (int i = 0; i < 4; ++i) out[i] = h->feed_stats[i];
     return 0;
 }
 
@@ -788,9 +947,16 @@ VS_API void vs_cdc_close(vs_cdc *h) {
     DevBuf *bufs[] = {&h->tabs,     &h->counts,    &h->offs,   &h->dslot,   &h->pool,
                       &h->flags,    &h->cstart,    &h->partials, &h->compact, &h->spec_cut,
                       &h->spec_n,   &h->spec_exit, &h->st_cut, &h->st_n,    &h->st_merge,
-                      &h->st_total, &h->exit_a,    &h->exit_b, &h->seg_off, &h->n_out,
-                      &h->sbuf[0],  &h->sbuf[1]};
+                      &h->st_total, &h->exit_a,    &h->exit_b, &h->seg_off, &h->n_out};
     for (DevBuf *b : bufs) b->release();
+    for (DevBuf &b : h->sbufs) b.release();
+    if (h->cstream) (void)hipStreamSynchronize(h->cstream);
+    for (int i = 0; i < 2; ++i) {
+        if (h->stage[i]) (void)hipHostFree(h->stage[i]);
+        if (h->stage_ev[i]) (void)hipEventDestroy(h->stage_ev[i]);
+    }
+    if (h->ev_copy) (void)hipEventDestroy(h->ev_copy);
+    if (h->cstream) (void)hipStreamDestroy(h->cstream);
     for (auto &s : h->slots) {
         s.start.release();
         s.end.release();
@@ -828,6 +994,7 @@ VS_API int vs_cdc_set_hash_stream(vs_cdc *h, void *hip_stream) {
 
 VS_API int vs_cdc_set_hash_slice(vs_cdc *h, uint32_t blocks) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
+    if (h->streaming) return fail(VS_ERR_STATE, "slice budget is fixed while a stream is fed (vs_cdc_reset first)");
     VS_TRY(cdc_wait(h));
     h->hash_budget = blocks ? blocks : 0xffffffffu;
     return size_ring(h);
@@ -899,6 +1066,8 @@ VS_API int vs_cdc_timing(vs_cdc *h, int enable, double ms_out[4], uint64_t launc
 struct vs_sha {
     int device = 0;
     ShaEngine eng;
+    DevBuf dd_tmp;                  // vs_blob_dedup scratch
+    uint64_t *dd_pinned = nullptr;
     hipEvent_t done = nullptr;  // after the last run, on its stream
     bool ran = false;
 };
@@ -952,6 +1121,28 @@ VS_API int vs_sha256_run_device(vs_sha *h, const void *dev_buf, const uint64_t *
                    (hipStream_t)hip_stream);
 }
 
+VS_API int vs_blob_dedup(vs_sha *h, const uint8_t *dev_ids, size_t n, uint32_t *dev_first,
+                         uint64_t *n_unique, void *hip_stream) {
+    if (!h || (n && (!dev_ids || !dev_first))) return fail(VS_ERR_ARG, "bad arguments");
+    if (n > 0xffffffffull) return fail(VS_ERR_ARG, "more than 2^32 blobs per call");
+    VS_HIP(hipSetDevice(h->device));
+    const hipStream_t s = (hipStream_t)hip_stream;
+    VS_TRY(h->dd_tmp.ensure(dedup_tmp_bytes(std::max<size_t>(n, 1)) + 64));
+    unsigned long long *cnt = (unsigned long long *)((uint8_t *)h->dd_tmp.p + h->dd_tmp.cap - 64);
+    VS_HIP(launch_dedup(dev_ids, n, dev_first, h->dd_tmp.p, h->dd_tmp.cap - 64, cnt, s));
+    if (n_unique) {
+        if (!h->dd_pinned &&
+            hipHostMalloc((void **)&h->dd_pinned, 64, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(VS_ERR_NOMEM, "pinned read-back buffer");
+        }
+        VS_HIP(hipMemcpyAsync(h->dd_pinned, cnt, 8, hipMemcpyDeviceToHost, s));
+        VS_HIP(hipStreamSynchronize(s));
+        *n_unique = h->dd_pinned[0];
+    }
+    return 0;
+}
+
 VS_API int vs_sha256_set_wide(vs_sha *h, uint32_t min_chains, uint32_t drain_blocks) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
     if (h->ran) VS_HIP(hipEventSynchronize(h->done));
@@ -962,6 +1153,9 @@ VS_API int vs_sha256_set_wide(vs_sha *h, uint32_t min_chains, uint32_t drain_blo
 VS_API void vs_sha256_close(vs_sha *h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    (void)hipDeviceSynchronize();
+    h->dd_tmp.release();
+    if (h->dd_pinned) (void)hipHostFree(h->dd_pinned);
     if (h->done) {
         (void)hipEventSynchronize(h->done);
         (void)hipEventDestroy(h->done);

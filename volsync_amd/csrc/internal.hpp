@@ -269,8 +269,19 @@ struct RsScanArgs {
 __host__ __device__ inline uint32_t rs_lds_filter_bits(uint32_t fbits) {
     return fbits < 20 ? fbits : 20;
 }
+// the device walk's L2-resident filter: a blocked Bloom filter of 2^fbits
+// bits in 64-bit words -- the word from a multiplicative hash of sum1, three
+// bits in it from sum1's low 18 bits -- so one gather per offset rejects all
+// but ~0.1 % of the offsets the LDS prefilter passes (about 2 keys per word)
+__host__ __device__ inline uint32_t rs_bloom_word(uint32_t sum1, uint32_t fbits) {
+    return (sum1 * 0x9E3779B1u) >> (32 - (fbits - 6));
+}
+__host__ __device__ inline uint64_t rs_bloom_mask(uint32_t sum1) {
+    return (1ull << (sum1 & 63)) | (1ull << ((sum1 >> 6) & 63)) | (1ull << ((sum1 >> 12) & 63));
+}
+// layout: filter [2^fbits bits], LDS prefilter [2^lbits bits], blocked filter [2^fbits bits]
 inline size_t rs_filter_bytes(uint32_t fbits) {
-    return ((size_t)1 << fbits) / 8 + (((size_t)1 << rs_lds_filter_bits(fbits)) / 8);
+    return 2 * (((size_t)1 << fbits) / 8) + (((size_t)1 << rs_lds_filter_bits(fbits)) / 8);
 }
 hipError_t launch_rs_scan(const RsScanArgs &a, int cus, hipStream_t s);
 // flag[0, n): some candidate sits exactly one block before or after off[c]
@@ -299,6 +310,7 @@ struct RsWalkArgs {
     const uint64_t *tkey;            // sorted (sum1 << 32 | ~index)
     const uint32_t *dir;
     const uint32_t *filt, *filt_l;
+    const uint64_t *filt_b;          // blocked filter (rs_bloom_word / rs_bloom_mask)
     uint32_t dbits, fbits, lbits;
     int64_t e0;                      // segment 0's entry (offset, want_i)
     int32_t w0;
@@ -328,10 +340,15 @@ struct RsWalkArgs {
     int64_t *exit_new;
     int32_t *exitw_new;
     uint64_t *dbg;                   // debug builds: per-wave progress records (host-mapped)
+    uint64_t *prof;                  // VSGPU_WALK_PROF: per-wave phase cycles/counts [waves][16]
 };
 hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t s);
 hipError_t launch_rs_pad_sum2(const uint8_t *sum2, uint32_t count, uint32_t s2length,
                               uint64_t *out, hipStream_t s);
+// SaveBlob dedup (dedup.hip): first[i] = smallest index with ids[i]'s ID
+size_t dedup_tmp_bytes(uint64_t n);
+hipError_t launch_dedup(const uint8_t *ids, uint64_t n, uint32_t *first, void *tmp,
+                        size_t tmp_bytes, unsigned long long *n_unique_dev, hipStream_t s);
 hipError_t launch_rs_sort_cands(void *tmp, size_t tmp_bytes, const uint64_t *off_in,
                                 uint64_t *off_out, const uint32_t *sum_in, uint32_t *sum_out,
                                 uint64_t n, int end_bit, hipStream_t s);

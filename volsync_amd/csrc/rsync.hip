@@ -301,6 +301,11 @@ __global__ void rs_dir_kernel(const uint64_t *tkey, uint32_t count, uint32_t dbi
         uint32_t *filt_l = filt + ((1ull << fbits) / 32);
         const uint32_t fl = (uint32_t)(tkey[p] >> (64 - rs_lds_filter_bits(fbits)));
         atomicOr(&filt_l[fl >> 5], 1u << (fl & 31));
+        // blocked filter over all 32 bits of sum1, stored after the prefilter
+        unsigned long long *filt_b =
+            (unsigned long long *)(filt_l + ((1ull << rs_lds_filter_bits(fbits)) / 32));
+        const uint32_t s1 = (uint32_t)(tkey[p] >> 32);
+        atomicOr(&filt_b[rs_bloom_word(s1, fbits)], (unsigned long long)rs_bloom_mask(s1));
     }
 }
 

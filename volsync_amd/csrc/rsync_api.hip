@@ -103,8 +103,8 @@ struct vs_rsync {
     // each launch; every entry point synchronises right after): [0] weak scan
     // / device walk, [1] strong verification, [2] signatures
     hipEvent_t kev[2] = {nullptr, nullptr};
-    double kms[3] = {0, 0, 0};
-    int64_t kn[3] = {0, 0, 0};
+    double kms[4] = {0, 0, 0, 0};
+    int64_t kn[4] = {0, 0, 0, 0};
     // signature table
     bool loaded = false;
     int32_t count = 0, blength = 0, s2length = 0, remainder = 0;
@@ -121,7 +121,7 @@ struct vs_rsync {
     DevBuf w_spec_off, w_spec_idx, w_spec_fab, w_spec_n, w_spec_fa, w_spec_exit, w_spec_exitw;
     DevBuf w_fin_entry, w_fin_entryw, w_fin_from, w_fin_n, w_fin_fa, w_fin_off, w_fin_idx,
         w_fin_fab;
-    DevBuf w_exit[2], w_exitw[2], w_ctl;
+    DevBuf w_exit[2], w_exitw[2], w_ctl, w_prof;
     // scan
     DevBuf px, pt, pxs, pts, partials, c_off, c_sum, c_off2, c_sum2, n_cand, sort_tmp;
     // verification
@@ -721,7 +721,7 @@ int walk_converge(vs_rsync *h, int64_t *x, int32_t *xw) {
         a.exit_new = h->w_exit[r.xcur ^ 1].as<int64_t>();
         a.exitw_new = h->w_exitw[r.xcur ^ 1].as<int32_t>();
         VS_HIP(hipMemsetAsync(a.flags, 0, 4, h->stream));
-        KernelTimer kt(h, 0);
+        KernelTimer kt(h, 3);
         walk_watch_arm(h, a);
         VS_HIP(launch_rs_walk(a, true, h->cus, h->stream));
         kt.stop();
@@ -838,6 +838,7 @@ int walk_scan(vs_rsync *h) {
     a.dbits = h->dbits;
     a.lbits = rs_lds_filter_bits(h->fbits);
     a.filt_l = h->d_filt.as<uint32_t>() + ((1ull << h->fbits) / 32);
+    a.filt_b = (const uint64_t *)(a.filt_l + ((1ull << a.lbits) / 32));
     const size_t ns = std::max<uint32_t>(a.nseg, 1), nc = ns * a.cap;
     VS_TRY(h->w_spec_off.ensure(nc * 8));
     VS_TRY(h->w_spec_idx.ensure(nc * 4));
@@ -859,6 +860,7 @@ int walk_scan(vs_rsync *h) {
         VS_TRY(h->w_exitw[i].ensure(ns * 4));
     }
     VS_TRY(h->w_ctl.ensure(64));
+    a.prof = nullptr;
     a.work = h->w_ctl.as<uint32_t>();
     a.flags = h->w_ctl.as<uint32_t>() + 4;
     a.spec_off = h->w_spec_off.as<int64_t>();
@@ -887,6 +889,14 @@ int walk_scan(vs_rsync *h) {
     a.exitw_new = h->w_exitw[0].as<int32_t>();
     const double t0 = now_ms();
     VS_HIP(hipMemsetAsync(a.flags, 0, 4, h->stream));
+    // VSGPU_WALK_PROF=1: per-wave phase cycles of the speculative pass on stderr
+    static const bool wprof = getenv("VSGPU_WALK_PROF") != nullptr;
+    const size_t nprof = (size_t)std::max(h->cus, 1) * 64 * 16;
+    if (wprof) {
+        VS_TRY(h->w_prof.ensure(nprof * 8));
+        VS_HIP(hipMemsetAsync(h->w_prof.p, 0, nprof * 8, h->stream));
+        a.prof = h->w_prof.as<uint64_t>();
+    }
     {
         KernelTimer kt(h, 0);
         walk_watch_arm(h, a);
@@ -898,6 +908,29 @@ int walk_scan(vs_rsync *h) {
         kt.fold();
         if ((uint32_t)h->pinned[0] & 2u)
             return fail(VS_ERR_STATE, "device walk: segment match capacity exceeded");
+    }
+    if (wprof) {
+        std::vector<uint64_t> pr(nprof);
+        VS_HIP(hipMemcpy(pr.data(), a.prof, nprof * 8, hipMemcpyDeviceToHost));
+        const char *names[5] = {"run", "step", "flush", "chain", "segment"};
+        double cyc[5] = {0}, cnt[5] = {0}, mx = 0;
+        int waves = 0;
+        for (size_t w = 0; w < nprof / 16; ++w) {
+            if (!pr[w * 16 + 8 + 4]) continue;
+            ++waves;
+            for (int i = 0; i < 5; ++i) {
+                cyc[i] += (double)pr[w * 16 + i];
+                cnt[i] += (double)pr[w * 16 + 8 + i];
+            }
+            mx = std::max(mx, (double)pr[w * 16 + 4]);
+        }
+        fprintf(stderr, "walk prof: %d waves; per wave:", waves);
+        for (int i = 0; i < 5; ++i)
+            fprintf(stderr, " %s %.3g cyc / %.4g calls (%.3g cyc each);", names[i],
+                    cyc[i] / std::max(waves, 1), cnt[i] / std::max(waves, 1),
+                    cyc[i] / std::max(cnt[i], 1.0));
+        fprintf(stderr, " max segment-total %.3g cyc\n", mx);
+        a.prof = nullptr;
     }
     int64_t x = 0;
     int32_t xw = 0;
@@ -1126,7 +1159,7 @@ VS_API void vs_rsync_close(vs_rsync *h) {
                       &h->w_spec_fab, &h->w_spec_n, &h->w_spec_fa, &h->w_spec_exit,
                       &h->w_spec_exitw, &h->w_fin_entry, &h->w_fin_entryw, &h->w_fin_from,
                       &h->w_fin_n, &h->w_fin_fa, &h->w_fin_off, &h->w_fin_idx, &h->w_fin_fab,
-                      &h->w_exit[0], &h->w_exit[1], &h->w_exitw[0], &h->w_exitw[1], &h->w_ctl})
+                      &h->w_exit[0], &h->w_exit[1], &h->w_exitw[0], &h->w_exitw[1], &h->w_ctl, &h->w_prof})
         b->release();
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (HostReg *r : {&h->reg_off, &h->reg_sum, &h->reg_flag}) r->release();
@@ -1276,7 +1309,7 @@ VS_API int vs_rsync_timing(vs_rsync *h, double ms_out[5]) {
 
 VS_API int vs_rsync_kernel_time(vs_rsync *h, int which, int reset, double *ms,
                                 int64_t *launches) {
-    if (!h || which < 0 || which > 2) return fail(VS_ERR_ARG, "bad handle or kernel index");
+    if (!h || which < 0 || which > 3) return fail(VS_ERR_ARG, "bad handle or kernel index");
     if (ms) *ms = h->kms[which];
     if (launches) *launches = h->kn[which];
     if (reset) {

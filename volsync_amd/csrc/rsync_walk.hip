@@ -34,7 +34,7 @@ namespace {
 
 using vsstrong::P32_1;
 
-constexpr uint32_t kWalkThreads = 1024;            // 16 waves; the 128 KiB prefilter admits one WG/CU
+constexpr uint32_t kWalkThreads = 768;             // 12 waves (168 VGPRs each); the 128 KiB prefilter admits one WG/CU
 constexpr uint32_t kLdsFiltWordsW = 1u << 15;      // 2^20-bit LDS prefilter
 constexpr uint64_t kBatch = 1024;                  // STEP offsets per wave batch (16 per lane)
 
@@ -93,24 +93,6 @@ __device__ __forceinline__ int dot4(uint32_t word, uint32_t w, int acc) {
     return __builtin_amdgcn_sdot4((int)word, (int)w, acc, false);
 }
 
-__device__ __forceinline__ uint64_t shx64(uint64_t v, int m) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
-    return ((uint64_t)hi << 32) | lo;
-}
-// sum over the 16 lanes with the same (lane & 3)
-__device__ __forceinline__ uint64_t red16(uint64_t v) {
-    v += shx64(v, 4);
-    v += shx64(v, 8);
-    v += shx64(v, 16);
-    v += shx64(v, 32);
-    return v;
-}
-__device__ __forceinline__ uint32_t red64(uint32_t v) {
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) v += (uint32_t)__shfl_xor((int)v, m, 64);
-    return v;
-}
 // wave-uniform values made explicit (scalar registers, scalar branches): the
 // walk's control flow is uniform by construction, and values the compiler
 // cannot prove uniform (shuffle results, per-lane loads of one address) would
@@ -127,44 +109,75 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, int lane) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
     return ((uint64_t)hi << 32) | lo;
 }
-// exclusive prefix sum over the wave (lane order)
-__device__ __forceinline__ uint32_t excl_scan(uint32_t v, uint32_t lane) {
+// exclusive prefix sum over the wave (lane order): the GFX9 DPP scan
+// (row_shr 1/2/4/8 inside each row, then row_bcast 15 / 31 across rows)
+__device__ __forceinline__ uint32_t excl_scan(uint32_t v, uint32_t) {
     uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-        if (lane >= (uint32_t)d) x += y;
-    }
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
     return x - v;
 }
 
-// Per-lane XXH3 secret words of the 16-bytes-per-lane layout: lane l holds
-// words 2m, 2m+1 of stripe s (l = 4s + m) of every 1 KiB block.
-struct LaneSec {
-    uint64_t s0, s1;    // stripe secret words s + 2m, s + 2m + 1
-    uint64_t sc0, sc1;  // scramble words 16 + 2m, 17 + 2m
-    uint64_t l0, l1;    // last stripe: byte offsets 121 + 16m, 129 + 16m
-    uint64_t i0, i1;    // initial accumulators 2m, 2m + 1
+// ---- four windows per wave ------------------------------------------------
+// A wave hashes up to kRows windows at once, one per 16-lane row: lane
+// (row r, q = 4s' + m) reads 16 bytes of each 256-byte quarter of every 1 KiB
+// XXH3 block of window r, i.e. words 2m, 2m+1 of stripes s' , s'+4, s'+8,
+// s'+12, so a row's load is 256 contiguous bytes and the per-block reduction
+// (over s') stays inside the row (two DPP row rotations).  Loads are issued
+// kRing blocks ahead of their use; the window bytes are read with unaligned
+// dwordx4 loads (gfx950 runs in unaligned-access mode; hipcc emits the same
+// for a byte-aligned memcpy).
+constexpr uint32_t kRows = 4;
+constexpr uint32_t kRing = 2;   // blocks in flight per lane
+
+// DPP move within the wave (row rotations, quad permutations)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+    return ((uint64_t)dpp<CTRL>((uint32_t)(v >> 32)) << 32) | dpp<CTRL>((uint32_t)v);
+}
+// sum over the 4 lanes of a row with the same q & 3 (row_ror 4, row_ror 8)
+__device__ __forceinline__ uint64_t row_sum_sp(uint64_t v) {
+    v += dpp64<0x124>(v);
+    v += dpp64<0x128>(v);
+    return v;
+}
+// sum over the 16 lanes of a row
+__device__ __forceinline__ uint32_t row_sum16(uint32_t v) {
+    v += dpp<0x121>(v);
+    v += dpp<0x122>(v);
+    v += dpp<0x124>(v);
+    v += dpp<0x128>(v);
+    return v;
+}
+// sum over a quad (quad_perm [1,0,3,2] then [2,3,0,1])
+__device__ __forceinline__ uint64_t quad_sum(uint64_t v) {
+    v += dpp64<0xB1>(v);
+    v += dpp64<0x4E>(v);
+    return v;
+}
+
+__device__ __forceinline__ uint4 ldu16(const uint8_t *p) {
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+}
+
+// The seeded custom secret (XXH3_initCustomSecret: even words + seed, odd
+// words - seed), 24 words, staged in LDS once per workgroup: a lane reads its
+// stripe's two words with one ds_read2_b64 instead of holding 20 registers.
+struct RowSec {
+    const uint64_t *w;   // LDS, [24]
 };
-__device__ __forceinline__ LaneSec lane_secrets(uint32_t lane, uint64_t seed) {
-    using namespace vsstrong;
-    const uint32_t s = lane >> 2, m = lane & 3;
-    LaneSec r;
-    r.s0 = sec64(s + 2 * m, seed);
-    r.s1 = sec64(s + 2 * m + 1, seed);
-    r.sc0 = sec64(16 + 2 * m, seed);
-    r.sc1 = sec64(17 + 2 * m, seed);
-    r.l0 = csec_at(121 + 16 * m, seed);
-    r.l1 = csec_at(129 + 16 * m, seed);
-    const uint64_t init[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
-    r.i0 = init[0];
-    r.i1 = init[1];
-#pragma unroll
-    for (uint32_t j = 1; j < 4; ++j) {
-        r.i0 = (m == j) ? init[2 * j] : r.i0;
-        r.i1 = (m == j) ? init[2 * j + 1] : r.i1;
-    }
-    return r;
+__device__ __forceinline__ void load_secret(uint64_t *lsec, uint64_t seed) {
+    if (threadIdx.x < 24) lsec[threadIdx.x] = vsstrong::sec64(threadIdx.x, seed);
 }
 
 __device__ __forceinline__ uint64_t scramble(uint64_t a, uint64_t sec) {
@@ -189,6 +202,15 @@ __device__ __forceinline__ void weak16(const uint32_t (&w)[4], uint32_t q, uint3
     sux += q * (uint32_t)s + (uint32_t)t;
 }
 
+// one 16-byte piece: XXH3 accumulate of words 2m, 2m+1 with secrets (k0, k1)
+__device__ __forceinline__ void acc16(const uint4 v, uint64_t k0s, uint64_t k1s, uint64_t &c0,
+                                      uint64_t &c1) {
+    const uint64_t d0 = ((uint64_t)v.y << 32) | v.x, d1 = ((uint64_t)v.w << 32) | v.z;
+    const uint64_t k0 = d0 ^ k0s, k1 = d1 ^ k1s;
+    c0 += (uint64_t)(uint32_t)k0 * (k0 >> 32) + d1;
+    c1 += (uint64_t)(uint32_t)k1 * (k1 >> 32) + d0;
+}
+
 #ifdef VS_WALK_DEBUG
 #define WPROG(A_, LANE_, PH_, OFF_, EX_)                                                  \
     do {                                                                                  \
@@ -208,90 +230,129 @@ __device__ __forceinline__ void weak16(const uint32_t (&w)[4], uint32_t q, uint3
     } while (0)
 #endif
 
-struct Win {
-    uint32_t weak;
-    uint64_t lo, hi;
+// Optional per-wave phase timing (a.prof != nullptr; VSGPU_WALK_PROF=1):
+// s_memtime cycles and counts per phase, summed into a.prof[wave * 16 + ...]
+enum : int { kPrRun = 0, kPrStep = 1, kPrFlush = 2, kPrChain = 3, kPrSeg = 4, kPrN = 5 };
+struct WProf {
+    bool on;
+    uint64_t cyc[kPrN], cnt[kPrN];
+};
+__device__ __forceinline__ uint64_t wclock(const WProf &w) {
+    return w.on ? (uint64_t)__builtin_amdgcn_s_memtime() : 0;
+}
+__device__ __forceinline__ void wadd(WProf &w, int ph, uint64_t t0) {
+    if (w.on) {
+        w.cyc[ph] += (uint64_t)__builtin_amdgcn_s_memtime() - t0;
+        w.cnt[ph] += 1;
+    }
+}
+
+struct RowWin {
+    uint32_t weak;     // get_checksum1 of the row's window (WEAK only)
+    uint64_t lo, hi;   // XXH3 low / high 64 bits (valid in lanes q < 4 of the row)
 };
 
-// Weak sum and XXH3 (64 / 128, seeded) of the window data[o, o + len),
-// len > 240, computed by the whole wave (every lane returns them).
-// Restates vsstrong::xxh3_long + merge and get_checksum1 (rsync.hip
-// weak_sum); tests compare both with the C oracle / libxxhash.
-__device__ Win wave_window(const RsWalkArgs &a, const LaneSec &ls, uint32_t lane, uint64_t o,
-                           uint64_t len) {
+// Weak sum (WEAK) and seeded XXH3 (64 / 128) of the window data[o, o + len),
+// len > 240, o per row (the lane's row's window; rows may repeat a window).
+// Every window is a full one inside the readable data.  Restates
+// vsstrong::xxh3_long + merge and get_checksum1 (rsync.hip weak_sum); tests
+// compare both with the C oracle / libxxhash.
+template <bool WEAK>
+__device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, uint64_t o,
+                              uint64_t len) {
     using namespace vsstrong;
-    const uint8_t *d = a.data;
-    const uint64_t dlen = a.dlen;
-    const uint32_t s = lane >> 2, m = lane & 3;
-    uint64_t A0 = ls.i0, A1 = ls.i1;
+    const uint32_t q = lane & 15, sp = q >> 2, m = q & 3;
+    const uint8_t *p = a.data + o + 16 * q;   // this lane's piece of each 256-byte quarter
+    uint64_t A0 = (m == 0) ? P32_3 : (m == 1) ? P64_2 : (m == 2) ? P64_4 : P64_5;
+    uint64_t A1 = (m == 0) ? P64_1 : (m == 1) ? P64_3 : (m == 2) ? P32_2 : P32_1;
     uint32_t sx = 0, sux = 0;
-    const uint32_t sh = (uint32_t)(o & 15);
-    const uint64_t nb = (len - 1) / 1024;
-    for (uint64_t b = 0; b < nb; ++b) {
-        uint32_t w[4];
-        const uint32_t q = (uint32_t)(b * 1024 + 16 * lane);
-        ld16(d, o + q, sh, dlen, w);
-        const uint64_t d0 = ((uint64_t)w[1] << 32) | w[0], d1 = ((uint64_t)w[3] << 32) | w[2];
-        const uint64_t k0 = d0 ^ ls.s0, k1 = d1 ^ ls.s1;
-        uint64_t c0 = (uint64_t)(uint32_t)k0 * (k0 >> 32) + d1;
-        uint64_t c1 = (uint64_t)(uint32_t)k1 * (k1 >> 32) + d0;
-        weak16(w, q, sx, sux);
-        c0 = red16(c0);
-        c1 = red16(c1);
-        A0 = scramble(A0 + c0, ls.sc0);
-        A1 = scramble(A1 + c1, ls.sc1);
+    const uint32_t nb = (uint32_t)((len - 1) / 1024);
+    auto block = [&](const uint4 (&v)[4], uint32_t b) {
+        uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            acc16(v[j], rs.w[4 * j + sp + 2 * m], rs.w[4 * j + sp + 2 * m + 1], c0, c1);
+            if (WEAK) {
+                const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+                weak16(w, b * 1024 + 256 * j + 16 * q, sx, sux);
+            }
+        }
+        A0 = scramble(A0 + row_sum_sp(c0), rs.w[16 + 2 * m]);
+        A1 = scramble(A1 + row_sum_sp(c1), rs.w[17 + 2 * m]);
+    };
+    auto load = [&](uint4 (&v)[4], uint32_t b) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = ldu16(p + (uint64_t)b * 1024 + 256 * j);
+    };
+    // full blocks through a ring of kRing blocks in flight
+    uint4 r0[4], r1[4];
+    if (nb > 0) load(r0, 0);
+    if (nb > 1) load(r1, 1);
+    for (uint32_t b = 0; b < nb; b += kRing) {
+        block(r0, b);
+        if (b + 2 < nb) load(r0, b + 2);
+        if (b + 1 >= nb) break;
+        block(r1, b + 1);
+        if (b + 3 < nb) load(r1, b + 3);
     }
-    const uint32_t ns = (uint32_t)(((len - 1) - nb * 1024) / 64);
+    // the partial block: ns stripes, no scramble
+    const uint32_t ns = (uint32_t)(((len - 1) - (uint64_t)nb * 1024) / 64);
     if (ns) {
-        uint32_t w[4] = {0, 0, 0, 0};
-        const uint32_t q = (uint32_t)(nb * 1024 + 16 * lane);
-        if (s < ns) ld16(d, o + q, sh, dlen, w);
-        const uint64_t d0 = ((uint64_t)w[1] << 32) | w[0], d1 = ((uint64_t)w[3] << 32) | w[2];
-        const uint64_t k0 = d0 ^ ls.s0, k1 = d1 ^ ls.s1;
-        uint64_t c0 = (s < ns) ? (uint64_t)(uint32_t)k0 * (k0 >> 32) + d1 : 0;
-        uint64_t c1 = (s < ns) ? (uint64_t)(uint32_t)k1 * (k1 >> 32) + d0 : 0;
-        if (s < ns) weak16(w, q, sx, sux);
-        A0 += red16(c0);
-        A1 += red16(c1);
+        uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (4 * j + sp < ns) {
+                const uint4 v = ldu16(p + (uint64_t)nb * 1024 + 256 * j);
+                acc16(v, rs.w[4 * j + sp + 2 * m], rs.w[4 * j + sp + 2 * m + 1], c0, c1);
+                if (WEAK) {
+                    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                    weak16(w, nb * 1024 + 256 * j + 16 * q, sx, sux);
+                }
+            }
+        }
+        A0 += row_sum_sp(c0);
+        A1 += row_sum_sp(c1);
     }
-    {
-        // last stripe [len - 64, len), secret offset 192 - 64 - 7; every
-        // group computes it (no reduction), lanes 0..3 weak-sum the bytes no
-        // earlier stripe covered
-        uint32_t w[4];
-        const uint64_t q = len - 64 + 16 * m;
-        ld16(d, o + q, (uint32_t)((o + len) & 15), dlen, w);
-        const uint64_t d0 = ((uint64_t)w[1] << 32) | w[0], d1 = ((uint64_t)w[3] << 32) | w[2];
-        const uint64_t k0 = d0 ^ ls.l0, k1 = d1 ^ ls.l1;
-        A0 += (uint64_t)(uint32_t)k0 * (k0 >> 32) + d1;
-        A1 += (uint64_t)(uint32_t)k1 * (k1 >> 32) + d0;
-        const uint64_t covered = nb * 1024 + (uint64_t)ns * 64;
-        if (lane < 4) {
-            // zero the bytes below `covered` (at most 64 - (len - covered) of them)
+    RowWin r;
+    // last stripe [len - 64, len), secret offset 192 - 64 - 7 = 121: lanes with
+    // s' == 0 (q == m) add it and weak-sum the bytes no earlier stripe covered
+    uint64_t tA = 0, tB = 0;
+    if (sp == 0) {
+        const uint32_t qq = (uint32_t)(len - 64 + 16 * m);
+        const uint4 v = ldu16(a.data + o + qq);
+        uint64_t c0 = 0, c1 = 0;
+        acc16(v, csec_at(121 + 16 * m, a.seed), csec_at(129 + 16 * m, a.seed), c0, c1);
+        A0 += c0;
+        A1 += c1;
+        if (WEAK) {
+            const uint64_t covered = (uint64_t)nb * 1024 + (uint64_t)ns * 64;
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
             uint32_t wm[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const uint64_t b0 = q + 4 * k;
+                const uint64_t b0 = qq + 4 * k;
                 uint32_t mask = 0xffffffffu;
                 if (b0 + 4 <= covered) mask = 0;
                 else if (b0 < covered) mask = 0xffffffffu << (8 * (uint32_t)(covered - b0));
                 wm[k] = w[k] & mask;
             }
-            weak16(wm, (uint32_t)q, sx, sux);
+            weak16(wm, qq, sx, sux);
         }
+        // merge terms of accumulators 2m, 2m + 1 (64-bit: offset 11; high half: 117)
+        tA = fold64(A0 ^ csec_at(11 + 16 * m, a.seed), A1 ^ csec_at(19 + 16 * m, a.seed));
+        if (a.csum_type == kXxh3_128)
+            tB = fold64(A0 ^ csec_at(117 + 16 * m, a.seed), A1 ^ csec_at(125 + 16 * m, a.seed));
     }
-    sx = red64(sx);
-    sux = red64(sux);
-    Win r;
-    r.weak = uni((sx & 0xffffu) | (((uint32_t)len * sx - sux) << 16));
-    Xxh3Long st;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        st.acc[2 * j] = rdl64(A0, j);
-        st.acc[2 * j + 1] = rdl64(A1, j);
+    tA = quad_sum(tA);
+    tB = quad_sum(tB);
+    r.lo = xxh3_aval(len * P64_1 + tA);
+    r.hi = (a.csum_type == kXxh3_128) ? xxh3_aval(~(len * P64_2) + tB) : 0;
+    r.weak = 0;
+    if (WEAK) {
+        sx = row_sum16(sx);
+        sux = row_sum16(sux);
+        r.weak = (sx & 0xffffu) | (((uint32_t)len * sx - sux) << 16);
     }
-    r.lo = st.merge(11, len * P64_1, a.seed);
-    r.hi = (a.csum_type == kXxh3_128) ? st.merge(192 - 64 - 11, ~(len * P64_2), a.seed) : 0;
     return r;
 }
 
@@ -330,11 +391,9 @@ __device__ int32_t chain_match(const RsWalkArgs &a, uint32_t sum, uint64_t lo, u
     return -1;
 }
 
-// does a full-length block with sum1 == sum exist?  LDS prefilter, filter,
-// then the directory (uniform per lane, divergent across lanes)
+// does a full-length block with sum1 == sum exist?  (the directory; the
+// filters were tested by the caller; uniform per lane, divergent across lanes)
 __device__ __forceinline__ bool probe_full(const RsWalkArgs &a, uint32_t sum) {
-    const uint32_t f = sum >> (32 - a.fbits);
-    if (!((a.filt[f >> 5] >> (f & 31)) & 1u)) return false;
     const uint32_t b = sum >> (32 - a.dbits);
     const uint32_t p0 = a.dir[b], p1 = a.dir[b + 1];
     for (uint32_t p = p0; p < p1; ++p) {
@@ -371,21 +430,59 @@ struct SegResult {
     int32_t exit_want;
 };
 
+// STEP batch [A, A + 1024): lane l's leaving bytes [A + 16 l, +16) and the
+// entering bytes one block later (A is 16-aligned); bytes past dlen read 0
+__device__ __forceinline__ void batch_load(const RsWalkArgs &a, uint64_t A, uint32_t lane,
+                                           uint4 &wo, uint4 &wi) {
+    const uint64_t c = A + 16 * (uint64_t)lane, L = a.blength;
+    if (A + kBatch + L + 16 <= a.dlen) {
+        wo = gl16(a.data + c);
+        wi = ldu16(a.data + c + L);
+        return;
+    }
+    wo = gl16_guard(a.data, c, a.dlen);
+    uint32_t w[4];
+    ld16(a.data, c + L, (uint32_t)((c + L) & 15), a.dlen, w);
+    wi = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// lane j's value, j < kRows, selected per lane by its row (rows >= nv take row 0)
+__device__ __forceinline__ int64_t by_row(int64_t v, uint32_t lane, uint32_t nv) {
+    const uint32_t r = lane >> 4;
+    const uint32_t src = r < nv ? r : 0;
+    int64_t out = (int64_t)rdl64((uint64_t)v, 0);
+#pragma unroll
+    for (uint32_t j = 1; j < kRows; ++j) {
+        const int64_t x = (int64_t)rdl64((uint64_t)v, (int)j);
+        out = (src == j) ? x : out;
+    }
+    return out;
+}
+
 // hash_search from (o, want) over [o, stop); full windows only below
 // min(stop, full_end).  Matches go to out_off/out_idx/out_fab (lane 0
 // writes); with `spec`, the walk ends at its first match the speculative walk
 // also made.
-__device__ SegResult walk_segment(const RsWalkArgs &a, const LaneSec &ls, const uint32_t *lfilt,
+//   RUN   windows o, o + L, o + 2L, o + 3L are hashed together (one per row;
+//         the later ones speculatively, after a match) and visited in order.
+//   STEP  batches of 1024 offsets (16 per lane) from a wave scan of the
+//         rolling deltas; weak hits are queued in offset order and hashed
+//         kRows at a time (rows), then visited in order.
+// Only visited windows count: a speculative window the walk does not reach
+// is dropped, so matches and false alarms are hash_search's.
+__device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const uint32_t *lfilt,
                                   uint32_t lane, int64_t o, int32_t want, int64_t stop,
                                   int64_t *out_off, int32_t *out_idx, int64_t *out_fab,
-                                  uint32_t cap, const SpecView *spec) {
+                                  uint32_t cap, const SpecView *spec, WProf &wp) {
     const int64_t fend = min(stop, (int64_t)a.full_end);
     const uint64_t L = a.blength;
     const uint8_t *d = a.data;
+    const uint32_t row = lane >> 4;
     SegResult res{0, 0xffffffffu, 0, 0, want};
     uint64_t fa = 0;
     uint32_t n = 0;
     bool run = true;
+    bool ahead = false;       // RUN: speculate past the first window (after a match)
     uint32_t S1 = 0, S2 = 0;  // STEP: window sums at o (low 16 bits meaningful)
     // after a match at h with block i: emit, merge check, next offset
     auto on_match = [&](int64_t h, int32_t i, uint64_t fa_visit) -> bool {
@@ -419,30 +516,44 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const LaneSec &ls, const 
         return false;
     };
     bool merged = false;
-    uint64_t it = 0;
     while (!merged && o < fend) {
-        ++it;
-        WPROG(a, lane, 1, o, it);
+        WPROG(a, lane, 1, o, n);
         if (run) {
-            const Win w = wave_window(a, ls, lane, (uint64_t)o, L);
-            const uint64_t fa_visit = fa;
-            const int32_t i = unis(chain_match(a, w.weak, w.lo, w.hi, want, (uint32_t)L, fa));
-            WPROG(a, lane, 3, o, i);
-            if (i >= 0) {
-                merged = on_match(o, i, fa_visit);
-                continue;
+            // windows o + j L below fend, j < k
+            const int64_t room = (fend - o + (int64_t)L - 1) / (int64_t)L;
+            const uint32_t k = ahead ? (uint32_t)min<int64_t>(kRows, room) : 1u;
+            const int64_t orow = o + (int64_t)L * (int64_t)(row < k ? row : 0);
+            uint64_t t0 = wclock(wp);
+            const RowWin w = rows_window<true>(a, rs, lane, (uint64_t)orow, L);
+            wadd(wp, kPrRun, t0);
+            for (uint32_t j = 0; j < k; ++j) {
+                const int64_t oj = o;
+                const uint32_t wk = (uint32_t)__builtin_amdgcn_readlane((int)w.weak, (int)(16 * j));
+                const uint64_t lo = rdl64(w.lo, (int)(16 * j)), hi = rdl64(w.hi, (int)(16 * j));
+                const uint64_t fa_visit = fa;
+                t0 = wclock(wp);
+                const int32_t i = unis(chain_match(a, wk, lo, hi, want, (uint32_t)L, fa));
+                wadd(wp, kPrChain, t0);
+                WPROG(a, lane, 3, oj, i);
+                if (i >= 0) {
+                    merged = on_match(oj, i, fa_visit);
+                    ahead = true;
+                    if (merged || o != oj + (int64_t)L) break;   // short last block: re-plan
+                    continue;
+                }
+                // roll the window one byte: hash_search's s1/s2 update
+                const int32_t xo = sbyte(d, (uint64_t)oj);
+                const int32_t xi = (oj + 1 < fend) ? sbyte(d, (uint64_t)oj + L) : 0;
+                S1 = uni((wk & 0xffffu) - (uint32_t)xo + (uint32_t)xi);
+                S2 = uni((wk >> 16) - (uint32_t)L * (uint32_t)xo + S1);
+                o = oj + 1;
+                run = false;
+                break;
             }
-            // roll the window one byte: hash_search's s1/s2 update
-            const int32_t xo = sbyte(d, (uint64_t)o);
-            const int32_t xi = (o + 1 < fend) ? sbyte(d, (uint64_t)o + L) : 0;
-            S1 = uni((w.weak & 0xffffu) - (uint32_t)xo + (uint32_t)xi);
-            S2 = uni((w.weak >> 16) - (uint32_t)L * (uint32_t)xo + S1);
-            ++o;
-            run = false;
             continue;
         }
-        // ---- STEP: offsets [A, A + 1024) of which [o, fend) count ----
-        const uint64_t A = (uint64_t)o & ~15ull;
+        // ---- STEP: batches [A, A + 1024) from o; offsets below `from` are done ----
+        uint64_t A = (uint64_t)o & ~15ull;
         // sums at A: roll back from o (at most 15 steps)
         uint32_t T1 = S1, T2 = S2;
         for (uint64_t u = (uint64_t)o; u > A; --u) {
@@ -453,94 +564,153 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const LaneSec &ls, const 
         }
         T1 = uni(T1);
         T2 = uni(T2);
-        const uint64_t c = A + 16 * (uint64_t)lane;
-        uint32_t wo[4], wi[4];
-        {
-            const uint4 v = gl16_guard(d, c, a.dlen);
-            wo[0] = v.x; wo[1] = v.y; wo[2] = v.z; wo[3] = v.w;
-        }
-        ld16(d, c + L, (uint32_t)((c + L) & 15), a.dlen, wi);
-        int Xo = 0, Xi = 0, Eo = 0, Ei = 0;
+        int64_t from = o;
+        uint32_t nq = 0;        // queued hits: lane j < nq holds hit j (offset, weak sum)
+        int64_t qh = 0;
+        uint32_t qsum = 0;
+        bool matched = false;
+        uint4 cwo, cwi;         // the batch's leaving / entering bytes (16 per lane)
+        batch_load(a, A, lane, cwo, cwi);
+        for (;;) {
+            uint64_t tb = wclock(wp);
+            const uint64_t c = A + 16 * (uint64_t)lane;
+            const uint32_t wo[4] = {cwo.x, cwo.y, cwo.z, cwo.w};
+            const uint32_t wi[4] = {cwi.x, cwi.y, cwi.z, cwi.w};
+            // the next batch's bytes, in flight while this one is tested
+            uint4 nwo = cwo, nwi = cwi;
+            if ((int64_t)(A + kBatch) < fend) batch_load(a, A + kBatch, lane, nwo, nwi);
+            int Xo = 0, Xi = 0, Eo = 0, Ei = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            Xo = dot4(wo[k], 0x01010101u, Xo);
-            Xi = dot4(wi[k], 0x01010101u, Xi);
-            // weights 16 - t for byte t = 4k .. 4k+3
-            const uint32_t wt = (uint32_t)((16 - 4 * k) | ((15 - 4 * k) << 8) | ((14 - 4 * k) << 16) |
-                                           ((13 - 4 * k) << 24));
-            Eo = dot4(wo[k], wt, Eo);
-            Ei = dot4(wi[k], wt, Ei);
-        }
-        const uint32_t D = (uint32_t)(Xi - Xo), E = (uint32_t)(Ei - Eo), X = (uint32_t)Xo;
-        const uint32_t P = excl_scan(D, lane);
-        const uint32_t Y = excl_scan(E + 16u * P - (uint32_t)L * X, lane);
-        uint32_t s1 = T1 + P;
-        uint32_t s2 = T2 + 16u * lane * T1 + Y;
-        uint32_t sums[16];
-        uint32_t valid = 0;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            sums[t] = __builtin_amdgcn_perm(s2, s1, 0x05040100u);  // (s1 & 0xffff) | (s2 << 16)
-            const int32_t xo = __builtin_amdgcn_sbfe((int)wo[t >> 2], 8 * (t & 3), 8);
-            const int32_t xi = __builtin_amdgcn_sbfe((int)wi[t >> 2], 8 * (t & 3), 8);
-            s1 += (uint32_t)(xi - xo);
-            s2 = s2 - (uint32_t)L * (uint32_t)xo + s1;
-            const int64_t q = (int64_t)c + t;
-            valid |= (uint32_t)(q >= o && q < fend) << t;
-        }
-        // membership: LDS prefilter, then filter + directory for the survivors
-        uint32_t hit = 0;
-        if (a.lbits) {
+            for (int k = 0; k < 4; ++k) {
+                Xo = dot4(wo[k], 0x01010101u, Xo);
+                Xi = dot4(wi[k], 0x01010101u, Xi);
+                // weights 16 - t for byte t = 4k .. 4k+3
+                const uint32_t wt = (uint32_t)((16 - 4 * k) | ((15 - 4 * k) << 8) |
+                                               ((14 - 4 * k) << 16) | ((13 - 4 * k) << 24));
+                Eo = dot4(wo[k], wt, Eo);
+                Ei = dot4(wi[k], wt, Ei);
+            }
+            const uint32_t D = (uint32_t)(Xi - Xo), E = (uint32_t)(Ei - Eo), X = (uint32_t)Xo;
+            const uint32_t P = excl_scan(D, lane);
+            const uint32_t Y = excl_scan(E + 16u * P - (uint32_t)L * X, lane);
+            uint32_t s1 = T1 + P;
+            uint32_t s2 = T2 + 16u * lane * T1 + Y;
+            uint32_t sums[16];
+            uint32_t valid = 0;
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
-                const uint32_t fl = sums[t] >> (32 - a.lbits);
-                hit |= ((lfilt[fl >> 5] >> (fl & 31)) & 1u) << t;
+                sums[t] = __builtin_amdgcn_perm(s2, s1, 0x05040100u);  // (s1 & 0xffff) | (s2 << 16)
+                const int32_t xo = __builtin_amdgcn_sbfe((int)wo[t >> 2], 8 * (t & 3), 8);
+                const int32_t xi = __builtin_amdgcn_sbfe((int)wi[t >> 2], 8 * (t & 3), 8);
+                s1 += (uint32_t)(xi - xo);
+                s2 = s2 - (uint32_t)L * (uint32_t)xo + s1;
+                const int64_t qo = (int64_t)c + t;
+                valid |= (uint32_t)(qo >= from && qo < fend) << t;
             }
-            hit &= valid;
-        } else {
-            hit = valid;
-        }
-        for (uint32_t m = hit; m;) {
-            const int t = __builtin_ctz(m);
-            m &= m - 1;
-            uint32_t st = sums[0];
+            // membership: the LDS prefilter (top lbits of the sum), then the
+            // L2-resident blocked filter for all 16 offsets at once -- offsets
+            // the prefilter rejected read word 0, so their loads coalesce --
+            // and the directory only for the few offsets that pass both
+            uint32_t hit = valid;
+            if (a.lbits) {
+                uint32_t lh = 0;
 #pragma unroll
-            for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
-            if (!probe_full(a, st)) hit &= ~(1u << t);
-        }
-        // visit the hits in offset order (lane order, then bit order)
-        bool matched = false;
-        uint64_t lanes = __ballot(hit != 0);
-        WPROG(a, lane, 5, o, lanes);
-        while (lanes) {
-            const uint32_t hl = (uint32_t)__builtin_ctzll(lanes);
-            const uint32_t hm = (uint32_t)__builtin_amdgcn_readlane((int)hit, (int)hl);
-            const uint32_t t = (uint32_t)__builtin_ctz(hm);
-            const int64_t h = (int64_t)A + 16 * (int64_t)hl + t;
-            WPROG(a, lane, 6, h, lanes);
-            const Win w = wave_window(a, ls, lane, (uint64_t)h, L);
-            WPROG(a, lane, 7, h, w.weak);
-            const uint64_t fa_visit = fa;
-            const int32_t i = unis(chain_match(a, w.weak, w.lo, w.hi, want, (uint32_t)L, fa));
-            if (i >= 0) {
-                merged = on_match(h, i, fa_visit);
-                matched = true;
-                run = true;
+                for (int t = 0; t < 16; ++t) {
+                    const uint32_t fl = sums[t] >> (32 - a.lbits);
+                    lh |= ((lfilt[fl >> 5] >> (fl & 31)) & 1u) << t;
+                }
+                hit &= lh;
+            }
+            {
+                uint32_t pass = 0;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const bool on = (hit >> t) & 1u;
+                    const uint32_t wi_ = on ? rs_bloom_word(sums[t], a.fbits) : 0u;
+                    const uint64_t m = rs_bloom_mask(sums[t]);
+                    pass |= (uint32_t)((a.filt_b[wi_] & m) == m) << t;
+                }
+                hit &= pass;
+            }
+            for (uint32_t mm = hit; mm;) {
+                const int t = __builtin_ctz(mm);
+                mm &= mm - 1;
+                uint32_t st = sums[0];
+#pragma unroll
+                for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
+                if (!probe_full(a, st)) hit &= ~(1u << t);
+            }
+            // queue the hits in offset order (lane order, then bit order)
+            uint64_t lanes = __ballot(hit != 0);
+            WPROG(a, lane, 5, (int64_t)A, lanes);
+            while (lanes && nq < kRows) {
+                const uint32_t hl = (uint32_t)__builtin_ctzll(lanes);
+                const uint32_t hm = (uint32_t)__builtin_amdgcn_readlane((int)hit, (int)hl);
+                const uint32_t t = (uint32_t)__builtin_ctz(hm);
+                uint32_t st = sums[0];
+#pragma unroll
+                for (uint32_t k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
+                const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)st, (int)hl);
+                const int64_t h = (int64_t)A + 16 * (int64_t)hl + t;
+                if (lane == nq) {
+                    qh = h;
+                    qsum = sv;
+                }
+                ++nq;
+                if (lane == hl) hit &= hit - 1;
+                lanes = __ballot(hit != 0);
+            }
+            wadd(wp, kPrStep, tb);
+            const bool more = lanes != 0;              // hits of this batch not yet queued
+            const uint64_t nx = A + kBatch;
+            const bool last = (int64_t)nx >= fend;
+            if (nq == kRows || (!more && last && nq)) {
+                // hash the queued windows together, visit them in order
+                const int64_t orow = by_row(qh, lane, nq);
+                uint64_t tf = wclock(wp);
+                const RowWin w = rows_window<false>(a, rs, lane, (uint64_t)orow, L);
+                wadd(wp, kPrFlush, tf);
+                int64_t hlast = 0;
+                for (uint32_t j = 0; j < nq; ++j) {
+                    const int64_t h = (int64_t)rdl64((uint64_t)qh, (int)j);
+                    const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)qsum, (int)j);
+                    const uint64_t lo = rdl64(w.lo, (int)(16 * j)), hi = rdl64(w.hi, (int)(16 * j));
+                    const uint64_t fa_visit = fa;
+                    WPROG(a, lane, 6, h, j);
+                    tf = wclock(wp);
+                    const int32_t i = unis(chain_match(a, sv, lo, hi, want, (uint32_t)L, fa));
+                    wadd(wp, kPrChain, tf);
+                    hlast = h;
+                    if (i >= 0) {
+                        merged = on_match(h, i, fa_visit);
+                        matched = true;
+                        break;
+                    }
+                }
+                nq = 0;
+                if (matched) break;
+                if (more) {
+                    // this batch has more hits: redo it past the last visited one
+                    from = hlast + 1;
+                    continue;
+                }
+            }
+            if (more) continue;   // not reached: the queue only stops filling when full
+            if (last) {
+                o = fend;
                 break;
             }
-            if (lane == hl) hit &= hit - 1;
-            lanes = __ballot(hit != 0);
+            T1 = (uint32_t)__builtin_amdgcn_readlane((int)s1, 63);
+            T2 = (uint32_t)__builtin_amdgcn_readlane((int)s2, 63);
+            A = nx;
+            from = (int64_t)A;
+            cwo = nwo;
+            cwi = nwi;
         }
-        if (matched) continue;
-        // no match in this batch: continue at A + 1024 with lane 63's sums
-        const uint64_t nx = A + kBatch;
-        if ((int64_t)nx >= fend) {
-            o = fend;
-            break;
+        if (matched) {
+            run = true;
+            ahead = true;
         }
-        S1 = (uint32_t)__builtin_amdgcn_readlane((int)s1, 63);
-        S2 = (uint32_t)__builtin_amdgcn_readlane((int)s2, 63);
-        o = (int64_t)nx;
     }
     WPROG(a, lane, 9, o, n);
     res.n = n;
@@ -556,12 +726,14 @@ __device__ __forceinline__ void load_prefilter(const RsWalkArgs &a, uint32_t *lf
     __syncthreads();
 }
 
-// segments are dealt to waves statically (grid-stride): wave w walks
-// segments w, w + W, w + 2W, ...
-__device__ __forceinline__ uint32_t wave_id() {
-    return uni(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+// segments are taken from a work counter (a.work, zeroed before each launch):
+// their cost varies with the edits they hold, so dealing them statically
+// leaves the grid waiting on its most loaded waves
+__device__ __forceinline__ uint32_t next_segment(const RsWalkArgs &a, uint32_t lane) {
+    uint32_t k = 0;
+    if (lane == 0) k = atomicAdd(a.work, 1u);
+    return uni(k);
 }
-__device__ __forceinline__ uint32_t wave_count() { return gridDim.x * (blockDim.x / 64); }
 
 __device__ __forceinline__ int64_t seg_lo(const RsWalkArgs &a, uint32_t k) {
     return a.lo + (int64_t)k * a.seg_len;
@@ -575,16 +747,21 @@ __device__ __forceinline__ int64_t seg_hi(const RsWalkArgs &a, uint32_t k) {
 // preference" = count)
 __global__ __launch_bounds__(kWalkThreads) void rs_walk_spec_kernel(RsWalkArgs a) {
     __shared__ uint32_t lfilt[kLdsFiltWordsW];
+    __shared__ uint64_t lsec[24];
+    load_secret(lsec, a.seed);
     load_prefilter(a, lfilt);
     const uint32_t lane = threadIdx.x & 63;
-    const LaneSec ls = lane_secrets(lane, a.seed);
-    for (uint32_t k = wave_id(); k < a.nseg; k += wave_count()) {
+    const RowSec rs{lsec};
+    WProf wp{a.prof != nullptr, {}, {}};
+    for (uint32_t k = next_segment(a, lane); k < a.nseg; k = next_segment(a, lane)) {
         WPROG(a, lane, 11, k, a.nseg);
+        const uint64_t ts = wclock(wp);
         const int64_t e = (int64_t)uni64((uint64_t)(k ? seg_lo(a, k) : a.e0));
         const int32_t w = unis(k ? (int32_t)a.count : a.w0);
         const uint64_t base = (uint64_t)k * a.cap;
-        const SegResult r = walk_segment(a, ls, lfilt, lane, e, w, seg_hi(a, k), a.spec_off + base,
-                                         a.spec_idx + base, a.spec_fab + base, a.cap, nullptr);
+        const SegResult r = walk_segment(a, rs, lfilt, lane, e, w, seg_hi(a, k), a.spec_off + base,
+                                         a.spec_idx + base, a.spec_fab + base, a.cap, nullptr, wp);
+        wadd(wp, kPrSeg, ts);
         if (lane == 0) {
             a.spec_n[k] = r.n;
             a.spec_fa[k] = r.fa;
@@ -601,6 +778,13 @@ __global__ __launch_bounds__(kWalkThreads) void rs_walk_spec_kernel(RsWalkArgs a
         }
         WPROG(a, lane, 10, k, r.n);
     }
+    if (wp.on && lane == 0) {
+        uint64_t *pr = a.prof + (uint64_t)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 16;
+        for (int i = 0; i < kPrN; ++i) {
+            pr[i] = wp.cyc[i];
+            pr[8 + i] = wp.cnt[i];
+        }
+    }
     WPROG(a, lane, 12, 0, 0);
 }
 
@@ -609,10 +793,13 @@ __global__ __launch_bounds__(kWalkThreads) void rs_walk_spec_kernel(RsWalkArgs a
 // re-walks from it, merging into its speculative walk
 __global__ __launch_bounds__(kWalkThreads) void rs_walk_stitch_kernel(RsWalkArgs a) {
     __shared__ uint32_t lfilt[kLdsFiltWordsW];
+    __shared__ uint64_t lsec[24];
+    load_secret(lsec, a.seed);
     load_prefilter(a, lfilt);
     const uint32_t lane = threadIdx.x & 63;
-    const LaneSec ls = lane_secrets(lane, a.seed);
-    for (uint32_t k = wave_id(); k < a.nseg; k += wave_count()) {
+    const RowSec rs{lsec};
+    WProf wp{false, {}, {}};
+    for (uint32_t k = next_segment(a, lane); k < a.nseg; k = next_segment(a, lane)) {
         WPROG(a, lane, 21, k, a.nseg);
         const int64_t e = (int64_t)uni64((uint64_t)(k ? a.exit_old[k - 1] : a.e0));
         const int32_t w = unis(k ? a.exitw_old[k - 1] : a.w0);
@@ -633,8 +820,8 @@ __global__ __launch_bounds__(kWalkThreads) void rs_walk_stitch_kernel(RsWalkArgs
             // back to the speculative entry
             r = SegResult{0, 0, sv.fa, sv.exit_off, sv.exit_want};
         } else {
-            r = walk_segment(a, ls, lfilt, lane, e, w, seg_hi(a, k), a.fin_off + base,
-                             a.fin_idx + base, a.fin_fab + base, a.cap, &sv);
+            r = walk_segment(a, rs, lfilt, lane, e, w, seg_hi(a, k), a.fin_off + base,
+                             a.fin_idx + base, a.fin_fab + base, a.cap, &sv, wp);
         }
         if (lane == 0) {
             a.fin_entry[k] = e;

@@ -163,7 +163,7 @@ class Matcher:
         check(lib.vs_rsync_timing(self._h, ms))
         return dict(zip(["signatures", "table", "scan", "verify", "walk"], list(ms)))
 
-    KERNELS = ("scan", "verify", "signatures")
+    KERNELS = ("scan", "verify", "signatures", "stitch")
 
     def kernel_time(self, reset: bool = False) -> dict:
         """{kernel: (ms summed over launches, launches)} from HIP events."""
