@@ -637,7 +637,7 @@ def host_main(args):
         nch = step()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    stats = (ctypes.c_double * 4)()
+    stats = (ctypes.c_double * 8)()
     check(lib.vs_cdc_stream_stats(h, stats))
     lib.vs_cdc_close(h)
     value = n * args.steps / dt / 1e9
@@ -653,7 +653,9 @@ def host_main(args):
                    "pol": "0x3DA3358B4DC173", "min": MinSize, "max": MaxSize, "avg_bits": 20},
         "h2d_GBps": round(h2d, 2), "frac_of_h2d": round(value / h2d, 4),
         "stream_stats": {"pinned_bytes": stats[0], "staged_bytes": stats[1],
-                         "collect_waits": stats[2], "batches": stats[3]},
+                         "collect_waits": stats[2], "batches": stats[3],
+                         "host_ms": {"h2d_wait": round(stats[4], 1), "batches": round(stats[5], 1),
+                                     "collect": round(stats[6], 1), "staging": round(stats[7], 1)}},
     }), flush=True)
 
 

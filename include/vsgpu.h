@@ -101,8 +101,11 @@ void vs_cdc_close(vs_cdc *h);
  * for them).  The batch size can only change between streams. */
 int vs_cdc_set_batch_bytes(vs_cdc *h, uint64_t bytes);
 /* Streaming counters: [0] bytes fed from pinned memory, [1] bytes fed through
- * the staging buffers, [2] times a call waited for a batch's IDs, [3] batches. */
-int vs_cdc_stream_stats(vs_cdc *h, double out[4]);
+ * the staging buffers, [2] times a call waited for a batch's IDs, [3] batches;
+ * host milliseconds spent [4] waiting for H2D copies, [5] running batches
+ * (fingerprint, cut selection, hash queueing), [6] collecting chunks, [7]
+ * copying pageable input into the staging buffers. */
+int vs_cdc_stream_stats(vs_cdc *h, double out[8]);
 
 /* ---- device-resident batch API (data already in HBM) ------------------
  * Chunks a device byte range that begins at a chunk boundary.  dev_data
@@ -270,11 +273,20 @@ int vs_rsync_stats(vs_rsync *h, int64_t *candidates, int64_t *false_alarms,
 /* Device time (ms) of the last run's stages: 0 signatures, 1 table, 2 scan
  * (prefix + weak scan + sort), 3 strong verification, 4 host walk. */
 int vs_rsync_timing(vs_rsync *h, double ms_out[5]);
+/* Replaces checksum.c sum_init / sum_update / sum_end over one file (match.c
+ * matched() streams every source byte into it; rsync 3.2.3 seeds none of the
+ * xxhash / MD5 file sums): the whole-file checksum of a device-resident file,
+ * as sum_end writes it -- xxh128: LE low64 then LE high64; xxh3 / xxh64: LE
+ * 64-bit value (out[8..15] zeroed); md5: the digest.  XXH3 runs as parallel
+ * block contributions plus one serial scramble chain; MD5 and
+ * XXH64 run the one-lane restatement.  Blocks until done. */
+int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_type,
+                      uint8_t out[16]);
 /* Device time of one kernel class summed over its launches since the handle
  * was opened (or the last reset), from HIP events on the handle's stream:
  * which 0 = weak scan / speculative device walk, 1 = strong-sum verification,
- * 2 = signatures, 3 = device walk stitch passes.  reset != 0 zeroes the
- * totals after reading them. */
+ * 2 = signatures, 3 = device walk stitch passes, 4 = whole-file checksum.
+ * reset != 0 zeroes the totals after reading them. */
 int vs_rsync_kernel_time(vs_rsync *h, int which, int reset, double *ms, int64_t *launches);
 
 /* Host-memory one-shot forms: copy in, run, copy out. */

@@ -411,7 +411,7 @@ def _stream_pinned(data: np.ndarray, pol, mn, mx, ab, read, batch=None, reuse=No
         take()
     check(lib.vs_cdc_feed(h, None, 0, 1))
     assert take()
-    st = (ctypes.c_double * 4)()
+    st = (ctypes.c_double * 8)()
     check(lib.vs_cdc_stream_stats(h, st))
     return res, h, list(st)
 

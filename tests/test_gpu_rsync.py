@@ -407,3 +407,53 @@ def test_c4plan_source_sharded_exact(gpu):
     for m in hs:
         m.close()
     assert got == want and gfa == fa
+
+
+def _file_sum_want(data: bytes, csum: int) -> bytes:
+    """rsync 3.2.3 sum_end over sum_update(whole file), pinned by libxxhash
+    (the xxhash package) and hashlib: no seed for these types."""
+    import hashlib
+    import xxhash
+    if csum == 8:
+        return xxhash.xxh3_128_intdigest(data).to_bytes(16, "little")
+    if csum == 7:
+        return xxhash.xxh3_64_intdigest(data).to_bytes(8, "little")
+    if csum == 6:
+        return xxhash.xxh64_intdigest(data, seed=0).to_bytes(8, "little")
+    return hashlib.md5(data).digest()
+
+
+@pytest.mark.parametrize("csum", [8, 7])
+def test_file_sum_xxh3_lengths(gpu, csum):
+    """Whole-file checksum (R7) across the XXH3 length classes: short paths,
+    exactly one block, partial stripes, the last-stripe overlap, and a 64 MiB
+    file (65 536-step scramble chain), against libxxhash."""
+    from volsync_amd import Matcher
+    m = Matcher()
+    base = O.synth(61, 0, (64 << 20) + 4099)
+    for n in [0, 1, 16, 17, 128, 129, 240, 241, 1023, 1024, 1025, 1087, 1088, 2048, 4095,
+              65536 + 63, (1 << 20) + 777, 64 << 20]:
+        data = base[:n]
+        t = to_dev(data)
+        assert m.file_sum(t.data_ptr(), n, csum) == _file_sum_want(data.tobytes(), csum), n
+    m.close()
+
+
+def test_file_sum_multi_pass_and_other_types(gpu, monkeypatch):
+    """The XXH3 chain carried across contribution passes (piece size forced
+    small), and the one-lane MD5 / XXH64 restatements, on C4-fixture sources."""
+    from volsync_amd import Matcher
+    m = Matcher()
+    data = O.synth(62, 0, (9 << 20) + 321)
+    t = to_dev(data)
+    monkeypatch.setenv("VSGPU_FS_PIECE", "1000")
+    assert m.file_sum(t.data_ptr(), len(data), 8) == _file_sum_want(data.tobytes(), 8)
+    monkeypatch.delenv("VSGPU_FS_PIECE")
+    for path in FIX[:6]:
+        _, _, src = load_fixture(path)
+        ts = to_dev(src)
+        for csum in (8, 7, 6, 5):
+            n = len(src) if csum in (8, 7) else min(len(src), 1 << 20)
+            got = m.file_sum(ts.data_ptr(), n, csum)
+            assert got == _file_sum_want(src[:n].tobytes(), csum), (path, csum)
+    m.close()

@@ -91,6 +91,7 @@ def _load() -> ctypes.CDLL:
         "vs_cdc_set_batch_bytes": (c_int, [vp, c_u64]),
         "vs_cdc_stream_stats": (c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
         "vs_blob_dedup": (c_int, [vp, vp, c_size, vp, ctypes.POINTER(c_u64), vp]),
+        "vs_rsync_file_sum": (c_int, [vp, vp, ctypes.c_int64, c_int, ctypes.c_char_p]),
         "vs_cdc_set_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_slice": (c_int, [vp, c_u32]),

@@ -7,6 +7,7 @@
 //   longest-first order -> SHA-256 blob IDs (sha256.hip).
 #include <algorithm>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -111,7 +112,9 @@ struct vs_cdc {
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
     bool stage_busy[2] = {false, false};
     int stage_i = 0;
-    double feed_stats[4] = {0, 0, 0, 0};  // bytes direct, bytes staged, collect waits, batches
+    // bytes direct, bytes staged, collect waits, batches, then host ms spent
+    // waiting for DMAs, processing batches, collecting chunks, staging memcpy
+    double feed_stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // timing
     bool timing = false;
     struct Pend {
@@ -624,6 +627,12 @@ static int cdc_process(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t o
 }
 
 // ---- streaming ------------------------------------------------------------
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
 // Batch s lives in ring slot / device buffer s % R.  A batch's chunks become
 // `ready` once the slice that finishes its longest chain has completed.
 static bool batch_done(vs_cdc *h, uint64_t s) {
@@ -673,6 +682,11 @@ static int collect_batch(vs_cdc *h, uint64_t s, bool block) {
 
 // collect finished batches in order (block: at least the oldest one)
 static int collect_ready(vs_cdc *h, bool block) {
+    const double t0 = now_ms();
+    struct Acc {
+        double *d, t0;
+        ~Acc() { *d += now_ms() - t0; }
+    } acc{&h->feed_stats[6], t0};
     while (!h->spend.empty()) {
         const int r = collect_batch(h, h->spend.front(), block);
         if (r < 0) return r;
@@ -728,7 +742,9 @@ static int stream_copy(vs_cdc *h, uint8_t *dst, const uint8_t *src, size_t n) {
     if (pinned) {
         VS_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, h->cstream));
         VS_HIP(hipEventRecord(h->ev_copy, h->cstream));
+        const double t0 = now_ms();
         VS_HIP(hipEventSynchronize(h->ev_copy));
+        h->feed_stats[4] += now_ms() - t0;
         h->feed_stats[0] += (double)n;
         h->copy_pending = true;
         return 0;
@@ -745,8 +761,12 @@ static int stream_copy(vs_cdc *h, uint8_t *dst, const uint8_t *src, size_t n) {
     for (size_t off = 0; off < n; off += piece) {
         const size_t k = std::min(piece, n - off);
         const int i = h->stage_i;
+        const double t0 = now_ms();
         if (h->stage_busy[i]) VS_HIP(hipEventSynchronize(h->stage_ev[i]));
+        const double t1 = now_ms();
         memcpy(h->stage[i], src + off, k);
+        h->feed_stats[4] += t1 - t0;
+        h->feed_stats[7] += now_ms() - t1;
         VS_HIP(hipMemcpyAsync(dst + off, h->stage[i], k, hipMemcpyHostToDevice, h->cstream));
         VS_HIP(hipEventRecord(h->stage_ev[i], h->cstream));
         h->stage_busy[i] = true;
@@ -769,8 +789,10 @@ static int stream_run(vs_cdc *h, bool final) {
     }
     const uint64_t s = h->seq;
     uint64_t n = 0, consumed = 0;
+    const double t0 = now_ms();
     VS_TRY(cdc_process(h, cur.p ? cur.p : h->tabs.p, h->sfill, h->sorigin, final ? 1 : 0, &n,
                        &consumed));
+    h->feed_stats[5] += now_ms() - t0;
     h->spend.push_back(s);
     h->feed_stats[3] += 1;
     const uint64_t rest = h->sfill - consumed;
@@ -933,9 +955,9 @@ VS_API int vs_cdc_next(vs_cdc *h, vs_chunk *out, size_t cap, size_t *n_out) {
     return 0;
 }
 
-VS_API int vs_cdc_stream_stats(vs_cdc *h, double out[4]) {
+VS_API int vs_cdc_stream_stats(vs_cdc *h, double out[8]) {
     if (!h || !out) return fail(VS_ERR_ARG, "bad arguments");
-    for (int i = 0; i < 4; ++i) out[i] = h->feed_stats[i];
+    for (int i = 0; i < 8; ++i) out[i] = h->feed_stats[i];
     return 0;
 }
 

@@ -345,6 +345,11 @@ struct RsWalkArgs {
 hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t s);
 hipError_t launch_rs_pad_sum2(const uint8_t *sum2, uint32_t count, uint32_t s2length,
                               uint64_t *out, hipStream_t s);
+// whole-file checksum (filesum.hip): out = sum_end's digest of p[0, len);
+// scratch holds filesum_scratch_bytes(len, piece_blocks)
+size_t filesum_scratch_bytes(uint64_t len, uint64_t piece_blocks);
+hipError_t launch_filesum(const uint8_t *p, uint64_t len, int csum_type, void *scratch,
+                          uint64_t piece_blocks, uint8_t *out, hipStream_t s);
 // SaveBlob dedup (dedup.hip): first[i] = smallest index with ids[i]'s ID
 size_t dedup_tmp_bytes(uint64_t n);
 hipError_t launch_dedup(const uint8_t *ids, uint64_t n, uint32_t *first, void *tmp,

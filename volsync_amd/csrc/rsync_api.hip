@@ -103,8 +103,8 @@ struct vs_rsync {
     // each launch; every entry point synchronises right after): [0] weak scan
     // / device walk, [1] strong verification, [2] signatures
     hipEvent_t kev[2] = {nullptr, nullptr};
-    double kms[4] = {0, 0, 0, 0};
-    int64_t kn[4] = {0, 0, 0, 0};
+    double kms[5] = {0, 0, 0, 0, 0};
+    int64_t kn[5] = {0, 0, 0, 0, 0};
     // signature table
     bool loaded = false;
     int32_t count = 0, blength = 0, s2length = 0, remainder = 0;
@@ -122,6 +122,7 @@ struct vs_rsync {
     DevBuf w_fin_entry, w_fin_entryw, w_fin_from, w_fin_n, w_fin_fa, w_fin_off, w_fin_idx,
         w_fin_fab;
     DevBuf w_exit[2], w_exitw[2], w_ctl, w_prof;
+    DevBuf fs_scratch, fs_out;      // whole-file checksum
     // scan
     DevBuf px, pt, pxs, pts, partials, c_off, c_sum, c_off2, c_sum2, n_cand, sort_tmp;
     // verification
@@ -1159,7 +1160,7 @@ VS_API void vs_rsync_close(vs_rsync *h) {
                       &h->w_spec_fab, &h->w_spec_n, &h->w_spec_fa, &h->w_spec_exit,
                       &h->w_spec_exitw, &h->w_fin_entry, &h->w_fin_entryw, &h->w_fin_from,
                       &h->w_fin_n, &h->w_fin_fa, &h->w_fin_off, &h->w_fin_idx, &h->w_fin_fab,
-                      &h->w_exit[0], &h->w_exit[1], &h->w_exitw[0], &h->w_exitw[1], &h->w_ctl, &h->w_prof})
+                      &h->w_exit[0], &h->w_exit[1], &h->w_exitw[0], &h->w_exitw[1], &h->w_ctl, &h->w_prof, &h->fs_scratch, &h->fs_out})
         b->release();
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (HostReg *r : {&h->reg_off, &h->reg_sum, &h->reg_flag}) r->release();
@@ -1307,9 +1308,37 @@ VS_API int vs_rsync_timing(vs_rsync *h, double ms_out[5]) {
     return 0;
 }
 
+VS_API int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_type,
+                             uint8_t out[16]) {
+    if (!h || !out || len < 0 || (len && !dev_src)) return fail(VS_ERR_ARG, "bad arguments");
+    if (csum_type != VS_CSUM_MD5 && csum_type != VS_CSUM_XXH64 && csum_type != VS_CSUM_XXH3_64 &&
+        csum_type != VS_CSUM_XXH3_128)
+        return fail(VS_ERR_ARG, "unsupported checksum type");
+    VS_TRY(rs_dev(h));
+    VS_TRY(order_after_null(h));
+    // 4 GiB of file per contribution pass (256 MiB scratch); VSGPU_FS_PIECE
+    // (blocks) overrides it so tests can cover the multi-pass carry
+    const char *pe = getenv("VSGPU_FS_PIECE");
+    const uint64_t pv = pe ? strtoull(pe, nullptr, 10) : 0;
+    const uint64_t piece = pv ? pv : (1ull << 22);
+    VS_TRY(h->fs_scratch.ensure(filesum_scratch_bytes((uint64_t)len, piece)));
+    VS_TRY(h->fs_out.ensure(16));
+    KernelTimer kt(h, 4);
+    VS_HIP(launch_filesum((const uint8_t *)dev_src, (uint64_t)len, csum_type, h->fs_scratch.p, piece,
+                          h->fs_out.as<uint8_t>(), h->stream));
+    kt.stop();
+    VS_HIP(hipMemcpyAsync(h->pinned, h->fs_out.p, 16, hipMemcpyDeviceToHost, h->stream));
+    VS_HIP(hipStreamSynchronize(h->stream));
+    kt.fold();
+    memset(out, 0, 16);
+    const int n = (csum_type == VS_CSUM_MD5 || csum_type == VS_CSUM_XXH3_128) ? 16 : 8;
+    memcpy(out, h->pinned, n);
+    return 0;
+}
+
 VS_API int vs_rsync_kernel_time(vs_rsync *h, int which, int reset, double *ms,
                                 int64_t *launches) {
-    if (!h || which < 0 || which > 3) return fail(VS_ERR_ARG, "bad handle or kernel index");
+    if (!h || which < 0 || which > 4) return fail(VS_ERR_ARG, "bad handle or kernel index");
     if (ms) *ms = h->kms[which];
     if (launches) *launches = h->kn[which];
     if (reset) {

@@ -163,7 +163,7 @@ class Matcher:
         check(lib.vs_rsync_timing(self._h, ms))
         return dict(zip(["signatures", "table", "scan", "verify", "walk"], list(ms)))
 
-    KERNELS = ("scan", "verify", "signatures", "stitch")
+    KERNELS = ("scan", "verify", "signatures", "stitch", "file_sum")
 
     def kernel_time(self, reset: bool = False) -> dict:
         """{kernel: (ms summed over launches, launches)} from HIP events."""
@@ -174,6 +174,13 @@ class Matcher:
                                            ctypes.byref(n)))
             out[name] = (ms.value, n.value)
         return out
+
+    def file_sum(self, dev_src: int, length: int, csum_type: int = 8) -> bytes:
+        """checksum.c sum_init/sum_update/sum_end over the whole device file
+        (vs_rsync_file_sum): 16 bytes for xxh128 / md5, 8 for xxh3 / xxh64."""
+        out = ctypes.create_string_buffer(16)
+        check(lib.vs_rsync_file_sum(self._h, ctypes.c_void_p(dev_src), length, csum_type, out))
+        return out.raw[: 16 if csum_type in (CSUM_MD5, CSUM_XXH3_128) else 8]
 
     def match_sums(self, dev_src: int, length: int) -> List[Tuple[int, int]]:
         return self.matches(0, self.match_device(dev_src, length))
