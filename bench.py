@@ -247,6 +247,19 @@ def rsync_main(args):
         nm = int(c.item())
     value = (dtotal + plan.total) * args.steps / dt / 1e9
     own_src = sspec.own_hi - sspec.own_lo
+    # R7's whole-file checksum (checksum.c sum_update over S, xxh128), timed
+    # on its own after the timed region: its scramble chain is one serial
+    # dependency over the whole file, so it is reported beside the step
+    fsum = None
+    if world == 1:
+        torch.cuda.synchronize(dev)
+        m.kernel_time(reset=False)
+        t1 = time.perf_counter()
+        m.file_sum(ds.data_ptr(), plan.total, CSUM_XXH3_128)
+        fs_dt = time.perf_counter() - t1
+        fk = m.kernel_time()["file_sum"]
+        fsum = {"ms": round(fs_dt * 1e3, 2), "GBps": round(plan.total / fs_dt / 1e9, 2),
+                "kernel_ms": round(fk[0], 2), "csum": "xxh128 (unseeded, as sum_init)"}
     # the dominant kernel: rs_walk_spec_kernel, one launch per step over the
     # rank's whole source range (algorithmic bytes = those source bytes, each
     # read once by the walk: a window hash where it matches, the rolling scan
@@ -287,6 +300,7 @@ def rsync_main(args):
             "match_stats": st,
             "rccl_world_size": dist.get_world_size() if world > 1 else 1,
             "exchange_rounds_last_step": xst.get("exchange_rounds", 0),
+            "file_sum": fsum,
         }
         try:
             tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))

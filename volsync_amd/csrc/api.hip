@@ -98,7 +98,7 @@ struct vs_cdc {
     // stream; finished batches are collected in order once their IDs are final
     static constexpr size_t kStreamSlots = 24;
     std::vector<DevBuf> sbufs;
-    uint64_t sfill = 0, sorigin = 0, batch_bytes = 512ull << 20;
+    uint64_t sorigin = 0, batch_bytes = 512ull << 20;
     bool streaming = false;          // the handle is in streaming mode (first feed .. reset)
     uint32_t pre_stream_budget = 0;  // hash_budget before streaming changed it
     std::deque<uint64_t> spend;      // batches whose chunks are not yet collected
@@ -107,6 +107,12 @@ struct vs_cdc {
     hipStream_t cstream = nullptr;   // H2D copies
     hipEvent_t ev_copy = nullptr;    // after the last copy into the filling buffer
     bool copy_pending = false;
+    bool dma_wait = false;           // a copy from pinned caller memory is in flight
+    uint64_t fill_seq = 0, fill_new = 0, carry = 0, skip = 0;   // the batch being filled
+    bool scanned = false;            // a batch is scanned, its cut selection pending
+    bool scan_final = false;
+    uint64_t scan_len = 0, scan_skip = 0;
+    uint8_t *scan_buf = nullptr;
     uint8_t *stage[2] = {nullptr, nullptr};   // pinned staging for pageable input
     size_t stage_cap = 0;
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
@@ -115,6 +121,7 @@ struct vs_cdc {
     // bytes direct, bytes staged, collect waits, batches, then host ms spent
     // waiting for DMAs, processing batches, collecting chunks, staging memcpy
     double feed_stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double dbg_ms[3] = {0, 0, 0};    // VSGPU_STREAM_TRACE: stitch, finish, scan host ms
     // timing
     bool timing = false;
     struct Pend {
@@ -696,15 +703,26 @@ static int collect_ready(vs_cdc *h, bool block) {
     return 0;
 }
 
-// the buffer of the next batch (seq = h->seq) is free: its slot's previous
-// batch has been collected (backpressure: wait for it)
-static int stream_buffer(vs_cdc *h, DevBuf **out) {
+// Batches of the stream: batch q is filled into device buffer q % R (R =
+// ring slots): [kStreamPad - carry, kStreamPad) holds the bytes carried over
+// from batch q - 1 (after its last determined cut), [kStreamPad, ...) the new
+// bytes.  A full batch is scanned (fingerprint launched) at once; its cut
+// selection, emit and hash queueing -- which wait for the GPU -- run in the
+// next call, after that call's copy is issued, so they overlap the H2D.
+static uint64_t stream_pad(const vs_cdc *h) {
+    return (2ull * h->max_size + (1 << 20) + 63) & ~63ull;
+}
+static uint64_t stream_new_bytes(const vs_cdc *h) {
+    return std::max<uint64_t>(h->batch_bytes, 2ull * h->max_size + (1 << 20));
+}
+
+// buffer of batch q, free for writing: slot q % R's previous batch collected
+// (backpressure: wait for it)
+static int stream_buffer(vs_cdc *h, uint64_t q, DevBuf **out) {
     const size_t R = h->slots.size();
-    const uint64_t s = h->seq;
-    while (!h->spend.empty() && h->spend.front() + R <= s) VS_TRY(collect_batch(h, h->spend.front(), true));
-    DevBuf &b = h->sbufs[s % R];
-    const uint64_t batch = std::max<uint64_t>(h->batch_bytes, 2ull * h->max_size + (1 << 20));
-    const uint64_t need = batch + 2ull * h->max_size + (2 << 20);
+    while (!h->spend.empty() && h->spend.front() + R <= q) VS_TRY(collect_batch(h, h->spend.front(), true));
+    DevBuf &b = h->sbufs[q % R];
+    const uint64_t need = stream_pad(h) + stream_new_bytes(h) + (1 << 20);
     if (b.cap < need) VS_TRY(b.ensure(need));
     *out = &b;
     return 0;
@@ -726,13 +744,19 @@ static int stream_begin(vs_cdc *h) {
     h->hash_budget = (uint32_t)std::max<uint64_t>(budget, 1);
     VS_TRY(size_ring(h));
     h->sbufs.resize(h->slots.size());
+    h->fill_seq = h->seq;
+    h->fill_new = 0;
+    h->carry = 0;
+    h->skip = 0;
+    h->scanned = false;
     h->streaming = true;
     return 0;
 }
 
-// copy n caller bytes to device dst on the copy stream.  Pinned caller memory
-// is DMA'd directly (and waited for before the call returns: the caller owns
-// it); pageable memory goes through two pinned staging buffers.
+// issue the copy of n caller bytes to device dst on the copy stream.  Pinned
+// caller memory is DMA'd directly (h->dma_wait: the call waits for it before
+// returning -- the caller owns the buffer); pageable memory goes through two
+// pinned staging buffers (the copy of each piece waits only for its buffer).
 static int stream_copy(vs_cdc *h, uint8_t *dst, const uint8_t *src, size_t n) {
     if (!n) return 0;
     hipPointerAttribute_t at;
@@ -742,11 +766,9 @@ static int stream_copy(vs_cdc *h, uint8_t *dst, const uint8_t *src, size_t n) {
     if (pinned) {
         VS_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, h->cstream));
         VS_HIP(hipEventRecord(h->ev_copy, h->cstream));
-        const double t0 = now_ms();
-        VS_HIP(hipEventSynchronize(h->ev_copy));
-        h->feed_stats[4] += now_ms() - t0;
         h->feed_stats[0] += (double)n;
         h->copy_pending = true;
+        h->dma_wait = true;
         return 0;
     }
     const size_t piece = 64ull << 20;
@@ -778,35 +800,79 @@ static int stream_copy(vs_cdc *h, uint8_t *dst, const uint8_t *src, size_t n) {
     return 0;
 }
 
-// run the pipeline over the filling buffer's sfill bytes, carry the bytes
-// after the last determined chunk over to the next batch's buffer
-static int stream_run(vs_cdc *h, bool final) {
-    const size_t R = h->slots.size();
-    DevBuf &cur = h->sbufs[h->seq % R];
+// launch the fingerprint pass of the filling batch (bytes carried + new)
+static int stream_scan(vs_cdc *h, bool final) {
+    DevBuf *cur = nullptr;
+    VS_TRY(stream_buffer(h, h->fill_seq, &cur));
     if (h->copy_pending) {
         VS_HIP(hipStreamWaitEvent(h->stream, h->ev_copy, 0));
         h->copy_pending = false;
     }
-    const uint64_t s = h->seq;
-    uint64_t n = 0, consumed = 0;
+    // the scan starts `skip` bytes before the carried ones (16-byte aligned
+    // data; those bytes belong to the previous batch's last chunk and are
+    // outside the owned range)
+    const uint64_t len = h->skip + h->carry + h->fill_new;
+    const uint8_t *p = (const uint8_t *)cur->p + stream_pad(h) - h->carry - h->skip;
+    const uint64_t origin = h->sorigin - h->skip;
+    h->scan_len = len;
+    h->scan_final = final;
+    h->scan_buf = (uint8_t *)p;
+    h->scan_skip = h->skip;
     const double t0 = now_ms();
-    VS_TRY(cdc_process(h, cur.p ? cur.p : h->tabs.p, h->sfill, h->sorigin, final ? 1 : 0, &n,
-                       &consumed));
+    VS_TRY(cdc_scan(h, len ? p : (const uint8_t *)h->tabs.p, len, origin, h->sorigin,
+                    origin + len, final ? 1 : 0));
     h->feed_stats[5] += now_ms() - t0;
-    h->spend.push_back(s);
+    h->dbg_ms[2] += now_ms() - t0;
+    h->scanned = true;
+    h->fill_seq += 1;
+    h->fill_new = 0;
+    return 0;
+}
+
+// cut selection, emit and hash queueing of the scanned batch; its bytes
+// after the last determined cut are carried into the filling buffer
+static int stream_finish(vs_cdc *h) {
+    if (!h->scanned) return 0;
+    const double t0 = now_ms();
+    uint64_t ex = 0, n = 0;
+    int complete = 0;
+    VS_TRY(cdc_stitch(h, h->sorigin, &ex, &complete));
+    const double t1 = now_ms();
+    const uint64_t q = h->seq;
+    VS_TRY(cdc_finish(h, &n));
+    h->dbg_ms[0] += t1 - t0;
+    h->dbg_ms[1] += now_ms() - t1;
+    // used = scanned bytes up to the last determined cut (skip included)
+    uint64_t used = h->scan_skip;
+    if (complete) {
+        used = ex - (h->sorigin - h->scan_skip);
+    } else if (n) {
+        uint64_t e = 0;
+        VS_HIP(hipMemcpy(&e, h->slots[h->last].end.as<uint64_t>() + (n - 1), 8,
+                         hipMemcpyDeviceToHost));
+        used = (e & kPosMask) + 1;
+    }
+    h->spend.push_back(q);
     h->feed_stats[3] += 1;
-    const uint64_t rest = h->sfill - consumed;
+    const uint64_t rest = h->scan_len - used;
+    // the next scan starts 16-byte aligned: skip = the bytes before the
+    // carried ones that align it (at most 15; a non-final batch uses at
+    // least MinSize >= 64 bytes, so they exist)
+    const uint64_t skip = (stream_pad(h) - rest) % 16;
+    if (rest + skip > stream_pad(h) || (rest && used < skip))
+        return fail(VS_ERR_STATE, "streaming carry exceeds its reserve");
     if (rest) {
         DevBuf *nxt = nullptr;
-        VS_TRY(stream_buffer(h, &nxt));
-        VS_HIP(hipMemcpyAsync(nxt->p, (uint8_t *)cur.p + consumed, rest, hipMemcpyDeviceToDevice,
+        VS_TRY(stream_buffer(h, h->fill_seq, &nxt));
+        VS_HIP(hipMemcpyAsync((uint8_t *)nxt->p + stream_pad(h) - rest - skip,
+                              h->scan_buf + used - skip, rest + skip, hipMemcpyDeviceToDevice,
                               h->stream));
-        // later H2D copies into the same buffer land after the carried bytes
-        VS_HIP(hipEventRecord(h->ev_copy, h->stream));
-        VS_HIP(hipStreamWaitEvent(h->cstream, h->ev_copy, 0));
     }
-    h->sorigin += consumed;
-    h->sfill = rest;
+    h->carry = rest;
+    h->skip = rest ? skip : 0;
+    h->sorigin += used - h->scan_skip;
+    h->scanned = false;
+    h->feed_stats[5] += now_ms() - t0;
     return collect_ready(h, false);
 }
 
@@ -889,13 +955,21 @@ VS_API int vs_cdc_reset(vs_cdc *h, uint64_t pol, uint32_t min_size, uint32_t max
     VS_TRY(cdc_wait(h));
     if (h->streaming) h->hash_budget = h->pre_stream_budget;   // the device API's budget again
     VS_TRY(set_params(h, pol, min_size, max_size, avg_bits));
+    static const bool trace = getenv("VSGPU_STREAM_TRACE") != nullptr;
+    if (trace && h->streaming)
+        fprintf(stderr, "stream: host ms stitch %.1f finish %.1f scan %.1f\n", h->dbg_ms[0],
+                h->dbg_ms[1], h->dbg_ms[2]);
     h->state = 0;
     h->ready.clear();
     h->spend.clear();
-    h->sfill = 0;
     h->sorigin = 0;
     h->final_fed = false;
     h->copy_pending = false;
+    h->dma_wait = false;
+    h->scanned = false;
+    h->fill_new = 0;
+    h->carry = 0;
+    h->skip = 0;
     if (h->cstream) VS_HIP(hipStreamSynchronize(h->cstream));
     h->streaming = false;   // the next feed re-derives the streaming slice budget
     return 0;
@@ -916,23 +990,31 @@ VS_API int vs_cdc_feed(vs_cdc *h, const void *buf, size_t n, int final) {
     VS_TRY(stream_begin(h));
     const uint8_t *src = (const uint8_t *)buf;
     size_t left = n;
-    // a batch of at least 2*MaxSize always determines its first chunk's cut,
-    // so every non-final run makes progress
-    const uint64_t batch = std::max<uint64_t>(h->batch_bytes, 2ull * h->max_size + (1 << 20));
+    const uint64_t batch = stream_new_bytes(h);
     while (left) {
         DevBuf *cur = nullptr;
-        VS_TRY(stream_buffer(h, &cur));
-        const uint64_t room = (h->sfill < batch) ? batch - h->sfill : 0;
-        const uint64_t take = std::min<uint64_t>(room, left);
-        VS_TRY(stream_copy(h, (uint8_t *)cur->p + h->sfill, src, take));
-        h->sfill += take;
+        VS_TRY(stream_buffer(h, h->fill_seq, &cur));
+        const uint64_t take = std::min<uint64_t>(batch - h->fill_new, left);
+        VS_TRY(stream_copy(h, (uint8_t *)cur->p + stream_pad(h) + h->fill_new, src, take));
+        h->fill_new += take;
         src += take;
         left -= take;
-        if (h->sfill >= batch) VS_TRY(stream_run(h, false));
+        // the previous batch's cut selection overlaps this copy
+        VS_TRY(stream_finish(h));
+        if (h->fill_new == batch) VS_TRY(stream_scan(h, false));
     }
     if (final) {
-        VS_TRY(stream_run(h, true));
+        VS_TRY(stream_finish(h));
+        VS_TRY(stream_scan(h, true));
+        VS_TRY(stream_finish(h));
         h->final_fed = true;
+    }
+    if (h->dma_wait) {
+        // pinned caller memory: its copies must be complete before returning
+        const double t0 = now_ms();
+        VS_HIP(hipStreamSynchronize(h->cstream));
+        h->feed_stats[4] += now_ms() - t0;
+        h->dma_wait = false;
     }
     return 0;
 }

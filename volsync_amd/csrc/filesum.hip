@@ -8,9 +8,9 @@
 // XXH3 of a long input is 8 64-bit accumulators; each 1 KiB block adds the
 // contributions of its 16 stripes and is then scrambled.  The contributions
 // of all blocks are independent (fs_contrib_kernel: HBM-bound, 64 B out per
-// KiB), the scrambles are one serial chain over the blocks (fs_chain_kernel:
-// one wave, one accumulator per lane, contributions read from LDS ahead of
-// the chain), run piece by piece with the accumulators
+// KiB), the scrambles are a serial chain over the blocks per accumulator
+// (fs_chain_kernel: eight independent scalar-unit chains, one wave each),
+// run piece by piece with the accumulators
 // carried in device memory.  Other types and short files run the one-lane
 // restatement (strong.hpp checksum2), which is serial by construction.
 #include "internal.hpp"
@@ -31,7 +31,8 @@ __device__ __forceinline__ uint4 ldu16(const uint8_t *p) {
 // lo32 * hi32 of word i ^ secret word s + i).  Lane (g, m) of a wave owns
 // block 16 w + g, accumulators 2m and 2m + 1.
 __global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint64_t b0,
-                                                         uint64_t nb, uint64_t *C) {
+                                                         uint64_t nb, uint64_t *C,
+                                                         uint64_t stride) {
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63, g = lane >> 2, m = lane & 3;
     const uint64_t b = (gid >> 6) * 16 + g;
@@ -46,64 +47,55 @@ __global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint6
         c0 += (uint64_t)(uint32_t)k0 * (k0 >> 32) + d1;
         c1 += (uint64_t)(uint32_t)k1 * (k1 >> 32) + d0;
     }
-    C[b * 8 + 2 * m] = c0;
-    C[b * 8 + 2 * m + 1] = c1;
+    // transposed: accumulator i's contributions are contiguous (Ct[i][b])
+    C[(2 * m) * stride + b] = c0;
+    C[(2 * m + 1) * stride + b] = c1;
 }
 
-constexpr uint32_t kChainStage = 512;   // contributions staged in LDS per round
-
-// acc_j <- scramble(acc_j + C[b][j]) for b in [0, nb); lanes 0..7 of wave 0
-// run the chain, wave 1 stages the next round's contributions into LDS.
+// acc_j <- scramble(acc_j + C[j][b]) for b in [0, nb): the 8 accumulators
+// are independent chains, one wave each, and the whole chain is wave-uniform,
+// so it runs on the scalar unit (s_mul_i32 / s_mul_hi_u32 / s_xor / s_add,
+// whose dependent issue is far shorter than a VALU round trip), with the
+// contributions read through scalar loads 16 blocks ahead.
 // state[0..7] = accumulators (in/out).
-__global__ __launch_bounds__(128) void fs_chain_kernel(const uint64_t *C, uint64_t nb,
-                                                       uint64_t *state) {
-    __shared__ uint64_t buf[2][kChainStage * 8];
-    const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63;
-    const uint32_t j = lane & 7;
+__global__ __launch_bounds__(64) void fs_chain_kernel(const uint64_t *__restrict__ C,
+                                                      uint64_t nb, uint64_t stride,
+                                                      uint64_t *state) {
+    const uint32_t j = blockIdx.x;
+    const uint64_t *__restrict__ cj = C + j * stride;
     const uint64_t sec = kSecret64[16 + j];
+    const uint32_t slo = (uint32_t)sec, shi = (uint32_t)(sec >> 32);
     uint64_t acc = state[j];
-    const uint64_t rounds = (nb + kChainStage - 1) / kChainStage;
-    auto stage = [&](uint64_t r, int k) {
-        const uint64_t lo = r * kChainStage, n = min<uint64_t>(kChainStage, nb - lo) * 8;
-        for (uint64_t i = lane; i < n; i += 64) buf[k][i] = C[lo * 8 + i];
-    };
-    if (w == 1 && rounds) stage(0, 0);
-    __syncthreads();
-    for (uint64_t r = 0; r < rounds; ++r) {
-        const int k = (int)(r & 1);
-        if (w == 1) {
-            if (r + 1 < rounds) stage(r + 1, k ^ 1);
-        } else if (lane < 8) {
-            const uint32_t n = (uint32_t)min<uint64_t>(kChainStage, nb - r * kChainStage);
-            const uint64_t *cb = buf[k] + j;
-            // contributions are read 8 steps ahead (LDS latency off the chain)
-            uint64_t nx[8];
+    uint64_t b = 0;
+    // scalar loads run 16 blocks ahead of the chain (double-buffered)
+    uint64_t nx[16];
+    if (nb >= 16) {
 #pragma unroll
-            for (uint32_t q = 0; q < 8; ++q) nx[q] = (q < n) ? cb[8 * q] : 0;
-            uint64_t u = acc;
-            for (uint32_t i = 0; i < n; i += 8) {
-                uint64_t cur[8];
-#pragma unroll
-                for (uint32_t q = 0; q < 8; ++q) {
-                    cur[q] = nx[q];
-                    nx[q] = (i + 8 + q < n) ? cb[8 * (i + 8 + q)] : 0;
-                }
-#pragma unroll
-                for (uint32_t q = 0; q < 8; ++q) {
-                    if (i + q >= n) break;
-                    u += cur[q];
-                    // scramble: a ^= a >> 47; a ^= secret; a *= P32_1, the
-                    // 64 x 32-bit product as lo * P + (hi * P << 32)
-                    const uint32_t lo = (uint32_t)u ^ (uint32_t)(u >> 47) ^ (uint32_t)sec;
-                    const uint32_t hi = (uint32_t)(u >> 32) ^ (uint32_t)(sec >> 32);
-                    u = (uint64_t)lo * P32_1 + ((uint64_t)(hi * P32_1) << 32);
-                }
-            }
-            acc = u;
-        }
-        __syncthreads();
+        for (int q = 0; q < 16; ++q) nx[q] = cj[q];
     }
-    if (w == 0 && lane < 8) state[j] = acc;
+    for (; b + 16 <= nb; b += 16) {
+        uint64_t c[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) c[q] = nx[q];
+        if (b + 32 <= nb) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) nx[q] = cj[b + 16 + q];
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const uint64_t u = acc + c[q];
+            const uint32_t lo = (uint32_t)u ^ (uint32_t)(u >> 47) ^ slo;
+            const uint32_t hi = (uint32_t)(u >> 32) ^ shi;
+            acc = (uint64_t)lo * P32_1 + ((uint64_t)(hi * P32_1) << 32);
+        }
+    }
+    for (; b < nb; ++b) {
+        const uint64_t u = acc + cj[b];
+        const uint32_t lo = (uint32_t)u ^ (uint32_t)(u >> 47) ^ slo;
+        const uint32_t hi = (uint32_t)(u >> 32) ^ shi;
+        acc = (uint64_t)lo * P32_1 + ((uint64_t)(hi * P32_1) << 32);
+    }
+    if (threadIdx.x == 0) state[j] = acc;
 }
 
 // the partial block, the last stripe, the merge; lanes 0..7
@@ -172,11 +164,12 @@ hipError_t launch_filesum(const uint8_t *p, uint64_t len, int csum_type, void *s
     }
     fs_init_kernel<<<1, 64, 0, s>>>(state);
     const uint64_t nb = (len - 1) / 1024;
+    const uint64_t stride = std::min(piece_blocks, std::max<uint64_t>(nb, 1));
     for (uint64_t b0 = 0; b0 < nb; b0 += piece_blocks) {
         const uint64_t n = std::min(piece_blocks, nb - b0);
         const uint64_t waves = (n + 15) / 16;
-        fs_contrib_kernel<<<(uint32_t)((waves + 3) / 4), 256, 0, s>>>(p, b0, n, C);
-        fs_chain_kernel<<<1, 128, 0, s>>>(C, n, state);
+        fs_contrib_kernel<<<(uint32_t)((waves + 3) / 4), 256, 0, s>>>(p, b0, n, C, stride);
+        fs_chain_kernel<<<8, 64, 0, s>>>(C, n, stride, state);
     }
     fs_tail_kernel<<<1, 64, 0, s>>>(p, len, csum_type, state, out);
     return hipGetLastError();
