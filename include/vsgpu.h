@@ -95,7 +95,7 @@ void vs_cdc_close(vs_cdc *h);
 /* Streaming pipeline: fed bytes are copied to the device on a
  * copy stream (pinned caller memory by DMA, waited for before the call
  * returns; pageable memory through two pinned 64 MiB staging buffers) and
- * chunked in batches of batch_bytes (default 512 MiB); up to 24 batches are
+ * chunked in batches of batch_bytes (default 512 MiB); up to 32 batches are
  * in flight while their blob IDs are computed, and vs_cdc_next returns chunks
  * in stream order as soon as theirs are final (after the final feed it waits
  * for them).  The batch size can only change between streams. */

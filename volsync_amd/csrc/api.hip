@@ -96,7 +96,7 @@ struct vs_cdc {
     // buffer per ring slot -- the hash engine reads a batch's chunks from its
     // buffer until their blob IDs are final -- filled by H2D copies on a copy
     // stream; finished batches are collected in order once their IDs are final
-    static constexpr size_t kStreamSlots = 24;
+    static constexpr size_t kStreamSlots = 32;
     std::vector<DevBuf> sbufs;
     uint64_t sorigin = 0, batch_bytes = 512ull << 20;
     bool streaming = false;          // the handle is in streaming mode (first feed .. reset)
@@ -105,6 +105,7 @@ struct vs_cdc {
     std::deque<vs_chunk> ready;
     bool final_fed = false;
     hipStream_t cstream = nullptr;   // H2D copies
+    hipStream_t own_hm = nullptr;    // hash stream masked to half the CUs (streaming)
     hipEvent_t ev_copy = nullptr;    // after the last copy into the filling buffer
     bool copy_pending = false;
     bool dma_wait = false;           // a copy from pinned caller memory is in flight
@@ -387,7 +388,12 @@ static int run_scan_kernels(vs_cdc *h) {
         a.n_edge = k_lo + (h->nstrips - k_hi);
         a.work = h->flags.as<uint32_t>() + 3;  // zeroed with the flags above
         const bool fast = !wide && h->idx_shift >= 8 && fast_fp_enabled();
-        VS_HIP(launch_fingerprint(a, wide, fast, h->cus, h->stream));
+        // a fed stream's hash slices hold up to a few hundred workgroups for
+        // ~10 ms on the masked half of the CUs: a persistent grid of one
+        // workgroup per CU would wait for them before it could complete, so
+        // streaming batches get a grid that fits beside them
+        VS_HIP(launch_fingerprint(a, wide, fast, h->streaming ? std::max(h->cus / 2, 1) : h->cus,
+                                  h->stream));
     }
     {
         StageTimer t(h, kStSel);
@@ -407,10 +413,11 @@ static int cdc_scan(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t orig
     if (own_lo < origin || own_hi < own_lo || own_hi > origin + len)
         return fail(VS_ERR_ARG, "own range must lie inside [origin, origin + len)");
     VS_TRY(set_dev(h));
-    if (h->stream == h->own) {
+    if (h->stream == h->own && !h->streaming) {
         // the handle's own stream is non-blocking: order the scan after work the
         // caller queued on the null stream (e.g. the kernel that wrote the data).
-        // With vs_cdc_set_stream the caller's stream carries that order instead.
+        // With vs_cdc_set_stream the caller's stream carries that order instead;
+        // a fed stream's bytes come from the handle's own copies.
         VS_HIP(hipEventRecord(h->ev_null, nullptr));
         VS_HIP(hipStreamWaitEvent(h->stream, h->ev_null, 0));
     }
@@ -670,10 +677,13 @@ static int collect_batch(vs_cdc *h, uint64_t s, bool block) {
     if (n) {
         std::vector<uint64_t> st(n), en(n), cu(n);
         std::vector<uint8_t> id(n * 32);
-        VS_HIP(hipMemcpy(st.data(), sl.start.p, n * 8, hipMemcpyDeviceToHost));
-        VS_HIP(hipMemcpy(en.data(), sl.end.p, n * 8, hipMemcpyDeviceToHost));
-        VS_HIP(hipMemcpy(cu.data(), sl.cut.p, n * 8, hipMemcpyDeviceToHost));
-        VS_HIP(hipMemcpy(id.data(), sl.id.p, n * 32, hipMemcpyDeviceToHost));
+        // on the handle's own (non-blocking) stream: a null-stream copy would
+        // wait for every blocking stream, the masked hash stream included
+        VS_HIP(hipMemcpyAsync(st.data(), sl.start.p, n * 8, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync(en.data(), sl.end.p, n * 8, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync(cu.data(), sl.cut.p, n * 8, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync(id.data(), sl.id.p, n * 32, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipStreamSynchronize(h->stream));
         for (uint64_t i = 0; i < n; ++i) {
             vs_chunk c;
             c.start = sl.origin + st[i];
@@ -707,8 +717,8 @@ static int collect_ready(vs_cdc *h, bool block) {
 // ring slots): [kStreamPad - carry, kStreamPad) holds the bytes carried over
 // from batch q - 1 (after its last determined cut), [kStreamPad, ...) the new
 // bytes.  A full batch is scanned (fingerprint launched) at once; its cut
-// selection, emit and hash queueing -- which wait for the GPU -- run in the
-// next call, after that call's copy is issued, so they overlap the H2D.
+// selection, emit and hash queueing -- which wait for the GPU -- run when the
+// next batch is full, so the fingerprint pass overlaps that batch's copies.
 static uint64_t stream_pad(const vs_cdc *h) {
     return (2ull * h->max_size + (1 << 20) + 63) & ~63ull;
 }
@@ -738,6 +748,23 @@ static int stream_begin(vs_cdc *h) {
         for (int i = 0; i < 2; ++i) VS_HIP(hipEventCreateWithFlags(&h->stage_ev[i], hipEventDisableTiming));
     }
     VS_TRY(cdc_wait(h));
+    // the hash slices of a stream run ~10 ms each (a MaxSize chain must finish
+    // within the ring); spread over every CU they starve the next batch's
+    // fingerprint pass, so the handle's own hash stream is swapped for one
+    // masked to every other CU (across all XCDs) while streaming.  (That
+    // stream is created blocking, so nothing in the streaming path orders
+    // work through the null stream.)
+    if (h->hstream == h->own_h) {
+        if (!h->own_hm) {
+            std::vector<uint32_t> mask(((size_t)std::max(h->cus, 1) + 31) / 32, 0x55555555u);
+            if (hipExtStreamCreateWithCUMask(&h->own_hm, (uint32_t)mask.size(), mask.data()) !=
+                hipSuccess) {
+                (void)hipGetLastError();
+                h->own_hm = nullptr;
+            }
+        }
+        if (h->own_hm) h->hstream = h->own_hm;
+    }
     h->pre_stream_budget = h->hash_budget;
     const uint64_t mb = sha_blocks(h->max_size);
     const uint64_t budget = (mb + vs_cdc::kStreamSlots - 3) / (vs_cdc::kStreamSlots - 2);
@@ -847,10 +874,10 @@ static int stream_finish(vs_cdc *h) {
     if (complete) {
         used = ex - (h->sorigin - h->scan_skip);
     } else if (n) {
-        uint64_t e = 0;
-        VS_HIP(hipMemcpy(&e, h->slots[h->last].end.as<uint64_t>() + (n - 1), 8,
-                         hipMemcpyDeviceToHost));
-        used = (e & kPosMask) + 1;
+        VS_HIP(hipMemcpyAsync(h->pinned, h->slots[h->last].end.as<uint64_t>() + (n - 1), 8,
+                              hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipStreamSynchronize(h->stream));
+        used = (h->pinned[0] & kPosMask) + 1;
     }
     h->spend.push_back(q);
     h->feed_stats[3] += 1;
@@ -953,7 +980,10 @@ VS_API int vs_cdc_reset(vs_cdc *h, uint64_t pol, uint32_t min_size, uint32_t max
     // write blob IDs into their ring slots, which size_ring() releases when
     // the new max_size changes the ring length
     VS_TRY(cdc_wait(h));
-    if (h->streaming) h->hash_budget = h->pre_stream_budget;   // the device API's budget again
+    if (h->streaming) {
+        h->hash_budget = h->pre_stream_budget;   // the device API's budget again
+        if (h->own_hm && h->hstream == h->own_hm) h->hstream = h->own_h;
+    }
     VS_TRY(set_params(h, pol, min_size, max_size, avg_bits));
     static const bool trace = getenv("VSGPU_STREAM_TRACE") != nullptr;
     if (trace && h->streaming)
@@ -999,9 +1029,12 @@ VS_API int vs_cdc_feed(vs_cdc *h, const void *buf, size_t n, int final) {
         h->fill_new += take;
         src += take;
         left -= take;
-        // the previous batch's cut selection overlaps this copy
-        VS_TRY(stream_finish(h));
-        if (h->fill_new == batch) VS_TRY(stream_scan(h, false));
+        // the previous batch's cut selection waits until this batch is full:
+        // its fingerprint pass then had the whole batch's copies to finish in
+        if (h->fill_new == batch) {
+            VS_TRY(stream_finish(h));
+            VS_TRY(stream_scan(h, false));
+        }
     }
     if (final) {
         VS_TRY(stream_finish(h));
@@ -1061,6 +1094,10 @@ VS_API void vs_cdc_close(vs_cdc *h) {
     }
     if (h->ev_copy) (void)hipEventDestroy(h->ev_copy);
     if (h->cstream) (void)hipStreamDestroy(h->cstream);
+    if (h->own_hm) {
+        (void)hipStreamSynchronize(h->own_hm);
+        (void)hipStreamDestroy(h->own_hm);
+    }
     for (auto &s : h->slots) {
         s.start.release();
         s.end.release();
