@@ -185,6 +185,22 @@ void vs_sha256_close(vs_sha *h);
  * default stream); scratch lives in the vs_sha handle. */
 int vs_blob_dedup(vs_sha *h, const uint8_t *dev_ids, size_t n, uint32_t *dev_first,
                   uint64_t *n_unique, void *hip_stream);
+/* syncthing's scanner (lib/scanner; SURVEY.md 8(f)4, mover-syncthing/entry.sh:
+ * 130-135): SHA-256 of every block_size block of a device buffer of len bytes
+ * (the last block short), n = ceil(len / block_size) digests into dev_out.
+ * Queued on hip_stream like vs_sha256_run_device. */
+int vs_sha256_blocks(vs_sha *h, const void *dev_buf, uint64_t len, uint32_t block_size,
+                     uint8_t *dev_out, void *hip_stream);
+/* syncthing lib/protocol BlockSize: the smallest power of two from 128 KiB to
+ * 16 MiB that keeps a file of file_size bytes under 2000 blocks (else 16 MiB). */
+int vs_syncthing_block_size(int64_t file_size);
+/* Restore-side check (restic Repository.LoadBlob, mover-restic/entry.sh:
+ * 215-228): hash n device blobs and compare with their expected IDs
+ * (dev_want, n*32 bytes); dev_bad[i] (optional) = 1 on mismatch, *n_bad
+ * (optional; waits) = the mismatches. */
+int vs_blob_verify(vs_sha *h, const void *dev_buf, const uint64_t *dev_off,
+                   const uint32_t *dev_len, size_t n, const uint8_t *dev_want,
+                   uint32_t *dev_bad, uint64_t *n_bad, void *hip_stream);
 /* Host-memory convenience form (copies in and out). */
 int vs_sha256_batch(int device, const void *buf, size_t buf_len, const uint64_t *off,
                     const uint32_t *len, size_t n, uint8_t (*out)[32]);
@@ -282,6 +298,15 @@ int vs_rsync_timing(vs_rsync *h, double ms_out[5]);
  * XXH64 run the one-lane restatement.  Blocks until done. */
 int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_type,
                       uint8_t out[16]);
+/* Replaces receiver.c receive_data: rebuild the new file
+ * (out_len bytes, device dev_out) from the basis (device, basis_len bytes,
+ * blocks of blength) and the token stream -- the match list (host array, in
+ * order: block i copied to offset) and the literal bytes of the gaps between
+ * matches, concatenated in order (device, literal_len bytes).  Blocks until
+ * done; vs_rsync_file_sum over dev_out then checks it as receive_data does. */
+int vs_rsync_reconstruct(vs_rsync *h, void *dev_out, int64_t out_len, const void *dev_basis,
+                         int64_t basis_len, int32_t blength, const vs_match *matches,
+                         int64_t n_matches, const void *dev_literals, int64_t literal_len);
 /* Device time of one kernel class summed over its launches since the handle
  * was opened (or the last reset), from HIP events on the handle's stream:
  * which 0 = weak scan / speculative device walk, 1 = strong-sum verification,

@@ -519,3 +519,50 @@ def test_blob_dedup_vs_hashlib(gpu):
     assert sh.dedup(ids.data_ptr(), 1, first.data_ptr()) == 1
     assert sh.dedup(ids.data_ptr(), 0, first.data_ptr()) == 0
     sh.close()
+
+
+def test_sha256_blocks_syncthing(gpu):
+    """syncthing's scanner blocks: SHA-256 of every block of a
+    device buffer, for the block size lib/protocol picks and a larger one,
+    against hashlib; a short last block and an empty buffer included."""
+    import torch
+    from volsync_amd import DeviceSha256, syncthing_block_size
+    data = O.synth(71, 0, (5 << 20) + 333)
+    d = to_dev(data)
+    sh = DeviceSha256()
+    for bs in (syncthing_block_size(len(data)), 1 << 20, 4096):
+        n = (len(data) + bs - 1) // bs
+        out = torch.zeros((n, 32), dtype=torch.uint8, device="cuda")
+        assert sh.blocks(d.data_ptr(), len(data), bs, out.data_ptr()) == n
+        torch.cuda.synchronize()
+        got = [bytes(r) for r in out.cpu().numpy()]
+        want = [hashlib.sha256(data[i * bs:(i + 1) * bs].tobytes()).digest() for i in range(n)]
+        assert got == want, bs
+    assert sh.blocks(d.data_ptr(), 0, 1 << 17, d.data_ptr()) == 0
+    sh.close()
+
+
+def test_blob_verify_restore(gpu):
+    """Repository.LoadBlob's ID check on restore: blobs whose
+    SHA-256 differs from the expected ID are flagged and counted."""
+    import torch
+    from volsync_amd import DeviceSha256
+    rng = np.random.default_rng(9)
+    sizes = rng.integers(0, 70000, 3000)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    data = O.synth(72, 0, int(sizes.sum()) + 16)
+    want = np.stack([np.frombuffer(hashlib.sha256(data[o:o + n].tobytes()).digest(), np.uint8)
+                     for o, n in zip(offs.tolist(), sizes.tolist())])
+    corrupt = sorted(set(rng.integers(0, 3000, 9).tolist()))
+    for i in corrupt:
+        want[i, i % 32] ^= 0x5A
+    d = to_dev(data)
+    do = torch.from_numpy(offs).cuda()
+    dl = torch.from_numpy(sizes.astype(np.int32)).cuda()
+    dw = torch.from_numpy(want).cuda()
+    bad = torch.zeros(3000, dtype=torch.int32, device="cuda")
+    sh = DeviceSha256()
+    assert sh.verify(d.data_ptr(), do.data_ptr(), dl.data_ptr(), 3000, dw.data_ptr(),
+                     bad.data_ptr()) == len(corrupt)
+    assert np.nonzero(bad.cpu().numpy())[0].tolist() == corrupt
+    sh.close()

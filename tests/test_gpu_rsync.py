@@ -457,3 +457,39 @@ def test_file_sum_multi_pass_and_other_types(gpu, monkeypatch):
             got = m.file_sum(ts.data_ptr(), n, csum)
             assert got == _file_sum_want(src[:n].tobytes(), csum), (path, csum)
     m.close()
+
+
+@pytest.mark.parametrize("path", FIX[:8], ids=os.path.basename)
+def test_receiver_reconstruct(gpu, path):
+    """receiver.c receive_data: the new file rebuilt on the device
+    from the basis, the match list and the gaps' literal bytes equals the
+    source, and its whole-file checksum equals the sender's."""
+    from volsync_amd import Matcher
+    doc, basis, src = load_fixture(path)
+    p = doc["params"] if "params" in doc else {}
+    m = Matcher()
+    db, ds = to_dev(basis), to_dev(src)
+    hdr = O.rsync_sizes(len(basis), p.get("block_size", 0))
+    bl = hdr[0]
+    csum, seed = 8, 0x5EED5EED
+    n1 = max(hdr[2], 1)
+    import torch
+    s1 = torch.zeros(n1, dtype=torch.int32, device="cuda")
+    s2 = torch.zeros(n1 * hdr[1], dtype=torch.uint8, device="cuda")
+    m.signatures_device(db.data_ptr(), len(basis), bl, hdr[1], csum, seed, s1.data_ptr(),
+                        s2.data_ptr())
+    m.load_sums_device(hdr[2], bl, hdr[1], hdr[3], s1.data_ptr(), s2.data_ptr(), csum, seed)
+    matches = m.match_sums(ds.data_ptr(), len(src))
+    lit, pos = [], 0
+    for o, i in matches:
+        lit.append(src[pos:o])
+        pos = o + min(bl, len(basis) - i * bl)
+    lit.append(src[pos:])
+    lits = np.concatenate(lit) if lit else np.zeros(0, np.uint8)
+    dl = to_dev(lits)
+    out = torch.zeros(max(len(src), 16), dtype=torch.uint8, device="cuda")
+    m.reconstruct(out.data_ptr(), len(src), db.data_ptr(), len(basis), bl, matches, dl.data_ptr(),
+                  len(lits))
+    assert (out[: len(src)].cpu().numpy() == src).all()
+    assert m.file_sum(out.data_ptr(), len(src), 8) == _file_sum_want(src.tobytes(), 8)
+    m.close()

@@ -92,6 +92,11 @@ def _load() -> ctypes.CDLL:
         "vs_cdc_stream_stats": (c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
         "vs_blob_dedup": (c_int, [vp, vp, c_size, vp, ctypes.POINTER(c_u64), vp]),
         "vs_rsync_file_sum": (c_int, [vp, vp, ctypes.c_int64, c_int, ctypes.c_char_p]),
+        "vs_sha256_blocks": (c_int, [vp, vp, c_u64, c_u32, vp, vp]),
+        "vs_syncthing_block_size": (c_int, [ctypes.c_int64]),
+        "vs_blob_verify": (c_int, [vp, vp, vp, vp, c_size, vp, vp, ctypes.POINTER(c_u64), vp]),
+        "vs_rsync_reconstruct": (c_int, [vp, vp, ctypes.c_int64, vp, ctypes.c_int64, ctypes.c_int32,
+                                         ctypes.POINTER(VsMatch), ctypes.c_int64, vp, ctypes.c_int64]),
         "vs_cdc_set_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_slice": (c_int, [vp, c_u32]),

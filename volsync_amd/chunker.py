@@ -35,7 +35,7 @@ TestPol = 0x3DA3358B4DC173  # chunker_test.go testPol
 
 __all__ = ["Chunk", "Chunker", "EOF", "New", "NewWithBoundaries", "Pol", "DeviceChunker",
            "DeviceSha256",
-           "MinSize", "MaxSize", "KiB", "MiB"]
+           "MinSize", "MaxSize", "KiB", "MiB", "syncthing_block_size"]
 
 
 class EOF(EOFError):
@@ -319,6 +319,25 @@ class DeviceSha256:
         """Throughput mode from min_chains active blobs (0 = default, 0xffffffff = never)."""
         check(lib.vs_sha256_set_wide(self._h, int(min_chains), int(drain_blocks)))
 
+    def blocks(self, dev_buf: int, length: int, block_size: int, dev_out: int,
+               stream: Optional[int] = None) -> int:
+        """syncthing's scanner: SHA-256 of every block_size block (vs_sha256_blocks);
+        returns the number of blocks."""
+        check(lib.vs_sha256_blocks(self._h, ctypes.c_void_p(dev_buf), length, block_size,
+                                   ctypes.c_void_p(dev_out), ctypes.c_void_p(stream or None)))
+        return (length + block_size - 1) // block_size
+
+    def verify(self, dev_buf: int, dev_off: int, dev_len: int, n: int, dev_want: int,
+               dev_bad: Optional[int] = None, stream: Optional[int] = None) -> int:
+        """Repository.LoadBlob's check (vs_blob_verify): the number of blobs
+        whose SHA-256 differs from the expected ID (waits)."""
+        bad = ctypes.c_uint64(0)
+        check(lib.vs_blob_verify(self._h, ctypes.c_void_p(dev_buf), ctypes.c_void_p(dev_off),
+                                 ctypes.c_void_p(dev_len), n, ctypes.c_void_p(dev_want),
+                                 ctypes.c_void_p(dev_bad or None), ctypes.byref(bad),
+                                 ctypes.c_void_p(stream or None)))
+        return int(bad.value)
+
     def dedup(self, dev_ids: int, n: int, dev_first: int, stream: Optional[int] = None,
               count: bool = True) -> Optional[int]:
         """Repository.SaveBlob's dedup over n device blob IDs (vs_blob_dedup):
@@ -340,6 +359,11 @@ class DeviceSha256:
             self.close()
         except Exception:
             pass
+
+
+def syncthing_block_size(file_size: int) -> int:
+    """syncthing lib/protocol BlockSize (vs_syncthing_block_size)."""
+    return int(lib.vs_syncthing_block_size(int(file_size)))
 
 
 def synth_fill_device(dev_ptr: int, seed: int, off: int, n: int, device: int = 0,

@@ -1209,6 +1209,8 @@ struct vs_sha {
     ShaEngine eng;
     DevBuf dd_tmp;                  // vs_blob_dedup scratch
     uint64_t *dd_pinned = nullptr;
+    DevBuf blk_off, blk_len;        // vs_sha256_blocks descriptors
+    DevBuf vf_ids, vf_cnt;          // vs_blob_verify scratch
     hipEvent_t done = nullptr;  // after the last run, on its stream
     bool ran = false;
 };
@@ -1262,6 +1264,58 @@ VS_API int vs_sha256_run_device(vs_sha *h, const void *dev_buf, const uint64_t *
                    (hipStream_t)hip_stream);
 }
 
+VS_API int vs_sha256_blocks(vs_sha *h, const void *dev_buf, uint64_t len, uint32_t block_size,
+                            uint8_t *dev_out, void *hip_stream) {
+    if (!h || !block_size || (len && (!dev_buf || !dev_out))) return fail(VS_ERR_ARG, "bad arguments");
+    const uint64_t n = (len + block_size - 1) / block_size;
+    if (!n) return 0;
+    VS_HIP(hipSetDevice(h->device));
+    const hipStream_t s = (hipStream_t)hip_stream;
+    if (h->ran) VS_HIP(hipStreamWaitEvent(s, h->done, 0));   // descriptors of the last run
+    VS_TRY(h->blk_off.ensure(n * 8));
+    VS_TRY(h->blk_len.ensure(n * 4));
+    VS_HIP(launch_blk_desc(len, block_size, n, h->blk_off.as<uint64_t>(), h->blk_len.as<uint32_t>(), s));
+    return sha_run(h, (const uint8_t *)dev_buf, h->blk_off.as<uint64_t>(), h->blk_len.as<uint32_t>(), n,
+                   dev_out, s);
+}
+
+VS_API int vs_syncthing_block_size(int64_t file_size) {
+    // lib/protocol BlockSize: the smallest of 128 KiB .. 16 MiB (powers of
+    // two) that keeps the file under 2000 blocks, else 16 MiB
+    int bs = 128 << 10;
+    for (; bs < (16 << 20); bs *= 2)
+        if (file_size < 2000ll * bs) break;
+    return bs;
+}
+
+VS_API int vs_blob_verify(vs_sha *h, const void *dev_buf, const uint64_t *dev_off,
+                          const uint32_t *dev_len, size_t n, const uint8_t *dev_want,
+                          uint32_t *dev_bad, uint64_t *n_bad, void *hip_stream) {
+    if (!h || (n && (!dev_buf || !dev_off || !dev_len || !dev_want)))
+        return fail(VS_ERR_ARG, "bad arguments");
+    if (n_bad) *n_bad = 0;
+    if (!n) return 0;
+    VS_HIP(hipSetDevice(h->device));
+    const hipStream_t s = (hipStream_t)hip_stream;
+    if (h->ran) VS_HIP(hipStreamWaitEvent(s, h->done, 0));
+    VS_TRY(h->vf_ids.ensure(n * 32));
+    VS_TRY(h->vf_cnt.ensure(8));
+    VS_TRY(sha_run(h, (const uint8_t *)dev_buf, dev_off, dev_len, n, h->vf_ids.as<uint8_t>(), s));
+    VS_HIP(launch_verify(h->vf_ids.as<uint8_t>(), dev_want, n, dev_bad,
+                         h->vf_cnt.as<unsigned long long>(), s));
+    if (n_bad) {
+        if (!h->dd_pinned &&
+            hipHostMalloc((void **)&h->dd_pinned, 64, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(VS_ERR_NOMEM, "pinned read-back buffer");
+        }
+        VS_HIP(hipMemcpyAsync(h->dd_pinned, h->vf_cnt.p, 8, hipMemcpyDeviceToHost, s));
+        VS_HIP(hipStreamSynchronize(s));
+        *n_bad = h->dd_pinned[0];
+    }
+    return 0;
+}
+
 VS_API int vs_blob_dedup(vs_sha *h, const uint8_t *dev_ids, size_t n, uint32_t *dev_first,
                          uint64_t *n_unique, void *hip_stream) {
     if (!h || (n && (!dev_ids || !dev_first))) return fail(VS_ERR_ARG, "bad arguments");
@@ -1296,6 +1350,7 @@ VS_API void vs_sha256_close(vs_sha *h) {
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
     h->dd_tmp.release();
+    for (DevBuf *b : {&h->blk_off, &h->blk_len, &h->vf_ids, &h->vf_cnt}) b->release();
     if (h->dd_pinned) (void)hipHostFree(h->dd_pinned);
     if (h->done) {
         (void)hipEventSynchronize(h->done);

@@ -350,6 +350,18 @@ hipError_t launch_rs_pad_sum2(const uint8_t *sum2, uint32_t count, uint32_t s2le
 size_t filesum_scratch_bytes(uint64_t len, uint64_t piece_blocks);
 hipError_t launch_filesum(const uint8_t *p, uint64_t len, int csum_type, void *scratch,
                           uint64_t piece_blocks, uint8_t *out, hipStream_t s);
+// adjacent-mover kernels (movers.hip)
+struct ReconPiece {
+    uint64_t dst, src, len;
+    uint32_t kind;   // 0: basis bytes, 1: literal bytes
+    uint32_t pad;
+};
+hipError_t launch_blk_desc(uint64_t len, uint32_t bs, uint64_t n, uint64_t *off, uint32_t *lens,
+                           hipStream_t s);
+hipError_t launch_verify(const uint8_t *got, const uint8_t *want, uint64_t n, uint32_t *bad,
+                         unsigned long long *count, hipStream_t s);
+hipError_t launch_recon(uint8_t *dst, const uint8_t *basis, const uint8_t *lit,
+                        const ReconPiece *pieces, uint64_t n, int cus, hipStream_t s);
 // SaveBlob dedup (dedup.hip): first[i] = smallest index with ids[i]'s ID
 size_t dedup_tmp_bytes(uint64_t n);
 hipError_t launch_dedup(const uint8_t *ids, uint64_t n, uint32_t *first, void *tmp,

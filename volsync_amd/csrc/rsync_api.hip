@@ -123,6 +123,7 @@ struct vs_rsync {
         w_fin_fab;
     DevBuf w_exit[2], w_exitw[2], w_ctl, w_prof;
     DevBuf fs_scratch, fs_out;      // whole-file checksum
+    DevBuf rc_pieces;               // receiver reconstruction
     // scan
     DevBuf px, pt, pxs, pts, partials, c_off, c_sum, c_off2, c_sum2, n_cand, sort_tmp;
     // verification
@@ -1160,7 +1161,7 @@ VS_API void vs_rsync_close(vs_rsync *h) {
                       &h->w_spec_fab, &h->w_spec_n, &h->w_spec_fa, &h->w_spec_exit,
                       &h->w_spec_exitw, &h->w_fin_entry, &h->w_fin_entryw, &h->w_fin_from,
                       &h->w_fin_n, &h->w_fin_fa, &h->w_fin_off, &h->w_fin_idx, &h->w_fin_fab,
-                      &h->w_exit[0], &h->w_exit[1], &h->w_exitw[0], &h->w_exitw[1], &h->w_ctl, &h->w_prof, &h->fs_scratch, &h->fs_out})
+                      &h->w_exit[0], &h->w_exit[1], &h->w_exitw[0], &h->w_exitw[1], &h->w_ctl, &h->w_prof, &h->fs_scratch, &h->fs_out, &h->rc_pieces})
         b->release();
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (HostReg *r : {&h->reg_off, &h->reg_sum, &h->reg_flag}) r->release();
@@ -1333,6 +1334,50 @@ VS_API int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int 
     memset(out, 0, 16);
     const int n = (csum_type == VS_CSUM_MD5 || csum_type == VS_CSUM_XXH3_128) ? 16 : 8;
     memcpy(out, h->pinned, n);
+    return 0;
+}
+
+VS_API int vs_rsync_reconstruct(vs_rsync *h, void *dev_out, int64_t out_len, const void *dev_basis,
+                                int64_t basis_len, int32_t blength, const vs_match *matches,
+                                int64_t n_matches, const void *dev_literals, int64_t literal_len) {
+    if (!h || out_len < 0 || basis_len < 0 || blength <= 0 || n_matches < 0 || literal_len < 0 ||
+        (out_len && !dev_out) || (n_matches && (!matches || !dev_basis)) ||
+        (literal_len && !dev_literals))
+        return fail(VS_ERR_ARG, "bad arguments");
+    // the token stream as pieces, in order (receiver.c receive_data: literal
+    // data is written as it comes, token i copies basis block i)
+    std::vector<ReconPiece> pc;
+    pc.reserve((size_t)n_matches * 2 + 1);
+    int64_t pos = 0, lit = 0;
+    const int64_t count = (basis_len + blength - 1) / blength;
+    for (int64_t k = 0; k < n_matches; ++k) {
+        const vs_match m = matches[k];
+        if (m.offset < pos || m.block_index < 0 || m.block_index >= count)
+            return fail(VS_ERR_ARG, "match list out of order or block index out of range");
+        const int64_t bo = (int64_t)m.block_index * blength;
+        const int64_t bl = std::min<int64_t>(blength, basis_len - bo);
+        if (m.offset + bl > out_len) return fail(VS_ERR_ARG, "match past the end of the file");
+        if (m.offset > pos) {
+            pc.push_back({(uint64_t)pos, (uint64_t)lit, (uint64_t)(m.offset - pos), 1, 0});
+            lit += m.offset - pos;
+        }
+        pc.push_back({(uint64_t)m.offset, (uint64_t)bo, (uint64_t)bl, 0, 0});
+        pos = m.offset + bl;
+    }
+    if (pos < out_len) {
+        pc.push_back({(uint64_t)pos, (uint64_t)lit, (uint64_t)(out_len - pos), 1, 0});
+        lit += out_len - pos;
+    }
+    if (lit != literal_len) return fail(VS_ERR_ARG, "literal bytes do not fill the gaps between matches");
+    if (pc.empty()) return 0;
+    VS_TRY(rs_dev(h));
+    VS_TRY(order_after_null(h));
+    VS_TRY(h->rc_pieces.ensure(pc.size() * sizeof(ReconPiece)));
+    VS_HIP(hipMemcpyAsync(h->rc_pieces.p, pc.data(), pc.size() * sizeof(ReconPiece),
+                          hipMemcpyHostToDevice, h->stream));
+    VS_HIP(launch_recon((uint8_t *)dev_out, (const uint8_t *)dev_basis, (const uint8_t *)dev_literals,
+                        h->rc_pieces.as<ReconPiece>(), pc.size(), h->cus, h->stream));
+    VS_HIP(hipStreamSynchronize(h->stream));
     return 0;
 }
 

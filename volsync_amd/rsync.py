@@ -182,6 +182,18 @@ class Matcher:
         check(lib.vs_rsync_file_sum(self._h, ctypes.c_void_p(dev_src), length, csum_type, out))
         return out.raw[: 16 if csum_type in (CSUM_MD5, CSUM_XXH3_128) else 8]
 
+    def reconstruct(self, dev_out: int, out_len: int, dev_basis: int, basis_len: int,
+                    blength: int, matches: List[Tuple[int, int]], dev_literals: int,
+                    literal_len: int) -> None:
+        """receiver.c receive_data (vs_rsync_reconstruct): rebuild the file from
+        the basis, the match list and the gaps' literal bytes."""
+        arr = (VsMatch * max(len(matches), 1))()
+        for k, (o, i) in enumerate(matches):
+            arr[k].offset, arr[k].block_index = o, i
+        check(lib.vs_rsync_reconstruct(self._h, ctypes.c_void_p(dev_out), out_len,
+                                       ctypes.c_void_p(dev_basis), basis_len, blength, arr,
+                                       len(matches), ctypes.c_void_p(dev_literals), literal_len))
+
     def match_sums(self, dev_src: int, length: int) -> List[Tuple[int, int]]:
         return self.matches(0, self.match_device(dev_src, length))
 
