@@ -326,6 +326,36 @@ typedef struct vs_sigtable {
 int vs_rsync_match(int device, const void *src, int64_t len, const vs_sigtable *t,
                    int csum_type, uint32_t seed, vs_match *out, size_t cap, size_t *n_out);
 
+/* ---- wire formats (host code, no device needed) -------
+ * rsync 3.2.3 io.c write_sum_head + generate_and_send_sums: count, blength,
+ * s2length, remainder (4-byte LE each), then per block sum1 (4-byte LE) and
+ * s2length bytes of sum2.  out == NULL: *n_out = the size only. */
+int vs_rsync_write_sums(int32_t count, int32_t blength, int32_t s2length, int32_t remainder,
+                        const uint32_t *sum1, const uint8_t *sum2, uint8_t *out, size_t cap,
+                        size_t *n_out);
+/* read_sum_head + the per-block sums (sum1 / sum2 NULL: the header only). */
+int vs_rsync_read_sums(const uint8_t *in, size_t n, int32_t *count, int32_t *blength,
+                       int32_t *s2length, int32_t *remainder, uint32_t *sum1, uint8_t *sum2,
+                       size_t cap_blocks);
+/* token.c simple_send_token as match.c matched() drives it (no -z): literal
+ * runs in <= 32 KiB pieces, each after its 4-byte LE length, the token
+ * -(i+1) per match of block i, and 0 after the file's last literal.  src is
+ * the source file (host).  out == NULL: *n_out = the size only. */
+int vs_rsync_write_tokens(const vs_match *matches, int64_t n_matches, int64_t file_len,
+                          int32_t blength, int64_t basis_len, const uint8_t *src, uint8_t *out,
+                          size_t cap, size_t *n_out);
+/* receiver.c's side: the match list (offsets in the new file) and the literal
+ * bytes, concatenated, of a token stream; matches / literals may be NULL to
+ * size them first. */
+int vs_rsync_read_tokens(const uint8_t *in, size_t n, int32_t blength, int64_t basis_len,
+                         vs_match *matches, size_t cap, size_t *n_matches, uint8_t *literals,
+                         size_t lit_cap, size_t *n_literal, int64_t *file_len);
+/* restic v0.13.1 internal/pack header plaintext: per blob its type (0 data,
+ * 1 tree), the length of its encrypted form (4-byte LE) and its 32-byte ID,
+ * 37 bytes per entry.  out == NULL: *n_out = the size only. */
+int vs_restic_pack_header(const uint8_t *types, const uint32_t *lengths, const uint8_t *ids,
+                          size_t n, uint8_t *out, size_t cap, size_t *n_out);
+
 /* ---- device utilities for benches and tests --------------------------- */
 /* Fill dev_out[0:n] with bytes [off, off+n) of the synthetic splitmix64
  * volume stream.  hip_stream NULL: returns when the fill is

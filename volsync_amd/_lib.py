@@ -97,6 +97,16 @@ def _load() -> ctypes.CDLL:
         "vs_blob_verify": (c_int, [vp, vp, vp, vp, c_size, vp, vp, ctypes.POINTER(c_u64), vp]),
         "vs_rsync_reconstruct": (c_int, [vp, vp, ctypes.c_int64, vp, ctypes.c_int64, ctypes.c_int32,
                                          ctypes.POINTER(VsMatch), ctypes.c_int64, vp, ctypes.c_int64]),
+        "vs_rsync_write_sums": (c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                        vp, vp, vp, c_size, ctypes.POINTER(c_size)]),
+        "vs_rsync_read_sums": (c_int, [vp, c_size, i32p, i32p, i32p, i32p, vp, vp, c_size]),
+        "vs_rsync_write_tokens": (c_int, [ctypes.POINTER(VsMatch), ctypes.c_int64, ctypes.c_int64,
+                                          ctypes.c_int32, ctypes.c_int64, vp, vp, c_size,
+                                          ctypes.POINTER(c_size)]),
+        "vs_rsync_read_tokens": (c_int, [vp, c_size, ctypes.c_int32, ctypes.c_int64,
+                                         ctypes.POINTER(VsMatch), c_size, ctypes.POINTER(c_size), vp,
+                                         c_size, ctypes.POINTER(c_size), i64p]),
+        "vs_restic_pack_header": (c_int, [vp, vp, vp, c_size, vp, c_size, ctypes.POINTER(c_size)]),
         "vs_cdc_set_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_slice": (c_int, [vp, c_u32]),
