@@ -326,6 +326,24 @@ typedef struct vs_sigtable {
 int vs_rsync_match(int device, const void *src, int64_t len, const vs_sigtable *t,
                    int csum_type, uint32_t seed, vs_match *out, size_t cap, size_t *n_out);
 
+/* ---- restic blob encryption (the pack stage) -----------
+ * restic v0.13.1 internal/crypto Key.Seal per blob: ciphertext =
+ * AES-256-CTR(enc_key, IV = the blob's 16-byte nonce, the whole block
+ * incremented as a 128-bit big-endian counter), mac = Poly1305(ciphertext,
+ * r = mac_r (clamped), s = AES-128(mac_k, nonce)).  The repository stores
+ * nonce || ciphertext || mac.  A vs_seal handle holds one repository key. */
+typedef struct vs_seal vs_seal;
+int vs_seal_open(int device, const uint8_t enc_key[32], const uint8_t mac_k[16],
+                 const uint8_t mac_r[16], vs_seal **h);
+/* Blob i = dev_in[off[i] : off[i]+len[i]] (device arrays); its ciphertext is
+ * written to dev_out at the same offset (dev_out may equal dev_in) and its
+ * mac to dev_macs[16*i]; nonces: device array of n*16 bytes.  Queued on
+ * hip_stream after a short read-back of the block count. */
+int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *dev_off,
+                       const uint32_t *dev_len, size_t n, const uint8_t *dev_nonces,
+                       uint8_t *dev_out, uint8_t *dev_macs, void *hip_stream);
+void vs_seal_close(vs_seal *h);
+
 /* ---- wire formats (host code, no device needed) -------
  * rsync 3.2.3 io.c write_sum_head + generate_and_send_sums: count, blength,
  * s2length, remainder (4-byte LE each), then per block sum1 (4-byte LE) and

@@ -1,0 +1,98 @@
+"""CPU restatement of restic's blob encryption -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/ may import this module; the product path never does.
+
+restic v0.13.1 internal/crypto/crypto.go (fetched at image build time by
+mover-restic/Dockerfile; not present under /root/reference):
+
+  Key.Seal(dst, nonce, plaintext, nil):
+    ciphertext = AES-256-CTR(EncryptionKey, IV = nonce)(plaintext)
+      (Go cipher.NewCTR: the 16-byte IV is the initial counter block and the
+      whole block is incremented as a 128-bit big-endian integer)
+    mac = poly1305MAC(ciphertext, nonce, MACKey)
+        = Poly1305(ciphertext, key = MACKey.R || AES-128(MACKey.K, nonce))
+    returns ciphertext || mac
+  The repository stores nonce || ciphertext || mac per blob
+  (internal/repository saveAndEncrypt).
+
+AES comes from the system OpenSSL libcrypto (EVP aes-256-ctr / aes-128-ecb,
+loaded with ctypes); Poly1305 is restated here with Python integers from RFC
+8439 section 2.5.  Both are pinned by their standards' vectors in
+tests/test_seal_oracle.py (FIPS-197 C.1/C.3, RFC 8439 2.5.2).
+"""
+from __future__ import annotations
+
+import ctypes
+
+_lib = None
+
+
+def _crypto():
+    global _lib
+    if _lib is None:
+        _lib = ctypes.CDLL("libcrypto.so.3")
+        for f in ("EVP_CIPHER_CTX_new", "EVP_aes_256_ctr", "EVP_aes_128_ecb", "EVP_aes_256_ecb"):
+            getattr(_lib, f).restype = ctypes.c_void_p
+        _lib.EVP_CIPHER_CTX_free.argtypes = [ctypes.c_void_p]
+        _lib.EVP_EncryptInit_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_char_p, ctypes.c_char_p]
+        _lib.EVP_EncryptUpdate.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.POINTER(ctypes.c_int), ctypes.c_char_p,
+                                           ctypes.c_int]
+        _lib.EVP_CIPHER_CTX_set_padding.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    return _lib
+
+
+def _evp(cipher: str, key: bytes, iv, data: bytes) -> bytes:
+    c = _crypto()
+    ctx = c.EVP_CIPHER_CTX_new()
+    try:
+        ok = c.EVP_EncryptInit_ex(ctx, getattr(c, cipher)(), None, key, iv)
+        assert ok == 1
+        c.EVP_CIPHER_CTX_set_padding(ctx, 0)
+        out = ctypes.create_string_buffer(len(data) + 32)
+        n = ctypes.c_int(0)
+        total = 0
+        # EVP_EncryptUpdate takes an int length: feed in pieces
+        for o in range(0, len(data), 1 << 30):
+            piece = data[o:o + (1 << 30)]
+            ok = c.EVP_EncryptUpdate(ctx, ctypes.addressof(out) + total, ctypes.byref(n), piece,
+                                     len(piece))
+            assert ok == 1
+            total += n.value
+        return out.raw[:total]
+    finally:
+        c.EVP_CIPHER_CTX_free(ctx)
+
+
+def aes256_ctr(key: bytes, iv: bytes, data: bytes) -> bytes:
+    return _evp("EVP_aes_256_ctr", key, iv, data)
+
+
+def aes128_block(key: bytes, block: bytes) -> bytes:
+    return _evp("EVP_aes_128_ecb", key, None, block)
+
+
+def aes256_block(key: bytes, block: bytes) -> bytes:
+    return _evp("EVP_aes_256_ecb", key, None, block)
+
+
+P1305 = (1 << 130) - 5
+
+
+def poly1305(msg: bytes, key: bytes) -> bytes:
+    """RFC 8439 2.5.1: r = clamp(key[0:16]), s = key[16:32]."""
+    r = int.from_bytes(key[:16], "little") & 0x0ffffffc0ffffffc0ffffffc0fffffff
+    s = int.from_bytes(key[16:32], "little")
+    acc = 0
+    for i in range(0, len(msg), 16):
+        blk = msg[i:i + 16] + b"\x01"
+        acc = (acc + int.from_bytes(blk, "little")) * r % P1305
+    return ((acc + s) % (1 << 128)).to_bytes(16, "little")
+
+
+def seal(enc_key: bytes, mac_k: bytes, mac_r: bytes, nonce: bytes, plaintext: bytes):
+    """(ciphertext, mac) of restic's Key.Seal."""
+    ct = aes256_ctr(enc_key, nonce, plaintext)
+    mac = poly1305(ct, mac_r + aes128_block(mac_k, nonce))
+    return ct, mac

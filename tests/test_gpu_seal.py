@@ -1,0 +1,112 @@
+"""restic Key.Seal on the device vs oracle/seal_ref.py.
+
+vs_seal_run_device encrypts every blob with AES-256-CTR under its own nonce
+and computes its Poly1305-AES tag; the oracle is libcrypto AES + the RFC 8439
+Poly1305 restatement, pinned by the standards' vectors in
+test_seal_oracle.py.  Bit-exact comparisons on ciphertext and tags.
+"""
+import numpy as np
+import pytest
+
+from oracle import seal_ref as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _keys(seed):
+    rng = np.random.default_rng(seed)
+    return tuple(rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (32, 16, 16))
+
+
+def _run(keys, data: np.ndarray, offs, lens, nonces: np.ndarray, in_place=False):
+    import torch
+    from volsync_amd import Sealer
+    d = torch.from_numpy(data.copy()).cuda()
+    out = d if in_place else torch.zeros_like(d)
+    do = torch.from_numpy(np.asarray(offs, np.uint64).view(np.int64)).cuda()
+    dl = torch.from_numpy(np.asarray(lens, np.uint32).view(np.int32)).cuda()
+    dn = torch.from_numpy(nonces.reshape(-1).copy()).cuda()
+    n = len(lens)
+    macs = torch.zeros(max(n, 1) * 16, dtype=torch.uint8, device="cuda")
+    s = Sealer(*keys)
+    s.run(d.data_ptr(), do.data_ptr(), dl.data_ptr(), n, dn.data_ptr(), out.data_ptr(),
+          macs.data_ptr())
+    torch.cuda.synchronize()
+    s.close()
+    return out.cpu().numpy(), macs.cpu().numpy()[:16 * n].reshape(n, 16)
+
+
+def _check(keys, data, offs, lens, nonces, ct, macs, which=None):
+    for i in (range(len(lens)) if which is None else which):
+        o, n = int(offs[i]), int(lens[i])
+        want_ct, want_mac = S.seal(*keys, nonces[i].tobytes(), data[o:o + n].tobytes())
+        assert ct[o:o + n].tobytes() == want_ct, (i, n)
+        assert macs[i].tobytes() == want_mac, (i, n)
+
+
+def test_seal_edge_lengths_and_counter_carries(gpu):
+    keys = _keys(1)
+    lens = [0, 1, 15, 16, 17, 31, 32, 33, 1000, 1023, 1024, 1025, 1039, 1040, 1041, 4096,
+            (1 << 20) + 7, 1 << 20, 5]
+    rng = np.random.default_rng(2)
+    # odd gaps between blobs: unaligned blob offsets
+    offs, pos = [], 3
+    for n in lens:
+        offs.append(pos)
+        pos += n + int(rng.integers(0, 40))
+    data = rng.integers(0, 256, pos + 16, dtype=np.uint8)
+    nonces = rng.integers(0, 256, (len(lens), 16), dtype=np.uint8)
+    nonces[16] = np.frombuffer(b"\xff" * 15 + b"\xf0", np.uint8)             # 128-bit wrap
+    nonces[17] = np.frombuffer(bytes(4) + b"\x00\x00\x00\x07" + b"\xff" * 8, np.uint8)  # 64-bit carry
+    nonces[12] = np.frombuffer(b"\x12" * 8 + b"\x00\x00\x00\x00\xff\xff\xff\xfa", np.uint8)  # 32-bit carry
+    ct, macs = _run(keys, data, offs, lens, nonces)
+    _check(keys, data, offs, lens, nonces, ct, macs)
+    # bytes outside the blobs are untouched (zero in the separate output)
+    mask = np.ones(len(data), bool)
+    for o, n in zip(offs, lens):
+        mask[o:o + n] = False
+    assert not ct[mask].any()
+
+
+def test_seal_many_blobs_in_place(gpu):
+    keys = _keys(3)
+    rng = np.random.default_rng(4)
+    lens = rng.integers(0, 9000, 4000)
+    lens[::97] = 0
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    data = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
+    nonces = rng.integers(0, 256, (len(lens), 16), dtype=np.uint8)
+    ct, macs = _run(keys, data, offs, lens, nonces, in_place=True)
+    _check(keys, data, offs, lens, nonces, ct, macs)
+
+
+def test_seal_restic_sized_blobs(gpu):
+    """restic chunker sizes (512 KiB .. 8 MiB): many waves per blob's CTR
+    stream, one wave per blob's tag; a sample of blobs checked in full."""
+    keys = _keys(5)
+    rng = np.random.default_rng(6)
+    lens = rng.integers(512 << 10, 8 << 20, 48)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    data = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    nonces = rng.integers(0, 256, (len(lens), 16), dtype=np.uint8)
+    ct, macs = _run(keys, data, offs, lens, nonces)
+    _check(keys, data, offs, lens, nonces, ct, macs, which=[0, 1, 23, 46, 47])
+    # every blob's ciphertext: CTR is AES(counter) XOR data, so XORing the
+    # plaintext back out must give libcrypto's keystream for the nonce
+    for i in range(0, 48, 7):
+        o, n = int(offs[i]), int(lens[i])
+        ks = S.aes256_ctr(keys[0], nonces[i].tobytes(), bytes(n))
+        assert (np.frombuffer(ks, np.uint8) ^ data[o:o + n] == ct[o:o + n]).all(), i
+
+
+def test_seal_key_clamping(gpu):
+    """MACKey.R with every bit set: the clamp (RFC 8439; restic's mask) must
+    be applied by the handle, not assumed of the caller."""
+    keys = (bytes(range(32)), bytes(range(16, 32)), b"\xff" * 16)
+    rng = np.random.default_rng(7)
+    lens = [0, 16, 100, 70000]
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    data = np.full(int(sum(lens)) + 16, 0xFF, np.uint8)
+    nonces = rng.integers(0, 256, (len(lens), 16), dtype=np.uint8)
+    ct, macs = _run(keys, data, offs, lens, nonces)
+    _check(keys, data, offs, lens, nonces, ct, macs)

@@ -107,6 +107,10 @@ def _load() -> ctypes.CDLL:
                                          ctypes.POINTER(VsMatch), c_size, ctypes.POINTER(c_size), vp,
                                          c_size, ctypes.POINTER(c_size), i64p]),
         "vs_restic_pack_header": (c_int, [vp, vp, vp, c_size, vp, c_size, ctypes.POINTER(c_size)]),
+        "vs_seal_open": (c_int, [c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                 ctypes.POINTER(vp)]),
+        "vs_seal_run_device": (c_int, [vp, vp, vp, vp, c_size, vp, vp, vp, vp]),
+        "vs_seal_close": (None, [vp]),
         "vs_cdc_set_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_slice": (c_int, [vp, c_u32]),

@@ -35,7 +35,7 @@ TestPol = 0x3DA3358B4DC173  # chunker_test.go testPol
 
 __all__ = ["Chunk", "Chunker", "EOF", "New", "NewWithBoundaries", "Pol", "DeviceChunker",
            "DeviceSha256",
-           "MinSize", "MaxSize", "KiB", "MiB", "syncthing_block_size"]
+           "MinSize", "MaxSize", "KiB", "MiB", "syncthing_block_size", "Sealer"]
 
 
 class EOF(EOFError):
@@ -352,6 +352,35 @@ class DeviceSha256:
     def close(self) -> None:
         if self._h:
             lib.vs_sha256_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Sealer:
+    """restic Key.Seal over many device-resident blobs (vs_seal_*): AES-256-CTR
+    + Poly1305-AES with one repository key."""
+
+    def __init__(self, enc_key: bytes, mac_k: bytes, mac_r: bytes, device: int = 0):
+        if len(enc_key) != 32 or len(mac_k) != 16 or len(mac_r) != 16:
+            raise ValueError("enc_key 32 bytes, mac_k and mac_r 16 bytes")
+        self._h = ctypes.c_void_p()
+        check(lib.vs_seal_open(device, enc_key, mac_k, mac_r, ctypes.byref(self._h)))
+
+    def run(self, dev_in: int, dev_off: int, dev_len: int, n: int, dev_nonces: int, dev_out: int,
+            dev_macs: int, stream: Optional[int] = None) -> None:
+        check(lib.vs_seal_run_device(self._h, ctypes.c_void_p(dev_in), ctypes.c_void_p(dev_off),
+                                     ctypes.c_void_p(dev_len), n, ctypes.c_void_p(dev_nonces),
+                                     ctypes.c_void_p(dev_out), ctypes.c_void_p(dev_macs),
+                                     ctypes.c_void_p(stream or None)))
+
+    def close(self) -> None:
+        if self._h:
+            lib.vs_seal_close(self._h)
             self._h = ctypes.c_void_p()
 
     def __del__(self):

@@ -1,0 +1,542 @@
+// crypto.hip -- restic's blob encryption on the device (the
+// pack stage after the blob ID: mover-restic/entry.sh:60-65).
+//
+// restic v0.13.1 internal/crypto Key.Seal(dst, nonce, plaintext, nil):
+//   ciphertext = AES-256-CTR(EncryptionKey, IV = nonce)(plaintext), the IV
+//     incremented as one 128-bit big-endian counter per 16-byte block
+//     (Go cipher.NewCTR);
+//   mac = Poly1305(ciphertext, r = MACKey.R, s = AES-128(MACKey.K, nonce)).
+// The repository stores nonce || ciphertext || mac per blob.
+//
+// seal_ctr_kernel: AES-256 counter blocks with a T-table in LDS (one 1 KiB
+//   table, rotations for the other three, 32 lane-private copies so a
+//   ds_read_b32 from 32 lanes never conflicts), XORed into the bytes; lane l
+//   of a wave takes blocks base + 64 j + l, so every load / store is a
+//   coalesced 1 KiB per wave.
+// seal_mac_kernel: one wave per blob.  Poly1305 is h = sum_i m_i r^(N-i+1)
+//   mod 2^130 - 5; lane j Horner-evaluates blocks j+1, j+65, ... with r^64
+//   and the lanes' sums are lifted by r^e_j (e_j = N - last_j + 1 <= 64) and
+//   added -- r is the repository's key, so r^1..r^64 are computed once per
+//   handle.  130-bit arithmetic in five 26-bit limbs (v_mad_u64_u32).
+#include <cstring>
+#include <vector>
+
+#include <hipcub/hipcub.hpp>
+
+#include "internal.hpp"
+
+#define VS_API extern "C" __attribute__((visibility("default")))
+
+namespace vsgpu {
+namespace {
+
+constexpr uint32_t kCopies = 32;   // lane-private copies of Te0 in LDS
+
+__device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
+__device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+__device__ __forceinline__ uint32_t rotl24(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 8); }
+
+// AES encryption of one block held as four little-endian column words, with
+// round keys rk[4 * (nr + 1)] (LE column words) and the LDS T-table te
+// (entry e of copy c at e * kCopies + c)
+__device__ __forceinline__ void aes_encrypt(uint32_t (&s)[4], const uint32_t *rk, int nr,
+                                            const uint32_t *te, uint32_t c) {
+    uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
+#define TE(x) te[((x) & 0xffu) * kCopies + c]
+    for (int r = 1; r < nr; ++r) {
+        const uint32_t *k = rk + 4 * r;
+        const uint32_t t0 = TE(s0) ^ rotl8(TE(s1 >> 8)) ^ rotl16(TE(s2 >> 16)) ^ rotl24(TE(s3 >> 24)) ^ k[0];
+        const uint32_t t1 = TE(s1) ^ rotl8(TE(s2 >> 8)) ^ rotl16(TE(s3 >> 16)) ^ rotl24(TE(s0 >> 24)) ^ k[1];
+        const uint32_t t2 = TE(s2) ^ rotl8(TE(s3 >> 8)) ^ rotl16(TE(s0 >> 16)) ^ rotl24(TE(s1 >> 24)) ^ k[2];
+        const uint32_t t3 = TE(s3) ^ rotl8(TE(s0 >> 8)) ^ rotl16(TE(s1 >> 16)) ^ rotl24(TE(s2 >> 24)) ^ k[3];
+        s0 = t0;
+        s1 = t1;
+        s2 = t2;
+        s3 = t3;
+    }
+    // last round: SubBytes + ShiftRows + AddRoundKey; S[x] is byte 1 of Te0[x]
+#define SB(x) ((TE(x) >> 8) & 0xffu)
+    const uint32_t *k = rk + 4 * nr;
+    s[0] = (SB(s0) | (SB(s1 >> 8) << 8) | (SB(s2 >> 16) << 16) | (SB(s3 >> 24) << 24)) ^ k[0];
+    s[1] = (SB(s1) | (SB(s2 >> 8) << 8) | (SB(s3 >> 16) << 16) | (SB(s0 >> 24) << 24)) ^ k[1];
+    s[2] = (SB(s2) | (SB(s3 >> 8) << 8) | (SB(s0 >> 16) << 16) | (SB(s1 >> 24) << 24)) ^ k[2];
+    s[3] = (SB(s3) | (SB(s0 >> 8) << 8) | (SB(s1 >> 16) << 16) | (SB(s2 >> 24) << 24)) ^ k[3];
+#undef SB
+#undef TE
+}
+
+// counter block nonce + q (128-bit big-endian) as LE column words
+__device__ __forceinline__ void ctr_block(const uint8_t *nonce, uint64_t q, uint32_t (&s)[4]) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        w[i] = ((uint32_t)nonce[4 * i] << 24) | ((uint32_t)nonce[4 * i + 1] << 16) |
+               ((uint32_t)nonce[4 * i + 2] << 8) | nonce[4 * i + 3];
+    // add q to the 128-bit big-endian value w[0..3] (w[3] least significant)
+    uint64_t acc = (uint64_t)w[3] + (uint32_t)q;
+    w[3] = (uint32_t)acc;
+    acc = (acc >> 32) + (uint64_t)w[2] + (uint32_t)(q >> 32);
+    w[2] = (uint32_t)acc;
+    acc = (acc >> 32) + w[1];
+    w[1] = (uint32_t)acc;
+    w[0] = w[0] + (uint32_t)(acc >> 32);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] = __builtin_bswap32(w[i]);
+}
+
+__device__ __forceinline__ void load_te(uint32_t *te, const uint32_t *g) {
+    for (uint32_t i = threadIdx.x; i < 256 * kCopies; i += blockDim.x) te[i] = g[i / kCopies];
+}
+
+// the blob holding global block g: the last b with prefix[b] <= g
+__device__ __forceinline__ uint64_t find_blob(const uint64_t *prefix, uint64_t n, uint64_t g) {
+    uint64_t lo = 0, hi = n;   // prefix[lo] <= g < prefix[hi]
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (prefix[mid] <= g) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void seal_ctr_kernel(SealArgs a) {
+    __shared__ uint32_t te[256 * kCopies];
+    __shared__ uint32_t rk[60];
+    load_te(te, a.te0);
+    if (threadIdx.x < 60) rk[threadIdx.x] = a.rk256[threadIdx.x];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, c = lane & (kCopies - 1);
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t base = wave * 256; base < a.total_blocks; base += nw * 256) {
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint64_t g0 = base + 64 * j;
+            if (g0 >= a.total_blocks) break;
+            const uint64_t g = g0 + lane;
+            // the blob: uniform when the 64 blocks lie in one blob (the usual case)
+            const uint64_t last = min(g0 + 63, a.total_blocks - 1);
+            const uint64_t b0 = find_blob(a.prefix, a.n, g0);
+            uint64_t b = b0;
+            if (a.prefix[b0 + 1] <= last) b = find_blob(a.prefix, a.n, min(g, a.total_blocks - 1));
+            if (g >= a.total_blocks) continue;
+            const uint64_t q = g - a.prefix[b];
+            const uint64_t off = a.off[b] + 16 * q;
+            const uint32_t len = a.len[b];
+            const uint32_t nb = (uint32_t)min<uint64_t>(16, len - 16 * q);
+            uint32_t s[4];
+            ctr_block(a.nonces + 16 * b, q, s);
+            aes_encrypt(s, rk, 14, te, c);
+            if (nb == 16) {
+                uint4 v;
+                __builtin_memcpy(&v, a.in + off, 16);
+                v.x ^= s[0];
+                v.y ^= s[1];
+                v.z ^= s[2];
+                v.w ^= s[3];
+                __builtin_memcpy(a.out + off, &v, 16);
+            } else {
+                for (uint32_t i = 0; i < nb; ++i)
+                    a.out[off + i] = a.in[off + i] ^ (uint8_t)(s[i >> 2] >> (8 * (i & 3)));
+            }
+        }
+    }
+}
+
+// ---- Poly1305 in five 26-bit limbs ------------------------------------------
+struct L5 {
+    uint32_t v[5];
+};
+constexpr uint32_t kM26 = 0x3ffffff;
+
+// h * r mod 2^130 - 5, h limbs < 2^27, r limbs < 2^26 (s = 5 r)
+__device__ __forceinline__ L5 pmul(const L5 &h, const L5 &r) {
+    const uint32_t s1 = r.v[1] * 5, s2 = r.v[2] * 5, s3 = r.v[3] * 5, s4 = r.v[4] * 5;
+    const uint64_t h0 = h.v[0], h1 = h.v[1], h2 = h.v[2], h3 = h.v[3], h4 = h.v[4];
+    uint64_t d0 = h0 * r.v[0] + h1 * s4 + h2 * s3 + h3 * s2 + h4 * s1;
+    uint64_t d1 = h0 * r.v[1] + h1 * r.v[0] + h2 * s4 + h3 * s3 + h4 * s2;
+    uint64_t d2 = h0 * r.v[2] + h1 * r.v[1] + h2 * r.v[0] + h3 * s4 + h4 * s3;
+    uint64_t d3 = h0 * r.v[3] + h1 * r.v[2] + h2 * r.v[1] + h3 * r.v[0] + h4 * s4;
+    uint64_t d4 = h0 * r.v[4] + h1 * r.v[3] + h2 * r.v[2] + h3 * r.v[1] + h4 * r.v[0];
+    L5 o;
+    d1 += d0 >> 26;
+    o.v[0] = (uint32_t)d0 & kM26;
+    d2 += d1 >> 26;
+    o.v[1] = (uint32_t)d1 & kM26;
+    d3 += d2 >> 26;
+    o.v[2] = (uint32_t)d2 & kM26;
+    d4 += d3 >> 26;
+    o.v[3] = (uint32_t)d3 & kM26;
+    const uint64_t c = d4 >> 26;
+    o.v[4] = (uint32_t)d4 & kM26;
+    const uint64_t t = (uint64_t)o.v[0] + c * 5;
+    o.v[0] = (uint32_t)t & kM26;
+    o.v[1] += (uint32_t)(t >> 26);
+    return o;
+}
+
+// 16 message bytes (n < 16: the partial final block, 0x01 appended)
+__device__ __forceinline__ void absorb(L5 &h, const uint8_t *p, uint32_t n) {
+    uint32_t t[4] = {0, 0, 0, 0};
+    uint32_t hib = 1u << 24;
+    if (n == 16) {
+        __builtin_memcpy(t, p, 16);
+    } else {
+        uint8_t b[16] = {0};
+        for (uint32_t i = 0; i < n; ++i) b[i] = p[i];
+        b[n] = 1;
+        __builtin_memcpy(t, b, 16);
+        hib = 0;
+    }
+    h.v[0] += t[0] & kM26;
+    h.v[1] += ((t[0] >> 26) | (t[1] << 6)) & kM26;
+    h.v[2] += ((t[1] >> 20) | (t[2] << 12)) & kM26;
+    h.v[3] += ((t[2] >> 14) | (t[3] << 18)) & kM26;
+    h.v[4] += (t[3] >> 8) | hib;
+}
+
+__device__ __forceinline__ uint64_t wsum64(uint64_t v) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+        v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(256) void seal_mac_kernel(SealArgs a) {
+    __shared__ uint32_t te[256 * kCopies];
+    __shared__ uint32_t rk[44];
+    load_te(te, a.te0);
+    if (threadIdx.x < 44) rk[threadIdx.x] = a.rk128[threadIdx.x];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, c = lane & (kCopies - 1);
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    L5 R64, Re;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) R64.v[i] = a.rpow[63 * 5 + i];
+    for (uint64_t b = wave; b < a.n; b += nw) {
+        const uint8_t *ct = a.out + a.off[b];
+        const uint32_t len = a.len[b];
+        const uint32_t N = (len + 15) / 16;
+        L5 h{{0, 0, 0, 0, 0}};
+        uint32_t last = 0;
+        for (uint32_t i = lane; i < N; i += 64) {
+            h = pmul(h, R64);
+            absorb(h, ct + 16 * (uint64_t)i, min(16u, len - 16 * i));
+            last = i + 1;   // 1-based index of this lane's last block
+        }
+        // lift by r^(N - last + 1) (1..64) and add the lanes
+        uint64_t sumv[5] = {0, 0, 0, 0, 0};
+        if (last) {
+            const uint32_t e = N - last + 1;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) Re.v[i] = a.rpow[(e - 1) * 5 + i];
+            const L5 t = pmul(h, Re);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) sumv[i] = t.v[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) sumv[i] = wsum64(sumv[i]);
+        // s = AES-128(MACKey.K, nonce): every lane computes it (uniform)
+        uint32_t s[4];
+        {
+            const uint8_t *nn = a.nonces + 16 * b;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                s[i] = (uint32_t)nn[4 * i] | ((uint32_t)nn[4 * i + 1] << 8) |
+                       ((uint32_t)nn[4 * i + 2] << 16) | ((uint32_t)nn[4 * i + 3] << 24);
+            aes_encrypt(s, rk, 10, te, c);
+        }
+        if (lane == 0) {
+            // carry the lane sums into limbs, reduce mod 2^130 - 5
+            uint64_t d[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) d[i] = sumv[i];
+            for (int pass = 0; pass < 2; ++pass) {
+                for (int i = 0; i < 4; ++i) {
+                    d[i + 1] += d[i] >> 26;
+                    d[i] &= kM26;
+                }
+                d[0] += (d[4] >> 26) * 5;
+                d[4] &= kM26;
+            }
+            d[1] += d[0] >> 26;
+            d[0] &= kM26;
+            uint32_t h0 = (uint32_t)d[0], h1 = (uint32_t)d[1], h2 = (uint32_t)d[2],
+                     h3 = (uint32_t)d[3], h4 = (uint32_t)d[4];
+            // h - p = h + 5 - 2^130: keep it when it does not borrow
+            uint32_t g0 = h0 + 5, cc = g0 >> 26;
+            g0 &= kM26;
+            uint32_t g1 = h1 + cc;
+            cc = g1 >> 26;
+            g1 &= kM26;
+            uint32_t g2 = h2 + cc;
+            cc = g2 >> 26;
+            g2 &= kM26;
+            uint32_t g3 = h3 + cc;
+            cc = g3 >> 26;
+            g3 &= kM26;
+            const uint32_t g4 = h4 + cc - (1u << 26);
+            if ((g4 >> 31) == 0) {
+                h0 = g0;
+                h1 = g1;
+                h2 = g2;
+                h3 = g3;
+                h4 = g4;
+            }
+            // (h + s) mod 2^128, packing the limbs by addition so a limb
+            // that is not fully normalised (h1 = 2^26) still lands right
+            uint64_t f = (uint64_t)h0 + ((uint64_t)h1 << 26) + s[0];
+            uint32_t o[4];
+            o[0] = (uint32_t)f;
+            f = (f >> 32) + ((uint64_t)h2 << 20) + s[1];
+            o[1] = (uint32_t)f;
+            f = (f >> 32) + ((uint64_t)h3 << 14) + s[2];
+            o[2] = (uint32_t)f;
+            f = (f >> 32) + ((uint64_t)h4 << 8) + s[3];
+            o[3] = (uint32_t)f;
+            uint8_t *mac = a.macs + 16 * b;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) mac[i] = (uint8_t)(o[i >> 2] >> (8 * (i & 3)));
+        }
+    }
+}
+
+// ---- host: tables, key schedules, r powers ----------------------------------
+uint8_t xtime(uint8_t x) { return (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1b : 0)); }
+uint8_t gmul(uint8_t a, uint8_t b) {
+    uint8_t p = 0;
+    while (b) {
+        if (b & 1) p ^= a;
+        a = xtime(a);
+        b >>= 1;
+    }
+    return p;
+}
+void sbox(uint8_t (&S)[256]) {
+    // S[x] = affine(x^-1) over GF(2^8) with the AES polynomial (FIPS-197 5.1.1)
+    for (int x = 0; x < 256; ++x) {
+        uint8_t inv = 0;
+        if (x)
+            for (int y = 1; y < 256; ++y)
+                if (gmul((uint8_t)x, (uint8_t)y) == 1) {
+                    inv = (uint8_t)y;
+                    break;
+                }
+        uint8_t b = inv, r = inv;
+        for (int i = 1; i < 5; ++i) {
+            b = (uint8_t)((b << 1) | (b >> 7));
+            r ^= b;
+        }
+        S[x] = r ^ 0x63;
+    }
+}
+// FIPS-197 5.2 key expansion, round keys as LE column words
+void expand(const uint8_t *key, int nk, const uint8_t (&S)[256], uint32_t *out) {
+    const int nr = nk + 6, total = 4 * (nr + 1);
+    std::vector<uint8_t> w((size_t)total * 4);
+    memcpy(w.data(), key, (size_t)nk * 4);
+    uint8_t rcon = 1;
+    for (int i = nk; i < total; ++i) {
+        uint8_t t[4];
+        memcpy(t, &w[(size_t)(i - 1) * 4], 4);
+        if (i % nk == 0) {
+            const uint8_t t0 = t[0];
+            t[0] = (uint8_t)(S[t[1]] ^ rcon);
+            t[1] = S[t[2]];
+            t[2] = S[t[3]];
+            t[3] = S[t0];
+            rcon = xtime(rcon);
+        } else if (nk > 6 && i % nk == 4) {
+            for (int k = 0; k < 4; ++k) t[k] = S[t[k]];
+        }
+        for (int k = 0; k < 4; ++k) w[(size_t)i * 4 + k] = w[(size_t)(i - nk) * 4 + k] ^ t[k];
+    }
+    for (int i = 0; i < total; ++i)
+        out[i] = (uint32_t)w[4 * i] | ((uint32_t)w[4 * i + 1] << 8) | ((uint32_t)w[4 * i + 2] << 16) |
+                 ((uint32_t)w[4 * i + 3] << 24);
+}
+// 130-bit host arithmetic for the r powers (limbs as the device uses them)
+struct H5 {
+    uint64_t v[5];
+};
+H5 hmul(const H5 &h, const H5 &r) {
+    const uint64_t s1 = r.v[1] * 5, s2 = r.v[2] * 5, s3 = r.v[3] * 5, s4 = r.v[4] * 5;
+    uint64_t d0 = h.v[0] * r.v[0] + h.v[1] * s4 + h.v[2] * s3 + h.v[3] * s2 + h.v[4] * s1;
+    uint64_t d1 = h.v[0] * r.v[1] + h.v[1] * r.v[0] + h.v[2] * s4 + h.v[3] * s3 + h.v[4] * s2;
+    uint64_t d2 = h.v[0] * r.v[2] + h.v[1] * r.v[1] + h.v[2] * r.v[0] + h.v[3] * s4 + h.v[4] * s3;
+    uint64_t d3 = h.v[0] * r.v[3] + h.v[1] * r.v[2] + h.v[2] * r.v[1] + h.v[3] * r.v[0] + h.v[4] * s4;
+    uint64_t d4 = h.v[0] * r.v[4] + h.v[1] * r.v[3] + h.v[2] * r.v[2] + h.v[3] * r.v[1] + h.v[4] * r.v[0];
+    H5 o;
+    d1 += d0 >> 26;
+    o.v[0] = d0 & kM26;
+    d2 += d1 >> 26;
+    o.v[1] = d1 & kM26;
+    d3 += d2 >> 26;
+    o.v[2] = d2 & kM26;
+    d4 += d3 >> 26;
+    o.v[3] = d3 & kM26;
+    o.v[4] = d4 & kM26;
+    o.v[0] += (d4 >> 26) * 5;
+    o.v[1] += o.v[0] >> 26;
+    o.v[0] &= kM26;
+    return o;
+}
+
+}  // namespace
+}  // namespace vsgpu
+
+using namespace vsgpu;
+
+struct vs_seal {
+    int device = 0;
+    int cus = 256;
+    DevBuf te0, rk256, rk128, rpow, prefix, tmp;
+};
+
+VS_API int vs_seal_open(int device, const uint8_t enc_key[32], const uint8_t mac_k[16],
+                        const uint8_t mac_r[16], vs_seal **out) {
+    if (!out || !enc_key || !mac_k || !mac_r) return fail(VS_ERR_ARG, "bad arguments");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        return fail(VS_ERR_NO_DEVICE, "no HIP device available (no CPU fallback)");
+    }
+    if (device < 0 || device >= ndev) return fail(VS_ERR_ARG, "device index out of range");
+    if (hipSetDevice(device) != hipSuccess) return fail(VS_ERR_NO_DEVICE, "hipSetDevice failed");
+    vs_seal *h = new vs_seal();
+    h->device = device;
+    if (hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+        h->cus = 256;
+    uint8_t S[256];
+    sbox(S);
+    uint32_t te[256];
+    for (int x = 0; x < 256; ++x) {
+        const uint8_t s = S[x], s2 = xtime(s), s3 = (uint8_t)(s2 ^ s);
+        te[x] = (uint32_t)s2 | ((uint32_t)s << 8) | ((uint32_t)s << 16) | ((uint32_t)s3 << 24);
+    }
+    uint32_t rk256[60], rk128[44];
+    expand(enc_key, 8, S, rk256);
+    expand(mac_k, 4, S, rk128);
+    // r clamped (RFC 8439; restic masks MACKey.R the same way), then r^1..r^64
+    uint8_t rb[16];
+    memcpy(rb, mac_r, 16);
+    rb[3] &= 15;
+    rb[7] &= 15;
+    rb[11] &= 15;
+    rb[15] &= 15;
+    rb[4] &= 252;
+    rb[8] &= 252;
+    rb[12] &= 252;
+    uint32_t t[4];
+    memcpy(t, rb, 16);
+    H5 r{{t[0] & kM26, ((t[0] >> 26) | (t[1] << 6)) & kM26, ((t[1] >> 20) | (t[2] << 12)) & kM26,
+          ((t[2] >> 14) | (t[3] << 18)) & kM26, (t[3] >> 8)}};
+    std::vector<uint32_t> rp(64 * 5);
+    H5 p = r;
+    for (int k = 0; k < 64; ++k) {
+        for (int i = 0; i < 5; ++i) rp[(size_t)k * 5 + i] = (uint32_t)p.v[i];
+        p = hmul(p, r);
+    }
+    int rc = 0;
+    if ((rc = h->te0.ensure(sizeof te)) < 0 || (rc = h->rk256.ensure(sizeof rk256)) < 0 ||
+        (rc = h->rk128.ensure(sizeof rk128)) < 0 || (rc = h->rpow.ensure(rp.size() * 4)) < 0) {
+        delete h;
+        return rc;
+    }
+    if (hipMemcpy(h->te0.p, te, sizeof te, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->rk256.p, rk256, sizeof rk256, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->rk128.p, rk128, sizeof rk128, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->rpow.p, rp.data(), rp.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipGetLastError();
+        delete h;
+        return fail(VS_ERR_HIP, "uploading the key tables failed");
+    }
+    *out = h;
+    return 0;
+}
+
+VS_API int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *dev_off,
+                              const uint32_t *dev_len, size_t n, const uint8_t *dev_nonces,
+                              uint8_t *dev_out, uint8_t *dev_macs, void *hip_stream) {
+    if (!h || (n && (!dev_in || !dev_off || !dev_len || !dev_nonces || !dev_out || !dev_macs)))
+        return fail(VS_ERR_ARG, "bad arguments");
+    if (!n) return 0;
+    if (hipSetDevice(h->device) != hipSuccess) return fail(VS_ERR_NO_DEVICE, "hipSetDevice failed");
+    const hipStream_t s = (hipStream_t)hip_stream;
+    VS_TRY(h->prefix.ensure((n + 1) * 8));
+    const size_t tb = seal_scan_tmp_bytes(n);
+    VS_TRY(h->tmp.ensure(tb + 16));
+    uint64_t total = 0;
+    VS_HIP(launch_seal_prefix(dev_len, n, h->prefix.as<uint64_t>(), h->tmp.p, tb, &total, s));
+    SealArgs a{};
+    a.in = (const uint8_t *)dev_in;
+    a.out = dev_out;
+    a.off = dev_off;
+    a.len = dev_len;
+    a.n = n;
+    a.nonces = dev_nonces;
+    a.prefix = h->prefix.as<uint64_t>();
+    a.total_blocks = total;
+    a.te0 = h->te0.as<uint32_t>();
+    a.rk256 = h->rk256.as<uint32_t>();
+    a.rk128 = h->rk128.as<uint32_t>();
+    a.rpow = h->rpow.as<uint32_t>();
+    a.macs = dev_macs;
+    VS_HIP(launch_seal(a, h->cus, s));
+    return 0;
+}
+
+VS_API void vs_seal_close(vs_seal *h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipDeviceSynchronize();
+    for (DevBuf *b : {&h->te0, &h->rk256, &h->rk128, &h->rpow, &h->prefix, &h->tmp}) b->release();
+    delete h;
+}
+
+namespace vsgpu {
+
+namespace {
+__global__ void seal_blocks_kernel(const uint32_t *len, uint64_t n, uint64_t *nb) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) nb[i] = (i < n) ? (len[i] + 15u) / 16u : 0;
+}
+}  // namespace
+
+size_t seal_scan_tmp_bytes(uint64_t n) {
+    size_t b = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const uint64_t *)nullptr,
+                                           (uint64_t *)nullptr, (int)(n + 1));
+    return b + (n + 1) * 8 + 64;
+}
+
+// prefix[i] = blocks of blobs [0, i), prefix[n] = *total (read back: waits)
+hipError_t launch_seal_prefix(const uint32_t *len, uint64_t n, uint64_t *prefix, void *tmp,
+                              size_t tmp_bytes, uint64_t *total, hipStream_t s) {
+    uint64_t *nb = (uint64_t *)tmp;
+    void *scratch = (uint8_t *)tmp + (n + 1) * 8 + 64;
+    size_t sb = tmp_bytes - (n + 1) * 8 - 64;
+    seal_blocks_kernel<<<(uint32_t)((n + 1 + 255) / 256), 256, 0, s>>>(len, n, nb);
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(scratch, sb, nb, prefix, (int)(n + 1), s);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(total, prefix + n, 8, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(s);
+}
+
+hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s) {
+    if (a.total_blocks) {
+        const uint64_t waves = (a.total_blocks + 255) / 256;
+        const uint64_t grid = std::min<uint64_t>((waves + 3) / 4, (uint64_t)std::max(cus, 1) * 20);
+        seal_ctr_kernel<<<(uint32_t)grid, 256, 0, s>>>(a);
+    }
+    const uint64_t mg = std::min<uint64_t>((a.n + 3) / 4, (uint64_t)std::max(cus, 1) * 8);
+    seal_mac_kernel<<<(uint32_t)std::max<uint64_t>(mg, 1), 256, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+}  // namespace vsgpu

@@ -350,6 +350,26 @@ hipError_t launch_rs_pad_sum2(const uint8_t *sum2, uint32_t count, uint32_t s2le
 size_t filesum_scratch_bytes(uint64_t len, uint64_t piece_blocks);
 hipError_t launch_filesum(const uint8_t *p, uint64_t len, int csum_type, void *scratch,
                           uint64_t piece_blocks, uint8_t *out, hipStream_t s);
+// restic Key.Seal (crypto.hip)
+struct SealArgs {
+    const uint8_t *in;
+    uint8_t *out;               // ciphertext at the same offsets
+    const uint64_t *off;
+    const uint32_t *len;
+    uint64_t n;
+    const uint8_t *nonces;      // [n][16]
+    const uint64_t *prefix;     // [n + 1] exclusive prefix of 16-byte blocks per blob
+    uint64_t total_blocks;
+    const uint32_t *te0;        // [256] AES T-table (LE column words)
+    const uint32_t *rk256;      // [60] AES-256 round keys (EncryptionKey)
+    const uint32_t *rk128;      // [44] AES-128 round keys (MACKey.K)
+    const uint32_t *rpow;       // [64][5] r^1..r^64 in 26-bit limbs (MACKey.R clamped)
+    uint8_t *macs;              // [n][16]
+};
+size_t seal_scan_tmp_bytes(uint64_t n);
+hipError_t launch_seal_prefix(const uint32_t *len, uint64_t n, uint64_t *prefix, void *tmp,
+                              size_t tmp_bytes, uint64_t *total, hipStream_t s);
+hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s);
 // adjacent-mover kernels (movers.hip)
 struct ReconPiece {
     uint64_t dst, src, len;
