@@ -466,6 +466,141 @@ def smallfiles_main(args):
         dist.destroy_process_group()
 
 
+def seal_cpu_baseline(sizes, keys, sample_bytes: int, threads: int):
+    """restic's Key.Seal on the host: libcrypto AES-256-CTR (AES-NI) + Poly1305
+    (oracle/seal_ref.seal_into, no copies) per blob over `threads` threads, on
+    the first blobs of the same size distribution up to `sample_bytes`."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
+    from oracle import seal_ref as S
+    cum = np.cumsum(sizes)
+    nb = max(1, int(np.searchsorted(cum, sample_bytes)))
+    sz = sizes[:nb]
+    src = np.random.default_rng(8).integers(0, 256, int(sz.max()), dtype=np.uint8)
+    dst = [np.empty(int(sz.max()), np.uint8) for _ in range(threads)]
+    nonces = np.random.default_rng(9).integers(0, 256, (nb, 16), dtype=np.uint8)
+
+    def work(t):
+        d = dst[t].ctypes.data
+        for k in range(t, nb, threads):
+            S.seal_into(*keys, nonces[k].tobytes(), src.ctypes.data, int(sz[k]), d)
+    S.seal_into(*keys, bytes(16), src.ctypes.data, 16, dst[0].ctypes.data)   # load libcrypto
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(work, range(threads)))
+    dt = time.perf_counter() - t0
+    return {"value": round(float(sz.sum()) / dt / 1e9, 3), "unit": "GB/s", "cores": threads,
+            "kind": "port", "sample": f"{nb} blobs ({float(sz.sum()) / 2**30:.2f} GiB) of the same "
+            f"size distribution, libcrypto AES-256-CTR + Poly1305 on {threads} threads",
+            "cpu": _cpu_model()}
+
+
+def seal_main(args):
+    """SURVEY.md 8(f)1, restic's pack stage: every unique blob of a backup is
+    encrypted with Key.Seal (AES-256-CTR under its own random nonce +
+    Poly1305-AES tag) before it is written to a pack.  The workload is one
+    volume's worth of blobs (--per-gpu-gib, default 64 GiB) with restic's chunk
+    size distribution (512 KiB + exponential mean 1 MiB, capped at 8 MiB),
+    device-resident; a step seals all of them into a separate output buffer
+    (vs_seal_run_device).  value = plaintext bytes sealed per second.  Ranks
+    are replicas (independent blobs, no collective)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from volsync_amd import Sealer, synth_fill_device
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    target = int(args.per_gpu_gib * (1 << 30))
+    rng = np.random.default_rng(11 + rank)
+    sizes = np.minimum((512 << 10) + rng.exponential(1 << 20, target // (1 << 20) + 16).astype(np.int64),
+                       8 << 20)
+    cum = np.cumsum(sizes)
+    nb = int(np.searchsorted(cum, target, side="right"))
+    sizes = sizes[:nb]
+    offs = np.concatenate([[0], cum[:nb - 1]]).astype(np.int64)
+    total = int(sizes.sum())
+    data = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    synth_fill_device(data.data_ptr(), 12, 0, total + 16, device=local)
+    out = torch.empty_like(data)
+    ofd = torch.from_numpy(offs).to(dev)
+    lens = torch.from_numpy(sizes.astype(np.int32)).to(dev)
+    nonces = torch.from_numpy(rng.integers(0, 256, (nb, 16), dtype=np.uint8)).to(dev)
+    macs = torch.zeros((nb, 16), dtype=torch.uint8, device=dev)
+    keys = tuple(rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (32, 16, 16))
+    sl = Sealer(*keys, device=local)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        sl.run(data.data_ptr(), ofd.data_ptr(), lens.data_ptr(), nb, nonces.data_ptr(),
+               out.data_ptr(), macs.data_ptr(), stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    # spot check: first and last blob against the oracle (libcrypto)
+    from oracle import seal_ref as S
+    for i in (0, nb - 1):
+        o, n = int(offs[i]), int(sizes[i])
+        ct, mac = S.seal(*keys, nonces[i].cpu().numpy().tobytes(), data[o:o + n].cpu().numpy().tobytes())
+        assert out[o:o + n].cpu().numpy().tobytes() == ct and macs[i].cpu().numpy().tobytes() == mac
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    sl.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ctr_ms, mac_ms, runs = sl.kernel_ms()
+    sl.close()
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ctr_ms, mac_ms = ctr_ms / max(runs, 1), mac_ms / max(runs, 1)
+    # algorithmic HBM bytes: CTR reads + writes every byte (2 B/B), the MAC
+    # re-reads the ciphertext (1 B/B)
+    ctr_gbs, mac_gbs = 2 * total / ctr_ms / 1e6, total / mac_ms / 1e6
+    dom = "ctr" if ctr_ms >= mac_ms else "mac"
+    kern = {"ctr": {"kernel": "seal_ctr_kernel", "avg_launch_ms": round(ctr_ms, 3),
+                    "achieved": round(ctr_gbs, 1), "bytes_per_launch": 2 * total},
+            "mac": {"kernel": "seal_mac_kernel", "avg_launch_ms": round(mac_ms, 3),
+                    "achieved": round(mac_gbs, 1), "bytes_per_launch": total}}
+    if rank == 0:
+        res = {
+            "metric": "GB/s sealed (restic pack stage: AES-256-CTR + Poly1305-AES per blob)",
+            "value": round(total * world * args.steps / dt / 1e9, 2), "unit": "GB/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (splitmix64 plaintext, random keys and nonces, device-resident)",
+            "config": {"workload": f"(f)1: {nb} blobs, {total / 2**30:.1f} GiB, restic chunk sizes"
+                                   f"{' per rank' if world > 1 else ''}",
+                       "bytes": total, "blobs": nb, "parallelism": f"replicas x{world}"},
+            "roofline": {"bound": "hbm", "achieved": kern[dom]["achieved"], "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(kern[dom]["achieved"] / HBM_PEAK_GBS, 4),
+                         "traffic": None, "kernel": kern[dom]["kernel"],
+                         "avg_launch_ms": kern[dom]["avg_launch_ms"]},
+            "kernels": kern,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = seal_cpu_baseline(sizes, keys, 32 << 30,
+                                                    args.cpu_threads)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def _free_port() -> int:
     import socket
     with socket.socket() as s:
@@ -698,7 +833,7 @@ def main():
                          "wavefronts (0 = library default, 0xffffffff = never)")
     ap.add_argument("--wide-drain", type=int, default=0,
                     help="blocks per throughput-mode drain launch (0 = library default)")
-    ap.add_argument("--mode", choices=["cdc", "rsync", "smallfiles", "host"], default="cdc",
+    ap.add_argument("--mode", choices=["cdc", "rsync", "smallfiles", "host", "seal"], default="cdc",
                     help="cdc: C2/C3 chunk+hash (the BASELINE metric); rsync: C4-shape delta "
                          "match; smallfiles: C5 per-file blob IDs; host: C2 streamed from "
                          "pinned host memory through vs_cdc_feed/next")
@@ -716,6 +851,8 @@ def main():
         return rsync_main(args)
     if args.mode == "smallfiles":
         return smallfiles_main(args)
+    if args.mode == "seal":
+        return seal_main(args)
     if args.mode == "host":
         return host_main(args)
 

@@ -342,6 +342,11 @@ int vs_seal_open(int device, const uint8_t enc_key[32], const uint8_t mac_k[16],
 int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *dev_off,
                        const uint32_t *dev_len, size_t n, const uint8_t *dev_nonces,
                        uint8_t *dev_out, uint8_t *dev_macs, void *hip_stream);
+/* Kernel timing for measurement: when on, each run records HIP events around
+ * its CTR and MAC kernels; vs_seal_kernel_ms waits for them and returns the
+ * summed milliseconds (ms[0] CTR, ms[1] MAC) and the run count, then resets. */
+int vs_seal_set_timing(vs_seal *h, int on);
+int vs_seal_kernel_ms(vs_seal *h, double ms[2], int *runs);
 void vs_seal_close(vs_seal *h);
 
 /* ---- wire formats (host code, no device needed) -------

@@ -91,8 +91,61 @@ def poly1305(msg: bytes, key: bytes) -> bytes:
     return ((acc + s) % (1 << 128)).to_bytes(16, "little")
 
 
+def poly1305_evp(msg, key: bytes) -> bytes:
+    """libcrypto's Poly1305 (EVP_MAC "POLY1305"): the CPU-baseline speed path,
+    checked equal to poly1305() in tests/test_seal_oracle.py.  msg: bytes or
+    an address (int) with msg_len given as a (addr, len) tuple."""
+    c = _crypto()
+    if not hasattr(c, "_vs_mac"):
+        c.EVP_MAC_fetch.restype = ctypes.c_void_p
+        c.EVP_MAC_fetch.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p]
+        c.EVP_MAC_CTX_new.restype = ctypes.c_void_p
+        c.EVP_MAC_CTX_new.argtypes = [ctypes.c_void_p]
+        c.EVP_MAC_CTX_free.argtypes = [ctypes.c_void_p]
+        c.EVP_MAC_init.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]
+        c.EVP_MAC_update.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        c.EVP_MAC_final.argtypes = [ctypes.c_void_p, ctypes.c_char_p,
+                                    ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t]
+        c._vs_mac = c.EVP_MAC_fetch(None, b"POLY1305", None)
+        assert c._vs_mac, "libcrypto has no POLY1305 EVP_MAC"
+    ctx = c.EVP_MAC_CTX_new(c._vs_mac)
+    try:
+        assert c.EVP_MAC_init(ctx, key, 32, None) == 1
+        if isinstance(msg, tuple):
+            addr, n = msg
+        else:
+            buf = ctypes.create_string_buffer(msg, max(len(msg), 1))
+            addr, n = ctypes.addressof(buf), len(msg)
+        if n:
+            assert c.EVP_MAC_update(ctx, addr, n) == 1
+        out = ctypes.create_string_buffer(16)
+        ol = ctypes.c_size_t(0)
+        assert c.EVP_MAC_final(ctx, out, ctypes.byref(ol), 16) == 1
+        return out.raw[:16]
+    finally:
+        c.EVP_MAC_CTX_free(ctx)
+
+
 def seal(enc_key: bytes, mac_k: bytes, mac_r: bytes, nonce: bytes, plaintext: bytes):
     """(ciphertext, mac) of restic's Key.Seal."""
     ct = aes256_ctr(enc_key, nonce, plaintext)
     mac = poly1305(ct, mac_r + aes128_block(mac_k, nonce))
     return ct, mac
+
+
+def seal_into(enc_key: bytes, mac_k: bytes, mac_r: bytes, nonce: bytes, src_addr: int, n: int,
+              dst_addr: int) -> bytes:
+    """seal() over raw addresses (libcrypto AES-256-CTR + Poly1305, no copies):
+    the CPU-baseline leg of bench.py --mode seal.  Returns the mac."""
+    c = _crypto()
+    ctx = c.EVP_CIPHER_CTX_new()
+    try:
+        assert c.EVP_EncryptInit_ex(ctx, c.EVP_aes_256_ctr(), None, enc_key, nonce) == 1
+        ol = ctypes.c_int(0)
+        for o in range(0, n, 1 << 30):
+            k = min(1 << 30, n - o)
+            assert c.EVP_EncryptUpdate(ctx, dst_addr + o, ctypes.byref(ol),
+                                       ctypes.c_char_p(src_addr + o), k) == 1
+    finally:
+        c.EVP_CIPHER_CTX_free(ctx)
+    return poly1305_evp((dst_addr, n), mac_r + aes128_block(mac_k, nonce))

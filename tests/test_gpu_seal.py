@@ -110,3 +110,16 @@ def test_seal_key_clamping(gpu):
     nonces = rng.integers(0, 256, (len(lens), 16), dtype=np.uint8)
     ct, macs = _run(keys, data, offs, lens, nonces)
     _check(keys, data, offs, lens, nonces, ct, macs)
+
+
+def test_seal_many_tiny_blobs_multi_tile_prefix(gpu):
+    """More blobs than one prefix tile (16 K): the block prefix carries across
+    tiles and the per-lane blob search spans many tiny blobs per wave."""
+    keys = _keys(8)
+    rng = np.random.default_rng(9)
+    lens = rng.integers(0, 70, 40000)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    data = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
+    nonces = rng.integers(0, 256, (len(lens), 16), dtype=np.uint8)
+    ct, macs = _run(keys, data, offs, lens, nonces)
+    _check(keys, data, offs, lens, nonces, ct, macs)

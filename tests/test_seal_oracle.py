@@ -36,3 +36,25 @@ def test_ctr_counter_carries_across_the_block():
     a = S.aes256_ctr(key, iv, bytes(32))
     assert a[:16] == S.aes256_block(key, iv)
     assert a[16:] == S.aes256_block(key, bytes(16))
+
+
+def test_libcrypto_poly1305_equals_restatement():
+    import os
+    key = bytes.fromhex("85d6be7857556d337f4452fe42d506a80103808afb0db2fd4abff6af4149f51b")
+    assert S.poly1305_evp(b"Cryptographic Forum Research Group", key).hex() == \
+        "a8061dc1305136c6c22b8baf0c0127a9"
+    rnd = os.urandom(5000)
+    for n in (0, 1, 15, 16, 17, 1000, 5000):
+        k = rnd[:32]
+        assert S.poly1305_evp(rnd[:n], k) == S.poly1305(rnd[:n], k), n
+
+
+def test_seal_into_equals_seal():
+    import ctypes
+    import os
+    keys = (os.urandom(32), os.urandom(16), os.urandom(16))
+    nonce, pt = os.urandom(16), os.urandom(3001)
+    src = ctypes.create_string_buffer(pt, len(pt))
+    dst = ctypes.create_string_buffer(len(pt))
+    mac = S.seal_into(*keys, nonce, ctypes.addressof(src), len(pt), ctypes.addressof(dst))
+    assert (dst.raw, mac) == S.seal(*keys, nonce, pt)

@@ -110,6 +110,8 @@ def _load() -> ctypes.CDLL:
         "vs_seal_open": (c_int, [c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                  ctypes.POINTER(vp)]),
         "vs_seal_run_device": (c_int, [vp, vp, vp, vp, c_size, vp, vp, vp, vp]),
+        "vs_seal_set_timing": (c_int, [vp, c_int]),
+        "vs_seal_kernel_ms": (c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int)]),
         "vs_seal_close": (None, [vp]),
         "vs_cdc_set_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_stream": (c_int, [vp, vp]),

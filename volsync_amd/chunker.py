@@ -378,6 +378,16 @@ class Sealer:
                                      ctypes.c_void_p(dev_out), ctypes.c_void_p(dev_macs),
                                      ctypes.c_void_p(stream or None)))
 
+    def set_timing(self, on: bool) -> None:
+        check(lib.vs_seal_set_timing(self._h, int(on)))
+
+    def kernel_ms(self):
+        """(ctr_ms, mac_ms, runs) summed over the timed runs since the last call."""
+        ms = (ctypes.c_double * 2)()
+        runs = ctypes.c_int()
+        check(lib.vs_seal_kernel_ms(self._h, ms, ctypes.byref(runs)))
+        return ms[0], ms[1], runs.value
+
     def close(self) -> None:
         if self._h:
             lib.vs_seal_close(self._h)

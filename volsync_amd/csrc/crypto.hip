@@ -21,8 +21,6 @@
 #include <cstring>
 #include <vector>
 
-#include <hipcub/hipcub.hpp>
-
 #include "internal.hpp"
 
 #define VS_API extern "C" __attribute__((visibility("default")))
@@ -393,7 +391,9 @@ using namespace vsgpu;
 struct vs_seal {
     int device = 0;
     int cus = 256;
-    DevBuf te0, rk256, rk128, rpow, prefix, tmp;
+    DevBuf te0, rk256, rk128, rpow, prefix;
+    bool timing = false;
+    std::vector<hipEvent_t> ev;   // 3 per timed run: before CTR, between, after MAC
 };
 
 VS_API int vs_seal_open(int device, const uint8_t enc_key[32], const uint8_t mac_k[16],
@@ -468,10 +468,8 @@ VS_API int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *de
     if (hipSetDevice(h->device) != hipSuccess) return fail(VS_ERR_NO_DEVICE, "hipSetDevice failed");
     const hipStream_t s = (hipStream_t)hip_stream;
     VS_TRY(h->prefix.ensure((n + 1) * 8));
-    const size_t tb = seal_scan_tmp_bytes(n);
-    VS_TRY(h->tmp.ensure(tb + 16));
     uint64_t total = 0;
-    VS_HIP(launch_seal_prefix(dev_len, n, h->prefix.as<uint64_t>(), h->tmp.p, tb, &total, s));
+    VS_HIP(launch_seal_prefix(dev_len, n, h->prefix.as<uint64_t>(), &total, s));
     SealArgs a{};
     a.in = (const uint8_t *)dev_in;
     a.out = dev_out;
@@ -486,7 +484,35 @@ VS_API int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *de
     a.rk128 = h->rk128.as<uint32_t>();
     a.rpow = h->rpow.as<uint32_t>();
     a.macs = dev_macs;
-    VS_HIP(launch_seal(a, h->cus, s));
+    hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+    if (h->timing) {
+        for (auto &x : e) VS_HIP(hipEventCreate(&x));
+        h->ev.insert(h->ev.end(), e, e + 3);
+    }
+    VS_HIP(launch_seal(a, h->cus, s, e));
+    return 0;
+}
+
+VS_API int vs_seal_set_timing(vs_seal *h, int on) {
+    if (!h) return fail(VS_ERR_ARG, "bad arguments");
+    h->timing = on != 0;
+    return 0;
+}
+
+VS_API int vs_seal_kernel_ms(vs_seal *h, double ms[2], int *runs) {
+    if (!h || !ms || !runs) return fail(VS_ERR_ARG, "bad arguments");
+    ms[0] = ms[1] = 0;
+    *runs = (int)(h->ev.size() / 3);
+    for (size_t i = 0; i + 2 < h->ev.size(); i += 3) {
+        float a = 0, b = 0;
+        VS_HIP(hipEventSynchronize(h->ev[i + 2]));
+        VS_HIP(hipEventElapsedTime(&a, h->ev[i], h->ev[i + 1]));
+        VS_HIP(hipEventElapsedTime(&b, h->ev[i + 1], h->ev[i + 2]));
+        ms[0] += a;
+        ms[1] += b;
+    }
+    for (hipEvent_t x : h->ev) (void)hipEventDestroy(x);
+    h->ev.clear();
     return 0;
 }
 
@@ -494,48 +520,75 @@ VS_API void vs_seal_close(vs_seal *h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
-    for (DevBuf *b : {&h->te0, &h->rk256, &h->rk128, &h->rpow, &h->prefix, &h->tmp}) b->release();
+    for (hipEvent_t x : h->ev) (void)hipEventDestroy(x);
+    for (DevBuf *b : {&h->te0, &h->rk256, &h->rk128, &h->rpow, &h->prefix}) b->release();
     delete h;
 }
 
 namespace vsgpu {
 
 namespace {
-__global__ void seal_blocks_kernel(const uint32_t *len, uint64_t n, uint64_t *nb) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i <= n) nb[i] = (i < n) ? (len[i] + 15u) / 16u : 0;
+constexpr uint32_t kScanThreads = 1024, kScanPer = 16;
+
+// prefix[i] = 16-byte blocks of blobs [0, i) for i <= n, in one workgroup:
+// tiles of 16 K blobs, 16 consecutive blobs per thread, a workgroup scan of
+// the thread sums in LDS carried from tile to tile.  n is a blob count
+// (~45 K for a 64 GiB volume), so a single workgroup is microseconds.
+__global__ __launch_bounds__(kScanThreads) void seal_prefix_kernel(const uint32_t *len, uint64_t n,
+                                                                   uint64_t *prefix) {
+    __shared__ uint64_t part[kScanThreads];
+    const uint32_t t = threadIdx.x;
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base <= n; base += (uint64_t)kScanThreads * kScanPer) {
+        const uint64_t i0 = base + (uint64_t)t * kScanPer;
+        uint64_t v[kScanPer], sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; ++k) {
+            v[k] = (i0 + k < n) ? (len[i0 + k] + 15u) / 16u : 0;
+            sum += v[k];
+        }
+        part[t] = sum;
+        __syncthreads();
+        for (uint32_t d = 1; d < kScanThreads; d <<= 1) {   // inclusive Hillis-Steele
+            const uint64_t x = t >= d ? part[t - d] : 0;
+            __syncthreads();
+            part[t] += x;
+            __syncthreads();
+        }
+        uint64_t run = carry + part[t] - sum;   // exclusive prefix of this thread's first blob
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; ++k) {
+            if (i0 + k <= n) prefix[i0 + k] = run;
+            run += v[k];
+        }
+        carry += part[kScanThreads - 1];
+        __syncthreads();
+    }
 }
 }  // namespace
 
-size_t seal_scan_tmp_bytes(uint64_t n) {
-    size_t b = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const uint64_t *)nullptr,
-                                           (uint64_t *)nullptr, (int)(n + 1));
-    return b + (n + 1) * 8 + 64;
-}
-
 // prefix[i] = blocks of blobs [0, i), prefix[n] = *total (read back: waits)
-hipError_t launch_seal_prefix(const uint32_t *len, uint64_t n, uint64_t *prefix, void *tmp,
-                              size_t tmp_bytes, uint64_t *total, hipStream_t s) {
-    uint64_t *nb = (uint64_t *)tmp;
-    void *scratch = (uint8_t *)tmp + (n + 1) * 8 + 64;
-    size_t sb = tmp_bytes - (n + 1) * 8 - 64;
-    seal_blocks_kernel<<<(uint32_t)((n + 1 + 255) / 256), 256, 0, s>>>(len, n, nb);
-    hipError_t e = hipcub::DeviceScan::ExclusiveSum(scratch, sb, nb, prefix, (int)(n + 1), s);
+hipError_t launch_seal_prefix(const uint32_t *len, uint64_t n, uint64_t *prefix, uint64_t *total,
+                              hipStream_t s) {
+    seal_prefix_kernel<<<1, kScanThreads, 0, s>>>(len, n, prefix);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     e = hipMemcpyAsync(total, prefix + n, 8, hipMemcpyDeviceToHost, s);
     if (e != hipSuccess) return e;
     return hipStreamSynchronize(s);
 }
 
-hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s) {
+hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s, hipEvent_t *ev) {
+    if (ev[0]) (void)hipEventRecord(ev[0], s);
     if (a.total_blocks) {
         const uint64_t waves = (a.total_blocks + 255) / 256;
         const uint64_t grid = std::min<uint64_t>((waves + 3) / 4, (uint64_t)std::max(cus, 1) * 20);
         seal_ctr_kernel<<<(uint32_t)grid, 256, 0, s>>>(a);
     }
+    if (ev[1]) (void)hipEventRecord(ev[1], s);
     const uint64_t mg = std::min<uint64_t>((a.n + 3) / 4, (uint64_t)std::max(cus, 1) * 8);
     seal_mac_kernel<<<(uint32_t)std::max<uint64_t>(mg, 1), 256, 0, s>>>(a);
+    if (ev[2]) (void)hipEventRecord(ev[2], s);
     return hipGetLastError();
 }
 

@@ -75,7 +75,7 @@ size_t dedup_tmp_bytes(uint64_t n) {
                                              (uint64_t *)nullptr, (const uint32_t *)nullptr,
                                              (uint32_t *)nullptr, (int)n, 0, 64);
     // keys, sorted keys, idx, sorted idx, counter, then the sort scratch
-    return n * (8 + 8 + 4 + 4) + 256 + b;
+    return n * (8 + 8 + 4 + 4) + 512 + b;
 }
 
 hipError_t launch_dedup(const uint8_t *ids, uint64_t n, uint32_t *first, void *tmp,
@@ -87,7 +87,9 @@ hipError_t launch_dedup(const uint8_t *ids, uint64_t n, uint32_t *first, void *t
     uint64_t *skeys = keys + n;
     uint32_t *idx = (uint32_t *)(skeys + n);
     uint32_t *sidx = idx + n;
-    uint8_t *scratch = (uint8_t *)(sidx + n) + 256;
+    // the sort's scratch 256-byte aligned (rocprim's look-back state is
+    // updated with wide atomics)
+    uint8_t *scratch = (uint8_t *)(((uintptr_t)(sidx + n) + 256 + 255) & ~(uintptr_t)255);
     size_t sb = tmp_bytes - (size_t)(scratch - t);
     const uint32_t blocks = (uint32_t)((n + 255) / 256);
     dd_keys_kernel<<<blocks, 256, 0, s>>>(ids, n, keys, idx);

@@ -366,10 +366,9 @@ struct SealArgs {
     const uint32_t *rpow;       // [64][5] r^1..r^64 in 26-bit limbs (MACKey.R clamped)
     uint8_t *macs;              // [n][16]
 };
-size_t seal_scan_tmp_bytes(uint64_t n);
-hipError_t launch_seal_prefix(const uint32_t *len, uint64_t n, uint64_t *prefix, void *tmp,
-                              size_t tmp_bytes, uint64_t *total, hipStream_t s);
-hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s);
+hipError_t launch_seal_prefix(const uint32_t *len, uint64_t n, uint64_t *prefix, uint64_t *total,
+                              hipStream_t s);
+hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s, hipEvent_t *ev);
 // adjacent-mover kernels (movers.hip)
 struct ReconPiece {
     uint64_t dst, src, len;
