@@ -337,7 +337,7 @@ int vs_seal_open(int device, const uint8_t enc_key[32], const uint8_t mac_k[16],
                  const uint8_t mac_r[16], vs_seal **h);
 /* Blob i = dev_in[off[i] : off[i]+len[i]] (device arrays); its ciphertext is
  * written to dev_out at the same offset (dev_out may equal dev_in) and its
- * mac to dev_macs[16*i]; nonces: device array of n*16 bytes.  Queued on
+ * mac to dev_macs[16*i]; nonces: device array of n*16 bytes, 16-byte aligned.  Queued on
  * hip_stream after a short read-back of the block count. */
 int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *dev_off,
                        const uint32_t *dev_len, size_t n, const uint8_t *dev_nonces,

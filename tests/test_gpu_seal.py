@@ -123,3 +123,18 @@ def test_seal_many_tiny_blobs_multi_tile_prefix(gpu):
     nonces = rng.integers(0, 256, (len(lens), 16), dtype=np.uint8)
     ct, macs = _run(keys, data, offs, lens, nonces)
     _check(keys, data, offs, lens, nonces, ct, macs)
+
+
+def test_seal_rejects_misaligned_nonces(gpu):
+    import torch
+    from volsync_amd import Sealer
+    from volsync_amd._lib import VsError
+    d = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    do = torch.zeros(1, dtype=torch.int64, device="cuda")
+    dl = torch.full((1,), 16, dtype=torch.int32, device="cuda")
+    dn = torch.zeros(48, dtype=torch.uint8, device="cuda")
+    s = Sealer(*_keys(10))
+    with pytest.raises(VsError, match="aligned"):
+        s.run(d.data_ptr(), do.data_ptr(), dl.data_ptr(), 1, dn.data_ptr() + 4, d.data_ptr(),
+              d.data_ptr() + 32)
+    s.close()

@@ -18,6 +18,7 @@
 //   and the lanes' sums are lifted by r^e_j (e_j = N - last_j + 1 <= 64) and
 //   added -- r is the repository's key, so r^1..r^64 are computed once per
 //   handle.  130-bit arithmetic in five 26-bit limbs (v_mad_u64_u32).
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -63,13 +64,12 @@ __device__ __forceinline__ void aes_encrypt(uint32_t (&s)[4], const uint32_t *rk
 #undef TE
 }
 
-// counter block nonce + q (128-bit big-endian) as LE column words
-__device__ __forceinline__ void ctr_block(const uint8_t *nonce, uint64_t q, uint32_t (&s)[4]) {
+// counter block nonce + q (128-bit big-endian) as LE column words; the nonce
+// as four little-endian words as loaded (n[0] = bytes 0..3)
+__device__ __forceinline__ void ctr_block(const uint32_t (&n)[4], uint64_t q, uint32_t (&s)[4]) {
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-        w[i] = ((uint32_t)nonce[4 * i] << 24) | ((uint32_t)nonce[4 * i + 1] << 16) |
-               ((uint32_t)nonce[4 * i + 2] << 8) | nonce[4 * i + 3];
+    for (int i = 0; i < 4; ++i) w[i] = __builtin_bswap32(n[i]);
     // add q to the 128-bit big-endian value w[0..3] (w[3] least significant)
     uint64_t acc = (uint64_t)w[3] + (uint32_t)q;
     w[3] = (uint32_t)acc;
@@ -80,6 +80,14 @@ __device__ __forceinline__ void ctr_block(const uint8_t *nonce, uint64_t q, uint
     w[0] = w[0] + (uint32_t)(acc >> 32);
 #pragma unroll
     for (int i = 0; i < 4; ++i) s[i] = __builtin_bswap32(w[i]);
+}
+
+__device__ __forceinline__ void load_nonce(const uint8_t *nonces, uint64_t b, uint32_t (&n)[4]) {
+    const uint4 v = *(const uint4 *)(nonces + 16 * b);   // 16-byte aligned (checked on the host)
+    n[0] = v.x;
+    n[1] = v.y;
+    n[2] = v.z;
+    n[3] = v.w;
 }
 
 __device__ __forceinline__ void load_te(uint32_t *te, const uint32_t *g) {
@@ -97,44 +105,159 @@ __device__ __forceinline__ uint64_t find_blob(const uint64_t *prefix, uint64_t n
     return lo;
 }
 
-__global__ __launch_bounds__(256) void seal_ctr_kernel(SealArgs a) {
-    __shared__ uint32_t te[256 * kCopies];
-    __shared__ uint32_t rk[60];
-    load_te(te, a.te0);
-    if (threadIdx.x < 60) rk[threadIdx.x] = a.rk256[threadIdx.x];
+// ---- CTR: two T-tables with the byte index written by SDWA ------------------
+// LDS row e (256 B) = [T0[e] x 32 lane copies | T1[e] = rotl8(T0[e]) x 32], so
+// lookup (byte x, table k, lane copy c) is at x * 256 + k * 128 + c * 4: bank
+// c, conflict-free within each 32-lane group.  Each lookup's address register
+// holds k * 128 + c * 4 in byte 0 and zeros above; one v_mov_b32_sdwa
+// writes the state byte into byte 1 and keeps the rest, so a lookup costs one
+// single-source VALU instead of a bfe + lshl_or pair.  A column is
+//   T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d]) ^ k   (one rotation, not three).
+constexpr uint32_t kCtrWords = 256 * 64;   // 64 KiB
+
+template <int B>
+__device__ __forceinline__ void pick(uint32_t &a, uint32_t x) {
+    if constexpr (B == 0)
+        asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0" : "+v"(a) : "v"(x));
+    else if constexpr (B == 1)
+        asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1" : "+v"(a) : "v"(x));
+    else if constexpr (B == 2)
+        asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(a) : "v"(x));
+    else
+        asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_3" : "+v"(a) : "v"(x));
+}
+
+__device__ __forceinline__ uint32_t tl(const uint32_t *tab, uint32_t a) {
+    return *(const uint32_t *)((const uint8_t *)tab + a);
+}
+
+template <int NB>
+__device__ __forceinline__ void pick_all(uint32_t (&ix)[NB][16], const uint32_t (&s)[NB][4]) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            pick<0>(ix[b][4 * j], s[b][j]);
+            pick<1>(ix[b][4 * j + 1], s[b][(j + 1) & 3]);
+            pick<2>(ix[b][4 * j + 2], s[b][(j + 2) & 3]);
+            pick<3>(ix[b][4 * j + 3], s[b][(j + 3) & 3]);
+        }
+}
+
+// AES-256 of NB counter blocks per lane; rk: the 60 round-key words (uniform,
+// read through the scalar cache)
+template <int NB>
+__device__ __forceinline__ void aes256_tab(uint32_t (&s)[NB][4], uint32_t (&ix)[NB][16],
+                                           const uint32_t *tab, const uint32_t *__restrict__ rk) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[b][j] ^= rk[j];
+#pragma unroll
+    for (int r = 1; r < 14; ++r) {
+        pick_all<NB>(ix, s);
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                s[b][j] = tl(tab, ix[b][4 * j]) ^ tl(tab, ix[b][4 * j + 1]) ^
+                          rotl16(tl(tab, ix[b][4 * j + 2]) ^ tl(tab, ix[b][4 * j + 3])) ^ rk[4 * r + j];
+    }
+    // last round: S[x] is byte 1 of T0[x] and byte 2 of T1[x] (T0 = 2s,s,s,3s)
+    pick_all<NB>(ix, s);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            s[b][j] = (((tl(tab, ix[b][4 * j]) >> 8) & 0xffu) | ((tl(tab, ix[b][4 * j + 1]) >> 8) & 0xff00u) |
+                       (tl(tab, ix[b][4 * j + 2]) & 0xff0000u) | (tl(tab, ix[b][4 * j + 3]) & 0xff000000u)) ^
+                      rk[56 + j];
+}
+
+// Each wave seals a contiguous range of 128-block steps (2 blocks per lane:
+// lane l takes blocks g0 + l and g0 + 64 + l, so each access is 1 KiB
+// contiguous per wave); the blob index follows the range forward and the
+// per-lane search runs only for steps that straddle a blob boundary.
+// kCtrPer blocks per lane per step (ILP); two workgroups per CU (64 KiB of
+// tables each), WPE waves per SIMD
+template <int kCtrPer, int kThreads, int WPE>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
+void seal_ctr_kernel(SealArgs a) {
+    __shared__ uint32_t tab[kCtrWords];
+    for (uint32_t i = threadIdx.x; i < kCtrWords; i += blockDim.x) {
+        const uint32_t t = a.te0[i >> 6];
+        tab[i] = (i & 32) ? rotl8(t) : t;
+    }
     __syncthreads();
-    const uint32_t lane = threadIdx.x & 63, c = lane & (kCopies - 1);
+    const uint32_t lane = threadIdx.x & 63, c4 = (lane & 31) * 4;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t base = wave * 256; base < a.total_blocks; base += nw * 256) {
-        for (uint32_t j = 0; j < 4; ++j) {
-            const uint64_t g0 = base + 64 * j;
-            if (g0 >= a.total_blocks) break;
-            const uint64_t g = g0 + lane;
-            // the blob: uniform when the 64 blocks lie in one blob (the usual case)
-            const uint64_t last = min(g0 + 63, a.total_blocks - 1);
-            const uint64_t b0 = find_blob(a.prefix, a.n, g0);
-            uint64_t b = b0;
-            if (a.prefix[b0 + 1] <= last) b = find_blob(a.prefix, a.n, min(g, a.total_blocks - 1));
-            if (g >= a.total_blocks) continue;
-            const uint64_t q = g - a.prefix[b];
-            const uint64_t off = a.off[b] + 16 * q;
-            const uint32_t len = a.len[b];
-            const uint32_t nb = (uint32_t)min<uint64_t>(16, len - 16 * q);
-            uint32_t s[4];
-            ctr_block(a.nonces + 16 * b, q, s);
-            aes_encrypt(s, rk, 14, te, c);
-            if (nb == 16) {
-                uint4 v;
-                __builtin_memcpy(&v, a.in + off, 16);
-                v.x ^= s[0];
-                v.y ^= s[1];
-                v.z ^= s[2];
-                v.w ^= s[3];
-                __builtin_memcpy(a.out + off, &v, 16);
+    constexpr uint32_t kStep = 64 * kCtrPer;
+    const uint64_t steps = (a.total_blocks + kStep - 1) / kStep;
+    const uint64_t per = (steps + nw - 1) / nw;
+    const uint64_t s0 = wave * per, s1 = min(s0 + per, steps);
+    if (s0 >= s1) return;
+    uint32_t ix[kCtrPer][16];
+#pragma unroll
+    for (int b = 0; b < (int)kCtrPer; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ix[b][i] = c4 + (i & 1) * 128;
+    uint64_t blob = find_blob(a.prefix, a.n, s0 * kStep);
+    for (uint64_t st = s0; st < s1; ++st) {
+        const uint64_t g0 = st * kStep;
+        const uint64_t glast = min(g0 + kStep - 1, a.total_blocks - 1);
+        while (a.prefix[blob + 1] <= g0) ++blob;
+        const bool one = a.prefix[blob + 1] > glast;
+        uint32_t s[kCtrPer][4];
+        uint64_t off[kCtrPer];
+        uint32_t nb[kCtrPer];
+        if (one) {
+            // the usual case: the whole step lies in one blob, so its
+            // metadata is wave-uniform (scalar loads)
+            const uint64_t pb = a.prefix[blob], ob = a.off[blob];
+            const uint32_t len = a.len[blob];
+            uint32_t nn[4];
+            load_nonce(a.nonces, blob, nn);
+#pragma unroll
+            for (int b = 0; b < (int)kCtrPer; ++b) {
+                const uint64_t g = g0 + 64 * b + lane;
+                const uint64_t q = g - pb;
+                off[b] = ob + 16 * q;
+                nb[b] = g < a.total_blocks ? (uint32_t)min<uint64_t>(16, len - 16 * q) : 0;
+                ctr_block(nn, q, s[b]);
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < (int)kCtrPer; ++b) {
+                const uint64_t g = g0 + 64 * b + lane;
+                const uint64_t gi = min(g, a.total_blocks - 1);
+                const uint64_t bi = find_blob(a.prefix, a.n, gi);
+                const uint64_t q = gi - a.prefix[bi];
+                off[b] = a.off[bi] + 16 * q;
+                const uint32_t len = a.len[bi];
+                nb[b] = g < a.total_blocks ? (uint32_t)min<uint64_t>(16, len - 16 * q) : 0;
+                uint32_t nn[4];
+                load_nonce(a.nonces, bi, nn);
+                ctr_block(nn, q, s[b]);
+            }
+        }
+        // plaintext loaded before the rounds so its latency hides behind them
+        uint4 v[kCtrPer];
+#pragma unroll
+        for (int b = 0; b < (int)kCtrPer; ++b)
+            if (nb[b] == 16) __builtin_memcpy(&v[b], a.in + off[b], 16);
+        aes256_tab<kCtrPer>(s, ix, tab, a.rk256);
+#pragma unroll
+        for (int b = 0; b < (int)kCtrPer; ++b) {
+            if (nb[b] == 16) {
+                v[b].x ^= s[b][0];
+                v[b].y ^= s[b][1];
+                v[b].z ^= s[b][2];
+                v[b].w ^= s[b][3];
+                __builtin_memcpy(a.out + off[b], &v[b], 16);
             } else {
-                for (uint32_t i = 0; i < nb; ++i)
-                    a.out[off + i] = a.in[off + i] ^ (uint8_t)(s[i >> 2] >> (8 * (i & 3)));
+                for (uint32_t i = 0; i < nb[b]; ++i)
+                    a.out[off[b] + i] = a.in[off[b] + i] ^ (uint8_t)(s[b][i >> 2] >> (8 * (i & 3)));
             }
         }
     }
@@ -239,14 +362,8 @@ __global__ __launch_bounds__(256) void seal_mac_kernel(SealArgs a) {
         for (int i = 0; i < 5; ++i) sumv[i] = wsum64(sumv[i]);
         // s = AES-128(MACKey.K, nonce): every lane computes it (uniform)
         uint32_t s[4];
-        {
-            const uint8_t *nn = a.nonces + 16 * b;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                s[i] = (uint32_t)nn[4 * i] | ((uint32_t)nn[4 * i + 1] << 8) |
-                       ((uint32_t)nn[4 * i + 2] << 16) | ((uint32_t)nn[4 * i + 3] << 24);
-            aes_encrypt(s, rk, 10, te, c);
-        }
+        load_nonce(a.nonces, b, s);
+        aes_encrypt(s, rk, 10, te, c);
         if (lane == 0) {
             // carry the lane sums into limbs, reduce mod 2^130 - 5
             uint64_t d[5];
@@ -465,6 +582,7 @@ VS_API int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *de
     if (!h || (n && (!dev_in || !dev_off || !dev_len || !dev_nonces || !dev_out || !dev_macs)))
         return fail(VS_ERR_ARG, "bad arguments");
     if (!n) return 0;
+    if ((uintptr_t)dev_nonces & 15) return fail(VS_ERR_ARG, "nonces must be 16-byte aligned");
     if (hipSetDevice(h->device) != hipSuccess) return fail(VS_ERR_NO_DEVICE, "hipSetDevice failed");
     const hipStream_t s = (hipStream_t)hip_stream;
     VS_TRY(h->prefix.ensure((n + 1) * 8));
@@ -581,9 +699,24 @@ hipError_t launch_seal_prefix(const uint32_t *len, uint64_t n, uint64_t *prefix,
 hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s, hipEvent_t *ev) {
     if (ev[0]) (void)hipEventRecord(ev[0], s);
     if (a.total_blocks) {
-        const uint64_t waves = (a.total_blocks + 255) / 256;
-        const uint64_t grid = std::min<uint64_t>((waves + 3) / 4, (uint64_t)std::max(cus, 1) * 20);
-        seal_ctr_kernel<<<(uint32_t)grid, 256, 0, s>>>(a);
+        // variants (VSGPU_SEAL_CTR, for measurement; 16 GiB of blobs, r02):
+        // 1 (default) = 1 block per lane, 1024 threads, 8 waves per SIMD:
+        // 22.0 ms; 0 = 2 blocks per lane, 512 threads: 22.6 ms; 2 = 3 blocks,
+        // 512 threads: 22.8 ms.  LDS-issue bound (2 cycles per ds_read_b32,
+        // 224 lookups per block): SQ_LDS_IDX_ACTIVE is ~65 % of the cycles.
+        static const int variant = [] {
+            const char *e = getenv("VSGPU_SEAL_CTR");
+            return e ? atoi(e) : 1;
+        }();
+        const int per = variant == 1 ? 1 : variant == 2 ? 3 : 2;
+        const int threads = variant == 1 ? 1024 : 512;
+        const uint64_t steps = (a.total_blocks + 64 * per - 1) / (64 * per);
+        const uint64_t wg_waves = threads / 64;
+        const uint64_t grid = std::min<uint64_t>((steps + wg_waves - 1) / wg_waves,
+                                                 (uint64_t)std::max(cus, 1) * 2);
+        if (variant == 1) seal_ctr_kernel<1, 1024, 8><<<(uint32_t)grid, 1024, 0, s>>>(a);
+        else if (variant == 2) seal_ctr_kernel<3, 512, 4><<<(uint32_t)grid, 512, 0, s>>>(a);
+        else seal_ctr_kernel<2, 512, 4><<<(uint32_t)grid, 512, 0, s>>>(a);
     }
     if (ev[1]) (void)hipEventRecord(ev[1], s);
     const uint64_t mg = std::min<uint64_t>((a.n + 3) / 4, (uint64_t)std::max(cus, 1) * 8);
