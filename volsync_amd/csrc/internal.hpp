@@ -164,11 +164,13 @@ struct ShaSliceArgs {
     uint32_t *n_next;
     uint32_t *tile_ctr;
     uint32_t budget;         // max blocks per chain in this slice (0xffffffff: all)
+    uint32_t quad_chains;    // the first (longest) chains of the order run in latency mode
 };
 
 // Host side of the engine: a double-buffered active list on the device, fed by
 // append_*() and advanced by slice(); every call queues on the given stream
 // (always the same one) without synchronising.
+enum { kShaSplit = 0, kShaWide = 1, kShaQuad = 2 };
 struct ShaEngine {
     struct Group {
         uint64_t n;
@@ -192,7 +194,12 @@ struct ShaEngine {
     std::function<hipEvent_t()> ev_get;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> kernel_pairs;
     int init(int dev);
-    int launch(uint32_t budget, bool wide, hipStream_t s);
+    // the final drain runs its longest chains in latency (quad) mode: those
+    // with at least quad_frac_pct % of the longest chain's remaining blocks
+    // (VSGPU_SHA_QUAD_PCT overrides; 0 disables, 100+ only the longest bucket)
+    uint32_t quad_pct = 80;
+    uint32_t *hist_h = nullptr;  // pinned: the drain's bucket histogram
+    int launch(uint32_t budget, int mode, hipStream_t s);
     void release();
     uint32_t *count(int which);
     int reserve(uint64_t n_new, hipStream_t s);

@@ -28,6 +28,7 @@
 // v_bitop3_b32 does Ch / Maj / three-way XORs, v_alignbit_b32 the rotates and
 // v_perm_b32 the big-endian, byte-misaligned message words.
 #include <algorithm>
+#include <cstdlib>
 
 #include "internal.hpp"
 
@@ -139,7 +140,10 @@ __device__ __forceinline__ void message(uint32_t (&w)[16], const uint32_t (&d)[1
 
 // Producer: W[t] for t = 0..63 into the LDS slot (word group q of
 // lane l at uint4 index q*64 + l: conflict-free ds_write_b128 / ds_read_b128).
-__device__ __forceinline__ void schedule_to_lds(uint32_t (&w)[16], uint4 *slot, uint32_t lane) {
+// quad: the compact latency-mode layout (16 chains: q * 16 + lane) with K
+// added here, so a lane that reads a zero slot instead gets exactly 0
+__device__ __forceinline__ void schedule_to_lds(uint32_t (&w)[16], uint4 *slot, uint32_t lane,
+                                                bool quad = false) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
         uint32_t o[4];
@@ -155,9 +159,9 @@ __device__ __forceinline__ void schedule_to_lds(uint32_t (&w)[16], uint4 *slot, 
                 const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
                 wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
             }
-            o[i] = wt;
+            o[i] = quad ? wt + kK256[t] : wt;
         }
-        slot[q * 64 + lane] = make_uint4(o[0], o[1], o[2], o[3]);
+        slot[q * (quad ? 16 : 64) + lane] = make_uint4(o[0], o[1], o[2], o[3]);
     }
 }
 
@@ -200,6 +204,65 @@ __device__ __forceinline__ void compress_lds(uint32_t (&st)[8], const uint4 *slo
 }
 #undef VS_SHA_ROUND
 
+// Latency (quad) consumer: four lanes per chain, so one wave's instruction
+// stream advances a chain with ~10 VALU per round instead of ~15.  Lane roles
+// in a quad: 0 runs the e-path (cur = e, history f, g, h), 1 the a-path
+// (cur = a, history b, c, d), 2 and 3 hold zeros.  Per round, with per-lane
+// rotation amounts and masks:
+//   S = Sigma1(e) | Sigma0(a)            (3 v_alignbit by per-lane amounts + xor3)
+//   X = e | ~(a ^ b)                      (one v_bitop3: o ^ (m & ~p))
+//   C = Ch(X, p1, p2) = Ch(e,f,g) | Maj(a,b,c)   (Maj(a,b,c) = Ch(~(a^b), b, c))
+//   Z = h + (K + W) | 0                   (DPP: lane 1 reads lane 2's zero)
+//   T = S + C + Z = T1 | T2
+//   new = DPP-swap(T1 | d) + T = d + T1 (e') | T1 + T2 (a')
+// K + W comes from the producer; lanes 1-3 read a zero slot instead.
+struct QuadLane {
+    uint32_t s1, s2, s3;  // rotation amounts: Sigma1 (6, 11, 25) / Sigma0 (2, 13, 22)
+    uint32_t m;           // 0 / ~0: the Maj transform in lane 1
+    bool l1;              // the a-path lane
+};
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+
+// z: this round's h + (K + W) | 0, computed one round ahead (from p2, the
+// next round's p3) so it fills the wait states between the select and the
+// DPP add that reads it
+#define VS_QUAD_ROUND(cur, p1, p2, p3, z, kwn)                                               \
+    {                                                                                        \
+        const uint32_t s_ = xor3(__builtin_amdgcn_alignbit(cur, cur, ql.s1),                \
+                                 __builtin_amdgcn_alignbit(cur, cur, ql.s2),                 \
+                                 __builtin_amdgcn_alignbit(cur, cur, ql.s3));                \
+        const uint32_t x_ = __builtin_amdgcn_bitop3_b32(cur, p1, ql.m, 0xD2);               \
+        const uint32_t c_ = ch(x_, p1, p2);                                                  \
+        const uint32_t t_ = s_ + c_ + z;                                                     \
+        const uint32_t a_ = ql.l1 ? p3 : t_;                                                 \
+        z = dpp_u32<0xA8>(p2) + (kwn); /* quad_perm [0,2,2,2] */                            \
+        p3 = dpp_u32<0xB1>(a_) + t_;   /* quad_perm [1,0,3,2] */                            \
+    }
+
+__device__ __forceinline__ void compress_quad(uint32_t (&x)[4], const uint4 *kw, const QuadLane &ql) {
+    uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3];
+    uint4 v = kw[0];
+    uint32_t z = dpp_u32<0xA8>(x3) + v.x;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const uint4 u = q < 15 ? kw[(q + 1) * 16] : make_uint4(0, 0, 0, 0);
+        VS_QUAD_ROUND(x0, x1, x2, x3, z, v.y)
+        VS_QUAD_ROUND(x3, x0, x1, x2, z, v.z)
+        VS_QUAD_ROUND(x2, x3, x0, x1, z, v.w)
+        VS_QUAD_ROUND(x1, x2, x3, x0, z, u.x)
+        v = u;
+    }
+    x[0] += x0;
+    x[1] += x1;
+    x[2] += x2;
+    x[3] += x3;
+}
+#undef VS_QUAD_ROUND
+
 // End of a chain's turn in a slice: write the digest of a finished chain, or
 // append the midstate of an unfinished one to the next active list
 // (wave-aggregated: one atomic per wave).
@@ -235,13 +298,89 @@ __device__ __forceinline__ void retire(const ShaSliceArgs &a, const ShaChain &ch
 // wave 0 produces, wave 1 consumes; both hold the same 64 chains (lane l of
 // each wave = chain l of the tile) and step through the same block loop, one
 // workgroup barrier per block.
+// Producer side of a tile (the W of each block into the LDS slots); QUAD: the
+// compact latency-mode layout with K added (schedule_to_lds).
+template <bool QUAD>
+__device__ __forceinline__ void produce_tile(uint4 (&wk)[2][16 * 64], const ShaChain &ch0, uint32_t mine,
+                                             uint32_t steps, uint32_t lane) {
+    const uint64_t p = ch0.ptr, e = ch0.end, L = ch0.len;
+    const uint64_t A = p & ~15ull;
+    const uint64_t safe =
+        L ? ((e - 1) & ~15ull) : ((uint64_t)(uintptr_t)ch0.out & ~15ull);
+    const uint32_t q = (uint32_t)(p & 15) >> 2;
+    // the chain this lane loads for in instruction i, and its segment offset
+    uint64_t LA[4], LE[4], LS[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int src = 16 * i + (int)(lane >> 2);
+        LA[i] = (uint64_t)__shfl((long long)A, src, 64);
+        LE[i] = (uint64_t)__shfl((long long)e, src, 64);
+        LS[i] = (uint64_t)__shfl((long long)safe, src, 64);
+    }
+    const uint64_t so = 16 + 16 * (lane & 3);
+    // staged segments: chain c, segment t at uint4 index 5 c + t (80-byte
+    // stride: conflict-free ds_write_b128 / ds_read_b128)
+    const uint32_t wr = 5 * (lane >> 2) + (lane & 3);
+    uint4 R[4], c = load_seg(A, e, safe), S[4];
+    uint32_t d[17], w[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + so, LE[i], LS[i]);
+    // block 0 -> slot 0
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wk[0][80 * i + wr] = R[i];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) S[t] = wk[0][5 * lane + t];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + 64 + so, LE[i], LS[i]);
+    window_words(d, c, S, q);
+    c = S[3];
+    if (mine > 0) {
+        message(w, d, p, e, L);
+        schedule_to_lds(w, wk[0], lane, QUAD);
+    }
+    __syncthreads();
+    for (uint32_t j = 0; j < steps; ++j) {
+        // produce block j+1 while the consumer runs block j; its segments
+        // arrived during step j-1, block j+2's are fetched now
+        uint4 *slot = wk[(j + 1) & 1];
+        const uint64_t nb = 64ull * (j + 2) + so;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) slot[80 * i + wr] = R[i];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + nb, LE[i], LS[i]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) S[t] = slot[5 * lane + t];
+        window_words(d, c, S, q);
+        c = S[3];
+        if (j + 1 < mine) {
+            message(w, d, p + 64ull * (j + 1), e, L);
+            schedule_to_lds(w, slot, lane, QUAD);
+        }
+        __syncthreads();
+    }
+}
+
+// Tiles [0, qt) hold the first (longest) a.quad_chains chains of the order, 16
+// per tile, consumed in latency mode (compress_quad; the producer's lanes
+// 16..63 idle); the later tiles hold 64 chains each in split mode.
 __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
     __shared__ uint4 wk[2][16 * 64];  // 2 x 16 KiB: W of one block of 64 chains
     __shared__ uint32_t tile_sh;
+    // the K + W that quad lanes 1-3 read: zeros in a part of buffer 0 that
+    // quad tiles never write (their W takes entries 0..255, the staged
+    // segments 0..318); a workgroup's tiles come in tile-counter order, so it
+    // runs every quad tile it gets before its first split tile
+    uint4 *const zero_kw = &wk[0][512];
     const uint32_t lane = threadIdx.x & 63;
     const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;  // wave-uniform
     const uint32_t n = *a.n_cur;
-    const uint32_t ntiles = (n + 63) / 64;
+    const uint32_t nq = min(a.quad_chains, n);
+    const uint32_t qt = (nq + 15) / 16;
+    const uint32_t ntiles = qt + (n - nq + 63) / 64;
+    if (qt) {
+        for (uint32_t i = threadIdx.x; i < 16 * 16; i += blockDim.x) zero_kw[i] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+    }
     if (!producer) __builtin_amdgcn_s_setprio(2);  // the rounds are the critical path
     for (;;) {
         if (threadIdx.x == 0) tile_sh = atomicAdd(a.tile_ctr, 1u);
@@ -249,8 +388,10 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
         const uint32_t t = tile_sh;
         __syncthreads();
         if (t >= ntiles) break;
-        const uint32_t idx = t * 64 + lane;
-        const bool valid = idx < n;
+        const bool quad = t < qt;  // wave-uniform
+        const uint32_t my = quad ? (producer ? lane : lane >> 2) : lane;
+        const uint32_t idx = quad ? t * 16 + my : nq + (t - qt) * 64 + my;
+        const bool valid = quad ? (my < 16 && idx < nq) : idx < n;
         const uint32_t ci = valid ? (a.order ? a.order[idx] : idx) : 0u;
         const ShaChain ch0 = a.cur[ci];
         const uint32_t left = valid ? blocks_left(ch0.ptr, ch0.end) : 0u;
@@ -262,61 +403,34 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
         steps = __builtin_amdgcn_readfirstlane(steps);
         if (steps == 0) continue;
         if (producer) {
-            const uint64_t p = ch0.ptr, e = ch0.end, L = ch0.len;
-            const uint64_t A = p & ~15ull;
-            const uint64_t safe =
-                L ? ((e - 1) & ~15ull) : ((uint64_t)(uintptr_t)ch0.out & ~15ull);
-            const uint32_t q = (uint32_t)(p & 15) >> 2;
-            // the chain this lane loads for in instruction i, and its segment offset
-            uint64_t LA[4], LE[4], LS[4];
+            if (quad) produce_tile<true>(wk, ch0, mine, steps, lane);
+            else produce_tile<false>(wk, ch0, mine, steps, lane);
+        } else if (quad) {
+            __builtin_amdgcn_s_setprio(3);  // the drain's critical path
+            const uint32_t role = lane & 3, c = lane >> 2;
+            QuadLane ql;
+            ql.s1 = role == 0 ? 6 : role == 1 ? 2 : 0;
+            ql.s2 = role == 0 ? 11 : role == 1 ? 13 : 0;
+            ql.s3 = role == 0 ? 25 : role == 1 ? 22 : 0;
+            ql.m = role == 1 ? 0xffffffffu : 0u;
+            ql.l1 = role == 1;
+            // lane 0: e f g h, lane 1: a b c d, lanes 2-3: zeros
+            uint32_t x[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int src = 16 * i + (int)(lane >> 2);
-                LA[i] = (uint64_t)__shfl((long long)A, src, 64);
-                LE[i] = (uint64_t)__shfl((long long)e, src, 64);
-                LS[i] = (uint64_t)__shfl((long long)safe, src, 64);
-            }
-            const uint64_t so = 16 + 16 * (lane & 3);
-            // staged segments: chain c, segment t at uint4 index 5 c + t (80-byte
-            // stride: conflict-free ds_write_b128 / ds_read_b128)
-            const uint32_t wr = 5 * (lane >> 2) + (lane & 3);
-            uint4 R[4], c = load_seg(A, e, safe), S[4];
-            uint32_t d[17], w[16];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + so, LE[i], LS[i]);
-            // block 0 -> slot 0
-#pragma unroll
-            for (int i = 0; i < 4; ++i) wk[0][80 * i + wr] = R[i];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) S[t] = wk[0][5 * lane + t];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + 64 + so, LE[i], LS[i]);
-            window_words(d, c, S, q);
-            c = S[3];
-            if (mine > 0) {
-                message(w, d, p, e, L);
-                schedule_to_lds(w, wk[0], lane);
-            }
+            for (int i = 0; i < 4; ++i) x[i] = role == 0 ? ch0.st[4 + i] : role == 1 ? ch0.st[i] : 0u;
             __syncthreads();
             for (uint32_t j = 0; j < steps; ++j) {
-                // produce block j+1 while the consumer runs block j; its segments
-                // arrived during step j-1, block j+2's are fetched now
-                uint4 *slot = wk[(j + 1) & 1];
-                const uint64_t nb = 64ull * (j + 2) + so;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) slot[80 * i + wr] = R[i];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + nb, LE[i], LS[i]);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) S[t] = slot[5 * lane + t];
-                window_words(d, c, S, q);
-                c = S[3];
-                if (j + 1 < mine) {
-                    message(w, d, p + 64ull * (j + 1), e, L);
-                    schedule_to_lds(w, slot, lane);
-                }
+                if (j < mine) compress_quad(x, role == 0 ? &wk[j & 1][c] : &zero_kw[c], ql);
                 __syncthreads();
             }
+            uint32_t st[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                st[i] = (uint32_t)__shfl((int)x[i], (int)(lane | 1), 64);
+                st[4 + i] = x[i];
+            }
+            retire(a, ch0, st, valid && role == 0, mine, left, lane);
+            __builtin_amdgcn_s_setprio(2);
         } else {
             uint32_t st[8];
 #pragma unroll
@@ -546,8 +660,18 @@ __global__ __launch_bounds__(256) void sha_scatter_kernel(const ShaChain *list,
 }
 
 // ---- ShaEngine (host) ------------------------------------------------------------
+// the fewest remaining blocks a chain in bucket key k can have (sha_key inverse)
+static uint64_t bucket_blocks(uint32_t k) {
+    const uint32_t f = kShaBuckets - 1 - k;
+    if (f < 1024) return f;
+    const uint32_t l = 10 + ((f - 1024) >> 6), m = (f - 1024) & 63;
+    return (64ull + m) << (l - 6);
+}
+
 int ShaEngine::init(int dev) {
     device = dev;
+    if (const char *q = getenv("VSGPU_SHA_QUAD_PCT")) quad_pct = (uint32_t)strtoul(q, nullptr, 0);
+    if (!hist_h) VS_HIP(hipHostMalloc((void **)&hist_h, kShaBuckets * 4, hipHostMallocDefault));
     VS_TRY(ctl.ensure(64));
     VS_TRY(hist.ensure((2 * kShaBuckets + 16) * 4));
     VS_HIP(hipMemset(ctl.p, 0, 64));
@@ -563,6 +687,8 @@ void ShaEngine::release() {
     cap = 0;
     if (live_h) (void)hipHostFree(live_h);
     live_h = nullptr;
+    if (hist_h) (void)hipHostFree(hist_h);
+    hist_h = nullptr;
 }
 
 uint32_t *ShaEngine::count(int which) { return ctl.as<uint32_t>() + which; }
@@ -624,7 +750,7 @@ int ShaEngine::slice(uint32_t budget, hipStream_t s) {
     if (ub == 0) return 0;
     // budgeted slices run beside the next volume's fingerprint pass: split
     // mode leaves that pass room (throughput mode measured slower there)
-    if (budget != 0xffffffffu) return launch(budget, false, s);
+    if (budget != 0xffffffffu) return launch(budget, kShaSplit, s);
     while (ub >= wide_min) {
         VS_HIP(hipMemcpyAsync(live_h, count(cur), 4, hipMemcpyDeviceToHost, s));
         VS_HIP(hipStreamSynchronize(s));
@@ -635,12 +761,14 @@ int ShaEngine::slice(uint32_t budget, hipStream_t s) {
             return 0;
         }
         if (live < wide_min) break;
-        VS_TRY(launch(std::max(wide_budget, 1u), true, s));
+        VS_TRY(launch(std::max(wide_budget, 1u), kShaWide, s));
     }
-    return launch(budget, false, s);
+    // the final drain: every remaining chain to its end; its longest chains
+    // set the finish time, so they run in latency (quad) mode
+    return launch(budget, quad_pct ? kShaQuad : kShaSplit, s);
 }
 
-int ShaEngine::launch(uint32_t budget, bool wide, hipStream_t s) {
+int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
     if (ub == 0) return 0;  // every chain finished within the previous budgets
     const int nxt = cur ^ 1;
     uint32_t *cursor = hist.as<uint32_t>() + kShaBuckets;
@@ -653,6 +781,28 @@ int ShaEngine::launch(uint32_t budget, bool wide, hipStream_t s) {
     VS_HIP(launch_scan_u32(hist.as<uint32_t>(), cursor, kShaBuckets, partials, 0xffffffffu, s));
     sha_scatter_kernel<<<sb, 256, 0, s>>>(list[cur].as<ShaChain>(), count(cur), budget, cursor,
                                           order.as<uint32_t>());
+    // quad drain: the chains within quad_pct % of the longest remaining one
+    // (bucket histogram read back: one synchronisation per drain)
+    uint32_t quad_chains = 0;
+    if (mode == kShaQuad) {
+        VS_HIP(hipMemcpyAsync(hist_h, hist.p, kShaBuckets * 4, hipMemcpyDeviceToHost, s));
+        VS_HIP(hipStreamSynchronize(s));
+        uint32_t first = 0;
+        while (first < kShaBuckets && hist_h[first] == 0) ++first;
+        double blocks = 0;
+        for (uint32_t k = first; k < kShaBuckets; ++k) blocks += (double)hist_h[k] * bucket_blocks(k);
+        // latency-bound only: the backlog at split-mode throughput (~1.45 TB/s,
+        // 22.7 G blocks/s) clears well before the longest chain would at
+        // split-mode chain speed (~1.95 us per block); otherwise the quad
+        // tiles' idle producer lanes only cost throughput
+        if (first < kShaBuckets && blocks / 22.7e9 < 0.8 * 1.95e-6 * (double)bucket_blocks(first)) {
+            const uint64_t lmax = bucket_blocks(first);
+            for (uint32_t k = first; k < kShaBuckets; ++k) {
+                if (bucket_blocks(k) * 100 < lmax * quad_pct) break;
+                quad_chains += hist_h[k];
+            }
+        }
+    }
     // zero the next list's count and the tile counter
     VS_HIP(hipMemsetAsync(count(nxt), 0, 4, s));
     VS_HIP(hipMemsetAsync(count(2), 0, 4, s));
@@ -664,10 +814,11 @@ int ShaEngine::launch(uint32_t budget, bool wide, hipStream_t s) {
     a.n_next = count(nxt);
     a.tile_ctr = count(2);
     a.budget = budget;
-    const uint64_t tiles = (ub + 63) / 64;
+    a.quad_chains = quad_chains;
+    const uint64_t tiles = (ub + 63) / 64 + (quad_chains + 15) / 16;
     hipEvent_t ka = ev_get ? ev_get() : nullptr, kb = ka ? ev_get() : nullptr;
     if (kb) VS_HIP(hipEventRecord(ka, s));
-    if (wide) {
+    if (mode == kShaWide) {
         // persistent grid: 3 waves per SIMD (launch bounds: <= 168 VGPRs)
         const uint64_t slots = (uint64_t)std::max(cus, 1) * 4 * 3 / kWideWaves;
         const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWideWaves - 1) / kWideWaves, slots);
