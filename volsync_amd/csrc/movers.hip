@@ -8,6 +8,8 @@
 //    row (f)4;
 //  * rsync's receiver reconstruction (receiver.c receive_data): the new file
 //    is literal runs and copies of basis blocks, in token order, row (f)2.
+#include <algorithm>
+
 #include "internal.hpp"
 
 namespace vsgpu {
@@ -47,15 +49,20 @@ __global__ __launch_bounds__(256) void recon_kernel(uint8_t *dst, const uint8_t 
         const ReconPiece p = pc[k];
         const uint8_t *src = (p.kind ? lit : basis) + p.src;
         uint8_t *d = dst + p.dst;
-        // bulk in 16-byte pieces when both sides are 16-byte aligned, else bytes
-        if (((p.dst | p.src) & 15) == 0) {
-            const uint64_t n16 = p.len / 16;
-            for (uint64_t i = threadIdx.x; i < n16; i += blockDim.x)
-                ((uint4 *)d)[i] = ((const uint4 *)src)[i];
-            for (uint64_t i = n16 * 16 + threadIdx.x; i < p.len; i += blockDim.x) d[i] = src[i];
-        } else {
-            for (uint64_t i = threadIdx.x; i < p.len; i += blockDim.x) d[i] = src[i];
+        // bytes up to the destination's 16-byte boundary, then 16-byte pieces:
+        // aligned stores, loads at whatever alignment the source has (gfx950
+        // global loads need none), then the tail bytes
+        const uint64_t head = std::min<uint64_t>((16 - ((uintptr_t)d & 15)) & 15, p.len);
+        if (threadIdx.x < head) d[threadIdx.x] = src[threadIdx.x];
+        const uint64_t n16 = (p.len - head) / 16;
+        uint4 *d16 = (uint4 *)(d + head);
+        const uint8_t *s16 = src + head;
+        for (uint64_t i = threadIdx.x; i < n16; i += blockDim.x) {
+            uint4 v;
+            __builtin_memcpy(&v, s16 + 16 * i, 16);
+            d16[i] = v;
         }
+        for (uint64_t i = head + n16 * 16 + threadIdx.x; i < p.len; i += blockDim.x) d[i] = src[i];
     }
 }
 
