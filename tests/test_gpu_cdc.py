@@ -538,6 +538,30 @@ def test_blob_dedup_vs_hashlib(gpu):
     sh.close()
 
 
+@pytest.mark.parametrize("n", [1_000_000, 999_983])
+def test_blob_dedup_c5_size(gpu, n):
+    """vs_blob_dedup at C5's own batch size (1 M blob IDs drawn from n/2 distinct
+    ones, as the C5 bench makes them) and at an odd size: first occurrences and
+    the distinct count against numpy's first-index unique.  Some IDs share
+    their first 8 bytes (the sort key) but differ later."""
+    import torch
+    from volsync_amd import DeviceSha256
+    rng = np.random.default_rng(11)
+    distinct = rng.integers(0, 256, (n // 2, 32), dtype=np.uint8)
+    distinct[1::1000, :8] = distinct[0:-1:1000, :8][: len(distinct[1::1000])]
+    ids_h = distinct[rng.integers(0, len(distinct), n)]
+    _, first_idx, inv = np.unique(ids_h.view(np.dtype((np.void, 32))).ravel(),
+                                  return_index=True, return_inverse=True)
+    want_first = first_idx[inv.ravel()]
+    ids = torch.from_numpy(ids_h).cuda()
+    first = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    sh = DeviceSha256()
+    for _ in range(2):    # the second call reuses the scratch
+        assert sh.dedup(ids.data_ptr(), n, first.data_ptr()) == len(first_idx)
+        assert np.array_equal(first.cpu().numpy(), want_first)
+    sh.close()
+
+
 def test_sha256_blocks_syncthing(gpu):
     """syncthing's scanner blocks: SHA-256 of every block of a
     device buffer, for the block size lib/protocol picks and a larger one,

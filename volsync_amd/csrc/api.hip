@@ -1322,9 +1322,13 @@ VS_API int vs_blob_dedup(vs_sha *h, const uint8_t *dev_ids, size_t n, uint32_t *
     if (n > 0xffffffffull) return fail(VS_ERR_ARG, "more than 2^32 blobs per call");
     VS_HIP(hipSetDevice(h->device));
     const hipStream_t s = (hipStream_t)hip_stream;
-    VS_TRY(h->dd_tmp.ensure(dedup_tmp_bytes(std::max<size_t>(n, 1)) + 64));
-    unsigned long long *cnt = (unsigned long long *)((uint8_t *)h->dd_tmp.p + h->dd_tmp.cap - 64);
-    VS_HIP(launch_dedup(dev_ids, n, dev_first, h->dd_tmp.p, h->dd_tmp.cap - 64, cnt, s));
+    // the distinct-ID counter takes the first 256 bytes: dd_first_kernel adds
+    // to it with a 64-bit atomic, which faults unless 8-byte aligned (at the
+    // buffer's end it sat wherever the sort's scratch size left it)
+    VS_TRY(h->dd_tmp.ensure(dedup_tmp_bytes(std::max<size_t>(n, 1)) + 256));
+    unsigned long long *cnt = (unsigned long long *)h->dd_tmp.p;
+    VS_HIP(launch_dedup(dev_ids, n, dev_first, (uint8_t *)h->dd_tmp.p + 256, h->dd_tmp.cap - 256,
+                        cnt, s));
     if (n_unique) {
         if (!h->dd_pinned &&
             hipHostMalloc((void **)&h->dd_pinned, 64, hipHostMallocDefault) != hipSuccess) {

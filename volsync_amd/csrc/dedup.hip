@@ -80,6 +80,8 @@ size_t dedup_tmp_bytes(uint64_t n) {
 
 hipError_t launch_dedup(const uint8_t *ids, uint64_t n, uint32_t *first, void *tmp,
                         size_t tmp_bytes, unsigned long long *n_unique_dev, hipStream_t s) {
+    // the counter takes a 64-bit atomic: a misaligned one is a memory violation
+    if (((uintptr_t)n_unique_dev & 7) || ((uintptr_t)tmp & 7)) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(n_unique_dev, 0, 8, s);
     if (e != hipSuccess || !n) return e;
     uint8_t *t = (uint8_t *)tmp;
