@@ -103,6 +103,47 @@ def rsync_cpu_baseline(sample_bytes: int):
             "cpu": _cpu_model()}
 
 
+
+def dist_setup():
+    """(world, rank, local device index, torch device) of this rank, with the
+    process group up when world > 1: one GPU per rank over RCCL ("nccl").
+    VSGPU_BENCH_SHARED_GPU=1 is the one-GPU rehearsal of the N-rank device
+    path: every rank on cuda:0, collectives over gloo (each rank's buffers
+    must then fit beside the others': use a small --per-gpu-gib)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    shared = os.environ.get("VSGPU_BENCH_SHARED_GPU") == "1"
+    local = 0 if shared else int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    return world, rank, local, dev
+
+
+def coll_device(dev):
+    """Where collective operands live: the GPU under RCCL, the host under
+    gloo (the VSGPU_BENCH_SHARED_GPU rehearsal)."""
+    import torch.distributed as dist
+    return dev if dist.get_backend() == "nccl" else None
+
+
+def all_gather_any(outs, t):
+    """dist.all_gather of a device tensor under either backend (gloo: staged
+    through host memory)."""
+    import torch.distributed as dist
+    if dist.get_backend() == "nccl":
+        return dist.all_gather(outs, t)
+    host = [o.cpu() for o in outs]
+    dist.all_gather(host, t.cpu())
+    for o, h in zip(outs, host):
+        o.copy_(h)
+
 class C4Plan:
     """The C4 source file S as a function of the destination D: D (synthetic
     stream, seed 4) with `frac` of its blocks edited (seed 5) -- a third each
@@ -186,13 +227,7 @@ def rsync_main(args):
     from volsync_amd.rsync_shard import (BlockShard, SourceShard, gather_sums, run_walk_shard,
                                          torch_pair_collectives)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    world, rank, local, dev = dist_setup()
     per = int(args.per_gpu_gib * (1 << 30))
     dtotal = per * world
     hdr = sum_sizes_sqroot(dtotal)
@@ -211,7 +246,7 @@ def rsync_main(args):
     m = Matcher(local)
     m.set_stream(stream)
     seed = 0x5EED5EED
-    coll = torch_pair_collectives(dev) if world > 1 else (lambda p: [p], lambda x: x)
+    coll = torch_pair_collectives(coll_device(dev)) if world > 1 else (lambda p: [p], lambda x: x)
     xst = {}
 
     def step():
@@ -219,7 +254,7 @@ def rsync_main(args):
                             s1.data_ptr(), s2.data_ptr())
         f1, f2 = s1, s2
         if world > 1:
-            f1, f2 = gather_sums(s1, s2, shard, hdr.s2length, dist.all_gather)
+            f1, f2 = gather_sums(s1, s2, shard, hdr.s2length, all_gather_any)
         m.load_sums_device(hdr.count, hdr.blength, hdr.s2length, hdr.remainder, f1.data_ptr(),
                            f2.data_ptr(), CSUM_XXH3_128, seed)
         return run_walk_shard(m, sspec, ds.data_ptr(), *coll, stats=xst)
@@ -244,10 +279,10 @@ def rsync_main(args):
     kt = m.kernel_time()
     st = m.stats()
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        c = torch.tensor([nm], dtype=torch.int64, device=dev)
+        c = torch.tensor([nm], dtype=torch.int64, device=coll_device(dev))
         dist.all_reduce(c)
         nm = int(c.item())
     value = (dtotal + plan.total) * args.steps / dt / 1e9
@@ -304,6 +339,7 @@ def rsync_main(args):
             "stages_ms_per_step": {k: round(v / args.steps, 3) for k, v in stages.items()},
             "match_stats": st,
             "rccl_world_size": dist.get_world_size() if world > 1 else 1,
+            "dist_backend": dist.get_backend() if world > 1 else None,
             "exchange_rounds_last_step": xst.get("exchange_rounds", 0),
             "file_sum": fsum,
         }
@@ -361,13 +397,7 @@ def smallfiles_main(args):
     import torch.distributed as dist
     from volsync_amd import DeviceSha256, synth_fill_device
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    world, rank, local, dev = dist_setup()
     nf, npay = args.files, max(1, args.files // 2)
     rng = np.random.default_rng(6 + rank)
     psize = rng.integers(4096, 65537, npay)
@@ -432,7 +462,7 @@ def smallfiles_main(args):
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     # kernel time: the hash launches ran on `stream` between the two events
@@ -510,13 +540,7 @@ def seal_main(args):
     import torch.distributed as dist
     from volsync_amd import Sealer, synth_fill_device
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    world, rank, local, dev = dist_setup()
     target = int(args.per_gpu_gib * (1 << 30))
     rng = np.random.default_rng(11 + rank)
     sizes = np.minimum((512 << 10) + rng.exponential(1 << 20, target // (1 << 20) + 16).astype(np.int64),
@@ -564,7 +588,7 @@ def seal_main(args):
     ctr_ms, mac_ms, runs = sl.kernel_ms()
     sl.close()
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ctr_ms, mac_ms = ctr_ms / max(runs, 1), mac_ms / max(runs, 1)
@@ -593,6 +617,13 @@ def seal_main(args):
                          "avg_launch_ms": kern[dom]["avg_launch_ms"]},
             "kernels": kern,
         }
+        try:
+            tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+            r = tj["seal_" + dom]
+            res["roofline"]["traffic"] = round(r["bytes_per_plain_byte"] * total)
+            res["roofline"]["traffic_source"] = r["source"]
+        except (OSError, ValueError, KeyError):
+            pass
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = seal_cpu_baseline(sizes, keys, 32 << 30,
                                                     args.cpu_threads)
@@ -861,13 +892,7 @@ def main():
     from volsync_amd import DeviceChunker, MaxSize, MinSize, TestPol, synth_fill_device
     from volsync_amd.shard import ShardSpec, run_shard, torch_collectives
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    world, rank, local, dev = dist_setup()
 
     per = int(args.per_gpu_gib * (1 << 30))
     total = per * world
@@ -886,7 +911,7 @@ def main():
         one = torch.cuda.Stream(dev)
         dc.set_stream(one.cuda_stream)
         dc.set_hash_stream(one.cuda_stream)
-    coll = torch_collectives(dev) if world > 1 else None
+    coll = torch_collectives(coll_device(dev)) if world > 1 else None
     xst = {}
 
     def step():
@@ -927,10 +952,10 @@ def main():
     lat = time.perf_counter() - t1
     iso_ms, iso_launch = dc.timing(False)
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        c = torch.tensor([nch], dtype=torch.int64, device=dev)
+        c = torch.tensor([nch], dtype=torch.int64, device=coll_device(dev))
         dist.all_reduce(c)
         nch = int(c.item())
 
@@ -1016,6 +1041,7 @@ def main():
             "hash_wide": args.hash_wide, "wide_drain": args.wide_drain,
             "sha_slices": launches[2],
             "rccl_world_size": dist.get_world_size() if world > 1 else 1,
+            "dist_backend": dist.get_backend() if world > 1 else None,
             "exchange_rounds_last_step": xst.get("exchange_rounds", 0),
             "single_volume": {"ms": round(lat * 1e3, 2),
                               "GBps": round(total / lat / 1e9, 2),

@@ -350,6 +350,12 @@ struct RsWalkArgs {
     uint64_t *prof;                  // VSGPU_WALK_PROF: per-wave phase cycles/counts [waves][16]
 };
 hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t s);
+// the final walks' match list in order as 16-byte vs_match records (offset,
+// block index, 0): cnt [nseg], pos [nseg + 1] (pos[nseg] = length),
+// partials >= nseg / 4096 + 2, out >= nseg * cap records; *fa_total = the
+// false alarms of the final walks
+hipError_t launch_rs_collect(const RsWalkArgs &a, uint32_t *cnt, uint32_t *pos, uint32_t *partials,
+                             uint4 *out, unsigned long long *fa_total, hipStream_t s);
 hipError_t launch_rs_pad_sum2(const uint8_t *sum2, uint32_t count, uint32_t s2length,
                               uint64_t *out, hipStream_t s);
 // whole-file checksum (filesum.hip): out = sum_end's digest of p[0, len);

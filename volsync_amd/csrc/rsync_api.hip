@@ -111,7 +111,10 @@ struct vs_rsync {
     int csum_type = 0;
     uint32_t seed = 0;
     uint32_t dbits = 0, fbits = 0;
-    std::vector<uint32_t> sum1;     // host copies for the walk
+    // host copies for the host walk and the short-last-block tail, fetched
+    // from the device table only when one of them runs (host_tables)
+    bool host_ok = false;
+    std::vector<uint32_t> sum1;
     std::vector<uint8_t> sum2;
     std::vector<uint64_t> tkey_h;   // sorted (sum1 << 32 | ~i)
     std::vector<uint32_t> dir_h;
@@ -142,6 +145,10 @@ struct vs_rsync {
     int32_t st_rounds = 0;
     double ms[5] = {0, 0, 0, 0, 0};
     uint64_t *pinned = nullptr;
+    // device walk's compacted match list (walk_collect)
+    DevBuf wc_cnt, wc_pos, wc_part, wc_out;
+    vs_match *wc_host = nullptr;    // pinned read-back
+    size_t wc_host_cap = 0;
 };
 
 namespace {
@@ -262,16 +269,39 @@ int build_table(vs_rsync *h) {
                            h->d_tkey.as<uint64_t>(), h->d_tmp.p, h->d_tmp.cap, h->dbits,
                            h->d_dir.as<uint32_t>(), h->fbits, h->d_filt.as<uint32_t>(),
                            h->stream));
+    VS_HIP(hipStreamSynchronize(h->stream));
+    h->host_ok = false;
+    h->loaded = true;
+    return 0;
+}
+
+// The table's host copies (sorted keys, directory, sum1, sum2 rows), read
+// back once per loaded table and only by the paths that walk on the host: the
+// device walk never needs them, and reading ~4 x count x 4 B through pageable
+// copies cost the C4 step ~14 ms.
+int host_tables(vs_rsync *h) {
+    if (h->host_ok) return 0;
+    const size_t count = (size_t)std::max(h->count, 0);
+    const size_t s2 = (size_t)h->s2length;
     h->tkey_h.resize(count);
     h->dir_h.resize((1ull << h->dbits) + 1);
+    h->sum1.resize(count);
+    h->sum2.resize(count * s2);
+    std::vector<uint64_t> pad(count * 2);
     if (count) {
-        VS_HIP(hipMemcpyAsync(h->tkey_h.data(), h->d_tkey.p, (size_t)count * 8,
-                              hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync(h->tkey_h.data(), h->d_tkey.p, count * 8, hipMemcpyDeviceToHost,
+                              h->stream));
         VS_HIP(hipMemcpyAsync(h->dir_h.data(), h->d_dir.p, h->dir_h.size() * 4,
                               hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync(h->sum1.data(), h->d_sum1.p, count * 4, hipMemcpyDeviceToHost,
+                              h->stream));
+        VS_HIP(hipMemcpyAsync(pad.data(), h->d_sum2p.p, count * 16, hipMemcpyDeviceToHost,
+                              h->stream));
     }
     VS_HIP(hipStreamSynchronize(h->stream));
-    h->loaded = true;
+    // d_sum2p rows are the strong sums zero-padded to 16 bytes
+    for (size_t i = 0; i < count; ++i) memcpy(h->sum2.data() + i * s2, pad.data() + 2 * i, s2);
+    h->host_ok = true;
     return 0;
 }
 
@@ -762,6 +792,7 @@ int walk_tail(vs_rsync *h, int64_t x, int32_t xw, int64_t *exit_off, int32_t *ex
         fprintf(stderr, "rs: walk tail: device exit %lld want %d, tail offset %lld, range end %lld\n",
                 (long long)x, xw, (long long)t, (long long)hi);
     if (h->remainder && o <= t && t < hi && t >= 0) {
+        VS_TRY(host_tables(h));
         std::vector<uint8_t> buf((size_t)h->remainder);
         VS_HIP(hipMemcpyAsync(buf.data(), r.dev + t, buf.size(), hipMemcpyDeviceToHost, h->stream));
         VS_HIP(hipStreamSynchronize(h->stream));
@@ -942,40 +973,55 @@ int walk_scan(vs_rsync *h) {
     return 0;
 }
 
-// the device walk's result (matches data-relative, in order) and false alarms
+// the device walk's result (matches data-relative, in order) and false alarms:
+// compacted on the device (launch_rs_collect), read back through pinned memory
 int walk_collect(vs_rsync *h, std::vector<vs_match> &out, int64_t *fa) {
     RsRun &r = h->run;
     const RsWalkArgs &a = r.wa;
     const size_t ns = a.nseg, nc = ns * a.cap;
-    std::vector<uint32_t> sn(ns), fn(ns), ff(ns);
-    std::vector<uint64_t> ffa(ns);
     out.clear();
-    int64_t total = 0;
+    int64_t total_fa = 0;
     if (ns) {
-        std::vector<int64_t> so(nc), fo(nc);
-        std::vector<int32_t> si(nc), fi(nc);
-        VS_HIP(hipMemcpyAsync(sn.data(), a.spec_n, ns * 4, hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipMemcpyAsync(fn.data(), a.fin_n, ns * 4, hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipMemcpyAsync(ff.data(), a.fin_from, ns * 4, hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipMemcpyAsync(ffa.data(), a.fin_fa, ns * 8, hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipMemcpyAsync(so.data(), a.spec_off, nc * 8, hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipMemcpyAsync(si.data(), a.spec_idx, nc * 4, hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipMemcpyAsync(fo.data(), a.fin_off, nc * 8, hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipMemcpyAsync(fi.data(), a.fin_idx, nc * 4, hipMemcpyDeviceToHost, h->stream));
+        VS_TRY(h->wc_cnt.ensure(ns * 4));
+        VS_TRY(h->wc_pos.ensure((ns + 1) * 4 + 64));
+        VS_TRY(h->wc_part.ensure((ns / 4096 + 2) * 4));
+        VS_TRY(h->wc_out.ensure(nc * sizeof(vs_match)));
+        static_assert(sizeof(vs_match) == 16, "vs_match is one 16-byte record");
+        uint32_t *pos = h->wc_pos.as<uint32_t>();
+        // the false-alarm total: 8-byte aligned, after pos[0, ns]
+        unsigned long long *fat =
+            (unsigned long long *)(((uintptr_t)(pos + ns + 1) + 7) & ~(uintptr_t)7);
+        VS_HIP(launch_rs_collect(a, h->wc_cnt.as<uint32_t>(), pos, h->wc_part.as<uint32_t>(),
+                                 h->wc_out.as<uint4>(), fat, h->stream));
+        VS_HIP(hipMemcpyAsync(h->pinned, fat, 8, hipMemcpyDeviceToHost, h->stream));
+        VS_HIP(hipMemcpyAsync((uint32_t *)(h->pinned + 1), pos + ns, 4, hipMemcpyDeviceToHost,
+                              h->stream));
         VS_HIP(hipStreamSynchronize(h->stream));
-        for (size_t k = 0; k < ns; ++k) {
-            const size_t b = k * a.cap;
-            uint32_t from = 0;
-            if (ff[k] != 0xffffffffu) {
-                for (uint32_t j = 0; j < fn[k]; ++j) out.push_back({fo[b + j], fi[b + j], 0});
-                from = ff[k];
+        total_fa = (int64_t)h->pinned[0];
+        const size_t n = *(const uint32_t *)(h->pinned + 1);
+        if (n > nc) return fail(VS_ERR_STATE, "device walk: match list longer than its capacity");
+        if (n > h->wc_host_cap) {
+            if (h->wc_host) (void)hipHostFree(h->wc_host);
+            h->wc_host = nullptr;
+            h->wc_host_cap = 0;
+            const size_t want = std::max(n, nc);
+            if (hipHostMalloc((void **)&h->wc_host, want * sizeof(vs_match), hipHostMallocDefault) !=
+                hipSuccess) {
+                (void)hipGetLastError();
+                h->wc_host = nullptr;
+                return fail(VS_ERR_NOMEM, "pinned match read-back buffer");
             }
-            for (uint32_t j = from; j < sn[k]; ++j) out.push_back({so[b + j], si[b + j], 0});
-            total += (int64_t)ffa[k];
+            h->wc_host_cap = want;
         }
+        if (n) {
+            VS_HIP(hipMemcpyAsync(h->wc_host, h->wc_out.p, n * sizeof(vs_match),
+                                  hipMemcpyDeviceToHost, h->stream));
+            VS_HIP(hipStreamSynchronize(h->stream));
+        }
+        out.assign(h->wc_host, h->wc_host + n);
     }
     for (const vs_match &m : r.tail) out.push_back(m);
-    *fa = total + r.tail_fa;
+    *fa = total_fa + r.tail_fa;
     return 0;
 }
 
@@ -1022,6 +1068,7 @@ int match_scan(vs_rsync *h, const void *dev_src, int64_t dlen, int64_t origin, i
         r.spec_fa = fa;
     } else {
         VS_TRY(order_after_null(h));
+        VS_TRY(host_tables(h));
         std::vector<uint64_t> &batch = h->h_batch;
         VS_TRY(scan_candidates(h, batch));
         WalkState ws;
@@ -1161,9 +1208,11 @@ VS_API void vs_rsync_close(vs_rsync *h) {
                       &h->w_spec_fab, &h->w_spec_n, &h->w_spec_fa, &h->w_spec_exit,
                       &h->w_spec_exitw, &h->w_fin_entry, &h->w_fin_entryw, &h->w_fin_from,
                       &h->w_fin_n, &h->w_fin_fa, &h->w_fin_off, &h->w_fin_idx, &h->w_fin_fab,
-                      &h->w_exit[0], &h->w_exit[1], &h->w_exitw[0], &h->w_exitw[1], &h->w_ctl, &h->w_prof, &h->fs_scratch, &h->fs_out, &h->rc_pieces})
+                      &h->w_exit[0], &h->w_exit[1], &h->w_exitw[0], &h->w_exitw[1], &h->w_ctl, &h->w_prof, &h->fs_scratch, &h->fs_out, &h->rc_pieces,
+                      &h->wc_cnt, &h->wc_pos, &h->wc_part, &h->wc_out})
         b->release();
     if (h->pinned) (void)hipHostFree(h->pinned);
+    if (h->wc_host) (void)hipHostFree(h->wc_host);
     for (HostReg *r : {&h->reg_off, &h->reg_sum, &h->reg_flag}) r->release();
     if (h->ev_null) (void)hipEventDestroy(h->ev_null);
     for (hipEvent_t e : h->kev)
@@ -1212,8 +1261,6 @@ VS_API int vs_rsync_load_sums(vs_rsync *h, int32_t count, int32_t blength, int32
     if (count && (!sum1 || !sum2)) return fail(VS_ERR_ARG, "null sum arrays");
     VS_TRY(rs_dev(h));
     const double t0 = now_ms();
-    h->sum1.assign(sum1, sum1 + count);
-    h->sum2.assign(sum2, sum2 + (size_t)count * s2length);
     VS_TRY(h->d_sum1.ensure((size_t)std::max(count, 1) * 4));
     VS_TRY(h->d_sum2p.ensure((size_t)std::max(count, 1) * 16));
     VS_TRY(h->d_sum2tmp.ensure((size_t)std::max(count, 1) * s2length));
@@ -1239,18 +1286,11 @@ VS_API int vs_rsync_load_sums_device(vs_rsync *h, int32_t count, int32_t blength
     if (count && (!dev_sum1 || !dev_sum2)) return fail(VS_ERR_ARG, "null sum arrays");
     VS_TRY(rs_dev(h));
     const double t0 = now_ms();
-    h->sum1.resize(count);
-    h->sum2.resize((size_t)count * s2length);
     VS_TRY(h->d_sum1.ensure((size_t)std::max(count, 1) * 4));
     VS_TRY(order_after_null(h));
-    if (count) {
+    if (count)
         VS_HIP(hipMemcpyAsync(h->d_sum1.p, dev_sum1, (size_t)count * 4, hipMemcpyDeviceToDevice,
                               h->stream));
-        VS_HIP(hipMemcpyAsync(h->sum1.data(), dev_sum1, (size_t)count * 4,
-                              hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipMemcpyAsync(h->sum2.data(), dev_sum2, h->sum2.size(), hipMemcpyDeviceToHost,
-                              h->stream));
-    }
     VS_TRY(h->d_sum2p.ensure((size_t)std::max(count, 1) * 16));
     if (count)
         VS_HIP(launch_rs_pad_sum2(dev_sum2, (uint32_t)count, (uint32_t)s2length,

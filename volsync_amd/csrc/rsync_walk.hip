@@ -868,6 +868,64 @@ hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t
     return hipGetLastError();
 }
 
+// ---- the walk's match list, compacted on the device ------------------------------
+// Segment k's final walk is fin[0, fin_n) then spec[fin_from, spec_n) when it
+// was re-walked (fin_from != ~0), else spec[0, spec_n): its match count, then
+// (after an exclusive scan) its matches at their list positions as 16-byte
+// vs_match records (offset, block index, 0), and the false-alarm total.
+__device__ __forceinline__ uint32_t seg_from(const RsWalkArgs &a, uint32_t k, uint32_t &nf) {
+    const uint32_t ff = a.fin_from[k];
+    nf = ff != 0xffffffffu ? a.fin_n[k] : 0u;
+    return ff != 0xffffffffu ? ff : 0u;
+}
+
+__global__ void rs_collect_count_kernel(RsWalkArgs a, uint32_t *cnt) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.nseg) return;
+    uint32_t nf;
+    const uint32_t from = seg_from(a, k, nf);
+    const uint32_t sn = a.spec_n[k];
+    cnt[k] = nf + (sn > from ? sn - from : 0u);
+}
+
+__global__ void rs_collect_kernel(RsWalkArgs a, const uint32_t *pos, uint4 *out,
+                                  unsigned long long *fa_total) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long fa = 0;
+    if (k < a.nseg) {
+        uint32_t nf;
+        const uint32_t from = seg_from(a, k, nf);
+        const uint64_t b = (uint64_t)k * a.cap;
+        uint4 *o = out + pos[k];
+        for (uint32_t j = 0; j < nf; ++j) {
+            const uint64_t off = (uint64_t)a.fin_off[b + j];
+            *o++ = make_uint4((uint32_t)off, (uint32_t)(off >> 32), (uint32_t)a.fin_idx[b + j], 0u);
+        }
+        for (uint32_t j = from; j < a.spec_n[k]; ++j) {
+            const uint64_t off = (uint64_t)a.spec_off[b + j];
+            *o++ = make_uint4((uint32_t)off, (uint32_t)(off >> 32), (uint32_t)a.spec_idx[b + j], 0u);
+        }
+        fa = a.fin_fa[k];
+    }
+    // one 64-bit atomic per wave
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) fa += __shfl_xor(fa, d, 64);
+    if ((threadIdx.x & 63) == 0 && fa) atomicAdd(fa_total, fa);
+}
+
+hipError_t launch_rs_collect(const RsWalkArgs &a, uint32_t *cnt, uint32_t *pos, uint32_t *partials,
+                             uint4 *out, unsigned long long *fa_total, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(fa_total, 0, 8, s);
+    if (e != hipSuccess || !a.nseg) return e;
+    const uint32_t blocks = (a.nseg + 255) / 256;
+    rs_collect_count_kernel<<<blocks, 256, 0, s>>>(a, cnt);
+    // pos[0, nseg] exclusive; pos[nseg] = the list length
+    e = launch_scan_u32(cnt, pos, a.nseg, partials, 0xffffffffu, s);
+    if (e != hipSuccess) return e;
+    rs_collect_kernel<<<blocks, 256, 0, s>>>(a, pos, out, fa_total);
+    return hipGetLastError();
+}
+
 hipError_t launch_rs_pad_sum2(const uint8_t *sum2, uint32_t count, uint32_t s2length,
                               uint64_t *out, hipStream_t s) {
     if (!count) return hipSuccess;
