@@ -13,6 +13,15 @@ from oracle import seal_ref as S
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["fused", "separate"])
+def seal_variant(request, monkeypatch):
+    """Every test runs on both launch paths: the MAC fused into the CTR pass
+    (default: per-lane Horner sums lifted by r^e and added per blob) and the
+    separate CTR + one-wave-per-blob MAC kernels (VSGPU_SEAL_FUSED=0)."""
+    monkeypatch.setenv("VSGPU_SEAL_FUSED", "1" if request.param == "fused" else "0")
+    return request.param
+
+
 def _keys(seed):
     rng = np.random.default_rng(seed)
     return tuple(rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (32, 16, 16))

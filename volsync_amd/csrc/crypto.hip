@@ -105,6 +105,183 @@ __device__ __forceinline__ uint64_t find_blob(const uint64_t *prefix, uint64_t n
     return lo;
 }
 
+// ---- Poly1305 in five 26-bit limbs ------------------------------------------
+struct L5 {
+    uint32_t v[5];
+};
+constexpr uint32_t kM26 = 0x3ffffff;
+
+// h * r mod 2^130 - 5, h limbs < 2^27, r limbs < 2^26 (s = 5 r)
+__device__ __forceinline__ L5 pmul(const L5 &h, const L5 &r) {
+    const uint32_t s1 = r.v[1] * 5, s2 = r.v[2] * 5, s3 = r.v[3] * 5, s4 = r.v[4] * 5;
+    const uint64_t h0 = h.v[0], h1 = h.v[1], h2 = h.v[2], h3 = h.v[3], h4 = h.v[4];
+    uint64_t d0 = h0 * r.v[0] + h1 * s4 + h2 * s3 + h3 * s2 + h4 * s1;
+    uint64_t d1 = h0 * r.v[1] + h1 * r.v[0] + h2 * s4 + h3 * s3 + h4 * s2;
+    uint64_t d2 = h0 * r.v[2] + h1 * r.v[1] + h2 * r.v[0] + h3 * s4 + h4 * s3;
+    uint64_t d3 = h0 * r.v[3] + h1 * r.v[2] + h2 * r.v[1] + h3 * r.v[0] + h4 * s4;
+    uint64_t d4 = h0 * r.v[4] + h1 * r.v[3] + h2 * r.v[2] + h3 * r.v[1] + h4 * r.v[0];
+    L5 o;
+    d1 += d0 >> 26;
+    o.v[0] = (uint32_t)d0 & kM26;
+    d2 += d1 >> 26;
+    o.v[1] = (uint32_t)d1 & kM26;
+    d3 += d2 >> 26;
+    o.v[2] = (uint32_t)d2 & kM26;
+    d4 += d3 >> 26;
+    o.v[3] = (uint32_t)d3 & kM26;
+    const uint64_t c = d4 >> 26;
+    o.v[4] = (uint32_t)d4 & kM26;
+    const uint64_t t = (uint64_t)o.v[0] + c * 5;
+    o.v[0] = (uint32_t)t & kM26;
+    o.v[1] += (uint32_t)(t >> 26);
+    return o;
+}
+
+// 16 message bytes (n < 16: the partial final block, 0x01 appended)
+__device__ __forceinline__ void absorb(L5 &h, const uint8_t *p, uint32_t n) {
+    uint32_t t[4] = {0, 0, 0, 0};
+    uint32_t hib = 1u << 24;
+    if (n == 16) {
+        __builtin_memcpy(t, p, 16);
+    } else {
+        uint8_t b[16] = {0};
+        for (uint32_t i = 0; i < n; ++i) b[i] = p[i];
+        b[n] = 1;
+        __builtin_memcpy(t, b, 16);
+        hib = 0;
+    }
+    h.v[0] += t[0] & kM26;
+    h.v[1] += ((t[0] >> 26) | (t[1] << 6)) & kM26;
+    h.v[2] += ((t[1] >> 20) | (t[2] << 12)) & kM26;
+    h.v[3] += ((t[2] >> 14) | (t[3] << 18)) & kM26;
+    h.v[4] += (t[3] >> 8) | hib;
+}
+
+// absorb one block given as four little-endian words (n < 16: the partial
+// final block, its bytes past n zero; 0x01 goes at byte n)
+__device__ __forceinline__ void absorb_words(L5 &h, uint32_t (&t)[4], uint32_t n) {
+    uint32_t hib = 1u << 24;
+    if (n < 16) {
+        t[n >> 2] |= 1u << (8 * (n & 3));
+        hib = 0;
+    }
+    h.v[0] += t[0] & kM26;
+    h.v[1] += ((t[0] >> 26) | (t[1] << 6)) & kM26;
+    h.v[2] += ((t[1] >> 20) | (t[2] << 12)) & kM26;
+    h.v[3] += ((t[2] >> 14) | (t[3] << 18)) & kM26;
+    h.v[4] += (t[3] >> 8) | hib;
+}
+
+__device__ __forceinline__ L5 ld_l5(const uint32_t *p) {
+    L5 r;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) r.v[i] = p[i];
+    return r;
+}
+
+__device__ __forceinline__ uint64_t wsum64(uint64_t v) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+        v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+
+// the tag: limb sums d (any size below 2^63) reduced mod 2^130 - 5, plus the
+// four words of s, mod 2^128, written as 16 little-endian bytes
+__device__ __forceinline__ void poly_final(uint64_t (&d)[5], const uint32_t (&s)[4], uint8_t *mac) {
+    for (int pass = 0; pass < 3; ++pass) {
+        for (int i = 0; i < 4; ++i) {
+            d[i + 1] += d[i] >> 26;
+            d[i] &= kM26;
+        }
+        d[0] += (d[4] >> 26) * 5;
+        d[4] &= kM26;
+    }
+    d[1] += d[0] >> 26;
+    d[0] &= kM26;
+    uint32_t h0 = (uint32_t)d[0], h1 = (uint32_t)d[1], h2 = (uint32_t)d[2], h3 = (uint32_t)d[3],
+             h4 = (uint32_t)d[4];
+    // h - p = h + 5 - 2^130: keep it when it does not borrow
+    uint32_t g0 = h0 + 5, cc = g0 >> 26;
+    g0 &= kM26;
+    uint32_t g1 = h1 + cc;
+    cc = g1 >> 26;
+    g1 &= kM26;
+    uint32_t g2 = h2 + cc;
+    cc = g2 >> 26;
+    g2 &= kM26;
+    uint32_t g3 = h3 + cc;
+    cc = g3 >> 26;
+    g3 &= kM26;
+    const uint32_t g4 = h4 + cc - (1u << 26);
+    if ((g4 >> 31) == 0) {
+        h0 = g0;
+        h1 = g1;
+        h2 = g2;
+        h3 = g3;
+        h4 = g4;
+    }
+    // (h + s) mod 2^128, packing the limbs by addition so a limb that is not
+    // fully normalised (h1 = 2^26) still lands right
+    uint64_t f = (uint64_t)h0 + ((uint64_t)h1 << 26) + s[0];
+    uint32_t o[4];
+    o[0] = (uint32_t)f;
+    f = (f >> 32) + ((uint64_t)h2 << 20) + s[1];
+    o[1] = (uint32_t)f;
+    f = (f >> 32) + ((uint64_t)h3 << 14) + s[2];
+    o[2] = (uint32_t)f;
+    f = (f >> 32) + ((uint64_t)h4 << 8) + s[3];
+    o[3] = (uint32_t)f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mac[i] = (uint8_t)(o[i >> 2] >> (8 * (i & 3)));
+}
+
+// h * r^e (e >= 1): r^u from the r^1..r^64 table (e = 64 t + u, u in 1..64),
+// then r^(64 t) by the binary expansion of t over r^(64 * 2^j)
+__device__ __noinline__ L5 lift(L5 h, uint64_t e, const SealArgs &a) {
+    const uint64_t u = ((e - 1) & 63) + 1;
+    uint64_t t = (e - u) >> 6;
+    h = pmul(h, ld_l5(a.rpow + (u - 1) * 5));
+    for (int j = 0; t && j < kSealSq; ++j, t >>= 1)
+        if (t & 1) h = pmul(h, ld_l5(a.rsq + j * 5));
+    return h;
+}
+
+// The fused MAC's flush: each flushing lane lifts its Horner sum h (blocks
+// last, last-64, ... of blob `blob`, 1-based `last`) to the blocks' final
+// weights r^(N - i + 1) and adds the limbs into acc[blob]; when every
+// flushing lane holds the same blob (a blob's end, a range's end) the wave
+// adds them first and one lane issues the five atomics.  Called by the whole
+// wave.
+__device__ __forceinline__ void mac_flush(const SealArgs &a, const L5 &h, uint64_t blob,
+                                          uint64_t last, bool fl, uint32_t lane) {
+    const uint64_t m = __ballot(fl);
+    if (!m) return;
+    uint64_t v[5] = {0, 0, 0, 0, 0};
+    if (fl) {
+        const uint64_t N = a.prefix[blob + 1] - a.prefix[blob];
+        const L5 x = lift(h, N - last + 1, a);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) v[i] = x.v[i];
+    }
+    const int first = __builtin_ctzll(m);
+    const uint64_t b0 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(blob >> 32), first, 64) << 32) |
+                        (uint32_t)__shfl((int)(uint32_t)blob, first, 64);
+    if (__ballot(fl && blob != b0) == 0) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const uint64_t t = wsum64(v[i]);
+            if (lane == (uint32_t)first) atomicAdd(a.acc + 5 * b0 + i, (unsigned long long)t);
+        }
+    } else if (fl) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) atomicAdd(a.acc + 5 * blob + i, (unsigned long long)v[i]);
+    }
+}
+
 // ---- CTR: two T-tables with the byte index written by SDWA ------------------
 // LDS row e (256 B) = [T0[e] x 32 lane copies | T1[e] = rotl8(T0[e]) x 32], so
 // lookup (byte x, table k, lane copy c) is at x * 256 + k * 128 + c * 4: bank
@@ -180,9 +357,10 @@ __device__ __forceinline__ void aes256_tab(uint32_t (&s)[NB][4], uint32_t (&ix)[
 // per-lane search runs only for steps that straddle a blob boundary.
 // kCtrPer blocks per lane per step (ILP); two workgroups per CU (64 KiB of
 // tables each), WPE waves per SIMD
-template <int kCtrPer, int kThreads, int WPE>
+template <int kCtrPer, int kThreads, int WPE, bool MAC = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 void seal_ctr_kernel(SealArgs a) {
+    static_assert(!MAC || kCtrPer == 1, "the fused MAC takes one block per lane per step");
     __shared__ uint32_t tab[kCtrWords];
     for (uint32_t i = threadIdx.x; i < kCtrWords; i += blockDim.x) {
         const uint32_t t = a.te0[i >> 6];
@@ -203,6 +381,12 @@ void seal_ctr_kernel(SealArgs a) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) ix[b][i] = c4 + (i & 1) * 128;
     uint64_t blob = find_blob(a.prefix, a.n, s0 * kStep);
+    // fused MAC (MAC): this lane's Horner sum over the ciphertext blocks it
+    // sealed of blob mb (blocks 64 apart, the last one 1-based mlast)
+    L5 mh{{0, 0, 0, 0, 0}};
+    uint64_t mb = ~0ull, mlast = 0;
+    L5 r64{{0, 0, 0, 0, 0}};
+    if constexpr (MAC) r64 = ld_l5(a.rpow + 63 * 5);
     for (uint64_t st = s0; st < s1; ++st) {
         const uint64_t g0 = st * kStep;
         const uint64_t glast = min(g0 + kStep - 1, a.total_blocks - 1);
@@ -211,6 +395,7 @@ void seal_ctr_kernel(SealArgs a) {
         uint32_t s[kCtrPer][4];
         uint64_t off[kCtrPer];
         uint32_t nb[kCtrPer];
+        uint64_t lb = blob, lq = 0;   // this lane's blob and block (MAC, kCtrPer == 1)
         if (one) {
             // the usual case: the whole step lies in one blob, so its
             // metadata is wave-uniform (scalar loads)
@@ -225,6 +410,7 @@ void seal_ctr_kernel(SealArgs a) {
                 off[b] = ob + 16 * q;
                 nb[b] = g < a.total_blocks ? (uint32_t)min<uint64_t>(16, len - 16 * q) : 0;
                 ctr_block(nn, q, s[b]);
+                lq = q;
             }
         } else {
 #pragma unroll
@@ -239,6 +425,8 @@ void seal_ctr_kernel(SealArgs a) {
                 uint32_t nn[4];
                 load_nonce(a.nonces, bi, nn);
                 ctr_block(nn, q, s[b]);
+                lb = bi;
+                lq = q;
             }
         }
         // plaintext loaded before the rounds so its latency hides behind them
@@ -249,80 +437,63 @@ void seal_ctr_kernel(SealArgs a) {
         aes256_tab<kCtrPer>(s, ix, tab, a.rk256);
 #pragma unroll
         for (int b = 0; b < (int)kCtrPer; ++b) {
+            uint32_t ct[4] = {0, 0, 0, 0};   // the ciphertext block, zero-padded (MAC)
             if (nb[b] == 16) {
                 v[b].x ^= s[b][0];
                 v[b].y ^= s[b][1];
                 v[b].z ^= s[b][2];
                 v[b].w ^= s[b][3];
                 __builtin_memcpy(a.out + off[b], &v[b], 16);
+                ct[0] = v[b].x;
+                ct[1] = v[b].y;
+                ct[2] = v[b].z;
+                ct[3] = v[b].w;
             } else {
-                for (uint32_t i = 0; i < nb[b]; ++i)
-                    a.out[off[b] + i] = a.in[off[b] + i] ^ (uint8_t)(s[b][i >> 2] >> (8 * (i & 3)));
+                for (uint32_t i = 0; i < nb[b]; ++i) {
+                    const uint8_t c = a.in[off[b] + i] ^ (uint8_t)(s[b][i >> 2] >> (8 * (i & 3)));
+                    a.out[off[b] + i] = c;
+                    ct[i >> 2] |= (uint32_t)c << (8 * (i & 3));
+                }
+            }
+            if constexpr (MAC) {
+                // a lane whose block starts another blob hands its sum over
+                const bool act = nb[b] > 0;
+                mac_flush(a, mh, mb, mlast, act && lb != mb && mb != ~0ull, lane);
+                if (act) {
+                    if (lb != mb) {
+                        mh = L5{{0, 0, 0, 0, 0}};
+                        mb = lb;
+                    } else {
+                        mh = pmul(mh, r64);
+                    }
+                    absorb_words(mh, ct, nb[b]);
+                    mlast = lq + 1;
+                }
             }
         }
     }
+    if constexpr (MAC) mac_flush(a, mh, mb, mlast, mb != ~0ull, lane);
 }
 
-// ---- Poly1305 in five 26-bit limbs ------------------------------------------
-struct L5 {
-    uint32_t v[5];
-};
-constexpr uint32_t kM26 = 0x3ffffff;
-
-// h * r mod 2^130 - 5, h limbs < 2^27, r limbs < 2^26 (s = 5 r)
-__device__ __forceinline__ L5 pmul(const L5 &h, const L5 &r) {
-    const uint32_t s1 = r.v[1] * 5, s2 = r.v[2] * 5, s3 = r.v[3] * 5, s4 = r.v[4] * 5;
-    const uint64_t h0 = h.v[0], h1 = h.v[1], h2 = h.v[2], h3 = h.v[3], h4 = h.v[4];
-    uint64_t d0 = h0 * r.v[0] + h1 * s4 + h2 * s3 + h3 * s2 + h4 * s1;
-    uint64_t d1 = h0 * r.v[1] + h1 * r.v[0] + h2 * s4 + h3 * s3 + h4 * s2;
-    uint64_t d2 = h0 * r.v[2] + h1 * r.v[1] + h2 * r.v[0] + h3 * s4 + h4 * s3;
-    uint64_t d3 = h0 * r.v[3] + h1 * r.v[2] + h2 * r.v[1] + h3 * r.v[0] + h4 * s4;
-    uint64_t d4 = h0 * r.v[4] + h1 * r.v[3] + h2 * r.v[2] + h3 * r.v[1] + h4 * r.v[0];
-    L5 o;
-    d1 += d0 >> 26;
-    o.v[0] = (uint32_t)d0 & kM26;
-    d2 += d1 >> 26;
-    o.v[1] = (uint32_t)d1 & kM26;
-    d3 += d2 >> 26;
-    o.v[2] = (uint32_t)d2 & kM26;
-    d4 += d3 >> 26;
-    o.v[3] = (uint32_t)d3 & kM26;
-    const uint64_t c = d4 >> 26;
-    o.v[4] = (uint32_t)d4 & kM26;
-    const uint64_t t = (uint64_t)o.v[0] + c * 5;
-    o.v[0] = (uint32_t)t & kM26;
-    o.v[1] += (uint32_t)(t >> 26);
-    return o;
-}
-
-// 16 message bytes (n < 16: the partial final block, 0x01 appended)
-__device__ __forceinline__ void absorb(L5 &h, const uint8_t *p, uint32_t n) {
-    uint32_t t[4] = {0, 0, 0, 0};
-    uint32_t hib = 1u << 24;
-    if (n == 16) {
-        __builtin_memcpy(t, p, 16);
-    } else {
-        uint8_t b[16] = {0};
-        for (uint32_t i = 0; i < n; ++i) b[i] = p[i];
-        b[n] = 1;
-        __builtin_memcpy(t, b, 16);
-        hib = 0;
-    }
-    h.v[0] += t[0] & kM26;
-    h.v[1] += ((t[0] >> 26) | (t[1] << 6)) & kM26;
-    h.v[2] += ((t[1] >> 20) | (t[2] << 12)) & kM26;
-    h.v[3] += ((t[2] >> 14) | (t[3] << 18)) & kM26;
-    h.v[4] += (t[3] >> 8) | hib;
-}
-
-__device__ __forceinline__ uint64_t wsum64(uint64_t v) {
+// fused MAC, last step: per blob, the limb sums reduced mod 2^130 - 5, plus
+// s = AES-128(MACKey.K, nonce), mod 2^128
+__global__ __launch_bounds__(256) void seal_fin_kernel(SealArgs a) {
+    __shared__ uint32_t te[256 * kCopies];
+    __shared__ uint32_t rk[44];
+    load_te(te, a.te0);
+    if (threadIdx.x < 44) rk[threadIdx.x] = a.rk128[threadIdx.x];
+    __syncthreads();
+    const uint32_t c = threadIdx.x & (kCopies - 1);
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < a.n;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t d[5];
 #pragma unroll
-    for (int m = 1; m < 64; m <<= 1) {
-        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
-        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
-        v += ((uint64_t)hi << 32) | lo;
+        for (int i = 0; i < 5; ++i) d[i] = a.acc[5 * b + i];
+        uint32_t s[4];
+        load_nonce(a.nonces, b, s);
+        aes_encrypt(s, rk, 10, te, c);
+        poly_final(d, s, a.macs + 16 * b);
     }
-    return v;
 }
 
 __global__ __launch_bounds__(256) void seal_mac_kernel(SealArgs a) {
@@ -365,56 +536,10 @@ __global__ __launch_bounds__(256) void seal_mac_kernel(SealArgs a) {
         load_nonce(a.nonces, b, s);
         aes_encrypt(s, rk, 10, te, c);
         if (lane == 0) {
-            // carry the lane sums into limbs, reduce mod 2^130 - 5
             uint64_t d[5];
 #pragma unroll
             for (int i = 0; i < 5; ++i) d[i] = sumv[i];
-            for (int pass = 0; pass < 2; ++pass) {
-                for (int i = 0; i < 4; ++i) {
-                    d[i + 1] += d[i] >> 26;
-                    d[i] &= kM26;
-                }
-                d[0] += (d[4] >> 26) * 5;
-                d[4] &= kM26;
-            }
-            d[1] += d[0] >> 26;
-            d[0] &= kM26;
-            uint32_t h0 = (uint32_t)d[0], h1 = (uint32_t)d[1], h2 = (uint32_t)d[2],
-                     h3 = (uint32_t)d[3], h4 = (uint32_t)d[4];
-            // h - p = h + 5 - 2^130: keep it when it does not borrow
-            uint32_t g0 = h0 + 5, cc = g0 >> 26;
-            g0 &= kM26;
-            uint32_t g1 = h1 + cc;
-            cc = g1 >> 26;
-            g1 &= kM26;
-            uint32_t g2 = h2 + cc;
-            cc = g2 >> 26;
-            g2 &= kM26;
-            uint32_t g3 = h3 + cc;
-            cc = g3 >> 26;
-            g3 &= kM26;
-            const uint32_t g4 = h4 + cc - (1u << 26);
-            if ((g4 >> 31) == 0) {
-                h0 = g0;
-                h1 = g1;
-                h2 = g2;
-                h3 = g3;
-                h4 = g4;
-            }
-            // (h + s) mod 2^128, packing the limbs by addition so a limb
-            // that is not fully normalised (h1 = 2^26) still lands right
-            uint64_t f = (uint64_t)h0 + ((uint64_t)h1 << 26) + s[0];
-            uint32_t o[4];
-            o[0] = (uint32_t)f;
-            f = (f >> 32) + ((uint64_t)h2 << 20) + s[1];
-            o[1] = (uint32_t)f;
-            f = (f >> 32) + ((uint64_t)h3 << 14) + s[2];
-            o[2] = (uint32_t)f;
-            f = (f >> 32) + ((uint64_t)h4 << 8) + s[3];
-            o[3] = (uint32_t)f;
-            uint8_t *mac = a.macs + 16 * b;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) mac[i] = (uint8_t)(o[i >> 2] >> (8 * (i & 3)));
+            poly_final(d, s, a.macs + 16 * b);
         }
     }
 }
@@ -508,7 +633,7 @@ using namespace vsgpu;
 struct vs_seal {
     int device = 0;
     int cus = 256;
-    DevBuf te0, rk256, rk128, rpow, prefix;
+    DevBuf te0, rk256, rk128, rpow, prefix, acc;
     bool timing = false;
     std::vector<hipEvent_t> ev;   // 3 per timed run: before CTR, between, after MAC
 };
@@ -552,11 +677,17 @@ VS_API int vs_seal_open(int device, const uint8_t enc_key[32], const uint8_t mac
     memcpy(t, rb, 16);
     H5 r{{t[0] & kM26, ((t[0] >> 26) | (t[1] << 6)) & kM26, ((t[1] >> 20) | (t[2] << 12)) & kM26,
           ((t[2] >> 14) | (t[3] << 18)) & kM26, (t[3] >> 8)}};
-    std::vector<uint32_t> rp(64 * 5);
-    H5 p = r;
+    // r^1..r^64, then r^(64 * 2^j) for j < kSealSq (the fused MAC's lifts)
+    std::vector<uint32_t> rp((64 + kSealSq) * 5);
+    H5 p = r, r64 = r;
     for (int k = 0; k < 64; ++k) {
         for (int i = 0; i < 5; ++i) rp[(size_t)k * 5 + i] = (uint32_t)p.v[i];
+        r64 = p;
         p = hmul(p, r);
+    }
+    for (int j = 0; j < kSealSq; ++j) {
+        for (int i = 0; i < 5; ++i) rp[(size_t)(64 + j) * 5 + i] = (uint32_t)r64.v[i];
+        r64 = hmul(r64, r64);
     }
     int rc = 0;
     if ((rc = h->te0.ensure(sizeof te)) < 0 || (rc = h->rk256.ensure(sizeof rk256)) < 0 ||
@@ -601,6 +732,9 @@ VS_API int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *de
     a.rk256 = h->rk256.as<uint32_t>();
     a.rk128 = h->rk128.as<uint32_t>();
     a.rpow = h->rpow.as<uint32_t>();
+    a.rsq = a.rpow + 64 * 5;
+    VS_TRY(h->acc.ensure(n * 5 * 8));
+    a.acc = h->acc.as<unsigned long long>();
     a.macs = dev_macs;
     hipEvent_t e[3] = {nullptr, nullptr, nullptr};
     if (h->timing) {
@@ -639,7 +773,7 @@ VS_API void vs_seal_close(vs_seal *h) {
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
     for (hipEvent_t x : h->ev) (void)hipEventDestroy(x);
-    for (DevBuf *b : {&h->te0, &h->rk256, &h->rk128, &h->rpow, &h->prefix}) b->release();
+    for (DevBuf *b : {&h->te0, &h->rk256, &h->rk128, &h->rpow, &h->prefix, &h->acc}) b->release();
     delete h;
 }
 
@@ -697,6 +831,26 @@ hipError_t launch_seal_prefix(const uint32_t *len, uint64_t n, uint64_t *prefix,
 }
 
 hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s, hipEvent_t *ev) {
+    // default: the MAC fused into the CTR pass (no re-read of the ciphertext),
+    // 768-thread workgroups at 6 waves per SIMD; VSGPU_SEAL_FUSED=0 selects
+    // the separate CTR + MAC kernels (A/B and tests)
+    const char *fe = getenv("VSGPU_SEAL_FUSED");
+    const bool fused = !(fe && atoi(fe) == 0);
+    if (fused) {
+        hipError_t e = hipMemsetAsync(a.acc, 0, a.n * 5 * 8, s);
+        if (e != hipSuccess) return e;
+        if (ev[0]) (void)hipEventRecord(ev[0], s);
+        if (a.total_blocks) {
+            const uint64_t steps = (a.total_blocks + 63) / 64;
+            const uint64_t grid = std::min<uint64_t>((steps + 11) / 12, (uint64_t)std::max(cus, 1) * 2);
+            seal_ctr_kernel<1, 768, 6, true><<<(uint32_t)grid, 768, 0, s>>>(a);
+        }
+        if (ev[1]) (void)hipEventRecord(ev[1], s);
+        const uint64_t fg = std::min<uint64_t>((a.n + 255) / 256, (uint64_t)std::max(cus, 1) * 4);
+        seal_fin_kernel<<<(uint32_t)std::max<uint64_t>(fg, 1), 256, 0, s>>>(a);
+        if (ev[2]) (void)hipEventRecord(ev[2], s);
+        return hipGetLastError();
+    }
     if (ev[0]) (void)hipEventRecord(ev[0], s);
     if (a.total_blocks) {
         // variants (VSGPU_SEAL_CTR, for measurement; 16 GiB of blobs, r02):

@@ -377,8 +377,11 @@ struct SealArgs {
     const uint32_t *rk256;      // [60] AES-256 round keys (EncryptionKey)
     const uint32_t *rk128;      // [44] AES-128 round keys (MACKey.K)
     const uint32_t *rpow;       // [64][5] r^1..r^64 in 26-bit limbs (MACKey.R clamped)
+    const uint32_t *rsq;        // [kSealSq][5] r^(64 * 2^j) (the fused MAC's long lifts)
+    unsigned long long *acc;    // [n][5] fused MAC: per-blob limb sums of the lifted partials
     uint8_t *macs;              // [n][16]
 };
+constexpr int kSealSq = 24;     // r^(64 * 2^j), j < 24: lifts up to 2^30 blocks (16 GiB blobs)
 hipError_t launch_seal_prefix(const uint32_t *len, uint64_t n, uint64_t *prefix, uint64_t *total,
                               hipStream_t s);
 hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s, hipEvent_t *ev);

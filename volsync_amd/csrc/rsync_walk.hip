@@ -745,7 +745,8 @@ __device__ __forceinline__ int64_t seg_hi(const RsWalkArgs &a, uint32_t k) {
 // speculative walk of every segment from its own start (segment 0 from the
 // range's speculative entry a.e0 / a.w0; the others with want_i "no
 // preference" = count)
-__global__ __launch_bounds__(kWalkThreads) void rs_walk_spec_kernel(RsWalkArgs a) {
+template <uint32_t T>
+__global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
     __shared__ uint32_t lfilt[kLdsFiltWordsW];
     __shared__ uint64_t lsec[24];
     load_secret(lsec, a.seed);
@@ -857,14 +858,23 @@ __global__ void rs_pad_sum2_kernel(const uint8_t *sum2, uint32_t count, uint32_t
 hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t s) {
     if (!a.nseg) return hipSuccess;
     if (a.lbits > 20) return hipErrorInvalidValue;
-    const uint32_t waves = kWalkThreads / 64;
+    // VSGPU_WALK_WG=1024: the speculative pass at 16 waves per CU (128
+    // VGPRs, some spilled) instead of 12 (160 VGPRs) -- an A/B knob
+    static const uint32_t spec_threads = [] {
+        const char *e = getenv("VSGPU_WALK_WG");
+        return (e && atoi(e) == 1024) ? 1024u : kWalkThreads;
+    }();
+    const uint32_t threads = stitch ? kWalkThreads : spec_threads;
+    const uint32_t waves = threads / 64;
     const uint64_t grid = std::min<uint64_t>((a.nseg + waves - 1) / waves, (uint64_t)std::max(cus, 1));
     hipError_t e = hipMemsetAsync(a.work, 0, 4, s);
     if (e != hipSuccess) return e;
     if (stitch)
         rs_walk_stitch_kernel<<<(uint32_t)grid, kWalkThreads, 0, s>>>(a);
+    else if (threads == 1024)
+        rs_walk_spec_kernel<1024><<<(uint32_t)grid, 1024, 0, s>>>(a);
     else
-        rs_walk_spec_kernel<<<(uint32_t)grid, kWalkThreads, 0, s>>>(a);
+        rs_walk_spec_kernel<kWalkThreads><<<(uint32_t)grid, kWalkThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 
