@@ -26,6 +26,8 @@
 // current group and the next.  The hot loop only notes which groups hold a
 // candidate; their exact offsets are found after the strip by re-rolling each
 // noted group from a 64-byte warm-up (the window property again).
+#include <cstdlib>
+
 #include "internal.hpp"
 
 namespace vsgpu {
@@ -364,8 +366,8 @@ __device__ __forceinline__ void run_strips(const FpArgs &a, const char *lds, uin
     }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kFpThreads) void fp_kernel(FpArgs a) {
+template <int MODE, int THREADS>
+__global__ __launch_bounds__(THREADS) void fp_kernel(FpArgs a) {
     __shared__ __attribute__((aligned(16))) uint64_t tabs[2 * kTabEntries];  // 128 KiB
     for (uint32_t i = threadIdx.x; i < kTabEntries; i += blockDim.x) {
         const uint32_t e = i / kFpCopies;
@@ -412,12 +414,22 @@ hipError_t launch_fingerprint(const FpArgs &a, bool wide, bool fast, int cus, hi
     if (units == 0 && a.n_edge == 0) return hipSuccess;
     const uint64_t grid =
         std::max<uint64_t>(1, std::min<uint64_t>(units, (uint64_t)std::max(cus, 1)));
+    // VSGPU_FP_WG=512: 8 fingerprint waves per CU instead of 12, which leaves
+    // registers (and, with the 32 KiB hash kernel, LDS) for a SHA-256
+    // workgroup on every CU beside the pass
+    const char *e = getenv("VSGPU_FP_WG");
+    if (e && atoi(e) == 512) {
+        if (wide) fp_kernel<kFpWide, 512><<<(uint32_t)grid, 512, 0, s>>>(a);
+        else if (fast) fp_kernel<kFpFast, 512><<<(uint32_t)grid, 512, 0, s>>>(a);
+        else fp_kernel<kFpNarrow, 512><<<(uint32_t)grid, 512, 0, s>>>(a);
+        return hipGetLastError();
+    }
     if (wide)
-        fp_kernel<kFpWide><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
+        fp_kernel<kFpWide, kFpThreads><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
     else if (fast)
-        fp_kernel<kFpFast><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
+        fp_kernel<kFpFast, kFpThreads><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
     else
-        fp_kernel<kFpNarrow><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
+        fp_kernel<kFpNarrow, kFpThreads><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 

@@ -365,7 +365,11 @@ __device__ __forceinline__ void produce_tile(uint4 (&wk)[2][16 * 64], const ShaC
 // 16..63 idle); the later tiles hold 64 chains each in split mode.
 __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
     __shared__ uint4 wk[2][16 * 64];  // 2 x 16 KiB: W of one block of 64 chains
-    __shared__ uint32_t tile_sh;
+    // the tile broadcast borrows W slot 1's first word: between tiles no block
+    // is in flight, and the next tile's producer writes slot 1 only after the
+    // barrier that follows block 0.  The kernel's LDS is then exactly 32 KiB,
+    // so a workgroup fits beside a 128 KiB fingerprint workgroup on one CU.
+    uint32_t &tile_sh = wk[1][0].x;
     // the K + W that quad lanes 1-3 read: zeros in a part of buffer 0 that
     // quad tiles never write (their W takes entries 0..255, the staged
     // segments 0..318); a workgroup's tiles come in tile-counter order, so it
