@@ -241,7 +241,7 @@ __device__ __forceinline__ void poly_final(uint64_t (&d)[5], const uint32_t (&s)
 
 // h * r^e (e >= 1): r^u from the r^1..r^64 table (e = 64 t + u, u in 1..64),
 // then r^(64 t) by the binary expansion of t over r^(64 * 2^j)
-__device__ __noinline__ L5 lift(L5 h, uint64_t e, const SealArgs &a) {
+__device__ __forceinline__ L5 lift(L5 h, uint64_t e, const SealArgs &a) {
     const uint64_t u = ((e - 1) & 63) + 1;
     uint64_t t = (e - u) >> 6;
     h = pmul(h, ld_l5(a.rpow + (u - 1) * 5));
