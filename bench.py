@@ -4,9 +4,10 @@ python bench.py --gpus N --steps K --warmup W
   N=1: config C2 -- one 64 GiB synthetic volume image (seed 2), device-resident,
        restic chunker (testPol, 512 KiB / 8 MiB, 20 bits) + SHA-256 blob IDs.
   N>1: launched by torch.distributed.run, one rank per GPU: one volume of
-       N x per-GPU bytes byte-range sharded across the ranks (C3 shape; weak
-       scaling, per-GPU work fixed); the only exchange is an RCCL all-gather of
-       one u64 per rank per stitch round (volsync_amd/shard.py).
+       N x 128 GiB (C3's per-GPU share; seed 3, so N=8 is C3's 1 TiB) byte-range
+       sharded across the ranks (weak scaling, per-GPU work fixed); the only
+       exchange is an RCCL all-gather of one u64 per rank per stitch round
+       (volsync_amd/shard.py).
 A step = one full pass of the hot path over the volume: fingerprint, cut
 selection, Cut values, SHA-256 of every chunk.  Steps are pipelined: the
 time-sliced SHA-256 engine keeps hashing step k's chunks while step k+1 is
@@ -714,6 +715,8 @@ def dry_main(args):
     if world > 1:
         dist.init_process_group("gloo")
     per = int(args.per_gpu_gib * (1 << 30))
+    if world > 1 and args.c3_default:
+        per = 128 << 30   # the CDC mode's C3 default (main)
     total = per * world
     mn, mx = 512 << 10, 8 << 20
     spec = ShardSpec.for_rank(total, world, rank, mx)
@@ -850,7 +853,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--per-gpu-gib", type=float, default=64.0)
+    ap.add_argument("--per-gpu-gib", type=float, default=None,
+                    help="bytes per GPU (default 64 GiB; the CDC mode at N > 1: C3's "
+                         "128 GiB per GPU, i.e. 1 TiB over 8)")
     ap.add_argument("--cpu-sample-gib", type=int, default=4)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -872,6 +877,11 @@ def main():
     ap.add_argument("--dry", action="store_true",
                     help="CPU/gloo rehearsal of the multi-rank protocol (no GPU; value null)")
     args = ap.parse_args()
+    # C3: 1 TiB of the seed-3 stream over 8 GPUs, 128 GiB
+    # resident per GPU; the CDC mode's N > 1 default is that per-GPU share
+    args.c3_default = args.per_gpu_gib is None
+    if args.per_gpu_gib is None:
+        args.per_gpu_gib = 64.0
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # not under a launcher: become one (a child process, started before
         # this process has touched the GPU)
@@ -895,12 +905,15 @@ def main():
     world, rank, local, dev = dist_setup()
 
     per = int(args.per_gpu_gib * (1 << 30))
+    seed = 2                      # C2's stream
+    if world > 1 and args.c3_default:
+        per, seed = 128 << 30, 3  # C3's per-GPU share of its 1 TiB stream
     total = per * world
     spec = ShardSpec.for_rank(total, world, rank, MaxSize)
     dlen = spec.data_hi - spec.data_lo
     buf = torch.empty(dlen, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    synth_fill_device(buf.data_ptr(), 2, spec.data_lo, dlen, device=local, stream=stream)
+    synth_fill_device(buf.data_ptr(), seed, spec.data_lo, dlen, device=local, stream=stream)
     torch.cuda.synchronize(dev)
 
     dc = DeviceChunker(TestPol, MinSize, MaxSize, 20, device=local)
@@ -1023,9 +1036,12 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 volume image, device-resident)",
-            "config": {"workload": "C2: 64 GiB volume, restic CDC + SHA-256, 1 GPU" if world == 1
-                       else f"C3-shape: {total >> 30} GiB volume byte-range sharded over {world} "
-                            f"GPUs ({per >> 30} GiB per GPU)",
+            "config": {"workload": (f"C2: {total >> 30} GiB volume, restic CDC + SHA-256, 1 GPU"
+                                    if world == 1 else
+                                    f"{'C3' if total == 1 << 40 else 'C3-shape'}: {total >> 30} GiB "
+                                    f"volume (seed {seed}) byte-range sharded over {world} GPUs "
+                                    f"({per >> 30} GiB per GPU)"),
+                       "seed": seed,
                        "volume_bytes": total, "per_gpu_bytes": per, "chunks": nch,
                        "pol": "0x3DA3358B4DC173", "min": MinSize, "max": MaxSize, "avg_bits": 20,
                        "parallelism": f"byte-range shards x{world}"},
