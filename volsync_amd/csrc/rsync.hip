@@ -184,6 +184,101 @@ __device__ __forceinline__ uint64_t coop_long(const uint8_t *p, uint64_t len, ui
     return acc;
 }
 
+// The same with 4 lanes per window: lane k owns accumulators 2k and 2k+1 and
+// reads bytes [16k, 16k + 16) of every stripe with one 16-byte load, so
+// acc[j ^ 1] += d[j] stays inside the lane (no swap) and a wave's load moves
+// 1 KiB.  The signature pass (all windows full blocks) uses this layout.
+__device__ __forceinline__ void coop4_stripe(uint64_t &a0, uint64_t &a1, uint64_t d0, uint64_t d1,
+                                             uint32_t sb, uint32_t k, uint64_t seed) {
+    const uint64_t x0 = d0 ^ vsstrong::csec_at(sb + 16 * k, seed);
+    const uint64_t x1 = d1 ^ vsstrong::csec_at(sb + 16 * k + 8, seed);
+    a0 += (uint64_t)(uint32_t)x0 * (x0 >> 32) + d1;
+    a1 += (uint64_t)(uint32_t)x1 * (x1 >> 32) + d0;
+}
+
+__device__ __forceinline__ void ld16u(const uint8_t *p, uint64_t &d0, uint64_t &d1) {
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);   // unaligned dwordx4 (gfx950 unaligned mode)
+    d0 = ((uint64_t)v.y << 32) | v.x;
+    d1 = ((uint64_t)v.w << 32) | v.z;
+}
+
+// window p[0, len), len > 240; k = lane within the 4-lane group.  a0 / a1 =
+// accumulators 2k / 2k+1; sx/sux = this lane's share of the weak-sum parts.
+__device__ __forceinline__ void coop4_long(const uint8_t *p, uint64_t len, uint64_t seed, uint32_t k,
+                                           uint64_t &a0, uint64_t &a1, uint32_t &sx, uint32_t &sux) {
+    using namespace vsstrong;
+    const uint64_t init[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+    a0 = init[0];
+    a1 = init[1];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+        a0 = (k == (uint32_t)j) ? init[2 * j] : a0;
+        a1 = (k == (uint32_t)j) ? init[2 * j + 1] : a1;
+    }
+    sx = 0;
+    sux = 0;
+    const uint64_t nb = (len - 1) / 1024;
+    const uint64_t scr0 = sec64(16 + 2 * k, seed), scr1 = sec64(17 + 2 * k, seed);
+    for (uint64_t b = 0; b < nb; ++b) {
+        const uint8_t *q = p + b * 1024 + 16 * k;
+#pragma unroll 8
+        for (uint32_t s = 0; s < 16; ++s) {
+            uint64_t d0, d1;
+            ld16u(q + 64 * s, d0, d1);
+            const uint32_t pos = (uint32_t)(b * 1024 + 64 * s + 16 * k);
+            weak8(d0, pos, sx, sux);
+            weak8(d1, pos + 8, sx, sux);
+            coop4_stripe(a0, a1, d0, d1, 8 * s, k, seed);
+        }
+        a0 ^= a0 >> 47;
+        a0 ^= scr0;
+        a0 *= P32_1;
+        a1 ^= a1 >> 47;
+        a1 ^= scr1;
+        a1 *= P32_1;
+    }
+    const uint32_t ns = (uint32_t)(((len - 1) - nb * 1024) / 64);
+    for (uint32_t s = 0; s < ns; ++s) {
+        const uint64_t off = nb * 1024 + 64 * s + 16 * k;
+        uint64_t d0, d1;
+        ld16u(p + off, d0, d1);
+        weak8(d0, (uint32_t)off, sx, sux);
+        weak8(d1, (uint32_t)off + 8, sx, sux);
+        coop4_stripe(a0, a1, d0, d1, 8 * s, k, seed);
+    }
+    // last stripe (overlaps): hashed whole, weak-summed from the first byte no
+    // earlier stripe covered
+    const uint64_t covered = (nb * 16 + ns) * 64;
+    const uint64_t off = len - 64 + 16 * k;
+    uint64_t d0, d1;
+    ld16u(p + off, d0, d1);
+    coop4_stripe(a0, a1, d0, d1, 192 - 64 - 7, k, seed);
+    const uint64_t sk0 = covered > off ? min<uint64_t>(covered - off, 8) : 0;
+    const uint64_t sk1 = covered > off + 8 ? min<uint64_t>(covered - off - 8, 8) : 0;
+    weak8(sk0 >= 8 ? 0 : d0 & (~0ull << (8 * sk0)), (uint32_t)off, sx, sux);
+    weak8(sk1 >= 8 ? 0 : d1 & (~0ull << (8 * sk1)), (uint32_t)off + 8, sx, sux);
+}
+
+__device__ __forceinline__ void coop4_finish(uint64_t a0, uint64_t a1, uint32_t sx, uint32_t sux,
+                                             uint64_t len, int csum_type, uint64_t seed,
+                                             uint32_t gbase, uint32_t &weak, uint64_t &lo,
+                                             uint64_t &hi) {
+#pragma unroll
+    for (int m = 1; m < 4; m <<= 1) {
+        sx += (uint32_t)__shfl_xor((int)sx, m, 64);
+        sux += (uint32_t)__shfl_xor((int)sux, m, 64);
+    }
+    const uint32_t s2 = (uint32_t)len * sx - sux;
+    weak = (sx & 0xffffu) | (s2 << 16);
+    vsstrong::Xxh3Long st;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) st.acc[j] = shfl64((j & 1) ? a1 : a0, (int)gbase + j / 2);
+    lo = st.merge(11, len * vsstrong::P64_1, seed);
+    hi = (csum_type == vsstrong::kXxh3_128) ? st.merge(192 - 64 - 11, ~(len * vsstrong::P64_2), seed)
+                                            : 0;
+}
+
 // group-wide finish: weak sum and strong sum of the window (every lane returns them)
 __device__ __forceinline__ void coop_finish(uint64_t acc, uint32_t sx, uint32_t sux, uint64_t len,
                                             int csum_type, uint64_t seed, uint32_t gbase,
@@ -208,17 +303,17 @@ __device__ __forceinline__ void put_strong(uint8_t *out, uint32_t s2length, uint
         out[j] = (uint8_t)(j < 8 ? lo >> (8 * j) : hi >> (8 * (j - 8)));
 }
 
-// signatures: 8 lanes per block (XXH3, every block > 240 bytes)
+// signatures: 4 lanes per block (XXH3, every block > 240 bytes)
 __global__ __launch_bounds__(256) void rs_sig_coop_kernel(RsSigArgs a) {
-    const uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
-    const uint32_t i = threadIdx.x & 7, gbase = (threadIdx.x & 63) & ~7u;
+    const uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+    const uint32_t i = threadIdx.x & 3, gbase = (threadIdx.x & 63) & ~3u;
     const uint64_t b = g < a.count ? g : a.count - 1;  // whole groups stay active (shuffles)
     const uint64_t pos = b * a.blength;
     const uint64_t n = (b == a.count - 1 && a.remainder) ? a.remainder : a.blength;
     uint32_t sx, sux, weak;
-    uint64_t lo, hi;
-    const uint64_t acc = coop_long(a.data + pos, n, a.seed, i, sx, sux);
-    coop_finish(acc, sx, sux, n, a.csum_type, a.seed, gbase, weak, lo, hi);
+    uint64_t lo, hi, a0, a1;
+    coop4_long(a.data + pos, n, a.seed, i, a0, a1, sx, sux);
+    coop4_finish(a0, a1, sx, sux, n, a.csum_type, a.seed, gbase, weak, lo, hi);
     if (g < a.count && i == 0) {
         a.sum1[g] = weak;
         put_strong(a.sum2 + g * a.s2length, a.s2length, lo, hi);
@@ -249,7 +344,7 @@ static bool coop_ok(int csum_type) {
 hipError_t launch_rs_signatures(const RsSigArgs &a, hipStream_t s) {
     if (!a.count) return hipSuccess;
     if (coop_ok(a.csum_type) && a.blength > 240 && (a.remainder == 0 || a.remainder > 240))
-        rs_sig_coop_kernel<<<(uint32_t)((a.count * 8 + 255) / 256), 256, 0, s>>>(a);
+        rs_sig_coop_kernel<<<(uint32_t)((a.count * 4 + 255) / 256), 256, 0, s>>>(a);
     else
         rs_sig_kernel<<<(uint32_t)((a.count + 127) / 128), 128, 0, s>>>(a);
     return hipGetLastError();
