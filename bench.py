@@ -230,23 +230,61 @@ def rsync_main(args):
 
     world, rank, local, dev = dist_setup()
     per = int(args.per_gpu_gib * (1 << 30))
-    dtotal = per * world
+    # --share R/N (one process, one GPU): rank R's work of the N-rank C4 --
+    # its block range of D, the FULL table (every rank's sums, computed before
+    # the timed region as the all-gather would deliver them) and its byte range
+    # of S, re-walked once from rank R-1's speculative exit as round 1 of the
+    # exit exchange does.  Only the two small collectives are absent.
+    share = None
+    if args.share:
+        share = tuple(int(x) for x in args.share.split("/"))
+        assert world == 1 and len(share) == 2 and 0 <= share[0] < share[1], args.share
+    sw, sr = (share[1], share[0]) if share else (world, rank)
+    dtotal = per * sw
     hdr = sum_sizes_sqroot(dtotal)
-    shard = BlockShard.for_rank(dtotal, hdr.blength, world, rank)
+    shard = BlockShard.for_rank(dtotal, hdr.blength, sw, sr)
     n = shard.byte_hi - shard.byte_lo
     stream = torch.cuda.current_stream(dev).cuda_stream
-    db = torch.empty(max(n, 16), dtype=torch.uint8, device=dev)
-    synth_fill_device(db.data_ptr(), C4Plan.D_SEED, shard.byte_lo, n, device=local, stream=stream)
+    parts = BlockShard.split(dtotal, hdr.blength, sw)
+    db = torch.empty(max(max(p.byte_hi - p.byte_lo for p in parts), 16), dtype=torch.uint8,
+                     device=dev)
     plan = C4Plan(dtotal, hdr.blength)
-    sspec = SourceShard.for_rank(plan.total, hdr.blength, world, rank)
-    ds = torch.empty(max(sspec.data_hi - sspec.data_lo, 16), dtype=torch.uint8, device=dev)
-    plan.fill_device(ds.data_ptr(), sspec.data_lo, sspec.data_hi, device=local, stream=stream)
+    sspec = SourceShard.for_rank(plan.total, hdr.blength, sw, sr)
+    prev = SourceShard.for_rank(plan.total, hdr.blength, sw, sr - 1) if share and sr else None
+    ds = torch.empty(max(sspec.data_hi - sspec.data_lo,
+                         prev.data_hi - prev.data_lo if prev else 0, 16),
+                     dtype=torch.uint8, device=dev)
     s1 = torch.zeros(max(shard.blocks, 1), dtype=torch.int32, device=dev)
     s2 = torch.zeros(max(shard.blocks, 1) * hdr.s2length, dtype=torch.uint8, device=dev)
-    torch.cuda.synchronize(dev)
     m = Matcher(local)
     m.set_stream(stream)
     seed = 0x5EED5EED
+    full1 = full2 = None
+    share_entry = None
+    if share:
+        # the table the all-gather would assemble: every rank's block range of
+        # D generated and signed in turn (untimed)
+        full1 = torch.zeros(hdr.count, dtype=torch.int32, device=dev)
+        full2 = torch.zeros(hdr.count * hdr.s2length, dtype=torch.uint8, device=dev)
+        for p in parts:
+            synth_fill_device(db.data_ptr(), C4Plan.D_SEED, p.byte_lo, p.byte_hi - p.byte_lo,
+                              device=local, stream=stream)
+            m.signatures_device(db.data_ptr(), p.byte_hi - p.byte_lo, hdr.blength, hdr.s2length,
+                                CSUM_XXH3_128, seed, full1[p.b_lo:].data_ptr(),
+                                full2[p.b_lo * hdr.s2length:].data_ptr())
+        torch.cuda.synchronize(dev)
+        if prev is not None:
+            # rank R-1's speculative exit: the entry round 1 hands rank R
+            plan.fill_device(ds.data_ptr(), prev.data_lo, prev.data_hi, device=local,
+                             stream=stream)
+            m.load_sums_device(hdr.count, hdr.blength, hdr.s2length, hdr.remainder,
+                               full1.data_ptr(), full2.data_ptr(), CSUM_XXH3_128, seed)
+            share_entry = m.match_scan(ds.data_ptr(), prev.data_hi - prev.data_lo, prev.data_lo,
+                                       prev.length, prev.own_lo, prev.own_hi)
+            m.match_finish()
+    synth_fill_device(db.data_ptr(), C4Plan.D_SEED, shard.byte_lo, n, device=local, stream=stream)
+    plan.fill_device(ds.data_ptr(), sspec.data_lo, sspec.data_hi, device=local, stream=stream)
+    torch.cuda.synchronize(dev)
     coll = torch_pair_collectives(coll_device(dev)) if world > 1 else (lambda p: [p], lambda x: x)
     xst = {}
 
@@ -254,10 +292,19 @@ def rsync_main(args):
         m.signatures_device(db.data_ptr(), n, hdr.blength, hdr.s2length, CSUM_XXH3_128, seed,
                             s1.data_ptr(), s2.data_ptr())
         f1, f2 = s1, s2
-        if world > 1:
+        if share:
+            f1, f2 = full1, full2
+        elif world > 1:
             f1, f2 = gather_sums(s1, s2, shard, hdr.s2length, all_gather_any)
         m.load_sums_device(hdr.count, hdr.blength, hdr.s2length, hdr.remainder, f1.data_ptr(),
                            f2.data_ptr(), CSUM_XXH3_128, seed)
+        if share:
+            m.match_scan(ds.data_ptr(), sspec.data_hi - sspec.data_lo, sspec.data_lo,
+                         sspec.length, sspec.own_lo, sspec.own_hi)
+            if share_entry is not None:
+                m.match_stitch(*share_entry)
+                xst["exchange_rounds"] = 1
+            return m.match_finish()
         return run_walk_shard(m, sspec, ds.data_ptr(), *coll, stats=xst)
 
     for _ in range(args.warmup):
@@ -286,13 +333,14 @@ def rsync_main(args):
         c = torch.tensor([nm], dtype=torch.int64, device=coll_device(dev))
         dist.all_reduce(c)
         nm = int(c.item())
-    value = (dtotal + plan.total) * args.steps / dt / 1e9
     own_src = sspec.own_hi - sspec.own_lo
+    # a --share line counts the rank's own bytes: its D blocks and S range
+    value = ((n + own_src) if share else (dtotal + plan.total)) * args.steps / dt / 1e9
     # R7's whole-file checksum (checksum.c sum_update over S, xxh128), timed
     # on its own after the timed region: its scramble chain is one serial
     # dependency over the whole file, so it is reported beside the step
     fsum = None
-    if world == 1:
+    if world == 1 and not share:
         torch.cuda.synchronize(dev)
         m.kernel_time(reset=False)
         t1 = time.perf_counter()
@@ -319,7 +367,11 @@ def rsync_main(args):
             "data": "synthetic (splitmix64 destination + C4 edits, device-resident)",
             "config": {"workload": f"C4-shape: {dtotal >> 30} GiB destination vs 10%-edited "
                                    f"source ({plan.edits} edits), "
-                                   + (f"D block-range and S byte-range sharded x{world} "
+                                   + (f"rank {sr} of {sw}: its {n >> 30} GiB of D, the full "
+                                      f"{hdr.count}-block table, its {own_src >> 30} GiB of S "
+                                      f"(one GPU; value = its own bytes per second; the sum "
+                                      f"all-gather and exit exchange not included)" if share else
+                                      f"D block-range and S byte-range sharded x{world} "
                                       f"({per >> 30} GiB of D per GPU; sums all-gathered, walks "
                                       f"stitched over RCCL)" if world > 1 else "1 GPU"),
                        "blength": hdr.blength, "s2length": hdr.s2length, "count": hdr.count,
@@ -351,7 +403,7 @@ def rsync_main(args):
             out["roofline"]["traffic_source"] = r["source"]
         except (OSError, ValueError, KeyError):
             pass
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not share:
             out["cpu_baseline"] = rsync_cpu_baseline(args.cpu_sample_gib << 28)
         print(json.dumps(out), flush=True)
     m.close()
@@ -874,6 +926,10 @@ def main():
                          "match; smallfiles: C5 per-file blob IDs; host: C2 streamed from "
                          "pinned host memory through vs_cdc_feed/next")
     ap.add_argument("--files", type=int, default=1_000_000, help="smallfiles: files per GPU")
+    ap.add_argument("--share", default=None, metavar="R/N",
+                    help="rsync: run rank R's share of the N-rank problem on this one GPU "
+                         "(full table, its D blocks and S range; e.g. 3/8 with --per-gpu-gib 32 "
+                         "is one rank of C4)")
     ap.add_argument("--dry", action="store_true",
                     help="CPU/gloo rehearsal of the multi-rank protocol (no GPU; value null)")
     args = ap.parse_args()
