@@ -1,0 +1,25 @@
+#!/bin/bash
+# A/B of the walk's filters: LDS prefilter on/off (VSGPU_WALK_LBITS=0) and
+# blocked-filter bits per key (VSGPU_RS_FBITS_ADD), at the 64 GiB C4 shape
+# and at one rank's share of the real C4 (2 M-block table)
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/ab
+run() {  # run <tag> <env...>
+  local tag=$1; shift
+  env "$@" timeout -k 10 200 python bench.py --mode rsync --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/ab/c4_$tag.log 2>&1 || return 1
+  env "$@" timeout -k 10 200 python bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 > gpurun_out/ab/share_$tag.log 2>&1 || return 1
+  python3 - "$tag" gpurun_out/ab/c4_$tag.log gpurun_out/ab/share_$tag.log <<'PY'
+import json, sys
+out = [sys.argv[1]]
+for f in sys.argv[2:]:
+    j = json.loads(open(f).read().strip().splitlines()[-1])
+    out.append(f"{j['value']:.1f} GB/s walk {j['kernels_ms_per_step']['walk_spec']:.2f} ms "
+               f"fa {j['match_stats']['false_alarms']} m {j['config']['matches']}")
+print(" | ".join(out), flush=True)
+PY
+}
+run q4 VSGPU_WALK_Q=4 || exit 1
+run q8 VSGPU_WALK_Q=8 || exit 1
+run q8_f4 VSGPU_WALK_Q=8 VSGPU_RS_FBITS_ADD=4 || exit 1
+run q4_f4 VSGPU_WALK_Q=4 VSGPU_RS_FBITS_ADD=4 || exit 1
+run f3 VSGPU_RS_FBITS_ADD=3 || exit 1
+run q8_f3 VSGPU_WALK_Q=8 VSGPU_RS_FBITS_ADD=3 || exit 1

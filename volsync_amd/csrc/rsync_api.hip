@@ -256,7 +256,20 @@ int build_table(vs_rsync *h) {
     const uint32_t count = (uint32_t)h->count;
     h->dbits = std::min<uint32_t>(std::max<uint32_t>(ceil_log2(std::max<uint32_t>(count, 1)) + 1, 4),
                                   26);
-    h->fbits = std::min<uint32_t>(std::max<uint32_t>(ceil_log2(std::max<uint32_t>(count, 1)) + 5, 10),
+    // Filter size: 32 bits per key, capped at 2^25 bits (4 MiB, one XCD's L2)
+    // so the walk's gathers stay L2-resident.  At C4's 2 M blocks the cap
+    // (16 bits per key) measured 745 -> 775-787 GB/s per rank; at 524 K
+    // blocks 32 and 16 bits per key are within 1 % and 8 bits per key loses
+    // 5 % (profiles/r02_walk_ab).  VSGPU_RS_FBITS_ADD=k: 2^k bits per key,
+    // uncapped (A/B knob).
+    static const int fadd = [] {
+        const char *e = getenv("VSGPU_RS_FBITS_ADD");
+        const int v = e ? atoi(e) : 0;
+        return v >= 2 && v <= 7 ? v : 0;
+    }();
+    const uint32_t lc = ceil_log2(std::max<uint32_t>(count, 1));
+    h->fbits = std::min<uint32_t>(std::max<uint32_t>(fadd ? lc + (uint32_t)fadd : std::min(lc + 5, 25u),
+                                                     10),
                                   28);
     const size_t n = std::max<uint32_t>(count, 1);
     VS_TRY(h->d_keys.ensure(n * 8));
@@ -872,6 +885,14 @@ int walk_scan(vs_rsync *h) {
     a.lbits = rs_lds_filter_bits(h->fbits);
     a.filt_l = h->d_filt.as<uint32_t>() + ((1ull << h->fbits) / 32);
     a.filt_b = (const uint64_t *)(a.filt_l + ((1ull << a.lbits) / 32));
+    // VSGPU_WALK_LBITS=0: the walk skips the LDS prefilter (A/B knob)
+    {
+        static const int lb = [] {
+            const char *e = getenv("VSGPU_WALK_LBITS");
+            return e ? atoi(e) : -1;
+        }();
+        if (lb == 0) a.lbits = 0;
+    }
     const size_t ns = std::max<uint32_t>(a.nseg, 1), nc = ns * a.cap;
     VS_TRY(h->w_spec_off.ensure(nc * 8));
     VS_TRY(h->w_spec_idx.ensure(nc * 4));
