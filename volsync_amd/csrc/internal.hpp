@@ -283,8 +283,14 @@ __host__ __device__ inline uint32_t rs_lds_filter_bits(uint32_t fbits) {
 __host__ __device__ inline uint32_t rs_bloom_word(uint32_t sum1, uint32_t fbits) {
     return (sum1 * 0x9E3779B1u) >> (32 - (fbits - 6));
 }
+#ifndef VS_BLOOM_K
+#define VS_BLOOM_K 3
+#endif
 __host__ __device__ inline uint64_t rs_bloom_mask(uint32_t sum1) {
-    return (1ull << (sum1 & 63)) | (1ull << ((sum1 >> 6) & 63)) | (1ull << ((sum1 >> 12) & 63));
+    uint64_t m = 0;
+#pragma unroll
+    for (int j = 0; j < VS_BLOOM_K; ++j) m |= 1ull << ((sum1 >> (6 * j)) & 63);
+    return m;
 }
 // layout: filter [2^fbits bits], LDS prefilter [2^lbits bits], blocked filter [2^fbits bits]
 inline size_t rs_filter_bytes(uint32_t fbits) {
