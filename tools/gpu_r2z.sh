@@ -17,9 +17,6 @@ for f in sys.argv[2:]:
 print(" | ".join(out), flush=True)
 PY
 }
-run q4 VSGPU_WALK_Q=4 || exit 1
-run q8 VSGPU_WALK_Q=8 || exit 1
-run q8_f4 VSGPU_WALK_Q=8 VSGPU_RS_FBITS_ADD=4 || exit 1
-run q4_f4 VSGPU_WALK_Q=4 VSGPU_RS_FBITS_ADD=4 || exit 1
-run f3 VSGPU_RS_FBITS_ADD=3 || exit 1
-run q8_f3 VSGPU_WALK_Q=8 VSGPU_RS_FBITS_ADD=3 || exit 1
+run k3 X=1 || exit 1
+run k5 VSGPU_LIB=$PWD/volsync_amd/lib_k5/libvsgpu.so || exit 1
+run k4 VSGPU_LIB=$PWD/volsync_amd/lib_k4/libvsgpu.so || exit 1
