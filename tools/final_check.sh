@@ -9,5 +9,7 @@ timeout -k 10 400 python bench.py --mode smallfiles > gpurun_out/bench_c5.log 2>
 tail -1 gpurun_out/bench_c5.log | cut -c1-300
 timeout -k 10 600 python bench.py --mode rsync --steps 3 --warmup 1 > gpurun_out/bench_c4.log 2>&1 || { tail -20 gpurun_out/bench_c4.log; exit 1; }
 tail -1 gpurun_out/bench_c4.log | cut -c1-300
+timeout -k 10 400 python bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 > gpurun_out/bench_c4_share.log 2>&1 || { tail -20 gpurun_out/bench_c4_share.log; exit 1; }
+tail -1 gpurun_out/bench_c4_share.log | cut -c1-300
 bash tools/profile.sh final || exit $?
 cat gpurun_out/prof_final/steps.log
