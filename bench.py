@@ -397,10 +397,8 @@ def rsync_main(args):
             "file_sum": fsum,
         }
         try:
-            if share:
-                raise KeyError("the committed counters are the 64 GiB shape's")
             tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
-            r = tj["rs_walk_spec"]
+            r = tj["rs_walk_spec_share" if share else "rs_walk_spec"]
             out["roofline"]["traffic"] = round(r["bytes_per_source_byte"] * own_src)
             out["roofline"]["traffic_source"] = r["source"]
         except (OSError, ValueError, KeyError):
