@@ -19,7 +19,7 @@ PY
 }
 timeout -k 10 600 python -u -m pytest tests/test_gpu_rsync.py tests/test_native_abi.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab/rsync_tests.log 2>&1 || { tail -30 gpurun_out/ab/rsync_tests.log; exit 1; }
 tail -1 gpurun_out/ab/rsync_tests.log
-run s0 VSGPU_WALK_SKEW=0 || exit 1
-run s24 VSGPU_WALK_SKEW=24 || exit 1
-run s8 VSGPU_WALK_SKEW=8 || exit 1
-run s64 VSGPU_WALK_SKEW=64 || exit 1
+run old VSGPU_LIB=$PWD/volsync_amd/lib_old/libvsgpu.so || exit 1
+run new X=1 || exit 1
+run old2 VSGPU_LIB=$PWD/volsync_amd/lib_old/libvsgpu.so || exit 1
+run new2 X=1 || exit 1

@@ -611,24 +611,31 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
             // L2-resident blocked filter for all 16 offsets at once -- offsets
             // the prefilter rejected read word 0, so their loads coalesce --
             // and the directory only for the few offsets that pass both
+            // all 16 reads of each stage are issued before any is consumed
+            // (one LDS and one L2 round trip per batch, not 16 of each)
             uint32_t hit = valid;
             if (a.lbits) {
+                uint32_t lw[16];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) lw[t] = lfilt[(sums[t] >> (32 - a.lbits)) >> 5];
                 uint32_t lh = 0;
 #pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    const uint32_t fl = sums[t] >> (32 - a.lbits);
-                    lh |= ((lfilt[fl >> 5] >> (fl & 31)) & 1u) << t;
-                }
+                for (int t = 0; t < 16; ++t)
+                    lh |= ((lw[t] >> ((sums[t] >> (32 - a.lbits)) & 31)) & 1u) << t;
                 hit &= lh;
             }
             {
-                uint32_t pass = 0;
+                uint64_t fw[16];
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
                     const bool on = (hit >> t) & 1u;
-                    const uint32_t wi_ = on ? rs_bloom_word(sums[t], a.fbits) : 0u;
+                    fw[t] = a.filt_b[on ? rs_bloom_word(sums[t], a.fbits) : 0u];
+                }
+                uint32_t pass = 0;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
                     const uint64_t m = rs_bloom_mask(sums[t]);
-                    pass |= (uint32_t)((a.filt_b[wi_] & m) == m) << t;
+                    pass |= (uint32_t)((fw[t] & m) == m) << t;
                 }
                 hit &= pass;
             }
