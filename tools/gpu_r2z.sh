@@ -17,9 +17,9 @@ for f in sys.argv[2:]:
 print(" | ".join(out), flush=True)
 PY
 }
-timeout -k 10 600 python -u -m pytest tests/test_gpu_rsync.py tests/test_native_abi.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab/rsync_tests.log 2>&1 || { tail -30 gpurun_out/ab/rsync_tests.log; exit 1; }
-tail -1 gpurun_out/ab/rsync_tests.log
-run old VSGPU_LIB=$PWD/volsync_amd/lib_old/libvsgpu.so || exit 1
-run new X=1 || exit 1
-run old2 VSGPU_LIB=$PWD/volsync_amd/lib_old/libvsgpu.so || exit 1
-run new2 X=1 || exit 1
+true
+true
+run k3 X=1 || exit 1
+run k5 VSGPU_LIB=$PWD/volsync_amd/lib_k5/libvsgpu.so || exit 1
+run k3b X=1 || exit 1
+run k5b VSGPU_LIB=$PWD/volsync_amd/lib_k5/libvsgpu.so || exit 1
