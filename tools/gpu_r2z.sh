@@ -19,7 +19,10 @@ PY
 }
 true
 true
-run k3 X=1 || exit 1
-run k5 VSGPU_LIB=$PWD/volsync_amd/lib_k5/libvsgpu.so || exit 1
-run k3b X=1 || exit 1
-run k5b VSGPU_LIB=$PWD/volsync_amd/lib_k5/libvsgpu.so || exit 1
+VSGPU_LIB=$PWD/volsync_amd/lib_r8/libvsgpu.so timeout -k 10 600 python -u -m pytest tests/test_gpu_rsync.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab/rsync_tests_r8.log 2>&1 || { tail -30 gpurun_out/ab/rsync_tests_r8.log; exit 1; }
+tail -1 gpurun_out/ab/rsync_tests_r8.log
+run base X=1 || exit 1
+run t512 VSGPU_LIB=$PWD/volsync_amd/lib_t512/libvsgpu.so || exit 1
+run r8 VSGPU_LIB=$PWD/volsync_amd/lib_r8/libvsgpu.so || exit 1
+run base2 X=1 || exit 1
+run r8b VSGPU_LIB=$PWD/volsync_amd/lib_r8/libvsgpu.so || exit 1
