@@ -41,6 +41,19 @@ def test_library_links_no_oracle():
     assert b"liboracle" not in strings and b"ref_chunk_all" not in strings
 
 
+def test_library_never_registers_host_memory():
+    """Round 2's driver failure: the library page-locked its
+    std::vector read-back storage with hipHostRegister; a stale registration
+    over heap bytes a later caller buffer reused made the runtime's pageable
+    copy of that buffer fail.  The library now pins only what it allocates
+    (hipHostMalloc) and stages caller memory: it must not import the call."""
+    from volsync_amd import _lib
+    out = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    assert "hipHostRegister" not in out and "hipHostUnregister" not in out
+    assert "hipHostMalloc" in out
+
+
 def test_pol_helpers_match_oracle():
     from volsync_amd import Pol
     p = Pol(P.TEST_POL)

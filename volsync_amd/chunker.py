@@ -294,7 +294,12 @@ def sha256_batch(buf: bytes, offs, lens, device: int = 0) -> List[bytes]:
     o = np.ascontiguousarray(offs, dtype=np.uint64)
     ln = np.ascontiguousarray(lens, dtype=np.uint32)
     out = np.zeros((max(n, 1), 32), dtype=np.uint8)
-    b = np.frombuffer(bytes(buf), dtype=np.uint8) if len(buf) else np.zeros(1, np.uint8)
+    if isinstance(buf, np.ndarray):   # the caller's bytes, no copy
+        b = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+    else:
+        b = np.frombuffer(bytes(buf), dtype=np.uint8)
+    if not len(b):
+        b = np.zeros(1, np.uint8)
     check(lib.vs_sha256_batch(device, b.ctypes.data, len(buf), o.ctypes.data, ln.ctypes.data, n,
                               out.ctypes.data))
     return [bytes(out[i]) for i in range(n)]

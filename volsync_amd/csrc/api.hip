@@ -92,6 +92,7 @@ struct vs_cdc {
     int state = 0;  // 0 idle, 1 scanned, 2 stitched, 3 finished
     // host staging
     uint64_t *pinned = nullptr;  // 8 u64 of pinned host memory
+    PinnedVec<uint8_t> rb;       // chunk-list read-back: start | end | cut | id per batch range
     // streaming (vs_cdc_feed / vs_cdc_next): one device batch
     // buffer per ring slot -- the hash engine reads a batch's chunks from its
     // buffer until their blob IDs are final -- filled by H2D copies on a copy
@@ -586,6 +587,29 @@ static int cdc_wait(vs_cdc *h) {
     return sync_stream(h, true);
 }
 
+// chunks [first, first+n) of a slot, read back into the handle's pinned
+// buffer on its own (non-blocking) stream -- a null-stream copy would wait for
+// every blocking stream, the masked hash stream included
+static int read_chunks(vs_cdc *h, const vs_cdc::Slot &sl, uint64_t first, uint64_t n,
+                       vs_chunk *out) {
+    VS_TRY(pv_resize(h->rb, n * 56));
+    uint64_t *st = (uint64_t *)h->rb.data(), *en = st + n, *cu = en + n;
+    uint8_t *id = (uint8_t *)(cu + n);
+    VS_HIP(hipMemcpyAsync(st, sl.start.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost, h->stream));
+    VS_HIP(hipMemcpyAsync(en, sl.end.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost, h->stream));
+    VS_HIP(hipMemcpyAsync(cu, sl.cut.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost, h->stream));
+    VS_HIP(hipMemcpyAsync(id, sl.id.as<uint8_t>() + first * 32, n * 32, hipMemcpyDeviceToHost,
+                          h->stream));
+    VS_HIP(hipStreamSynchronize(h->stream));
+    for (uint64_t i = 0; i < n; ++i) {
+        out[i].start = sl.origin + st[i];
+        out[i].length = (en[i] & kPosMask) - st[i] + 1;
+        out[i].cut = cu[i];
+        memcpy(out[i].id, id + i * 32, 32);
+    }
+    return 0;
+}
+
 // chunks [first, first+n) of batch `seq` (while its ring slot still holds it)
 static int cdc_get_batch(vs_cdc *h, uint64_t seq, uint64_t first, uint64_t n, vs_chunk *out) {
     if (!h || h->slots.empty() || seq >= h->seq) return fail(VS_ERR_STATE, "no such finished batch");
@@ -595,18 +619,7 @@ static int cdc_get_batch(vs_cdc *h, uint64_t seq, uint64_t first, uint64_t n, vs
     if (first + n > sl.n) return fail(VS_ERR_ARG, "chunk range out of bounds");
     if (!n) return 0;
     VS_TRY(cdc_wait(h));
-    std::vector<uint64_t> st(n), en(n), cu(n);
-    std::vector<uint8_t> id(n * 32);
-    VS_HIP(hipMemcpy(st.data(), sl.start.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost));
-    VS_HIP(hipMemcpy(en.data(), sl.end.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost));
-    VS_HIP(hipMemcpy(cu.data(), sl.cut.as<uint64_t>() + first, n * 8, hipMemcpyDeviceToHost));
-    VS_HIP(hipMemcpy(id.data(), sl.id.as<uint8_t>() + first * 32, n * 32, hipMemcpyDeviceToHost));
-    for (uint64_t i = 0; i < n; ++i) {
-        out[i].start = sl.origin + st[i];
-        out[i].length = (en[i] & kPosMask) - st[i] + 1;
-        out[i].cut = cu[i];
-        memcpy(out[i].id, &id[i * 32], 32);
-    }
+    VS_TRY(read_chunks(h, sl, first, n, out));
     return 0;
 }
 
@@ -629,10 +642,10 @@ static int cdc_process(vs_cdc *h, const void *dev_data, uint64_t len, uint64_t o
         if (complete) {
             *consumed = ex - origin;
         } else if (n) {
-            uint64_t e = 0;
-            VS_HIP(hipMemcpy(&e, h->slots[h->last].end.as<uint64_t>() + (n - 1), 8,
-                             hipMemcpyDeviceToHost));
-            *consumed = (e & kPosMask) + 1;
+            VS_HIP(hipMemcpyAsync(h->pinned, h->slots[h->last].end.as<uint64_t>() + (n - 1), 8,
+                                  hipMemcpyDeviceToHost, h->stream));
+            VS_HIP(hipStreamSynchronize(h->stream));
+            *consumed = (h->pinned[0] & kPosMask) + 1;
         } else {
             *consumed = 0;
         }
@@ -675,23 +688,9 @@ static int collect_batch(vs_cdc *h, uint64_t s, bool block) {
     }
     const uint64_t n = sl.n;
     if (n) {
-        std::vector<uint64_t> st(n), en(n), cu(n);
-        std::vector<uint8_t> id(n * 32);
-        // on the handle's own (non-blocking) stream: a null-stream copy would
-        // wait for every blocking stream, the masked hash stream included
-        VS_HIP(hipMemcpyAsync(st.data(), sl.start.p, n * 8, hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipMemcpyAsync(en.data(), sl.end.p, n * 8, hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipMemcpyAsync(cu.data(), sl.cut.p, n * 8, hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipMemcpyAsync(id.data(), sl.id.p, n * 32, hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipStreamSynchronize(h->stream));
-        for (uint64_t i = 0; i < n; ++i) {
-            vs_chunk c;
-            c.start = sl.origin + st[i];
-            c.length = (en[i] & kPosMask) - st[i] + 1;
-            c.cut = cu[i];
-            memcpy(c.id, &id[i * 32], 32);
-            h->ready.push_back(c);
-        }
+        std::vector<vs_chunk> got(n);
+        VS_TRY(read_chunks(h, sl, 0, n, got.data()));
+        h->ready.insert(h->ready.end(), got.begin(), got.end());
     }
     h->spend.pop_front();
     return 0;
@@ -786,11 +785,7 @@ static int stream_begin(vs_cdc *h) {
 // pinned staging buffers (the copy of each piece waits only for its buffer).
 static int stream_copy(vs_cdc *h, uint8_t *dst, const uint8_t *src, size_t n) {
     if (!n) return 0;
-    hipPointerAttribute_t at;
-    bool pinned = false;
-    if (hipPointerGetAttributes(&at, src) == hipSuccess) pinned = at.type == hipMemoryTypeHost;
-    else (void)hipGetLastError();
-    if (pinned) {
+    if (host_range_pinned(src, n)) {
         VS_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, h->cstream));
         VS_HIP(hipEventRecord(h->ev_copy, h->cstream));
         h->feed_stats[0] += (double)n;
@@ -946,10 +941,11 @@ VS_API int vs_cdc_open(int device, uint64_t pol, uint32_t min_size, uint32_t max
         hipStreamCreateWithFlags(&h->own_h, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_ready, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_null, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc((void **)&h->pinned, 64, hipHostMallocDefault) != hipSuccess) {
-        (void)hipGetLastError();
+        !(h->pinned = (uint64_t *)pinned_alloc(64))) {
+        const hipError_t e = hipGetLastError();
         vs_cdc_close(h);
-        return fail(VS_ERR_HIP, "stream / pinned buffer creation failed");
+        return fail(VS_ERR_HIP, std::string("stream / event / pinned word creation failed: ") +
+                                    hipGetErrorName(e));
     }
     h->stream = h->own;
     h->hstream = h->own_h;
@@ -1112,7 +1108,8 @@ VS_API void vs_cdc_close(vs_cdc *h) {
     for (auto e : h->ev_pool) (void)hipEventDestroy(e);
     for (auto e : h->slice_ev)
         if (e) (void)hipEventDestroy(e);
-    if (h->pinned) (void)hipHostFree(h->pinned);
+    pinned_free(h->pinned);
+    PinnedVec<uint8_t>().swap(h->rb);
     if (h->ev_ready) (void)hipEventDestroy(h->ev_ready);
     if (h->ev_null) (void)hipEventDestroy(h->ev_null);
     if (h->own_h) (void)hipStreamDestroy(h->own_h);
@@ -1211,8 +1208,9 @@ struct vs_sha {
     uint64_t *dd_pinned = nullptr;
     DevBuf blk_off, blk_len;        // vs_sha256_blocks descriptors
     DevBuf vf_ids, vf_cnt;          // vs_blob_verify scratch
-    hipEvent_t done = nullptr;  // after the last run, on its stream
+    hipEvent_t done = nullptr;  // after the last use of the handle's scratch, on its stream
     bool ran = false;
+    Stager stage;                   // vs_sha256_batch: caller host buffers
 };
 
 VS_API int vs_sha256_open(int device, vs_sha **out) {
@@ -1303,6 +1301,7 @@ VS_API int vs_blob_verify(vs_sha *h, const void *dev_buf, const uint64_t *dev_of
     VS_TRY(sha_run(h, (const uint8_t *)dev_buf, dev_off, dev_len, n, h->vf_ids.as<uint8_t>(), s));
     VS_HIP(launch_verify(h->vf_ids.as<uint8_t>(), dev_want, n, dev_bad,
                          h->vf_cnt.as<unsigned long long>(), s));
+    VS_HIP(hipEventRecord(h->done, s));   // vf_ids / vf_cnt are read until here
     if (n_bad) {
         if (!h->dd_pinned &&
             hipHostMalloc((void **)&h->dd_pinned, 64, hipHostMallocDefault) != hipSuccess) {
@@ -1319,16 +1318,21 @@ VS_API int vs_blob_verify(vs_sha *h, const void *dev_buf, const uint64_t *dev_of
 VS_API int vs_blob_dedup(vs_sha *h, const uint8_t *dev_ids, size_t n, uint32_t *dev_first,
                          uint64_t *n_unique, void *hip_stream) {
     if (!h || (n && (!dev_ids || !dev_first))) return fail(VS_ERR_ARG, "bad arguments");
-    if (n > 0xffffffffull) return fail(VS_ERR_ARG, "more than 2^32 blobs per call");
     VS_HIP(hipSetDevice(h->device));
     const hipStream_t s = (hipStream_t)hip_stream;
     // the distinct-ID counter takes the first 256 bytes: dd_first_kernel adds
     // to it with a 64-bit atomic, which faults unless 8-byte aligned (at the
     // buffer's end it sat wherever the sort's scratch size left it)
+    if (n > 0x7fffffffull) return fail(VS_ERR_ARG, "more than 2^31 - 1 blobs per call (radix sort count)");
+    if (((uintptr_t)dev_ids & 15) != 0) return fail(VS_ERR_ARG, "blob IDs must be 16-byte aligned");
+    // dd_tmp may still be read by the previous dedup on another stream
+    if (h->ran) VS_HIP(hipStreamWaitEvent(s, h->done, 0));
     VS_TRY(h->dd_tmp.ensure(dedup_tmp_bytes(std::max<size_t>(n, 1)) + 256));
     unsigned long long *cnt = (unsigned long long *)h->dd_tmp.p;
     VS_HIP(launch_dedup(dev_ids, n, dev_first, (uint8_t *)h->dd_tmp.p + 256, h->dd_tmp.cap - 256,
                         cnt, s));
+    VS_HIP(hipEventRecord(h->done, s));
+    h->ran = true;
     if (n_unique) {
         if (!h->dd_pinned &&
             hipHostMalloc((void **)&h->dd_pinned, 64, hipHostMallocDefault) != hipSuccess) {
@@ -1356,6 +1360,7 @@ VS_API void vs_sha256_close(vs_sha *h) {
     h->dd_tmp.release();
     for (DevBuf *b : {&h->blk_off, &h->blk_len, &h->vf_ids, &h->vf_cnt}) b->release();
     if (h->dd_pinned) (void)hipHostFree(h->dd_pinned);
+    h->stage.release();
     if (h->done) {
         (void)hipEventSynchronize(h->done);
         (void)hipEventDestroy(h->done);
@@ -1377,14 +1382,12 @@ VS_API int vs_sha256_batch(int device, const void *buf, size_t buf_len, const ui
     int rc = 0;
     if ((rc = d.ensure(std::max<size_t>(buf_len, 16))) < 0 || (rc = o.ensure(n * 8)) < 0 ||
         (rc = l.ensure(n * 4)) < 0 || (rc = r.ensure(n * 32)) < 0) {
-    } else if (hipMemcpy(d.p, buf, buf_len, hipMemcpyHostToDevice) != hipSuccess ||
-               hipMemcpy(o.p, off, n * 8, hipMemcpyHostToDevice) != hipSuccess ||
-               hipMemcpy(l.p, len, n * 4, hipMemcpyHostToDevice) != hipSuccess) {
-        rc = fail(VS_ERR_HIP, "host to device copy failed");
+    } else if ((rc = h->stage.h2d(d.p, buf, buf_len, nullptr)) < 0 ||
+               (rc = h->stage.h2d(o.p, off, n * 8, nullptr)) < 0 ||
+               (rc = h->stage.h2d(l.p, len, n * 4, nullptr)) < 0) {
     } else if ((rc = sha_run(h, d.as<uint8_t>(), o.as<uint64_t>(), l.as<uint32_t>(), n,
                              r.as<uint8_t>(), nullptr)) == 0) {
-        if (hipMemcpy(out, r.p, n * 32, hipMemcpyDeviceToHost) != hipSuccess)
-            rc = fail(VS_ERR_HIP, "SHA-256 batch failed");
+        rc = h->stage.d2h(out, r.p, n * 32, nullptr);
     }
     vs_sha256_close(h);
     d.release();

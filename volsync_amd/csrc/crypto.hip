@@ -634,6 +634,11 @@ struct vs_seal {
     int device = 0;
     int cus = 256;
     DevBuf te0, rk256, rk128, rpow, prefix, acc;
+    uint64_t *pinned = nullptr;   // the prefix total, read back
+    // after the last run's kernels, on its stream: the next run (maybe on
+    // another stream) waits for it before it rewrites prefix / acc
+    hipEvent_t done = nullptr;
+    bool ran = false;
     bool timing = false;
     std::vector<hipEvent_t> ev;   // 3 per timed run: before CTR, between, after MAC
 };
@@ -689,19 +694,30 @@ VS_API int vs_seal_open(int device, const uint8_t enc_key[32], const uint8_t mac
         for (int i = 0; i < 5; ++i) rp[(size_t)(64 + j) * 5 + i] = (uint32_t)r64.v[i];
         r64 = hmul(r64, r64);
     }
-    int rc = 0;
-    if ((rc = h->te0.ensure(sizeof te)) < 0 || (rc = h->rk256.ensure(sizeof rk256)) < 0 ||
-        (rc = h->rk128.ensure(sizeof rk128)) < 0 || (rc = h->rpow.ensure(rp.size() * 4)) < 0) {
-        delete h;
+    auto init = [&]() -> int {
+        VS_TRY(h->te0.ensure(sizeof te));
+        VS_TRY(h->rk256.ensure(sizeof rk256));
+        VS_TRY(h->rk128.ensure(sizeof rk128));
+        VS_TRY(h->rpow.ensure(rp.size() * 4));
+        if (!(h->pinned = (uint64_t *)pinned_alloc(64)))
+            return fail(VS_ERR_NOMEM, "pinned read-back word");
+        VS_HIP(hipEventCreateWithFlags(&h->done, hipEventDisableTiming));
+        // the key tables live in this frame: staged like any host memory the
+        // library does not own (xfer.cpp)
+        Stager st;
+        int r = st.h2d(h->te0.p, te, sizeof te, nullptr);
+        if (!r) r = st.h2d(h->rk256.p, rk256, sizeof rk256, nullptr);
+        if (!r) r = st.h2d(h->rk128.p, rk128, sizeof rk128, nullptr);
+        if (!r) r = st.h2d(h->rpow.p, rp.data(), rp.size() * 4, nullptr);
+        st.release();   // waits for the copies
+        return r;
+    };
+    const int rc = init();
+    if (rc < 0) {
+        const std::string msg = vs_last_error();
+        vs_seal_close(h);
+        set_error(msg);
         return rc;
-    }
-    if (hipMemcpy(h->te0.p, te, sizeof te, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(h->rk256.p, rk256, sizeof rk256, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(h->rk128.p, rk128, sizeof rk128, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(h->rpow.p, rp.data(), rp.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipGetLastError();
-        delete h;
-        return fail(VS_ERR_HIP, "uploading the key tables failed");
     }
     *out = h;
     return 0;
@@ -716,9 +732,11 @@ VS_API int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *de
     if ((uintptr_t)dev_nonces & 15) return fail(VS_ERR_ARG, "nonces must be 16-byte aligned");
     if (hipSetDevice(h->device) != hipSuccess) return fail(VS_ERR_NO_DEVICE, "hipSetDevice failed");
     const hipStream_t s = (hipStream_t)hip_stream;
+    // the previous run's CTR / MAC kernels read prefix and add into acc
+    if (h->ran) VS_HIP(hipStreamWaitEvent(s, h->done, 0));
     VS_TRY(h->prefix.ensure((n + 1) * 8));
-    uint64_t total = 0;
-    VS_HIP(launch_seal_prefix(dev_len, n, h->prefix.as<uint64_t>(), &total, s));
+    VS_HIP(launch_seal_prefix(dev_len, n, h->prefix.as<uint64_t>(), h->pinned, s));
+    const uint64_t total = h->pinned[0];
     SealArgs a{};
     a.in = (const uint8_t *)dev_in;
     a.out = dev_out;
@@ -742,6 +760,8 @@ VS_API int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *de
         h->ev.insert(h->ev.end(), e, e + 3);
     }
     VS_HIP(launch_seal(a, h->cus, s, e));
+    VS_HIP(hipEventRecord(h->done, s));
+    h->ran = true;
     return 0;
 }
 
@@ -774,6 +794,8 @@ VS_API void vs_seal_close(vs_seal *h) {
     (void)hipDeviceSynchronize();
     for (hipEvent_t x : h->ev) (void)hipEventDestroy(x);
     for (DevBuf *b : {&h->te0, &h->rk256, &h->rk128, &h->rpow, &h->prefix, &h->acc}) b->release();
+    pinned_free(h->pinned);
+    if (h->done) (void)hipEventDestroy(h->done);
     delete h;
 }
 

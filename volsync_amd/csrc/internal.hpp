@@ -15,18 +15,75 @@ namespace vsgpu {
 // ---- error plumbing -------------------------------------------------------
 void set_error(const std::string &msg);
 int fail(int code, const std::string &msg);
+// VS_ERR_HIP with the call, hipGetErrorName, the numeric code, the message and
+// the source line (xfer.cpp); clears the runtime's last error
+int fail_hip(hipError_t e, const char *what, const char *file, int line);
 #define VS_HIP(call)                                                                  \
     do {                                                                              \
         hipError_t e_ = (call);                                                       \
-        if (e_ != hipSuccess)                                                         \
-            return ::vsgpu::fail(VS_ERR_HIP, std::string(#call) + ": " +              \
-                                                 hipGetErrorString(e_));              \
+        if (e_ != hipSuccess) return ::vsgpu::fail_hip(e_, #call, __FILE__, __LINE__); \
     } while (0)
 #define VS_TRY(expr)                 \
     do {                             \
         int r_ = (expr);             \
         if (r_ < 0) return r_;       \
     } while (0)
+
+// ---- host memory the DMA engines touch (xfer.cpp) -------------------------------
+// The library page-locks only memory it allocated itself (hipHostMalloc):
+// registering heap storage pins pages it shares with the caller's buffers.
+void *pinned_alloc(size_t bytes);   // nullptr on failure
+void pinned_free(void *p);
+// [p, p + n) lies inside one page-locked host allocation (DMA it directly)
+bool host_range_pinned(const void *p, size_t n);
+
+// std::vector storage in owned pinned pages: read-back targets the DMA engine
+// writes directly (grows like any vector; every allocation is hipHostMalloc)
+template <class T>
+struct PinnedAlloc {
+    using value_type = T;
+    PinnedAlloc() = default;
+    template <class U>
+    PinnedAlloc(const PinnedAlloc<U> &) {}
+    T *allocate(size_t n) {
+        T *p = (T *)pinned_alloc(n * sizeof(T));
+        if (!p) throw std::bad_alloc();
+        return p;
+    }
+    void deallocate(T *p, size_t) { pinned_free(p); }
+    template <class U>
+    bool operator==(const PinnedAlloc<U> &) const { return true; }
+    template <class U>
+    bool operator!=(const PinnedAlloc<U> &) const { return false; }
+};
+template <class T>
+using PinnedVec = std::vector<T, PinnedAlloc<T>>;
+// resize without letting bad_alloc cross the C ABI
+template <class V>
+int pv_resize(V &v, size_t n) {
+    try {
+        v.resize(n);
+    } catch (const std::bad_alloc &) {
+        return fail(VS_ERR_NOMEM, "pinned host buffer of " + std::to_string(n) + " elements");
+    }
+    return 0;
+}
+
+// Copies between caller host memory (pageable or not) and the device through
+// two owned pinned chunks.  h2d returns once the caller's bytes are staged
+// (the DMA stays queued on s); d2h returns once dst holds the bytes.
+struct Stager {
+    static constexpr size_t kChunk = 8u << 20;
+    uint8_t *buf[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool busy[2] = {false, false};
+    int next = 0;
+    int init();
+    int wait(int i);
+    int h2d(void *dst, const void *src, size_t n, hipStream_t s);
+    int d2h(void *dst, const void *src, size_t n, hipStream_t s);
+    void release();
+};
 
 // ---- device buffer that only grows ------------------------------------------
 struct DevBuf {
@@ -38,10 +95,12 @@ struct DevBuf {
         p = nullptr;
         cap = 0;
         size_t want = std::max<size_t>(bytes, 256);
-        if (hipMalloc(&p, want) != hipSuccess) {
+        const hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
             p = nullptr;
             (void)hipGetLastError();
-            return fail(VS_ERR_NOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
+            return fail(VS_ERR_NOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed: " +
+                                          hipGetErrorName(e));
         }
         cap = want;
         return 0;

@@ -30,44 +30,6 @@
 
 using namespace vsgpu;
 
-// Page-locks a host vector's storage for the candidate read-backs (≈ 115 MB
-// at C4 shape; a pageable copy goes through staging buffers at a fraction of
-// the link rate).  Re-registered only when the vector's storage moves.  A
-// failed registration (e.g. hipErrorHostMemoryAlreadyRegistered when a small
-// vector shares a page with a registered one) is remembered for that storage,
-// so it is not retried on every call: the copy just stays pageable.
-struct HostReg {
-    void *p = nullptr;
-    size_t n = 0;
-    bool registered = false;
-    template <typename T>
-    hipError_t cover(std::vector<T> &v) {
-        const size_t bytes = v.capacity() * sizeof(T);
-        if (!bytes || (v.data() == p && bytes <= n)) return hipSuccess;
-        release();
-        p = v.data();
-        n = bytes;
-        if (hipHostRegister(v.data(), bytes, hipHostRegisterDefault) == hipSuccess) {
-            registered = true;
-        } else {
-            (void)hipGetLastError();  // not fatal; remembered until the storage moves
-        }
-        return hipSuccess;
-    }
-    // before the vector may reallocate (its old pages must not stay registered)
-    template <typename T>
-    void grow(std::vector<T> &v, size_t count) {
-        if (count > v.capacity()) release();
-        v.resize(count);
-    }
-    void release() {
-        if (registered) (void)hipHostUnregister(p);
-        registered = false;
-        p = nullptr;
-        n = 0;
-    }
-};
-
 // One sharded match run (vs_rsync_match_scan .. _finish).  Offsets in spec /
 // fin are data-relative (file offset - origin).
 struct RsRun {
@@ -134,11 +96,15 @@ struct vs_rsync {
     // results
     std::vector<vs_match> matches;
     // host scratch of match_device, reused across calls
-    std::vector<uint64_t> h_off, h_batch;
-    std::vector<uint32_t> h_sum;
-    std::vector<uint8_t> h_known, h_strong, h_flag;
+    // candidate read-backs (~115 MB at C4 shape): owned pinned pages, written
+    // by the DMA engine directly (xfer.cpp: never register heap storage)
+    PinnedVec<uint64_t> h_off;
+    PinnedVec<uint32_t> h_sum;
+    PinnedVec<uint8_t> h_flag;
+    std::vector<uint64_t> h_batch;
+    std::vector<uint8_t> h_known, h_strong;
     DevBuf d_flag;
-    HostReg reg_off, reg_sum, reg_flag;
+    Stager stage;                   // copies of caller / heap host memory
     std::vector<vs_match> h_out;
     RsRun run;
     int64_t st_cand = 0, st_fa = 0, st_hashed = 0;
@@ -302,16 +268,11 @@ int host_tables(vs_rsync *h) {
     h->sum2.resize(count * s2);
     std::vector<uint64_t> pad(count * 2);
     if (count) {
-        VS_HIP(hipMemcpyAsync(h->tkey_h.data(), h->d_tkey.p, count * 8, hipMemcpyDeviceToHost,
-                              h->stream));
-        VS_HIP(hipMemcpyAsync(h->dir_h.data(), h->d_dir.p, h->dir_h.size() * 4,
-                              hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipMemcpyAsync(h->sum1.data(), h->d_sum1.p, count * 4, hipMemcpyDeviceToHost,
-                              h->stream));
-        VS_HIP(hipMemcpyAsync(pad.data(), h->d_sum2p.p, count * 16, hipMemcpyDeviceToHost,
-                              h->stream));
+        VS_TRY(h->stage.d2h(h->tkey_h.data(), h->d_tkey.p, count * 8, h->stream));
+        VS_TRY(h->stage.d2h(h->dir_h.data(), h->d_dir.p, h->dir_h.size() * 4, h->stream));
+        VS_TRY(h->stage.d2h(h->sum1.data(), h->d_sum1.p, count * 4, h->stream));
+        VS_TRY(h->stage.d2h(pad.data(), h->d_sum2p.p, count * 16, h->stream));
     }
-    VS_HIP(hipStreamSynchronize(h->stream));
     // d_sum2p rows are the strong sums zero-padded to 16 bytes
     for (size_t i = 0; i < count; ++i) memcpy(h->sum2.data() + i * s2, pad.data() + 2 * i, s2);
     h->host_ok = true;
@@ -375,8 +336,8 @@ struct WalkGeom {
 // entry the walk would have compared it with?  If none did, treating each as
 // a non-match was exactly rsync's decision, so the walk's output stands and
 // only its false-alarm count lacks their compares (`extra_fa`).
-bool needs_match(vs_rsync *h, int64_t F, const std::vector<uint64_t> &off,
-                 const std::vector<uint32_t> &sum, const std::vector<uint8_t> &strong,
+bool needs_match(vs_rsync *h, int64_t F, const PinnedVec<uint64_t> &off,
+                 const PinnedVec<uint32_t> &sum, const std::vector<uint8_t> &strong,
                  const std::vector<uint64_t> &need, int64_t *extra_fa) {
     const uint32_t s2 = (uint32_t)h->s2length;
     int64_t fa = 0;
@@ -412,8 +373,8 @@ struct SpecWalk {
 // its first match that the speculative walk also made (same offset, same
 // block): both walks continue identically from there, so the rest of the
 // output, the false alarms and the exit are the speculative walk's.
-void walk(vs_rsync *h, const WalkGeom &g, const std::vector<uint64_t> &off,
-          const std::vector<uint32_t> &sum, const std::vector<uint8_t> &known,
+void walk(vs_rsync *h, const WalkGeom &g, const PinnedVec<uint64_t> &off,
+          const PinnedVec<uint32_t> &sum, const std::vector<uint8_t> &known,
           const std::vector<uint8_t> &strong, std::vector<uint64_t> &need,
           std::vector<vs_match> &out, std::vector<int64_t> &out_fa, WalkState &st,
           const SpecWalk *merge) {
@@ -504,7 +465,7 @@ void walk(vs_rsync *h, const WalkGeom &g, const std::vector<uint64_t> &off,
 }
 
 // strong sums of candidate windows idx[] on the device -> strong/known
-int verify(vs_rsync *h, const uint8_t *dev, int64_t F, const std::vector<uint64_t> &off,
+int verify(vs_rsync *h, const uint8_t *dev, int64_t F, const PinnedVec<uint64_t> &off,
            const std::vector<uint64_t> &idx, std::vector<uint8_t> &known,
            std::vector<uint8_t> &strong) {
     std::vector<uint64_t> todo;
@@ -525,15 +486,14 @@ int verify(vs_rsync *h, const uint8_t *dev, int64_t F, const std::vector<uint64_
     VS_TRY(h->v_off.ensure(n * 8));
     VS_TRY(h->v_len.ensure(n * 4));
     VS_TRY(h->v_out.ensure(n * s2));
-    VS_HIP(hipMemcpyAsync(h->v_off.p, vo.data(), n * 8, hipMemcpyHostToDevice, h->stream));
-    VS_HIP(hipMemcpyAsync(h->v_len.p, vl.data(), n * 4, hipMemcpyHostToDevice, h->stream));
+    VS_TRY(h->stage.h2d(h->v_off.p, vo.data(), n * 8, h->stream));
+    VS_TRY(h->stage.h2d(h->v_len.p, vl.data(), n * 4, h->stream));
     KernelTimer kt(h, 1);
     VS_HIP(launch_rs_strong(dev, h->v_off.as<uint64_t>(), h->v_len.as<uint32_t>(), n,
                             h->csum_type, h->seed, s2, h->v_out.as<uint8_t>(), min_len, h->stream));
     kt.stop();
     std::vector<uint8_t> res(n * s2);
-    VS_HIP(hipMemcpyAsync(res.data(), h->v_out.p, n * s2, hipMemcpyDeviceToHost, h->stream));
-    VS_HIP(hipStreamSynchronize(h->stream));
+    VS_TRY(h->stage.d2h(res.data(), h->v_out.p, n * s2, h->stream));
     kt.fold();
     for (size_t j = 0; j < n; ++j) {
         memcpy(strong.data() + todo[j] * s2, res.data() + j * s2, s2);
@@ -551,7 +511,7 @@ int run_walk(vs_rsync *h, int64_t entry, int32_t want, const SpecWalk *merge,
              std::vector<int64_t> &out_fa, WalkState &ws) {
     RsRun &r = h->run;
     const WalkGeom g{r.flen - r.origin, r.own_hi - r.origin};
-    const std::vector<uint64_t> &off = h->h_off;
+    const PinnedVec<uint64_t> &off = h->h_off;
     ws = WalkState{};
     ws.offset = entry;
     ws.want_i = want;
@@ -656,10 +616,10 @@ int scan_candidates(vs_rsync *h, std::vector<uint64_t> &batch) {
     }
     // 3. sort candidates by offset; host scratch kept in the handle (first-touch
     // page faults on ~160 MB of fresh vectors per call cost ~100 ms at C4 shape)
-    std::vector<uint64_t> &off = h->h_off;
-    std::vector<uint32_t> &sum = h->h_sum;
-    h->reg_off.grow(off, nc);
-    h->reg_sum.grow(sum, nc);
+    PinnedVec<uint64_t> &off = h->h_off;
+    PinnedVec<uint32_t> &sum = h->h_sum;
+    VS_TRY(pv_resize(off, nc));
+    VS_TRY(pv_resize(sum, nc));
     if (nc) {
         VS_TRY(h->c_off2.ensure(nc * 8));
         VS_TRY(h->c_sum2.ensure(nc * 4));
@@ -668,8 +628,6 @@ int scan_candidates(vs_rsync *h, std::vector<uint64_t> &batch) {
         VS_HIP(launch_rs_sort_cands(h->sort_tmp.p, h->sort_tmp.cap, h->c_off.as<uint64_t>(),
                                     h->c_off2.as<uint64_t>(), h->c_sum.as<uint32_t>(),
                                     h->c_sum2.as<uint32_t>(), nc, end_bit, h->stream));
-        VS_HIP(h->reg_off.cover(off));
-        VS_HIP(h->reg_sum.cover(sum));
         VS_HIP(hipMemcpyAsync(off.data(), h->c_off2.p, nc * 8, hipMemcpyDeviceToHost, h->stream));
         VS_HIP(hipMemcpyAsync(sum.data(), h->c_sum2.p, nc * 4, hipMemcpyDeviceToHost, h->stream));
         VS_HIP(hipStreamSynchronize(h->stream));
@@ -685,8 +643,7 @@ int scan_candidates(vs_rsync *h, std::vector<uint64_t> &batch) {
         VS_TRY(h->d_flag.ensure(2 * nc));
         VS_HIP(launch_rs_chained(h->c_off2.as<uint64_t>(), nc, (uint64_t)h->blength,
                                  h->d_flag.as<uint8_t>(), h->stream));
-        h->reg_flag.grow(h->h_flag, nc);
-        VS_HIP(h->reg_flag.cover(h->h_flag));
+        VS_TRY(pv_resize(h->h_flag, nc));
         VS_HIP(hipMemcpyAsync(h->h_flag.data(), h->d_flag.as<uint8_t>() + nc, nc,
                               hipMemcpyDeviceToHost, h->stream));
         VS_HIP(hipStreamSynchronize(h->stream));
@@ -807,25 +764,27 @@ int walk_tail(vs_rsync *h, int64_t x, int32_t xw, int64_t *exit_off, int32_t *ex
     if (h->remainder && o <= t && t < hi && t >= 0) {
         VS_TRY(host_tables(h));
         std::vector<uint8_t> buf((size_t)h->remainder);
-        VS_HIP(hipMemcpyAsync(buf.data(), r.dev + t, buf.size(), hipMemcpyDeviceToHost, h->stream));
-        VS_HIP(hipStreamSynchronize(h->stream));
+        VS_TRY(h->stage.d2h(buf.data(), r.dev + t, buf.size(), h->stream));
         const uint32_t sum = host_weak(buf.data(), h->remainder);
         const uint32_t s2 = (uint32_t)h->s2length;
         // the strong sum on the device (the same kernel the walk's windows use)
         uint8_t st[16] = {0};
         {
-            const uint64_t vo = (uint64_t)t;
             const uint32_t vl = (uint32_t)h->remainder;
             VS_TRY(h->v_off.ensure(8));
             VS_TRY(h->v_len.ensure(4));
             VS_TRY(h->v_out.ensure(16));
-            VS_HIP(hipMemcpyAsync(h->v_off.p, &vo, 8, hipMemcpyHostToDevice, h->stream));
-            VS_HIP(hipMemcpyAsync(h->v_len.p, &vl, 4, hipMemcpyHostToDevice, h->stream));
+            // through the handle's pinned words: [4] offset, [5] length, [6..7] sum
+            h->pinned[4] = (uint64_t)t;
+            h->pinned[5] = vl;
+            VS_HIP(hipMemcpyAsync(h->v_off.p, h->pinned + 4, 8, hipMemcpyHostToDevice, h->stream));
+            VS_HIP(hipMemcpyAsync(h->v_len.p, h->pinned + 5, 4, hipMemcpyHostToDevice, h->stream));
             VS_HIP(launch_rs_strong(r.dev, h->v_off.as<uint64_t>(), h->v_len.as<uint32_t>(), 1,
                                     h->csum_type, h->seed, s2, h->v_out.as<uint8_t>(), vl,
                                     h->stream));
-            VS_HIP(hipMemcpyAsync(st, h->v_out.p, s2, hipMemcpyDeviceToHost, h->stream));
+            VS_HIP(hipMemcpyAsync(h->pinned + 6, h->v_out.p, s2, hipMemcpyDeviceToHost, h->stream));
             VS_HIP(hipStreamSynchronize(h->stream));
+            memcpy(st, h->pinned + 6, s2);
             h->st_hashed += 1;
         }
         o = t + 1;   // no match: hash_search's loop ends (end = F + 1 - remainder)
@@ -965,7 +924,7 @@ int walk_scan(vs_rsync *h) {
     }
     if (wprof) {
         std::vector<uint64_t> pr(nprof);
-        VS_HIP(hipMemcpy(pr.data(), a.prof, nprof * 8, hipMemcpyDeviceToHost));
+        VS_TRY(h->stage.d2h(pr.data(), a.prof, nprof * 8, h->stream));
         const char *names[5] = {"run", "step", "flush", "chain", "segment"};
         double cyc[5] = {0}, cnt[5] = {0}, mx = 0;
         int waves = 0;
@@ -1202,10 +1161,11 @@ VS_API int vs_rsync_open(int device, vs_rsync **out) {
     if (rs_dev(h) < 0 || hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_null, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&h->kev[0]) != hipSuccess || hipEventCreate(&h->kev[1]) != hipSuccess ||
-        hipHostMalloc((void **)&h->pinned, 64, hipHostMallocDefault) != hipSuccess) {
-        (void)hipGetLastError();
+        !(h->pinned = (uint64_t *)pinned_alloc(64))) {
+        const hipError_t e = hipGetLastError();
         vs_rsync_close(h);
-        return fail(VS_ERR_HIP, "stream / pinned buffer creation failed");
+        return fail(VS_ERR_HIP, std::string("stream / event / pinned word creation failed: ") +
+                                    hipGetErrorName(e));
     }
     h->stream = h->own;
     *out = h;
@@ -1232,9 +1192,12 @@ VS_API void vs_rsync_close(vs_rsync *h) {
                       &h->w_exit[0], &h->w_exit[1], &h->w_exitw[0], &h->w_exitw[1], &h->w_ctl, &h->w_prof, &h->fs_scratch, &h->fs_out, &h->rc_pieces,
                       &h->wc_cnt, &h->wc_pos, &h->wc_part, &h->wc_out})
         b->release();
-    if (h->pinned) (void)hipHostFree(h->pinned);
+    pinned_free(h->pinned);
     if (h->wc_host) (void)hipHostFree(h->wc_host);
-    for (HostReg *r : {&h->reg_off, &h->reg_sum, &h->reg_flag}) r->release();
+    h->stage.release();
+    PinnedVec<uint64_t>().swap(h->h_off);
+    PinnedVec<uint32_t>().swap(h->h_sum);
+    PinnedVec<uint8_t>().swap(h->h_flag);
     if (h->ev_null) (void)hipEventDestroy(h->ev_null);
     for (hipEvent_t e : h->kev)
         if (e) (void)hipEventDestroy(e);
@@ -1286,10 +1249,8 @@ VS_API int vs_rsync_load_sums(vs_rsync *h, int32_t count, int32_t blength, int32
     VS_TRY(h->d_sum2p.ensure((size_t)std::max(count, 1) * 16));
     VS_TRY(h->d_sum2tmp.ensure((size_t)std::max(count, 1) * s2length));
     if (count) {
-        VS_HIP(hipMemcpyAsync(h->d_sum1.p, sum1, (size_t)count * 4, hipMemcpyHostToDevice,
-                              h->stream));
-        VS_HIP(hipMemcpyAsync(h->d_sum2tmp.p, sum2, (size_t)count * s2length,
-                              hipMemcpyHostToDevice, h->stream));
+        VS_TRY(h->stage.h2d(h->d_sum1.p, sum1, (size_t)count * 4, h->stream));
+        VS_TRY(h->stage.h2d(h->d_sum2tmp.p, sum2, (size_t)count * s2length, h->stream));
         VS_HIP(launch_rs_pad_sum2(h->d_sum2tmp.as<uint8_t>(), (uint32_t)count, (uint32_t)s2length,
                                   h->d_sum2p.as<uint64_t>(), h->stream));
     }
@@ -1434,8 +1395,7 @@ VS_API int vs_rsync_reconstruct(vs_rsync *h, void *dev_out, int64_t out_len, con
     VS_TRY(rs_dev(h));
     VS_TRY(order_after_null(h));
     VS_TRY(h->rc_pieces.ensure(pc.size() * sizeof(ReconPiece)));
-    VS_HIP(hipMemcpyAsync(h->rc_pieces.p, pc.data(), pc.size() * sizeof(ReconPiece),
-                          hipMemcpyHostToDevice, h->stream));
+    VS_TRY(h->stage.h2d(h->rc_pieces.p, pc.data(), pc.size() * sizeof(ReconPiece), h->stream));
     VS_HIP(launch_recon((uint8_t *)dev_out, (const uint8_t *)dev_basis, (const uint8_t *)dev_literals,
                         h->rc_pieces.as<ReconPiece>(), pc.size(), h->cus, h->stream));
     VS_HIP(hipStreamSynchronize(h->stream));
@@ -1470,15 +1430,14 @@ VS_API int vs_rsync_signatures(int device, const void *basis, int64_t len, int32
         vs_rsync_close(h);
         return r;
     }
-    if (len && hipMemcpy(d.p, basis, (size_t)len, hipMemcpyHostToDevice) != hipSuccess)
-        r = fail(VS_ERR_HIP, "basis upload failed");
+    // the caller's buffers are staged through the handle's own pinned chunks
+    // (xfer.cpp): the runtime is never asked to pin caller memory
+    if (len) r = h->stage.h2d(d.p, basis, (size_t)len, h->stream);
     if (!r)
         r = vs_rsync_signatures_device(h, d.p, len, blength, s2length, csum_type, seed,
                                        s1.as<uint32_t>(), s2.as<uint8_t>());
-    if (!r && count &&
-        (hipMemcpy(sum1, s1.p, (size_t)count * 4, hipMemcpyDeviceToHost) != hipSuccess ||
-         hipMemcpy(sum2, s2.p, (size_t)count * s2length, hipMemcpyDeviceToHost) != hipSuccess))
-        r = fail(VS_ERR_HIP, "signature download failed");
+    if (!r && count) r = h->stage.d2h(sum1, s1.p, (size_t)count * 4, h->stream);
+    if (!r && count) r = h->stage.d2h(sum2, s2.p, (size_t)count * s2length, h->stream);
     d.release();
     s1.release();
     s2.release();
@@ -1498,8 +1457,7 @@ VS_API int vs_rsync_match(int device, const void *src, int64_t len, const vs_sig
     DevBuf d;
     int64_t nm = 0;
     if (!r) r = d.ensure((size_t)std::max<int64_t>(len, 16));
-    if (!r && len && hipMemcpy(d.p, src, (size_t)len, hipMemcpyHostToDevice) != hipSuccess)
-        r = fail(VS_ERR_HIP, "source upload failed");
+    if (!r && len) r = h->stage.h2d(d.p, src, (size_t)len, h->stream);
     if (!r) r = vs_rsync_match_device(h, d.p, len, &nm);
     if (!r) {
         *n_out = (size_t)nm;

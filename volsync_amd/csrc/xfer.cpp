@@ -1,0 +1,145 @@
+// xfer.cpp -- host <-> device copies of caller (pageable) memory, and the
+// error plumbing of HIP calls.
+//
+// The library never page-locks memory it does not own.  Round 2 pinned its
+// std::vector read-back storage with hipHostRegister; that storage shares
+// pages with the rest of the process heap, and a later pageable hipMemcpy of a
+// caller buffer >= 1 MiB -- which the runtime pins on the fly
+// (DmaBlitManager's pinned path) -- failed when its pages overlapped a
+// registered range.  Now every copy whose host side is not
+// hipHostMalloc'd by the library goes through a Stager: two owned pinned
+// buffers, the CPU memcpy of chunk k overlapping the DMA of chunk k-1.  The
+// runtime is never handed a caller pointer to pin.
+#include <cstring>
+#include <string>
+
+#include "internal.hpp"
+
+namespace vsgpu {
+
+int fail_hip(hipError_t e, const char *what, const char *file, int line) {
+    (void)hipGetLastError();  // clear the runtime's last error: it is reported here
+    const char *base = strrchr(file, '/');
+    return fail(VS_ERR_HIP, std::string(what) + ": " + hipGetErrorName(e) + " (" +
+                                std::to_string((int)e) + ", " + hipGetErrorString(e) + ") at " +
+                                (base ? base + 1 : file) + ":" + std::to_string(line));
+}
+
+void *pinned_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, std::max<size_t>(bytes, 64), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return p;
+}
+
+void pinned_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
+bool host_range_pinned(const void *p, size_t n) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (at.type != hipMemoryTypeHost) return false;
+    // the whole range must lie in one page-locked allocation: a DMA that runs
+    // past a registered range's end fails (hipErrorInvalidValue)
+    uintptr_t start = 0;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) !=
+            hipSuccess ||
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) !=
+            hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const uintptr_t a = (uintptr_t)p;
+    return start <= a && a + n <= start + size;
+}
+
+int Stager::init() {
+    if (buf[0]) return 0;
+    for (int i = 0; i < 2; ++i) {
+        buf[i] = (uint8_t *)pinned_alloc(kChunk);
+        if (!buf[i] || hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            release();
+            return fail(VS_ERR_NOMEM, "pinned staging buffers (2 x " + std::to_string(kChunk) +
+                                          " bytes) could not be allocated");
+        }
+        busy[i] = false;
+    }
+    return 0;
+}
+
+int Stager::wait(int i) {
+    if (busy[i]) VS_HIP(hipEventSynchronize(ev[i]));
+    busy[i] = false;
+    return 0;
+}
+
+int Stager::h2d(void *dst, const void *src, size_t n, hipStream_t s) {
+    if (!n) return 0;
+    VS_TRY(init());
+    const uint8_t *p = (const uint8_t *)src;
+    uint8_t *d = (uint8_t *)dst;
+    for (size_t off = 0; off < n; off += kChunk) {
+        const size_t k = std::min(kChunk, n - off);
+        VS_TRY(wait(next));
+        memcpy(buf[next], p + off, k);
+        VS_HIP(hipMemcpyAsync(d + off, buf[next], k, hipMemcpyHostToDevice, s));
+        VS_HIP(hipEventRecord(ev[next], s));
+        busy[next] = true;
+        next ^= 1;
+    }
+    // the caller's bytes are all in staging memory: it may reuse src now; the
+    // DMA stays ordered on s, and the next use of a buffer waits for its event
+    return 0;
+}
+
+int Stager::d2h(void *dst, const void *src, size_t n, hipStream_t s) {
+    if (!n) return 0;
+    VS_TRY(init());
+    const uint8_t *d = (const uint8_t *)src;
+    uint8_t *p = (uint8_t *)dst;
+    // chunk k's DMA runs while chunk k-1 is copied out of staging
+    size_t prev_off = 0, prev_k = 0;
+    int prev = -1;
+    for (size_t off = 0; off < n; off += kChunk) {
+        const size_t k = std::min(kChunk, n - off);
+        VS_TRY(wait(next));
+        VS_HIP(hipMemcpyAsync(buf[next], d + off, k, hipMemcpyDeviceToHost, s));
+        VS_HIP(hipEventRecord(ev[next], s));
+        busy[next] = true;
+        if (prev >= 0) {
+            VS_TRY(wait(prev));
+            memcpy(p + prev_off, buf[prev], prev_k);
+        }
+        prev = next;
+        prev_off = off;
+        prev_k = k;
+        next ^= 1;
+    }
+    VS_TRY(wait(prev));
+    memcpy(p + prev_off, buf[prev], prev_k);
+    return 0;
+}
+
+void Stager::release() {
+    for (int i = 0; i < 2; ++i) {
+        if (ev[i]) {
+            (void)hipEventSynchronize(ev[i]);
+            (void)hipEventDestroy(ev[i]);
+        }
+        pinned_free(buf[i]);
+        buf[i] = nullptr;
+        ev[i] = nullptr;
+        busy[i] = false;
+    }
+    next = 0;
+}
+
+}  // namespace vsgpu
