@@ -311,10 +311,18 @@ static inline uint64_t splitmix_word(uint64_t seed, uint64_t i) {
 
 /* bytes [off, off+n) of the little-endian word stream w_0, w_1, ... */
 void ref_synth_fill(uint64_t seed, uint64_t off, uint64_t n, uint8_t *out) {
-    for (uint64_t k = 0; k < n; ++k) {
-        uint64_t pos = off + k;
-        uint64_t w = splitmix_word(seed, pos >> 3);
-        out[k] = (uint8_t)(w >> (8 * (pos & 7)));
+    uint64_t k = 0;
+    for (; k < n && ((off + k) & 7); ++k) {   /* head: up to the next word */
+        const uint64_t pos = off + k;
+        out[k] = (uint8_t)(splitmix_word(seed, pos >> 3) >> (8 * (pos & 7)));
+    }
+    for (; k + 8 <= n; k += 8) {               /* whole words, little-endian */
+        const uint64_t w = splitmix_word(seed, (off + k) >> 3);
+        for (int b = 0; b < 8; ++b) out[k + b] = (uint8_t)(w >> (8 * b));
+    }
+    for (; k < n; ++k) {                        /* tail */
+        const uint64_t pos = off + k;
+        out[k] = (uint8_t)(splitmix_word(seed, pos >> 3) >> (8 * (pos & 7)));
     }
 }
 

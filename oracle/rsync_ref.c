@@ -19,6 +19,7 @@
  * library rsync 3.2.3 links); MD5 is restated here (RFC 1321).
  */
 #include <dlfcn.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -232,6 +233,70 @@ int ref_rsync_signatures(const uint8_t *basis, int64_t len, int32_t blength, int
         memcpy(sum2 + i * (int64_t)s2length, s, (size_t)s2length);
     }
     return 0;
+}
+
+/* generate_and_send_sums over the synthetic stream `dseed` (cdc_ref.c
+ * ref_synth_fill) of len bytes, on `threads` threads: each thread generates
+ * and sums whole blocks, so a destination far larger than host memory (C4's
+ * 256 GiB) is signed without ever existing in one buffer.  Same output as
+ * ref_rsync_signatures over the materialised stream. */
+void ref_synth_fill(uint64_t seed, uint64_t off, uint64_t n, uint8_t *out);
+
+typedef struct {
+    uint64_t dseed;
+    int64_t len, count, next;
+    int32_t blength, s2length;
+    int csum_type;
+    uint32_t seed;
+    uint32_t *sum1;
+    uint8_t *sum2;
+    int err;
+} sig_job;
+
+static void *sig_worker(void *arg) {
+    sig_job *j = (sig_job *)arg;
+    uint8_t *buf = (uint8_t *)malloc((size_t)j->blength);
+    if (!buf) {
+        __atomic_store_n(&j->err, 1, __ATOMIC_RELAXED);
+        return NULL;
+    }
+    for (;;) {
+        const int64_t b0 = __atomic_fetch_add(&j->next, 64, __ATOMIC_RELAXED);
+        if (b0 >= j->count) break;
+        const int64_t b1 = b0 + 64 < j->count ? b0 + 64 : j->count;
+        for (int64_t i = b0; i < b1; ++i) {
+            const int64_t off = i * (int64_t)j->blength;
+            const int32_t n = (int32_t)((j->len - off < j->blength) ? j->len - off : j->blength);
+            ref_synth_fill(j->dseed, (uint64_t)off, (uint64_t)n, buf);
+            j->sum1[i] = ref_rsync_checksum1(buf, n);
+            uint8_t s[16];
+            if (ref_rsync_checksum2(buf, n, j->csum_type, j->seed, s) < 0) {
+                __atomic_store_n(&j->err, 1, __ATOMIC_RELAXED);
+                break;
+            }
+            memcpy(j->sum2 + i * (int64_t)j->s2length, s, (size_t)j->s2length);
+        }
+    }
+    free(buf);
+    return NULL;
+}
+
+int ref_rsync_signatures_synth_mt(uint64_t dseed, int64_t len, int32_t blength, int32_t s2length,
+                                  int csum_type, uint32_t seed, int threads, uint32_t *sum1,
+                                  uint8_t *sum2) {
+    if (len < 0 || blength <= 0 || s2length < 1 || s2length > 16) return -1;
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    if (csum_type != CSUM_MD5 && !ref_have_xxhash()) return -1;   /* resolve before the threads */
+    sig_job j = {dseed, len, (len + blength - 1) / blength, 0, blength, s2length, csum_type, seed,
+                 sum1, sum2, 0};
+    pthread_t th[256];
+    int started = 0;
+    for (int t = 0; t < threads; ++t)
+        if (pthread_create(&th[t], NULL, sig_worker, &j) == 0) ++started;
+    if (!started) sig_worker(&j);
+    for (int t = 0; t < started; ++t) pthread_join(th[t], NULL);
+    return j.err ? -1 : 0;
 }
 
 /* match_sums -> build_hash_table + hash_search.  Emits the ordered match list

@@ -124,6 +124,25 @@ def rsync_signatures(basis: np.ndarray, blength: int, s2length: int, csum_type: 
     return s1[:count], s2[:count * s2length].reshape(count, s2length)
 
 
+def rsync_signatures_synth_mt(dseed: int, length: int, blength: int, s2length: int,
+                              csum_type: int, seed: int, threads: int = 16):
+    """generate_and_send_sums over the synthetic stream `dseed` of `length`
+    bytes on `threads` threads (oracle/rsync_ref.c ref_rsync_signatures_synth_mt)."""
+    L = _rs()
+    if not getattr(L, "_sigmt_ready", False):
+        L.ref_rsync_signatures_synth_mt.argtypes = [
+            ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
+            ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L._sigmt_ready = True
+    count = (length + blength - 1) // blength
+    s1 = np.zeros(max(count, 1), np.uint32)
+    s2 = np.zeros(max(count, 1) * s2length, np.uint8)
+    if L.ref_rsync_signatures_synth_mt(dseed, length, blength, s2length, csum_type, seed, threads,
+                                       s1.ctypes.data, s2.ctypes.data) < 0:
+        raise RuntimeError("multi-threaded signature restatement failed")
+    return s1[:count], s2[:count * s2length].reshape(count, s2length)
+
+
 def rsync_match(src: np.ndarray, sum1: np.ndarray, sum2: np.ndarray, blength: int,
                 remainder: int, csum_type: int, seed: int):
     count = len(sum1)

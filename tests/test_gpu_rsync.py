@@ -493,3 +493,76 @@ def test_receiver_reconstruct(gpu, path):
     assert (out[: len(src)].cpu().numpy() == src).all()
     assert m.file_sum(out.data_ptr(), len(src), 8) == _file_sum_want(src.tobytes(), 8)
     m.close()
+
+
+def test_c4_real_density_window_exact(gpu):
+    """C4 at its real table density: the 2,097,152-block table of the 256 GiB
+    destination (blength 131072, s2length 5, xxh128, checksum_seed
+    0x5EED5EED) from the device signature pass -- D generated on the device
+    32 GiB at a time -- equals a 16-thread C signature pass over the same
+    stream; then a 2 GiB window of rank 3's (of 8) source range, entered at the
+    walk's true state there, gives exactly the C hash_search's match list,
+    false-alarm count and exit state.  This is the density at which one rank
+    meets ~1.7 M false alarms; the 1 GiB test above is 256x
+    sparser.
+
+    Entry: the C walk from 64 MiB before the window (want_i = count, "no
+    preference") gives the state at the window start; every walk that makes a
+    match continues identically from there (the exit-stitch argument of
+    DESIGN.md 6), and random data leaves no duplicate blocks for want_i to
+    choose among, so this is the state the walk from offset 0 reaches."""
+    import bench
+    import torch
+    from volsync_amd import Matcher, sum_sizes_sqroot, synth_fill_device
+    from volsync_amd.rsync_shard import SourceShard
+    dlen, csum, seed = 256 << 30, R.CSUM_XXH3_128, 0x5EED5EED
+    hdr = sum_sizes_sqroot(dlen)
+    bl, s2l, cnt, rem = hdr.blength, hdr.s2length, hdr.count, hdr.remainder
+    assert (bl, s2l, cnt, rem) == (131072, 5, 2097152, 0)
+    # 1. signatures on the device, 32 GiB of D at a time
+    s1 = torch.zeros(cnt, dtype=torch.int32, device="cuda")
+    s2 = torch.zeros(cnt * s2l, dtype=torch.uint8, device="cuda")
+    piece = 32 << 30
+    buf = torch.empty(piece, dtype=torch.uint8, device="cuda")
+    m = Matcher()
+    for p0 in range(0, dlen, piece):
+        synth_fill_device(buf.data_ptr(), bench.C4Plan.D_SEED, p0, piece)
+        b0 = p0 // bl
+        m.signatures_device(buf.data_ptr(), piece, bl, s2l, csum, seed, s1.data_ptr() + 4 * b0,
+                            s2.data_ptr() + s2l * b0)
+    torch.cuda.synchronize()
+    del buf
+    torch.cuda.empty_cache()
+    c1, c2 = O.rsync_signatures_synth_mt(bench.C4Plan.D_SEED, dlen, bl, s2l, csum, seed, 16)
+    assert (s1.cpu().numpy().view(np.uint32) == c1).all()
+    assert (s2.cpu().numpy().reshape(-1, s2l) == c2).all()
+    # 2. the window: rank 3's range start + 2 GiB of the C4Plan source
+    plan = bench.C4Plan(dlen, bl)
+    sh = SourceShard.for_rank(plan.total, bl, 8, 3)
+    lo, hi = sh.own_lo, sh.own_lo + (2 << 30)
+    pre = lo - (64 << 20)
+    win_lo = pre & ~15
+    host = _plan_host(plan, win_lo, min(hi + bl - 1, plan.total))
+    _, _, e, w = O.rsync_walk(host, win_lo, plan.total, lo, pre, cnt, c1, c2, bl, rem, csum, seed)
+    assert lo <= e < lo + bl
+    want, fa, wexit, wwant = O.rsync_walk(host, win_lo, plan.total, hi, e, w, c1, c2, bl, rem,
+                                          csum, seed)
+    # 3. the device: the rank's scan + speculative walk of [lo, hi), then the
+    # stitch from the true entry (run_walk_shard's protocol)
+    data_lo = lo & ~15
+    n = min(hi + bl - 1, plan.total) - data_lo
+    ds = torch.empty(n, dtype=torch.uint8, device="cuda")
+    plan.fill_device(ds.data_ptr(), data_lo, data_lo + n)
+    torch.cuda.synchronize()
+    assert (ds[:4096].cpu().numpy() == host[data_lo - win_lo:data_lo - win_lo + 4096]).all()
+    m.load_sums_device(cnt, bl, s2l, rem, s1.data_ptr(), s2.data_ptr(), csum, seed)
+    m.match_scan(ds.data_ptr(), n, data_lo, plan.total, lo, hi)
+    gexit = m.match_stitch(e, w)
+    nm = m.match_finish()
+    got = m.matches(0, nm)
+    st = m.stats()
+    m.close()
+    assert len(want) > 14000 and fa > 50000   # the density this test is for
+    assert got == want
+    assert st["false_alarms"] == fa
+    assert gexit == (wexit, wwant)
