@@ -34,6 +34,7 @@ def case(label, n, reg_off, reg_len, src_off, pages=None, unregister_first=False
     if unregister_first and r == 0:
         hip.hipHostUnregister(vp(base + reg_off))
     e = hip.hipMemcpy(dev, vp(base + src_off), n, 1)
+    hip.hipGetLastError()
     print(f"{label:58s} n={n:>9d} register={name(r):28s} memcpy={name(e)}", flush=True)
     if r == 0 and not unregister_first:
         hip.hipHostUnregister(vp(base + reg_off))
@@ -53,7 +54,7 @@ for n in (512 << 10, 1_061_078, 4 << 20, 64 << 20):
 # How a stale registration can arise: two registrations sharing a page.
 print("--- two registrations sharing a page", flush=True)
 for order in ("low-then-high", "high-then-low"):
-    m, buf, base = region(64)
+    m, buf, base = region(1024)
     A, B = (base + 64, 4096 + 100), (base + 4096 + 512, 8192)   # B starts in A's last page
     first, second = (A, B) if order == "low-then-high" else (B, A)
     r1 = hip.hipHostRegister(vp(first[0]), first[1], 0)
@@ -62,6 +63,7 @@ for order in ("low-then-high", "high-then-low"):
     u2 = hip.hipHostUnregister(vp(second[0]))
     # after both were "released": a pageable copy over their bytes
     e = hip.hipMemcpy(dev, vp(base + 128), 2 << 20, 1)
+    hip.hipGetLastError()
     print(f"{order}: reg1={name(r1)} reg2={name(r2)} unreg1={name(u1)} unreg2={name(u2)} "
           f"memcpy-after={name(e)}", flush=True)
     del buf

@@ -138,13 +138,7 @@ struct vs_cdc {
 
 namespace vsgpu {
 
-static int set_dev(vs_cdc *h) {
-    if (hipSetDevice(h->device) != hipSuccess) {
-        (void)hipGetLastError();
-        return fail(VS_ERR_NO_DEVICE, "hipSetDevice(" + std::to_string(h->device) + ") failed");
-    }
-    return 0;
-}
+static int set_dev(vs_cdc *h) { return enter_device(h->device); }
 
 static hipEvent_t get_event(vs_cdc *h) {
     if (!h->ev_pool.empty()) {
@@ -1219,7 +1213,7 @@ VS_API int vs_sha256_open(int device, vs_sha **out) {
     const int ndev = vs_device_count();
     if (ndev <= 0) return fail(VS_ERR_NO_DEVICE, "no HIP device available (no CPU fallback)");
     if (device < 0 || device >= ndev) return fail(VS_ERR_ARG, "device index out of range");
-    VS_HIP(hipSetDevice(device));
+    VS_TRY(enter_device(device));
     vs_sha *h = new vs_sha();
     h->device = device;
     // many independent blobs (C5): throughput mode from 384 active blobs per
@@ -1257,7 +1251,7 @@ VS_API int vs_sha256_run_device(vs_sha *h, const void *dev_buf, const uint64_t *
     if (n && (!dev_buf || !dev_off || !dev_len || !dev_out))
         return fail(VS_ERR_ARG, "null device pointer");
     if (!n) return 0;
-    VS_HIP(hipSetDevice(h->device));
+    VS_TRY(enter_device(h->device));
     return sha_run(h, (const uint8_t *)dev_buf, dev_off, dev_len, n, dev_out,
                    (hipStream_t)hip_stream);
 }
@@ -1267,7 +1261,7 @@ VS_API int vs_sha256_blocks(vs_sha *h, const void *dev_buf, uint64_t len, uint32
     if (!h || !block_size || (len && (!dev_buf || !dev_out))) return fail(VS_ERR_ARG, "bad arguments");
     const uint64_t n = (len + block_size - 1) / block_size;
     if (!n) return 0;
-    VS_HIP(hipSetDevice(h->device));
+    VS_TRY(enter_device(h->device));
     const hipStream_t s = (hipStream_t)hip_stream;
     if (h->ran) VS_HIP(hipStreamWaitEvent(s, h->done, 0));   // descriptors of the last run
     VS_TRY(h->blk_off.ensure(n * 8));
@@ -1293,7 +1287,7 @@ VS_API int vs_blob_verify(vs_sha *h, const void *dev_buf, const uint64_t *dev_of
         return fail(VS_ERR_ARG, "bad arguments");
     if (n_bad) *n_bad = 0;
     if (!n) return 0;
-    VS_HIP(hipSetDevice(h->device));
+    VS_TRY(enter_device(h->device));
     const hipStream_t s = (hipStream_t)hip_stream;
     if (h->ran) VS_HIP(hipStreamWaitEvent(s, h->done, 0));
     VS_TRY(h->vf_ids.ensure(n * 32));
@@ -1318,7 +1312,7 @@ VS_API int vs_blob_verify(vs_sha *h, const void *dev_buf, const uint64_t *dev_of
 VS_API int vs_blob_dedup(vs_sha *h, const uint8_t *dev_ids, size_t n, uint32_t *dev_first,
                          uint64_t *n_unique, void *hip_stream) {
     if (!h || (n && (!dev_ids || !dev_first))) return fail(VS_ERR_ARG, "bad arguments");
-    VS_HIP(hipSetDevice(h->device));
+    VS_TRY(enter_device(h->device));
     const hipStream_t s = (hipStream_t)hip_stream;
     // the distinct-ID counter takes the first 256 bytes: dd_first_kernel adds
     // to it with a 64-bit atomic, which faults unless 8-byte aligned (at the
@@ -1400,7 +1394,7 @@ VS_API int vs_sha256_batch(int device, const void *buf, size_t buf_len, const ui
 VS_API int vs_synth_fill_device(int device, uint64_t seed, uint64_t off, uint64_t n,
                                 void *dev_out, void *hip_stream) {
     if (vs_device_count() <= 0) return fail(VS_ERR_NO_DEVICE, "no HIP device available");
-    VS_HIP(hipSetDevice(device));
+    VS_TRY(enter_device(device));
     VS_HIP(launch_synth(seed, off, n, (uint8_t *)dev_out, (hipStream_t)hip_stream));
     if (!hip_stream) VS_HIP(hipStreamSynchronize(nullptr));  // NULL stream: blocking fill
     return 0;

@@ -653,7 +653,7 @@ VS_API int vs_seal_open(int device, const uint8_t enc_key[32], const uint8_t mac
         return fail(VS_ERR_NO_DEVICE, "no HIP device available (no CPU fallback)");
     }
     if (device < 0 || device >= ndev) return fail(VS_ERR_ARG, "device index out of range");
-    if (hipSetDevice(device) != hipSuccess) return fail(VS_ERR_NO_DEVICE, "hipSetDevice failed");
+    VS_TRY(enter_device(device));
     vs_seal *h = new vs_seal();
     h->device = device;
     if (hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
@@ -730,7 +730,7 @@ VS_API int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *de
         return fail(VS_ERR_ARG, "bad arguments");
     if (!n) return 0;
     if ((uintptr_t)dev_nonces & 15) return fail(VS_ERR_ARG, "nonces must be 16-byte aligned");
-    if (hipSetDevice(h->device) != hipSuccess) return fail(VS_ERR_NO_DEVICE, "hipSetDevice failed");
+    VS_TRY(enter_device(h->device));
     const hipStream_t s = (hipStream_t)hip_stream;
     // the previous run's CTR / MAC kernels read prefix and add into acc
     if (h->ran) VS_HIP(hipStreamWaitEvent(s, h->done, 0));

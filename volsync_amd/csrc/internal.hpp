@@ -23,6 +23,9 @@ int fail_hip(hipError_t e, const char *what, const char *file, int line);
         hipError_t e_ = (call);                                                       \
         if (e_ != hipSuccess) return ::vsgpu::fail_hip(e_, #call, __FILE__, __LINE__); \
     } while (0)
+// every entry point that launches work: clears a stale last error the caller
+// left on this thread, then hipSetDevice (VS_ERR_NO_DEVICE on failure)
+int enter_device(int device);
 #define VS_TRY(expr)                 \
     do {                             \
         int r_ = (expr);             \

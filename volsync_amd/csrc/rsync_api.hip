@@ -119,13 +119,7 @@ struct vs_rsync {
 
 namespace {
 
-int rs_dev(vs_rsync *h) {
-    if (hipSetDevice(h->device) != hipSuccess) {
-        (void)hipGetLastError();
-        return fail(VS_ERR_NO_DEVICE, "hipSetDevice failed");
-    }
-    return 0;
-}
+int rs_dev(vs_rsync *h) { return enter_device(h->device); }
 
 // The handle's own stream is non-blocking: an entry point that reads or
 // writes caller device memory first waits for work the caller queued on the

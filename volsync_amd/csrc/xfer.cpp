@@ -25,6 +25,20 @@ int fail_hip(hipError_t e, const char *what, const char *file, int line) {
                                 (base ? base + 1 : file) + ":" + std::to_string(line));
 }
 
+int enter_device(int device) {
+    // the runtime's last error is per thread and sticky until read: an error
+    // the caller left (a failed hipMemcpy of its own, say) would otherwise be
+    // returned by the hipGetLastError() after this call's first kernel launch
+    (void)hipGetLastError();
+    const hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(VS_ERR_NO_DEVICE, "hipSetDevice(" + std::to_string(device) + "): " +
+                                          hipGetErrorName(e));
+    }
+    return 0;
+}
+
 void *pinned_alloc(size_t bytes) {
     void *p = nullptr;
     if (hipHostMalloc(&p, std::max<size_t>(bytes, 64), hipHostMallocDefault) != hipSuccess) {
