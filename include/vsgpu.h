@@ -294,10 +294,37 @@ int vs_rsync_timing(vs_rsync *h, double ms_out[5]);
  * xxhash / MD5 file sums): the whole-file checksum of a device-resident file,
  * as sum_end writes it -- xxh128: LE low64 then LE high64; xxh3 / xxh64: LE
  * 64-bit value (out[8..15] zeroed); md5: the digest.  XXH3 runs as parallel
- * block contributions plus one serial scramble chain; MD5 and
- * XXH64 run the one-lane restatement.  Blocks until done. */
+ * block contributions on the device plus one serial scramble chain on a host
+ * thread; MD5 and XXH64 run the one-lane restatement.  Blocks
+ * until done. */
 int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_type,
                       uint8_t out[16]);
+/* The same, asynchronous: _start queues the device part (after work queued on
+ * the null stream and on the handle's stream) and returns; the host chain
+ * runs on a library thread while the caller goes on (e.g. with the match walk
+ * over the same file).  dev_src must stay valid and unchanged until _wait,
+ * which returns the digest.  One job per handle: a _start with a job not yet
+ * waited for drops that job's result.  MD5 / XXH64 file sums are one serial
+ * chain on one GPU lane and are refused above 256 MiB (VS_ERR_ARG). */
+int vs_rsync_file_sum_start(vs_rsync *h, const void *dev_src, int64_t len, int csum_type);
+int vs_rsync_file_sum_wait(vs_rsync *h, uint8_t out[16]);
+/* A file split by byte range across ranks: the XXH3 state is a
+ * relay.  _blocks_start chains the nblocks whole 1 KiB blocks at dev_blocks
+ * (file offset a multiple of 1024) from acc_in (NULL: the initial state,
+ * vs_rsync_file_sum_init); _blocks_wait returns the state after them, which
+ * the next range's owner takes as its acc_in.  The owner of the file's last
+ * byte finishes with vs_rsync_file_sum_finish over the file's last
+ * min(len, 1088) bytes (host memory).  XXH3 only (xxh128 and xxh3 share the
+ * state; len > 240). */
+int vs_rsync_file_sum_init(uint64_t acc[8]);
+int vs_rsync_file_sum_blocks_start(vs_rsync *h, const void *dev_blocks, int64_t nblocks,
+                                   const uint64_t acc_in[8]);
+int vs_rsync_file_sum_blocks_wait(vs_rsync *h, uint64_t acc_out[8]);
+int vs_rsync_file_sum_finish(const uint64_t acc[8], const uint8_t *last, int64_t len,
+                             int csum_type, uint8_t out[16]);
+/* The last file-sum job's device time (the contribution kernel, ms) and host
+ * time (the scramble chain, ms). */
+int vs_rsync_file_sum_timing(vs_rsync *h, double *device_ms, double *host_ms);
 /* Replaces receiver.c receive_data: rebuild the new file
  * (out_len bytes, device dev_out) from the basis (device, basis_len bytes,
  * blocks of blength) and the token stream -- the match list (host array, in

@@ -110,6 +110,19 @@ typedef uint64_t (*xxh64_fn)(const void *, size_t, uint64_t);
 static xxh3_128_seed_fn g_x128;
 static xxh3_64_seed_fn g_x3;
 static xxh64_fn g_x64;
+/* streaming API (the whole-file oracle at sizes no host buffer holds) */
+typedef void *(*xxh3_new_fn)(void);
+typedef int (*xxh3_free_fn)(void *);
+typedef int (*xxh3_reset_fn)(void *);
+typedef int (*xxh3_update_fn)(void *, const void *, size_t);
+typedef xxh128_t (*xxh3_128_digest_fn)(const void *);
+typedef uint64_t (*xxh3_64_digest_fn)(const void *);
+static xxh3_new_fn g_xnew;
+static xxh3_free_fn g_xfree;
+static xxh3_reset_fn g_xreset128, g_xreset64;
+static xxh3_update_fn g_xupd128, g_xupd64;
+static xxh3_128_digest_fn g_xdig128;
+static xxh3_64_digest_fn g_xdig64;
 
 int ref_have_xxhash(void) {
     static int probed = 0;
@@ -121,6 +134,14 @@ int ref_have_xxhash(void) {
             g_x128 = (xxh3_128_seed_fn)dlsym(h, "XXH3_128bits_withSeed");
             g_x3 = (xxh3_64_seed_fn)dlsym(h, "XXH3_64bits_withSeed");
             g_x64 = (xxh64_fn)dlsym(h, "XXH64");
+            g_xnew = (xxh3_new_fn)dlsym(h, "XXH3_createState");
+            g_xfree = (xxh3_free_fn)dlsym(h, "XXH3_freeState");
+            g_xreset128 = (xxh3_reset_fn)dlsym(h, "XXH3_128bits_reset");
+            g_xreset64 = (xxh3_reset_fn)dlsym(h, "XXH3_64bits_reset");
+            g_xupd128 = (xxh3_update_fn)dlsym(h, "XXH3_128bits_update");
+            g_xupd64 = (xxh3_update_fn)dlsym(h, "XXH3_64bits_update");
+            g_xdig128 = (xxh3_128_digest_fn)dlsym(h, "XXH3_128bits_digest");
+            g_xdig64 = (xxh3_64_digest_fn)dlsym(h, "XXH3_64bits_digest");
         }
     }
     return g_x128 && g_x3 && g_x64;
@@ -297,6 +318,89 @@ int ref_rsync_signatures_synth_mt(uint64_t dseed, int64_t len, int32_t blength, 
     if (!started) sig_worker(&j);
     for (int t = 0; t < started; ++t) pthread_join(th[t], NULL);
     return j.err ? -1 : 0;
+}
+
+/* checksum.c sum_init/sum_update/sum_end (xxh128 / xxh3, unseeded) over the
+ * synthetic stream `dseed`'s first len bytes, through libxxhash's streaming
+ * API: the R7 oracle at C2/C4 sizes.  Pieces of 64 MiB are generated by
+ * `threads` threads, a batch ahead of the (serial) hashing. */
+typedef struct {
+    uint64_t dseed, off, n;
+    uint8_t *buf;
+} gen_job;
+
+static void *gen_worker(void *arg) {
+    gen_job *g = (gen_job *)arg;
+    ref_synth_fill(g->dseed, g->off, g->n, g->buf);
+    return NULL;
+}
+
+int ref_xxh3_synth(uint64_t dseed, uint64_t len, int csum_type, int threads, uint8_t out[16]) {
+    if (!ref_have_xxhash() || !g_xnew || !g_xupd128 || !g_xdig128) return -1;
+    if (csum_type != CSUM_XXH3_128 && csum_type != CSUM_XXH3_64) return -1;
+    if (threads < 1) threads = 1;
+    if (threads > 64) threads = 64;
+    const uint64_t piece = 64ull << 20, batch = piece * (uint64_t)threads;
+    uint8_t *buf[2];
+    buf[0] = (uint8_t *)malloc(batch);
+    buf[1] = (uint8_t *)malloc(batch);
+    void *st = g_xnew();
+    if (!buf[0] || !buf[1] || !st) {
+        free(buf[0]);
+        free(buf[1]);
+        if (st) g_xfree(st);
+        return -1;
+    }
+    const int x128 = csum_type == CSUM_XXH3_128;
+    (x128 ? g_xreset128 : g_xreset64)(st);
+    gen_job jobs[2][64];
+    pthread_t th[2][64];
+    int nth[2] = {0, 0};
+    /* generate batch k+1 while batch k is hashed */
+    uint64_t boff = 0;
+    int cur = 0;
+    for (uint64_t b = 0; b * batch < len + batch; ++b) {
+        /* start batch b (if any) into buf[cur] */
+        nth[cur] = 0;
+        if (boff < len) {
+            for (int t = 0; t < threads && boff + (uint64_t)t * piece < len; ++t) {
+                const uint64_t o = boff + (uint64_t)t * piece;
+                gen_job *g = &jobs[cur][t];
+                g->dseed = dseed;
+                g->off = o;
+                g->n = len - o < piece ? len - o : piece;
+                g->buf = buf[cur] + (uint64_t)t * piece;
+                if (pthread_create(&th[cur][t], NULL, gen_worker, g) != 0) gen_worker(g), th[cur][t] = 0;
+                nth[cur]++;
+            }
+        }
+        /* hash batch b-1 from buf[cur ^ 1] */
+        const int prv = cur ^ 1;
+        for (int t = 0; t < nth[prv]; ++t) {
+            if (th[prv][t]) pthread_join(th[prv][t], NULL);
+            (x128 ? g_xupd128 : g_xupd64)(st, jobs[prv][t].buf, (size_t)jobs[prv][t].n);
+        }
+        nth[prv] = 0;
+        if (boff >= len) break;
+        boff += batch;
+        cur ^= 1;
+    }
+    for (int k = 0; k < 2; ++k)
+        for (int t = 0; t < nth[k]; ++t)
+            if (th[k][t]) pthread_join(th[k][t], NULL);
+    memset(out, 0, 16);
+    if (x128) {
+        const xxh128_t d = g_xdig128(st);
+        for (int i = 0; i < 8; ++i) out[i] = (uint8_t)(d.low64 >> (8 * i));
+        for (int i = 0; i < 8; ++i) out[8 + i] = (uint8_t)(d.high64 >> (8 * i));
+    } else {
+        const uint64_t d = g_xdig64(st);
+        for (int i = 0; i < 8; ++i) out[i] = (uint8_t)(d >> (8 * i));
+    }
+    g_xfree(st);
+    free(buf[0]);
+    free(buf[1]);
+    return 0;
 }
 
 /* match_sums -> build_hash_table + hash_search.  Emits the ordered match list

@@ -143,6 +143,21 @@ def rsync_signatures_synth_mt(dseed: int, length: int, blength: int, s2length: i
     return s1[:count], s2[:count * s2length].reshape(count, s2length)
 
 
+def xxh3_synth(dseed: int, length: int, csum_type: int, threads: int = 16) -> bytes:
+    """sum_end's 16 bytes of the whole-file XXH3 (xxh128 / xxh3) of the
+    synthetic stream's first `length` bytes (oracle/rsync_ref.c ref_xxh3_synth,
+    libxxhash streaming)."""
+    L = _rs()
+    if not getattr(L, "_xs_ready", False):
+        L.ref_xxh3_synth.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_void_p]
+        L._xs_ready = True
+    out = np.zeros(16, np.uint8)
+    if L.ref_xxh3_synth(dseed, length, csum_type, threads, out.ctypes.data) < 0:
+        raise RuntimeError("streaming XXH3 oracle failed (libxxhash streaming API missing?)")
+    return bytes(out[: 16 if csum_type == 8 else 8])
+
+
 def rsync_match(src: np.ndarray, sum1: np.ndarray, sum2: np.ndarray, blength: int,
                 remainder: int, csum_type: int, seed: int):
     count = len(sum1)

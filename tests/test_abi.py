@@ -96,3 +96,18 @@ def test_no_cpu_fallback_without_device():
     import volsync_amd
     with pytest.raises(volsync_amd.VsError):
         list(volsync_amd.New(__import__("io").BytesIO(b"x" * 100), P.TEST_POL))
+
+
+def test_file_sum_finish_on_host_vs_xxhash():
+    """The host end of the whole-file XXH3 (vs_rsync_file_sum_finish: last
+    partial block, last stripe, merge) from the initial accumulators: for files
+    of 241..1024 bytes there are no whole blocks before it, so the result must
+    be XXH3 of the file itself (no GPU needed)."""
+    import xxhash
+    import volsync_amd as V
+    rng = np.random.default_rng(3)
+    for n in [241, 255, 256, 300, 512, 1000, 1023, 1024]:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        acc = V.file_sum_init()
+        assert V.file_sum_finish(acc, d, n, 8) == xxhash.xxh3_128(d).intdigest().to_bytes(16, "little")
+        assert V.file_sum_finish(acc, d, n, 7) == xxhash.xxh3_64(d).intdigest().to_bytes(8, "little")

@@ -566,3 +566,91 @@ def test_c4_real_density_window_exact(gpu):
     assert got == want
     assert st["false_alarms"] == fa
     assert gexit == (wexit, wwant)
+
+
+def test_file_sum_async_overlaps_match(gpu):
+    """vs_rsync_file_sum_start / _wait (R7 beside the walk, as the C4 step runs
+    it): the digest equals libxxhash while a match run proceeds on the same
+    handle, and the timing split is reported."""
+    import torch
+    from volsync_amd import Matcher, sum_sizes_sqroot
+    n = (96 << 20) + 333
+    basis = O.synth(63, 0, n)
+    src = R.mutate(basis, 4096, seed=3, frac=0.1)
+    hdr = sum_sizes_sqroot(n, 4096)
+    db, ds = to_dev(basis), to_dev(src)
+    s1 = torch.zeros(hdr.count, dtype=torch.int32, device="cuda")
+    s2 = torch.zeros(hdr.count * hdr.s2length, dtype=torch.uint8, device="cuda")
+    m = Matcher()
+    m.signatures_device(db.data_ptr(), n, hdr.blength, hdr.s2length, 8, 5, s1.data_ptr(),
+                        s2.data_ptr())
+    m.load_sums_device(hdr.count, hdr.blength, hdr.s2length, hdr.remainder, s1.data_ptr(),
+                       s2.data_ptr(), 8, 5)
+    for csum in (8, 7):
+        m.file_sum_start(ds.data_ptr(), len(src), csum)
+        got_m = m.match_sums(ds.data_ptr(), len(src))
+        assert m.file_sum_wait() == _file_sum_want(src.tobytes(), csum)
+        assert len(got_m) > 0.8 * hdr.count
+        t = m.file_sum_timing()
+        assert t["device_ms"] > 0 and t["host_chain_ms"] > 0
+    m.close()
+
+
+def test_file_sum_relay_across_ranges(gpu):
+    """A file split across ranks: each range's whole 1 KiB blocks chained from
+    the previous range's accumulators (vs_rsync_file_sum_blocks_*), the last
+    owner finishing with the file's last bytes == one whole-file XXH3."""
+    import volsync_amd as V
+    from volsync_amd import Matcher
+    n = (40 << 20) + 4321
+    data = O.synth(64, 0, n)
+    t = to_dev(data)
+    nb = (n - 1) // 1024
+    cuts = [0, 7 * 1024 + 0, (13 << 20) // 1024, nb]   # block indices: ranges of 7, ~13 K, rest
+    m = Matcher()
+    acc = V.file_sum_init()
+    for lo, hi in zip(cuts, cuts[1:]):
+        m.file_sum_blocks_start(t.data_ptr() + lo * 1024, hi - lo, acc)
+        acc = m.file_sum_blocks_wait()
+    keep = min(n, 1088)
+    for csum in (8, 7):
+        got = V.file_sum_finish(acc, data[n - keep:].tobytes(), n, csum)
+        assert got == _file_sum_want(data.tobytes(), csum)
+    # an empty range passes the state through unchanged
+    m.file_sum_blocks_start(t.data_ptr(), 0, acc)
+    assert (m.file_sum_blocks_wait() == acc).all()
+    m.close()
+
+
+def test_file_sum_64g_exact(gpu):
+    """R7 at C2 / C4 scale: the whole-file XXH3-128 of 64 GiB of the synthetic
+    stream (device-generated) equals libxxhash's streaming digest of the same
+    stream (oracle/rsync_ref.c ref_xxh3_synth, 16 generator threads)."""
+    import torch
+    from volsync_amd import Matcher, synth_fill_device
+    n = (64 << 30) + 777
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    synth_fill_device(t.data_ptr(), 5, 0, n)
+    torch.cuda.synchronize()
+    m = Matcher()
+    got = m.file_sum(t.data_ptr(), n, 8)
+    tm = m.file_sum_timing()
+    m.close()
+    del t
+    torch.cuda.empty_cache()
+    assert got == O.xxh3_synth(5, n, 8, 16)
+    print(f"64 GiB file sum: device {tm['device_ms']:.1f} ms, host chain {tm['host_chain_ms']:.1f} ms")
+
+
+def test_file_sum_serial_types_refused_when_large(gpu):
+    """MD5 / XXH64 whole-file sums are one serial chain on one GPU lane: above
+    256 MiB the library refuses them instead of running minutes."""
+    import torch
+    from volsync_amd import Matcher, VsError
+    t = torch.zeros((256 << 20) + 1, dtype=torch.uint8, device="cuda")
+    m = Matcher()
+    for csum in (5, 6):
+        with pytest.raises(VsError) as e:
+            m.file_sum(t.data_ptr(), t.numel(), csum)
+        assert e.value.code == -1 and "serial" in str(e.value)
+    m.close()

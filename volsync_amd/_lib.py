@@ -92,6 +92,14 @@ def _load() -> ctypes.CDLL:
         "vs_cdc_stream_stats": (c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
         "vs_blob_dedup": (c_int, [vp, vp, c_size, vp, ctypes.POINTER(c_u64), vp]),
         "vs_rsync_file_sum": (c_int, [vp, vp, ctypes.c_int64, c_int, ctypes.c_char_p]),
+        "vs_rsync_file_sum_start": (c_int, [vp, vp, ctypes.c_int64, c_int]),
+        "vs_rsync_file_sum_wait": (c_int, [vp, ctypes.c_char_p]),
+        "vs_rsync_file_sum_init": (c_int, [vp]),
+        "vs_rsync_file_sum_blocks_start": (c_int, [vp, vp, ctypes.c_int64, vp]),
+        "vs_rsync_file_sum_blocks_wait": (c_int, [vp, vp]),
+        "vs_rsync_file_sum_finish": (c_int, [vp, vp, ctypes.c_int64, c_int, ctypes.c_char_p]),
+        "vs_rsync_file_sum_timing": (c_int, [vp, ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(ctypes.c_double)]),
         "vs_sha256_blocks": (c_int, [vp, vp, c_u64, c_u32, vp, vp]),
         "vs_syncthing_block_size": (c_int, [ctypes.c_int64]),
         "vs_blob_verify": (c_int, [vp, vp, vp, vp, c_size, vp, vp, ctypes.POINTER(c_u64), vp]),

@@ -426,11 +426,20 @@ hipError_t launch_rs_collect(const RsWalkArgs &a, uint32_t *cnt, uint32_t *pos, 
                              uint4 *out, unsigned long long *fa_total, hipStream_t s);
 hipError_t launch_rs_pad_sum2(const uint8_t *sum2, uint32_t count, uint32_t s2length,
                               uint64_t *out, hipStream_t s);
-// whole-file checksum (filesum.hip): out = sum_end's digest of p[0, len);
-// scratch holds filesum_scratch_bytes(len, piece_blocks)
-size_t filesum_scratch_bytes(uint64_t len, uint64_t piece_blocks);
-hipError_t launch_filesum(const uint8_t *p, uint64_t len, int csum_type, void *scratch,
-                          uint64_t piece_blocks, uint8_t *out, hipStream_t s);
+// whole-file checksum (filesum.hip + filesum_host.cpp):
+// contributions of nb whole 1 KiB blocks -> C[nb][8] (block-major)
+hipError_t launch_fs_contrib(const uint8_t *p, uint64_t nb, uint64_t *C, hipStream_t s);
+// the one-lane digest (MD5, XXH64, XXH3 of <= 240 bytes) -> out[16]
+hipError_t launch_fs_serial(const uint8_t *p, uint64_t len, int csum_type, uint8_t *out,
+                            hipStream_t s);
+// host: the XXH3 scramble chain over nb contribution rows (AVX-512 when the
+// CPU has it); the last partial block, last stripe and merge from the file's
+// last min(len, 1088) bytes -> sum_end's 16 bytes
+void xxh3_init_acc(uint64_t acc[8]);
+void xxh3_chain_rows(const uint64_t *C, uint64_t nb, uint64_t acc[8]);
+void xxh3_file_finish(const uint8_t *last, uint64_t len, const uint64_t acc[8], int csum_type,
+                      uint8_t out[16]);
+const char *xxh3_chain_isa();
 // restic Key.Seal (crypto.hip)
 struct SealArgs {
     const uint8_t *in;

@@ -19,6 +19,8 @@
 //      made exactly rsync's decisions.
 #include <chrono>
 #include <cstring>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include <cstdio>
@@ -56,6 +58,28 @@ struct RsRun {
     int64_t tail_fa = 0;
 };
 
+// One whole-file checksum in flight (R7): the block
+// contributions on the device (one launch, HBM-bound), read back piece by
+// piece into a pinned ring on the job's own stream -- the copy engine runs
+// beside the walk's kernels -- and chained on a host thread as each piece
+// lands.  XXH3 of <= 240 bytes, XXH64 and MD5 run the one-lane kernel.
+struct FsJob {
+    static constexpr int kRing = 3;
+    uint64_t piece = 1ull << 18;          // blocks per read-back piece (16 MiB of rows)
+    hipStream_t s = nullptr;
+    hipEvent_t ev[kRing] = {}, ev_in = nullptr, kev[2] = {};
+    uint64_t *hC[kRing] = {};             // pinned ring
+    uint8_t *hlast = nullptr;             // pinned: the file's last <= 1088 bytes / the digest
+    DevBuf dC, dout;
+    std::thread th;
+    bool active = false, whole = false, serial = false;
+    int device = 0, csum = 0, rc = 0;
+    std::string err;
+    uint64_t len = 0, nb = 0;
+    uint64_t acc[8] = {};
+    double host_ms = 0, dev_ms = 0;
+};
+
 struct vs_rsync {
     int device = 0;
     int cus = 256;
@@ -87,7 +111,7 @@ struct vs_rsync {
     DevBuf w_fin_entry, w_fin_entryw, w_fin_from, w_fin_n, w_fin_fa, w_fin_off, w_fin_idx,
         w_fin_fab;
     DevBuf w_exit[2], w_exitw[2], w_ctl, w_prof;
-    DevBuf fs_scratch, fs_out;      // whole-file checksum
+    FsJob fs;                       // whole-file checksum
     DevBuf rc_pieces;               // receiver reconstruction
     // scan
     DevBuf px, pt, pxs, pts, partials, c_off, c_sum, c_off2, c_sum2, n_cand, sort_tmp;
@@ -1135,6 +1159,143 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
     return match_finish(h, n_matches);
 }
 
+// ---- whole-file checksum jobs (FsJob) ----------------------------------------
+constexpr uint64_t kFsSerialMax = 256ull << 20;
+
+void fs_thread(FsJob *j, const uint64_t *dC) {
+    const uint64_t np = (j->nb + j->piece - 1) / j->piece;
+    const double t0 = now_ms();
+    double chain = 0;
+    auto fail_here = [&](hipError_t e, const char *what) {
+        j->rc = VS_ERR_HIP;
+        j->err = std::string(what) + ": " + hipGetErrorName(e);
+        (void)hipGetLastError();
+    };
+    if (hipSetDevice(j->device) != hipSuccess) return fail_here(hipGetLastError(), "hipSetDevice");
+    auto issue = [&](uint64_t i) -> bool {
+        const uint64_t b0 = i * j->piece, n = std::min(j->piece, j->nb - b0);
+        hipError_t e = hipMemcpyAsync(j->hC[i % FsJob::kRing], dC + b0 * 8, n * 64,
+                                      hipMemcpyDeviceToHost, j->s);
+        if (e == hipSuccess) e = hipEventRecord(j->ev[i % FsJob::kRing], j->s);
+        if (e != hipSuccess) fail_here(e, "contribution read-back");
+        return e == hipSuccess;
+    };
+    for (uint64_t i = 0; i < std::min<uint64_t>(np, FsJob::kRing); ++i)
+        if (!issue(i)) return;
+    for (uint64_t i = 0; i < np; ++i) {
+        const hipError_t e = hipEventSynchronize(j->ev[i % FsJob::kRing]);
+        if (e != hipSuccess) return fail_here(e, "contribution read-back wait");
+        const uint64_t b0 = i * j->piece, n = std::min(j->piece, j->nb - b0);
+        const double c0 = now_ms();
+        xxh3_chain_rows(j->hC[i % FsJob::kRing], n, j->acc);
+        chain += now_ms() - c0;
+        if (i + FsJob::kRing < np && !issue(i + FsJob::kRing)) return;
+    }
+    j->host_ms = chain;
+    (void)t0;
+}
+
+int fs_setup(FsJob &j, int device) {
+    if (j.s) return 0;
+    j.device = device;
+    VS_HIP(hipStreamCreateWithFlags(&j.s, hipStreamNonBlocking));
+    VS_HIP(hipEventCreateWithFlags(&j.ev_in, hipEventDisableTiming));
+    for (auto &e : j.ev) VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto &e : j.kev) VS_HIP(hipEventCreate(&e));
+    if (!(j.hlast = (uint8_t *)pinned_alloc(2048))) return fail(VS_ERR_NOMEM, "pinned tail buffer");
+    const char *pe = getenv("VSGPU_FS_PIECE");   // tests: many ring turns on small files
+    if (pe && strtoull(pe, nullptr, 10)) j.piece = strtoull(pe, nullptr, 10);
+    for (auto &p : j.hC)
+        if (!(p = (uint64_t *)pinned_alloc(j.piece * 64)))
+            return fail(VS_ERR_NOMEM, "pinned contribution ring");
+    return 0;
+}
+
+// waits for the job (if any); the job's status becomes the return value
+int fs_finish(FsJob &j) {
+    if (!j.active) return 0;
+    if (j.th.joinable()) j.th.join();
+    const hipError_t e = hipStreamSynchronize(j.s);
+    float ms = 0;
+    if (!j.serial && j.nb && hipEventElapsedTime(&ms, j.kev[0], j.kev[1]) == hipSuccess) j.dev_ms = ms;
+    (void)hipGetLastError();
+    if (j.rc < 0) {
+        const int rc = j.rc;
+        j.rc = 0;
+        j.active = false;
+        return fail(rc, "whole-file checksum: " + j.err);
+    }
+    if (e != hipSuccess) {
+        j.active = false;
+        return fail_hip(e, "whole-file checksum stream", __FILE__, __LINE__);
+    }
+    return 0;
+}
+
+void fs_release(FsJob &j) {
+    if (j.th.joinable()) j.th.join();
+    if (j.s) (void)hipStreamSynchronize(j.s);
+    for (auto &p : j.hC) pinned_free(p), p = nullptr;
+    pinned_free(j.hlast);
+    j.hlast = nullptr;
+    j.dC.release();
+    j.dout.release();
+    for (auto &e : j.ev)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
+    for (auto &e : j.kev)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
+    if (j.ev_in) (void)hipEventDestroy(j.ev_in), j.ev_in = nullptr;
+    if (j.s) (void)hipStreamDestroy(j.s), j.s = nullptr;
+    j.active = false;
+}
+
+// whole: the digest of the file p[0, len); else the accumulators after the
+// whole blocks p[0, len) (len a multiple of 1024) chained from acc_in
+int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
+             const uint64_t *acc_in) {
+    FsJob &j = h->fs;
+    VS_TRY(fs_setup(j, h->device));
+    j.whole = whole;
+    j.csum = csum;
+    j.len = len;
+    j.rc = 0;
+    j.err.clear();
+    j.host_ms = j.dev_ms = 0;
+    const bool xxh3 = csum == VS_CSUM_XXH3_64 || csum == VS_CSUM_XXH3_128;
+    j.serial = whole && (!xxh3 || len <= 240);
+    // after the caller's null-stream work and this handle's queued work
+    VS_HIP(hipEventRecord(j.ev_in, h->stream));
+    VS_HIP(hipStreamWaitEvent(j.s, j.ev_in, 0));
+    if (j.serial) {
+        VS_TRY(j.dout.ensure(16));
+        VS_HIP(launch_fs_serial(p, len, csum, j.dout.as<uint8_t>(), j.s));
+        VS_HIP(hipMemcpyAsync(j.hlast, j.dout.p, 16, hipMemcpyDeviceToHost, j.s));
+        j.nb = 0;
+        j.active = true;
+        return 0;
+    }
+    j.nb = whole ? (len - 1) / 1024 : len / 1024;
+    if (whole) {
+        xxh3_init_acc(j.acc);
+    } else {
+        if (acc_in) memcpy(j.acc, acc_in, 64);
+        else xxh3_init_acc(j.acc);
+    }
+    if (whole) {   // the last partial block, last stripe: read back for the finish
+        const uint64_t keep = std::min<uint64_t>(len, 1088);
+        VS_HIP(hipMemcpyAsync(j.hlast, p + len - keep, keep, hipMemcpyDeviceToHost, j.s));
+    }
+    if (j.nb) {
+        VS_TRY(j.dC.ensure(j.nb * 64));
+        VS_HIP(hipEventRecord(j.kev[0], j.s));
+        VS_HIP(launch_fs_contrib(p, j.nb, j.dC.as<uint64_t>(), j.s));
+        VS_HIP(hipEventRecord(j.kev[1], j.s));
+        j.th = std::thread(fs_thread, &j, j.dC.as<const uint64_t>());
+    }
+    j.active = true;
+    return 0;
+}
+
 }  // namespace
 
 VS_API int vs_rsync_sizes(int64_t len, int32_t block_size, int32_t *blength, int32_t *s2length,
@@ -1175,6 +1336,7 @@ VS_API int vs_rsync_set_stream(vs_rsync *h, void *hip_stream) {
 VS_API void vs_rsync_close(vs_rsync *h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    fs_release(h->fs);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (DevBuf *b : {&h->d_sum1, &h->d_keys, &h->d_tkey, &h->d_dir, &h->d_filt, &h->d_tmp, &h->px,
                       &h->pt, &h->pxs, &h->pts, &h->partials, &h->c_off, &h->c_sum, &h->c_off2,
@@ -1183,7 +1345,7 @@ VS_API void vs_rsync_close(vs_rsync *h) {
                       &h->w_spec_fab, &h->w_spec_n, &h->w_spec_fa, &h->w_spec_exit,
                       &h->w_spec_exitw, &h->w_fin_entry, &h->w_fin_entryw, &h->w_fin_from,
                       &h->w_fin_n, &h->w_fin_fa, &h->w_fin_off, &h->w_fin_idx, &h->w_fin_fab,
-                      &h->w_exit[0], &h->w_exit[1], &h->w_exitw[0], &h->w_exitw[1], &h->w_ctl, &h->w_prof, &h->fs_scratch, &h->fs_out, &h->rc_pieces,
+                      &h->w_exit[0], &h->w_exit[1], &h->w_exitw[0], &h->w_exitw[1], &h->w_ctl, &h->w_prof, &h->rc_pieces,
                       &h->wc_cnt, &h->wc_pos, &h->wc_part, &h->wc_out})
         b->release();
     pinned_free(h->pinned);
@@ -1325,31 +1487,96 @@ VS_API int vs_rsync_timing(vs_rsync *h, double ms_out[5]) {
     return 0;
 }
 
-VS_API int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_type,
-                             uint8_t out[16]) {
-    if (!h || !out || len < 0 || (len && !dev_src)) return fail(VS_ERR_ARG, "bad arguments");
+VS_API int vs_rsync_file_sum_start(vs_rsync *h, const void *dev_src, int64_t len, int csum_type) {
+    if (!h || len < 0 || (len && !dev_src)) return fail(VS_ERR_ARG, "bad arguments");
     if (csum_type != VS_CSUM_MD5 && csum_type != VS_CSUM_XXH64 && csum_type != VS_CSUM_XXH3_64 &&
         csum_type != VS_CSUM_XXH3_128)
         return fail(VS_ERR_ARG, "unsupported checksum type");
+    const bool xxh3 = csum_type == VS_CSUM_XXH3_64 || csum_type == VS_CSUM_XXH3_128;
+    if (!xxh3 && len > kFsSerialMax)
+        return fail(VS_ERR_ARG, "whole-file MD5 / XXH64 is one serial chain (one GPU lane, "
+                                "~0.1 GB/s): refused above " + std::to_string(kFsSerialMax) +
+                                " bytes -- negotiate xxh128 (DESIGN.md 3.4)");
     VS_TRY(rs_dev(h));
+    VS_TRY(fs_finish(h->fs));   // a job never waited for: its result is dropped
+    h->fs.active = false;
     VS_TRY(order_after_null(h));
-    // 4 GiB of file per contribution pass (256 MiB scratch); VSGPU_FS_PIECE
-    // (blocks) overrides it so tests can cover the multi-pass carry
-    const char *pe = getenv("VSGPU_FS_PIECE");
-    const uint64_t pv = pe ? strtoull(pe, nullptr, 10) : 0;
-    const uint64_t piece = pv ? pv : (1ull << 22);
-    VS_TRY(h->fs_scratch.ensure(filesum_scratch_bytes((uint64_t)len, piece)));
-    VS_TRY(h->fs_out.ensure(16));
-    KernelTimer kt(h, 4);
-    VS_HIP(launch_filesum((const uint8_t *)dev_src, (uint64_t)len, csum_type, h->fs_scratch.p, piece,
-                          h->fs_out.as<uint8_t>(), h->stream));
-    kt.stop();
-    VS_HIP(hipMemcpyAsync(h->pinned, h->fs_out.p, 16, hipMemcpyDeviceToHost, h->stream));
-    VS_HIP(hipStreamSynchronize(h->stream));
-    kt.fold();
+    return fs_start(h, (const uint8_t *)dev_src, (uint64_t)len, csum_type, true, nullptr);
+}
+
+VS_API int vs_rsync_file_sum_wait(vs_rsync *h, uint8_t out[16]) {
+    if (!h || !out) return fail(VS_ERR_ARG, "bad arguments");
+    FsJob &j = h->fs;
+    if (!j.active || !j.whole) return fail(VS_ERR_STATE, "no whole-file checksum in flight");
+    VS_TRY(rs_dev(h));
+    VS_TRY(fs_finish(j));
+    j.active = false;
+    h->kms[4] += j.dev_ms;
+    h->kn[4] += 1;
     memset(out, 0, 16);
-    const int n = (csum_type == VS_CSUM_MD5 || csum_type == VS_CSUM_XXH3_128) ? 16 : 8;
-    memcpy(out, h->pinned, n);
+    const int n = (j.csum == VS_CSUM_MD5 || j.csum == VS_CSUM_XXH3_128) ? 16 : 8;
+    if (j.serial) {
+        memcpy(out, j.hlast, (size_t)n);
+    } else {
+        uint8_t o[16];
+        xxh3_file_finish(j.hlast, j.len, j.acc, j.csum, o);
+        memcpy(out, o, (size_t)n);
+    }
+    return 0;
+}
+
+VS_API int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_type,
+                             uint8_t out[16]) {
+    VS_TRY(vs_rsync_file_sum_start(h, dev_src, len, csum_type));
+    return vs_rsync_file_sum_wait(h, out);
+}
+
+VS_API int vs_rsync_file_sum_blocks_start(vs_rsync *h, const void *dev_blocks, int64_t nblocks,
+                                          const uint64_t acc_in[8]) {
+    if (!h || nblocks < 0 || (nblocks && !dev_blocks)) return fail(VS_ERR_ARG, "bad arguments");
+    VS_TRY(rs_dev(h));
+    VS_TRY(fs_finish(h->fs));
+    h->fs.active = false;
+    VS_TRY(order_after_null(h));
+    return fs_start(h, (const uint8_t *)dev_blocks, (uint64_t)nblocks * 1024, VS_CSUM_XXH3_128,
+                    false, acc_in);
+}
+
+VS_API int vs_rsync_file_sum_blocks_wait(vs_rsync *h, uint64_t acc_out[8]) {
+    if (!h || !acc_out) return fail(VS_ERR_ARG, "bad arguments");
+    FsJob &j = h->fs;
+    if (!j.active || j.whole) return fail(VS_ERR_STATE, "no block-range checksum in flight");
+    VS_TRY(rs_dev(h));
+    VS_TRY(fs_finish(j));
+    j.active = false;
+    h->kms[4] += j.dev_ms;
+    h->kn[4] += 1;
+    memcpy(acc_out, j.acc, 64);
+    return 0;
+}
+
+VS_API int vs_rsync_file_sum_finish(const uint64_t acc[8], const uint8_t *last, int64_t len,
+                                    int csum_type, uint8_t out[16]) {
+    if (!acc || !last || !out || len <= 240 ||
+        (csum_type != VS_CSUM_XXH3_64 && csum_type != VS_CSUM_XXH3_128))
+        return fail(VS_ERR_ARG, "bad arguments (XXH3 of a file over 240 bytes)");
+    uint8_t o[16];
+    xxh3_file_finish(last, (uint64_t)len, acc, csum_type, o);
+    memset(out, 0, 16);
+    memcpy(out, o, csum_type == VS_CSUM_XXH3_128 ? 16 : 8);
+    return 0;
+}
+
+VS_API int vs_rsync_file_sum_init(uint64_t acc[8]) {
+    if (!acc) return fail(VS_ERR_ARG, "null accumulators");
+    xxh3_init_acc(acc);
+    return 0;
+}
+
+VS_API int vs_rsync_file_sum_timing(vs_rsync *h, double *device_ms, double *host_ms) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    if (device_ms) *device_ms = h->fs.dev_ms;
+    if (host_ms) *host_ms = h->fs.host_ms;
     return 0;
 }
 

@@ -182,6 +182,38 @@ class Matcher:
         check(lib.vs_rsync_file_sum(self._h, ctypes.c_void_p(dev_src), length, csum_type, out))
         return out.raw[: 16 if csum_type in (CSUM_MD5, CSUM_XXH3_128) else 8]
 
+    def file_sum_start(self, dev_src: int, length: int, csum_type: int = 8) -> None:
+        """vs_rsync_file_sum_start: the device part queued, the host chain on a
+        library thread; dev_src must stay valid until file_sum_wait."""
+        check(lib.vs_rsync_file_sum_start(self._h, ctypes.c_void_p(dev_src or None), length,
+                                          csum_type))
+        self._fs_csum = csum_type
+
+    def file_sum_wait(self) -> bytes:
+        out = ctypes.create_string_buffer(16)
+        check(lib.vs_rsync_file_sum_wait(self._h, out))
+        return out.raw[: 16 if self._fs_csum in (CSUM_MD5, CSUM_XXH3_128) else 8]
+
+    def file_sum_blocks_start(self, dev_blocks: int, nblocks: int, acc_in=None) -> None:
+        """One byte range of a file split across ranks: chain its whole 1 KiB
+        blocks from acc_in (None: the initial state)."""
+        a = None if acc_in is None else np.ascontiguousarray(acc_in, np.uint64)
+        self._acc_in = a
+        check(lib.vs_rsync_file_sum_blocks_start(self._h, ctypes.c_void_p(dev_blocks or None),
+                                                 nblocks, None if a is None else a.ctypes.data))
+
+    def file_sum_blocks_wait(self) -> np.ndarray:
+        acc = np.zeros(8, np.uint64)
+        check(lib.vs_rsync_file_sum_blocks_wait(self._h, acc.ctypes.data))
+        return acc
+
+    def file_sum_timing(self) -> dict:
+        d, hm = ctypes.c_double(0), ctypes.c_double(0)
+        check(lib.vs_rsync_file_sum_timing(self._h, ctypes.byref(d), ctypes.byref(hm)))
+        return {"device_ms": d.value, "host_chain_ms": hm.value}
+
+    _fs_csum = 8
+
     def reconstruct(self, dev_out: int, out_len: int, dev_basis: int, basis_len: int,
                     blength: int, matches: List[Tuple[int, int]], dev_literals: int,
                     literal_len: int) -> None:
@@ -198,6 +230,24 @@ class Matcher:
         return self.matches(0, self.match_device(dev_src, length))
 
     _last_n = 0
+
+
+def file_sum_init() -> np.ndarray:
+    """The XXH3 accumulators of an empty file (the relay's first acc_in)."""
+    acc = np.zeros(8, np.uint64)
+    check(lib.vs_rsync_file_sum_init(acc.ctypes.data))
+    return acc
+
+
+def file_sum_finish(acc, last: bytes, length: int, csum_type: int = CSUM_XXH3_128) -> bytes:
+    """sum_end for a file split across ranks: the accumulators after the
+    file's whole 1 KiB blocks ((length - 1) // 1024 of them) and its last
+    min(length, 1088) bytes."""
+    a = np.ascontiguousarray(acc, np.uint64)
+    b = np.frombuffer(bytes(last), np.uint8)
+    out = ctypes.create_string_buffer(16)
+    check(lib.vs_rsync_file_sum_finish(a.ctypes.data, b.ctypes.data, length, csum_type, out))
+    return out.raw[: 16 if csum_type == CSUM_XXH3_128 else 8]
 
 
 def match_sums(src, s: SumStruct, csum_type: int = CSUM_XXH3_128, seed: int = 0,
