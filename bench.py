@@ -287,8 +287,45 @@ def rsync_main(args):
     torch.cuda.synchronize(dev)
     coll = torch_pair_collectives(coll_device(dev)) if world > 1 else (lambda p: [p], lambda x: x)
     xst = {}
+    # R7 inside the step (checksum.c sum_update over S, xxh128 unseeded as
+    # sum_init): device contributions + a host scramble chain on its own
+    # handle.  The chain is one serial dependency per KiB of
+    # the file, so file k's chain runs beside file k+1's step (two jobs in
+    # flight, each on its own host thread) and the timed region ends when the
+    # last one is done.  One GPU: the whole file S.  --share: the rank's whole
+    # 1 KiB blocks of S from a stand-in relay state (the value rank R-1 would
+    # hand over; the chain's cost does not depend on it).
+    fsm = Matcher(local)
+    fsm.set_stream(stream)
+    nb_file = (plan.total - 1) // 1024
+    fs_blocks = None
+    if share:
+        b_lo = min(-(-sspec.own_lo // 1024), nb_file)
+        b_hi = min(-(-sspec.own_hi // 1024), nb_file)
+        fs_blocks = (ds.data_ptr() + b_lo * 1024 - sspec.data_lo, b_hi - b_lo)
+    fs_on = (world == 1 or share) and not args.no_file_sum
+    fs_out = []
+    fs_inflight = [0]
+
+    def fs_start():
+        if not fs_on:
+            return
+        if fs_inflight[0] == 2:
+            fs_wait()
+        if fs_blocks is None:
+            fsm.file_sum_start(ds.data_ptr(), plan.total, CSUM_XXH3_128)
+        else:
+            fsm.file_sum_blocks_start(fs_blocks[0], fs_blocks[1], None)
+        fs_inflight[0] += 1
+
+    def fs_wait():
+        r = fsm.file_sum_wait() if fs_blocks is None else fsm.file_sum_blocks_wait()
+        fs_inflight[0] -= 1
+        fs_out.append((r.hex() if isinstance(r, bytes) else
+                       "".join(f"{int(x):016x}" for x in r), fsm.file_sum_timing()))
 
     def step():
+        fs_start()
         m.signatures_device(db.data_ptr(), n, hdr.blength, hdr.s2length, CSUM_XXH3_128, seed,
                             s1.data_ptr(), s2.data_ptr())
         f1, f2 = s1, s2
@@ -309,6 +346,9 @@ def rsync_main(args):
 
     for _ in range(args.warmup):
         step()
+    while fs_inflight[0]:
+        fs_wait()
+    fs_out.clear()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -320,6 +360,9 @@ def rsync_main(args):
         nm = step()
         for k, v in m.timing().items():
             stages[k] += v
+    t_gpu = time.perf_counter()
+    while fs_inflight[0]:
+        fs_wait()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -336,19 +379,28 @@ def rsync_main(args):
     own_src = sspec.own_hi - sspec.own_lo
     # a --share line counts the rank's own bytes: its D blocks and S range
     value = ((n + own_src) if share else (dtotal + plan.total)) * args.steps / dt / 1e9
-    # R7's whole-file checksum (checksum.c sum_update over S, xxh128), timed
-    # on its own after the timed region: its scramble chain is one serial
-    # dependency over the whole file, so it is reported beside the step
     fsum = None
-    if world == 1 and not share:
+    if fs_on:
+        # the same checksum alone, after the timed region: its latency
         torch.cuda.synchronize(dev)
-        m.kernel_time(reset=False)
         t1 = time.perf_counter()
-        m.file_sum(ds.data_ptr(), plan.total, CSUM_XXH3_128)
+        fs_start()
+        fs_wait()
         fs_dt = time.perf_counter() - t1
-        fk = m.kernel_time()["file_sum"]
-        fsum = {"ms": round(fs_dt * 1e3, 2), "GBps": round(plan.total / fs_dt / 1e9, 2),
-                "kernel_ms": round(fk[0], 2), "csum": "xxh128 (unseeded, as sum_init)"}
+        digests = {d for d, _ in fs_out}
+        tm = fs_out[-1][1]
+        fbytes = plan.total if fs_blocks is None else fs_blocks[1] * 1024
+        fsum = {"inside_step": True, "jobs_in_flight": 2,
+                "ms_alone": round(fs_dt * 1e3, 2), "GBps_alone": round(fbytes / fs_dt / 1e9, 2),
+                "contrib_kernel_ms": round(tm["device_ms"], 2),
+                "host_chain_ms": round(tm["host_chain_ms"], 2),
+                "host_chain_ns_per_KiB": round(tm["host_chain_ms"] * 1e6 / max(fbytes / 1024, 1), 3),
+                "gpu_steps_done_ms_per_step": round((t_gpu - t0) / args.steps * 1e3, 3),
+                "bytes": fbytes, "csum": "xxh128 (unseeded, as sum_init)",
+                "scope": ("whole file S" if fs_blocks is None else
+                          f"the rank's {fs_blocks[1]} whole 1 KiB blocks of S (stand-in relay state)"),
+                "digest" if fs_blocks is None else "state_out": sorted(digests)[0],
+                "identical_every_step": len(digests) == 1}
     # the dominant kernel: rs_walk_spec_kernel, one launch per step over the
     # rank's whole source range (algorithmic bytes = those source bytes, each
     # read once by the walk: a window hash where it matches, the rolling scan
@@ -407,6 +459,7 @@ def rsync_main(args):
             out["cpu_baseline"] = rsync_cpu_baseline(args.cpu_sample_gib << 28)
         print(json.dumps(out), flush=True)
     m.close()
+    fsm.close()
     if world > 1:
         dist.destroy_process_group()
 
@@ -911,6 +964,8 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=int, default=4)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-file-sum", action="store_true",
+                    help="rsync: leave R7 (the whole-file checksum) out of the step (A/B)")
     ap.add_argument("--hash-stream", choices=["own", "main"], default="own",
                     help="SHA-256 slices on the handle's own hash stream (overlapping the next "
                          "fingerprint pass) or serialised on the main stream")

@@ -302,10 +302,12 @@ int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_ty
 /* The same, asynchronous: _start queues the device part (after work queued on
  * the null stream and on the handle's stream) and returns; the host chain
  * runs on a library thread while the caller goes on (e.g. with the match walk
- * over the same file).  dev_src must stay valid and unchanged until _wait,
- * which returns the digest.  One job per handle: a _start with a job not yet
- * waited for drops that job's result.  MD5 / XXH64 file sums are one serial
- * chain on one GPU lane and are refused above 256 MiB (VS_ERR_ARG). */
+ * over the same file).  dev_src must stay valid and unchanged until its _wait.
+ * Up to 4 jobs (whole files or block ranges) may be in flight per handle,
+ * each with its own host thread: _wait returns the OLDEST job's digest (jobs
+ * complete in start order; the _blocks_ form shares the queue).  MD5 / XXH64
+ * file sums are one serial chain on one GPU lane and are refused above
+ * 256 MiB (VS_ERR_ARG). */
 int vs_rsync_file_sum_start(vs_rsync *h, const void *dev_src, int64_t len, int csum_type);
 int vs_rsync_file_sum_wait(vs_rsync *h, uint8_t out[16]);
 /* A file split by byte range across ranks: the XXH3 state is a

@@ -654,3 +654,23 @@ def test_file_sum_serial_types_refused_when_large(gpu):
             m.file_sum(t.data_ptr(), t.numel(), csum)
         assert e.value.code == -1 and "serial" in str(e.value)
     m.close()
+
+
+def test_file_sum_jobs_fifo(gpu):
+    """Several whole-file checksums in flight on one handle (the C4 bench keeps
+    two: file k's chain overlaps file k+1's walk): digests come back in start
+    order; a fifth job is refused until one is waited for."""
+    from volsync_amd import Matcher, VsError
+    files = [O.synth(70 + k, 0, (k + 1) * (3 << 20) + 17 * k + 241) for k in range(4)]
+    devs = [to_dev(f) for f in files]
+    m = Matcher()
+    for csum in (8, 7):
+        for f, t in zip(files, devs):
+            m.file_sum_start(t.data_ptr(), len(f), csum)
+        with pytest.raises(VsError):
+            m.file_sum_start(devs[0].data_ptr(), len(files[0]), csum)
+        for f in files:
+            assert m.file_sum_wait() == _file_sum_want(f.tobytes(), csum)
+    with pytest.raises(VsError):
+        m.file_sum_wait()
+    m.close()

@@ -111,7 +111,12 @@ struct vs_rsync {
     DevBuf w_fin_entry, w_fin_entryw, w_fin_from, w_fin_n, w_fin_fa, w_fin_off, w_fin_idx,
         w_fin_fab;
     DevBuf w_exit[2], w_exitw[2], w_ctl, w_prof;
-    FsJob fs;                       // whole-file checksum
+    // whole-file checksums in flight, FIFO: a file's chain may overlap the
+    // next file's walk (and the next file's chain, on another host thread)
+    static constexpr uint32_t kFsJobs = 4;
+    FsJob fs[kFsJobs];
+    uint32_t fs_head = 0, fs_tail = 0;   // jobs [head, tail) are in flight
+    double fs_dev_ms = 0, fs_host_ms = 0; // the last job waited for
     DevBuf rc_pieces;               // receiver reconstruction
     // scan
     DevBuf px, pt, pxs, pts, partials, c_off, c_sum, c_off2, c_sum2, n_cand, sort_tmp;
@@ -1249,11 +1254,20 @@ void fs_release(FsJob &j) {
     j.active = false;
 }
 
+void fs_account(vs_rsync *h, const FsJob &j) {
+    h->kms[4] += j.dev_ms;
+    h->kn[4] += 1;
+    h->fs_dev_ms = j.dev_ms;
+    h->fs_host_ms = j.host_ms;
+}
+
 // whole: the digest of the file p[0, len); else the accumulators after the
 // whole blocks p[0, len) (len a multiple of 1024) chained from acc_in
 int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
              const uint64_t *acc_in) {
-    FsJob &j = h->fs;
+    if (h->fs_tail - h->fs_head == vs_rsync::kFsJobs)
+        return fail(VS_ERR_STATE, "4 whole-file checksums in flight: wait for one first");
+    FsJob &j = h->fs[h->fs_tail % vs_rsync::kFsJobs];
     VS_TRY(fs_setup(j, h->device));
     j.whole = whole;
     j.csum = csum;
@@ -1272,6 +1286,7 @@ int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
         VS_HIP(hipMemcpyAsync(j.hlast, j.dout.p, 16, hipMemcpyDeviceToHost, j.s));
         j.nb = 0;
         j.active = true;
+        h->fs_tail++;
         return 0;
     }
     j.nb = whole ? (len - 1) / 1024 : len / 1024;
@@ -1293,6 +1308,7 @@ int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
         j.th = std::thread(fs_thread, &j, j.dC.as<const uint64_t>());
     }
     j.active = true;
+    h->fs_tail++;
     return 0;
 }
 
@@ -1336,7 +1352,7 @@ VS_API int vs_rsync_set_stream(vs_rsync *h, void *hip_stream) {
 VS_API void vs_rsync_close(vs_rsync *h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
-    fs_release(h->fs);
+    for (FsJob &j : h->fs) fs_release(j);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (DevBuf *b : {&h->d_sum1, &h->d_keys, &h->d_tkey, &h->d_dir, &h->d_filt, &h->d_tmp, &h->px,
                       &h->pt, &h->pxs, &h->pts, &h->partials, &h->c_off, &h->c_sum, &h->c_off2,
@@ -1498,21 +1514,20 @@ VS_API int vs_rsync_file_sum_start(vs_rsync *h, const void *dev_src, int64_t len
                                 "~0.1 GB/s): refused above " + std::to_string(kFsSerialMax) +
                                 " bytes -- negotiate xxh128 (DESIGN.md 3.4)");
     VS_TRY(rs_dev(h));
-    VS_TRY(fs_finish(h->fs));   // a job never waited for: its result is dropped
-    h->fs.active = false;
     VS_TRY(order_after_null(h));
     return fs_start(h, (const uint8_t *)dev_src, (uint64_t)len, csum_type, true, nullptr);
 }
 
 VS_API int vs_rsync_file_sum_wait(vs_rsync *h, uint8_t out[16]) {
     if (!h || !out) return fail(VS_ERR_ARG, "bad arguments");
-    FsJob &j = h->fs;
-    if (!j.active || !j.whole) return fail(VS_ERR_STATE, "no whole-file checksum in flight");
+    if (h->fs_head == h->fs_tail) return fail(VS_ERR_STATE, "no whole-file checksum in flight");
+    FsJob &j = h->fs[h->fs_head % vs_rsync::kFsJobs];
+    if (!j.whole) return fail(VS_ERR_STATE, "the oldest checksum job is a block range");
     VS_TRY(rs_dev(h));
-    VS_TRY(fs_finish(j));
+    h->fs_head++;
     j.active = false;
-    h->kms[4] += j.dev_ms;
-    h->kn[4] += 1;
+    VS_TRY(fs_finish(j));
+    fs_account(h, j);
     memset(out, 0, 16);
     const int n = (j.csum == VS_CSUM_MD5 || j.csum == VS_CSUM_XXH3_128) ? 16 : 8;
     if (j.serial) {
@@ -1535,8 +1550,6 @@ VS_API int vs_rsync_file_sum_blocks_start(vs_rsync *h, const void *dev_blocks, i
                                           const uint64_t acc_in[8]) {
     if (!h || nblocks < 0 || (nblocks && !dev_blocks)) return fail(VS_ERR_ARG, "bad arguments");
     VS_TRY(rs_dev(h));
-    VS_TRY(fs_finish(h->fs));
-    h->fs.active = false;
     VS_TRY(order_after_null(h));
     return fs_start(h, (const uint8_t *)dev_blocks, (uint64_t)nblocks * 1024, VS_CSUM_XXH3_128,
                     false, acc_in);
@@ -1544,13 +1557,14 @@ VS_API int vs_rsync_file_sum_blocks_start(vs_rsync *h, const void *dev_blocks, i
 
 VS_API int vs_rsync_file_sum_blocks_wait(vs_rsync *h, uint64_t acc_out[8]) {
     if (!h || !acc_out) return fail(VS_ERR_ARG, "bad arguments");
-    FsJob &j = h->fs;
-    if (!j.active || j.whole) return fail(VS_ERR_STATE, "no block-range checksum in flight");
+    if (h->fs_head == h->fs_tail) return fail(VS_ERR_STATE, "no block-range checksum in flight");
+    FsJob &j = h->fs[h->fs_head % vs_rsync::kFsJobs];
+    if (j.whole) return fail(VS_ERR_STATE, "the oldest checksum job is a whole file");
     VS_TRY(rs_dev(h));
-    VS_TRY(fs_finish(j));
+    h->fs_head++;
     j.active = false;
-    h->kms[4] += j.dev_ms;
-    h->kn[4] += 1;
+    VS_TRY(fs_finish(j));
+    fs_account(h, j);
     memcpy(acc_out, j.acc, 64);
     return 0;
 }
@@ -1575,8 +1589,8 @@ VS_API int vs_rsync_file_sum_init(uint64_t acc[8]) {
 
 VS_API int vs_rsync_file_sum_timing(vs_rsync *h, double *device_ms, double *host_ms) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
-    if (device_ms) *device_ms = h->fs.dev_ms;
-    if (host_ms) *host_ms = h->fs.host_ms;
+    if (device_ms) *device_ms = h->fs_dev_ms;
+    if (host_ms) *host_ms = h->fs_host_ms;
     return 0;
 }
 
