@@ -402,6 +402,29 @@ int vs_rsync_write_tokens(const vs_match *matches, int64_t n_matches, int64_t fi
 int vs_rsync_read_tokens(const uint8_t *in, size_t n, int32_t blength, int64_t basis_len,
                          vs_match *matches, size_t cap, size_t *n_matches, uint8_t *literals,
                          size_t lit_cap, size_t *n_literal, int64_t *file_len);
+/* token.c send_zstd_token / recv_zstd_token: the token stream under rsync -z
+ * between two rsync 3.2.3 (UBI9) peers, which negotiate zstd (DESIGN.md
+ * 3.11).  A vs_ztok is one transfer's zstd state: rsync creates the
+ * compressor / decompressor once per transfer and every file continues the
+ * same stream, so write / read the files of a transfer through one handle,
+ * in order (a receiver uses its own handle).  level: rsync's
+ * --compress-level (3, ZSTD_CLEVEL_DEFAULT, when not given).
+ * write: the stream of one file from its match list (as match.c drives
+ * send_token, including hash_search's early literal flushes), into a buffer
+ * owned by the handle (*out, valid until the next call); last_block_len is
+ * sums[count - 1].len (the remainder, or blength).
+ * read: one file's stream from in (*consumed bytes), as write's inputs. */
+typedef struct vs_ztok vs_ztok;
+int vs_ztok_open(int level, vs_ztok **out);
+void vs_ztok_close(vs_ztok *z);
+int vs_rsync_write_tokens_zstd(vs_ztok *z, const vs_match *matches, int64_t n_matches,
+                               int64_t file_len, int32_t blength, int64_t basis_len,
+                               int32_t last_block_len, const uint8_t *src, const uint8_t **out,
+                               size_t *n_out);
+int vs_rsync_read_tokens_zstd(vs_ztok *z, const uint8_t *in, size_t n, int32_t blength,
+                              int64_t basis_len, vs_match *matches, size_t cap, size_t *n_matches,
+                              uint8_t *literals, size_t lit_cap, size_t *n_literal,
+                              int64_t *file_len, size_t *consumed);
 /* restic v0.13.1 internal/pack header plaintext: per blob its type (0 data,
  * 1 tree), the length of its encrypted form (4-byte LE) and its 32-byte ID,
  * 37 bytes per entry.  out == NULL: *n_out = the size only. */

@@ -145,3 +145,151 @@ def test_restic_pack_header_entries():
     bad = (ctypes.c_uint8 * 1)(2)
     with pytest.raises(VsError, match="blob type"):
         check(lib.vs_restic_pack_header(bad, lens, ids, 1, out, sz.value, ctypes.byref(sz)))
+
+
+# ---- rsync -z: the zstd token stream (token.c send_zstd_token / recv_zstd_token)
+class _ZIn(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("size", ctypes.c_size_t), ("pos", ctypes.c_size_t)]
+
+
+class _ZOut(ctypes.Structure):
+    _fields_ = [("dst", ctypes.c_void_p), ("size", ctypes.c_size_t), ("pos", ctypes.c_size_t)]
+
+
+class PyZstdReceiver:
+    """An independent restatement of recv_zstd_token's framing in Python (flag
+    bytes, relative runs, DEFLATED_DATA pieces), decompressing through
+    libzstd directly: test infrastructure for the library's writer."""
+
+    def __init__(self):
+        self.z = ctypes.CDLL("libzstd.so.1")
+        self.z.ZSTD_createDCtx.restype = ctypes.c_void_p
+        self.z.ZSTD_decompressStream.restype = ctypes.c_size_t
+        self.z.ZSTD_decompressStream.argtypes = [ctypes.c_void_p, ctypes.POINTER(_ZOut),
+                                                 ctypes.POINTER(_ZIn)]
+        self.z.ZSTD_isError.argtypes = [ctypes.c_size_t]
+        self.d = self.z.ZSTD_createDCtx()
+
+    def inflate(self, data: bytes) -> bytes:
+        src = ctypes.create_string_buffer(data, len(data))
+        zin = _ZIn(ctypes.addressof(src), len(data), 0)
+        out = b""
+        while True:
+            dst = ctypes.create_string_buffer(1 << 18)
+            zo = _ZOut(ctypes.addressof(dst), len(dst), 0)
+            r = self.z.ZSTD_decompressStream(self.d, ctypes.byref(zo), ctypes.byref(zin))
+            assert not self.z.ZSTD_isError(r)
+            out += dst.raw[: zo.pos]
+            if zin.pos == zin.size and zo.pos < zo.size:
+                return out
+
+    def file(self, s: bytes, blength: int, basis_len: int):
+        r, tok, pos, matches, lit = 0, 0, 0, [], b""
+
+        def token(t):
+            nonlocal pos
+            matches.append((pos, t))
+            pos += min(blength, basis_len - t * blength)
+
+        while True:
+            flag = s[r]
+            r += 1
+            if flag & 0xC0 == 0x40:
+                n = ((flag & 0x3F) << 8) + s[r]
+                data = self.inflate(s[r + 1:r + 1 + n])
+                r += 1 + n
+                lit += data
+                pos += len(data)
+                continue
+            if flag == 0:
+                return matches, lit, pos, r
+            if flag & 0x80:
+                tok += flag & 0x3F
+                flag >>= 6
+            else:
+                tok = struct.unpack_from("<i", s, r)[0]
+                r += 4
+            token(tok)
+            if flag & 1:
+                run = s[r] | (s[r + 1] << 8)
+                r += 2
+                for _ in range(run):
+                    tok += 1
+                    token(tok)
+
+
+def _fixture_file(path):
+    doc = G.load(path)
+    _, src = G.rsync_pair(doc["input"])
+    z = doc["sizes"]
+    last = z["remainder"] or z["blength"]
+    basis_len = (z["count"] - 1) * z["blength"] + last if z["count"] else 0
+    return [tuple(m) for m in doc["matches"]], src.tobytes(), z["blength"], basis_len, last
+
+
+def _gaps(matches, src, blength, basis_len):
+    out, last = b"", 0
+    for o, i in matches:
+        out += src[last:o]
+        last = o + min(blength, basis_len - i * blength)
+    return out + src[last:]
+
+
+def test_zstd_tokens_round_trip_every_fixture():
+    """Every rsync fixture's match list through the -z token stream: the
+    library's reader and an independent Python receiver both recover the
+    matches, the literal bytes and the file length."""
+    from volsync_amd import ZstdTokens
+    for path in FIX:
+        matches, src, bl, blen, last = _fixture_file(path)
+        tx, rx = ZstdTokens(), ZstdTokens()
+        s = tx.write(matches, src, bl, blen, last)
+        got = rx.read(s, bl, blen, len(matches) + 8, len(src) + 8)
+        assert got[0] == matches and got[1] == _gaps(matches, src, bl, blen), path
+        assert got[2] == len(src) and got[3] == len(s), path
+        py = PyZstdReceiver().file(s, bl, blen)
+        assert py == got, path
+
+
+def test_zstd_tokens_one_transfer_many_files():
+    """rsync keeps one zstd stream per transfer: the fixtures sent as the
+    files of ONE transfer decode in order on one receiver, and the second
+    file's stream does not decode on a fresh receiver (it continues the
+    first's zstd stream only when the first was read)."""
+    from volsync_amd import ZstdTokens
+    files = [_fixture_file(p) for p in FIX]
+    tx, rx = ZstdTokens(), ZstdTokens()
+    streams = [tx.write(m, src, bl, blen, last) for m, src, bl, blen, last in files]
+    for (m, src, bl, blen, last), s in zip(files, streams):
+        got = rx.read(s, bl, blen, len(m) + 8, len(src) + 8)
+        assert got[0] == m and got[1] == _gaps(m, src, bl, blen) and got[2] == len(src)
+
+
+def test_zstd_tokens_runs_and_long_tokens():
+    """Token runs (consecutive blocks: TOKENRUN_REL with a 16-bit count, split
+    at 65536), far jumps (TOKEN_LONG / TOKENRUN_LONG) and literal runs long
+    enough for hash_search's early flushes (> blength + 32 KiB)."""
+    from volsync_amd import ZstdTokens
+    bl, nblk = 64, 70000
+    basis_len = bl * nblk
+    rng = np.random.default_rng(9)
+    lit = rng.integers(0, 4, 200_000, dtype=np.uint8).tobytes()
+    # blocks 0..66999 in order (a run past 65536), then a jump back to 5,
+    # a 150 KB literal, blocks 69990..69999
+    matches, src, pos = [], b"", 0
+    for i in list(range(67000)) + [5]:
+        matches.append((pos, i))
+        pos += bl
+    src = bytes(pos) + lit[:150_000]
+    pos += 150_000
+    for i in range(69990, 70000):
+        matches.append((pos, i))
+        pos += bl
+    src += bytes(pos - len(src))
+    tx, rx = ZstdTokens(), ZstdTokens()
+    s = tx.write(matches, src, bl, basis_len, bl)
+    got = rx.read(s, bl, basis_len, len(matches) + 8, len(src))
+    assert got[0] == matches and got[2] == len(src)
+    assert got[1] == lit[:150_000]
+    assert PyZstdReceiver().file(s, bl, basis_len) == got
+    assert len(s) < len(src) // 4   # zero runs and 2-bit literals compress

@@ -10,6 +10,6 @@ from .chunker import (Chunk, Chunker, DeviceChunker, DeviceSha256, EOF, MaxSize,
                       NewWithBoundaries, Pol, TestPol, sha256_batch, synth_fill_device,
                       syncthing_block_size, Sealer)
 from .rsync import (CSUM_MD5, CSUM_XXH3_64, CSUM_XXH3_128, CSUM_XXH64, Matcher, file_sum_finish, file_sum_init,  # noqa: F401
-                    SumStruct, generate_sums, match_sums, sum_sizes_sqroot)
+                    SumStruct, ZstdTokens, generate_sums, match_sums, sum_sizes_sqroot)
 
 __version__ = "0.1.0"

@@ -114,6 +114,16 @@ def _load() -> ctypes.CDLL:
         "vs_rsync_read_tokens": (c_int, [vp, c_size, ctypes.c_int32, ctypes.c_int64,
                                          ctypes.POINTER(VsMatch), c_size, ctypes.POINTER(c_size), vp,
                                          c_size, ctypes.POINTER(c_size), i64p]),
+        "vs_ztok_open": (c_int, [c_int, ctypes.POINTER(vp)]),
+        "vs_ztok_close": (None, [vp]),
+        "vs_rsync_write_tokens_zstd": (c_int, [vp, ctypes.POINTER(VsMatch), ctypes.c_int64,
+                                               ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
+                                               ctypes.c_int32, vp, ctypes.POINTER(vp),
+                                               ctypes.POINTER(c_size)]),
+        "vs_rsync_read_tokens_zstd": (c_int, [vp, vp, c_size, ctypes.c_int32, ctypes.c_int64,
+                                              ctypes.POINTER(VsMatch), c_size, ctypes.POINTER(c_size),
+                                              vp, c_size, ctypes.POINTER(c_size),
+                                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(c_size)]),
         "vs_restic_pack_header": (c_int, [vp, vp, vp, c_size, vp, c_size, ctypes.POINTER(c_size)]),
         "vs_seal_open": (c_int, [c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                  ctypes.POINTER(vp)]),

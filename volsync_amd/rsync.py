@@ -232,6 +232,53 @@ class Matcher:
     _last_n = 0
 
 
+class ZstdTokens:
+    """One rsync -z transfer's token-stream state (token.c send_zstd_token /
+    recv_zstd_token, vs_ztok): write() the files of a transfer in order on the
+    sender's object, read() them in order on the receiver's."""
+
+    def __init__(self, level: int = 3):
+        self._z = ctypes.c_void_p()
+        check(lib.vs_ztok_open(level, ctypes.byref(self._z)))
+
+    def close(self) -> None:
+        if self._z:
+            lib.vs_ztok_close(self._z)
+            self._z = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def write(self, matches, src, blength: int, basis_len: int, last_block_len: int) -> bytes:
+        arr = (VsMatch * max(len(matches), 1))()
+        for k, (o, i) in enumerate(matches):
+            arr[k].offset, arr[k].block_index = o, i
+        b = _host_bytes(src)
+        out, n = ctypes.c_void_p(), ctypes.c_size_t()
+        check(lib.vs_rsync_write_tokens_zstd(self._z, arr, len(matches), len(b), blength, basis_len,
+                                             last_block_len, b.ctypes.data if len(b) else None,
+                                             ctypes.byref(out), ctypes.byref(n)))
+        return ctypes.string_at(out, n.value) if n.value else b""
+
+    def read(self, stream: bytes, blength: int, basis_len: int, max_matches: int,
+             max_literal: int):
+        """-> (matches, literal bytes, file length, bytes consumed)"""
+        buf = np.frombuffer(stream, np.uint8) if len(stream) else np.zeros(1, np.uint8)
+        arr = (VsMatch * max(max_matches, 1))()
+        lit = np.zeros(max(max_literal, 1), np.uint8)
+        nm, nl, used = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        flen = ctypes.c_int64()
+        check(lib.vs_rsync_read_tokens_zstd(self._z, buf.ctypes.data, len(stream), blength,
+                                            basis_len, arr, max_matches, ctypes.byref(nm),
+                                            lit.ctypes.data, len(lit), ctypes.byref(nl),
+                                            ctypes.byref(flen), ctypes.byref(used)))
+        return ([(arr[k].offset, arr[k].block_index) for k in range(nm.value)],
+                lit[: nl.value].tobytes(), flen.value, used.value)
+
+
 def file_sum_init() -> np.ndarray:
     """The XXH3 accumulators of an empty file (the relay's first acc_in)."""
     acc = np.zeros(8, np.uint64)
