@@ -376,6 +376,47 @@ int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *dev_off,
  * summed milliseconds (ms[0] CTR, ms[1] MAC) and the run count, then resets. */
 int vs_seal_set_timing(vs_seal *h, int on);
 int vs_seal_kernel_ms(vs_seal *h, double ms[2], int *runs);
+/* Key.Seal into the pack layout: blob i's record nonce || ciphertext || tag
+ * is written around dev_out + ct_off[i] (the nonce at ct_off - 16, the tag
+ * at ct_off + len) -- restic Packer.Add of repository.saveAndEncrypt's
+ * output. */
+int vs_seal_records_device(vs_seal *h, const void *dev_in, const uint64_t *dev_off,
+                           const uint32_t *dev_len, size_t n, const uint8_t *dev_nonces,
+                           uint8_t *dev_out, const uint64_t *dev_ct_off, void *hip_stream);
+/* restic internal/crypto Key.Open over a batch of stored blobs (restic
+ * Repository.LoadBlob on restore, mover-restic/entry.sh:224): record i at
+ * dev_in + rec_off[i] is nonce || ciphertext (len[i] bytes) || tag.  Every
+ * tag is verified (Poly1305 over the ciphertext, as Open does before it
+ * decrypts) and the ciphertext is decrypted to dev_out + out_off[i]
+ * (out_off NULL: in the same layout, i.e. at rec_off[i] + 16 of dev_out;
+ * dev_out == dev_in decrypts in place).  bad[i] (device) = 1 where the tag
+ * does not match: that plaintext must be discarded (Open returns
+ * ErrUnauthenticated); n_bad (host, optional: waits) counts them. */
+int vs_open_run_device(vs_seal *h, const void *dev_in, const uint64_t *dev_rec_off,
+                       const uint32_t *dev_len, size_t n, uint8_t *dev_out,
+                       const uint64_t *dev_out_off, uint32_t *dev_bad, uint64_t *n_bad,
+                       void *hip_stream);
+/* restic v0.13.1 pack files from sealed blobs (internal/pack Packer +
+ * internal/repository's packer managers): blobs (plaintext on the device at
+ * off[i], len[i] bytes; host arrays, in save order, with their types 0 data /
+ * 1 tree and 32-byte IDs) are appended to their type's open pack, finalised
+ * once it holds >= min_pack_size bytes (v0.13.1: 4 MiB); at the end the data
+ * pack, then the tree pack.  Each pack = the blob records, the header (per
+ * blob: type, record length, ID; sealed with hdr_nonces[p]) and the sealed
+ * header's length (4-byte LE).  dev_out receives the packs back to back;
+ * packs[p] = {offset, length, first blob in pack order, n blobs}; pack_ids =
+ * SHA-256 of each pack file (its name in the repository), by the vs_sha
+ * engine.  dev_out NULL: *n_packs, *out_len (and packs, if given) only.
+ * hdr_nonces needs one 16-byte row per pack (n rows always suffice). */
+typedef struct {
+    uint64_t offset, length;
+    uint32_t first_blob, n_blobs;
+} vs_pack;
+int vs_restic_pack(vs_seal *h, vs_sha *sha, const void *dev_in, const uint64_t *off,
+                   const uint32_t *len, const uint8_t *types, const uint8_t *ids, size_t n,
+                   const uint8_t *blob_nonces, const uint8_t *hdr_nonces, uint64_t min_pack_size,
+                   uint8_t *dev_out, uint64_t out_cap, vs_pack *packs, size_t pack_cap,
+                   size_t *n_packs, uint64_t *out_len, uint8_t *pack_ids, void *hip_stream);
 void vs_seal_close(vs_seal *h);
 
 /* ---- wire formats (host code, no device needed) -------

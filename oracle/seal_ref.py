@@ -149,3 +149,67 @@ def seal_into(enc_key: bytes, mac_k: bytes, mac_r: bytes, nonce: bytes, src_addr
     finally:
         c.EVP_CIPHER_CTX_free(ctx)
     return poly1305_evp((dst_addr, n), mac_r + aes128_block(mac_k, nonce))
+
+
+# ---- restic v0.13.1 pack files (internal/pack, internal/repository) ----------
+MIN_PACK_SIZE = 4 * 1024 * 1024   # repository packer_manager.go minPackSize
+
+
+def seal_fast(enc_key: bytes, mac_k: bytes, mac_r: bytes, nonce: bytes, plaintext: bytes):
+    """seal() with libcrypto's Poly1305 (equal to the restatement, checked in
+    tests/test_seal_oracle.py): for the large pack cases."""
+    ct = aes256_ctr(enc_key, nonce, plaintext)
+    return ct, poly1305_evp(ct, mac_r + aes128_block(mac_k, nonce))
+
+
+def pack_files(keys, blobs, hdr_nonces, min_pack_size: int = MIN_PACK_SIZE, fast: bool = False):
+    """Packer.Add / Finalize as repository.SaveBlob drives them with one
+    packer per blob type: blobs = [(type, plaintext, id32, nonce16)] in save
+    order.  A blob's record is nonce || Seal(plaintext) (ciphertext || tag);
+    a pack is finalised once its records reach min_pack_size bytes (and at
+    Flush: the data pack, then the tree pack); Finalize appends the header
+    (per blob: type byte, uint32 LE record length, ID) sealed with the pack's
+    nonce (nonce || ciphertext || tag) and the sealed header's length (uint32
+    LE).  The pack ID is the SHA-256 of the pack file.  Returns
+    [(pack bytes, pack id, [blob indices])] in the order packs are written."""
+    import hashlib
+    enc, mk, mr = keys
+    sl = seal_fast if fast else seal
+    out, cur, size = [], {0: [], 1: []}, {0: 0, 1: 0}
+    recs = {}
+
+    def close(t):
+        if not cur[t]:
+            return
+        body = b"".join(recs[i] for i in cur[t])
+        hdr = b""
+        for i in cur[t]:
+            typ, _, bid, _ = blobs[i]
+            hdr += bytes([typ]) + len(recs[i]).to_bytes(4, "little") + bid
+        hn = hdr_nonces[len(out)]
+        ct, tag = sl(enc, mk, mr, hn, hdr)
+        sealed = hn + ct + tag
+        pack = body + sealed + len(sealed).to_bytes(4, "little")
+        out.append((pack, hashlib.sha256(pack).digest(), list(cur[t])))
+        cur[t], size[t] = [], 0
+
+    for i, (typ, plain, _, nonce) in enumerate(blobs):
+        ct, tag = sl(enc, mk, mr, nonce, plain)
+        recs[i] = nonce + ct + tag
+        t = 1 if typ else 0
+        cur[t].append(i)
+        size[t] += len(recs[i])
+        if size[t] >= min_pack_size:
+            close(t)
+    close(0)
+    close(1)
+    return out
+
+
+def open_blob(keys, record: bytes):
+    """Key.Open of one stored blob: (plaintext, ok).  The tag is checked
+    before decryption; ok False means Open would return ErrUnauthenticated."""
+    enc, mk, mr = keys
+    nonce, ct, tag = record[:16], record[16:-16], record[-16:]
+    ok = poly1305(ct, mr + aes128_block(mk, nonce)) == tag
+    return aes256_ctr(enc, nonce, ct), ok

@@ -147,3 +147,128 @@ def test_seal_rejects_misaligned_nonces(gpu):
         s.run(d.data_ptr(), do.data_ptr(), dl.data_ptr(), 1, dn.data_ptr() + 4, d.data_ptr(),
               d.data_ptr() + 32)
     s.close()
+
+
+# ---- (f)1 pack stage: pack files, pack IDs; restore: Key.Open -----------------
+def _blobs(seed, sizes, tree_every=0):
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 256, int(sum(sizes)), dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    types = np.array([(1 if tree_every and i % tree_every == tree_every - 1 else 0)
+                      for i in range(len(sizes))], np.uint8)
+    ids = rng.integers(0, 256, (len(sizes), 32), dtype=np.uint8)
+    nonces = rng.integers(0, 256, (len(sizes), 16), dtype=np.uint8)
+    hnon = rng.integers(0, 256, (len(sizes), 16), dtype=np.uint8)
+    return data, offs, types, ids, nonces, hnon
+
+
+def _pack(keys, data, offs, sizes, types, ids, nonces, hnon, min_pack):
+    import torch
+    from volsync_amd import DeviceSha256, Sealer
+    d = torch.from_numpy(data.copy()).cuda()
+    s, sha = Sealer(*keys), DeviceSha256()
+    out, packs, pids = s.pack(sha, d.data_ptr(), offs, sizes, types, ids, nonces, hnon, min_pack)
+    torch.cuda.synchronize()
+    s.close()
+    sha.close()
+    return out.cpu().numpy(), packs, pids
+
+
+def test_restic_pack_files_vs_oracle(gpu):
+    """vs_restic_pack: pack bytes (records, sealed header, trailer) and pack IDs
+    equal the restatement of v0.13.1's Packer / packer managers, with data and
+    tree blobs interleaved, edge blob sizes and packs closed by size."""
+    keys = _keys(11)
+    sizes = [1, 15, 16, 17, 1000, 70_000, 33, 200_000, 5, 150_000, 64, 100_000, 3000, 90_000,
+             120_000, 7, 16 * 1024, 250_000, 1, 99_999]
+    data, offs, types, ids, nonces, hnon = _blobs(12, sizes, tree_every=4)
+    got, packs, pids = _pack(keys, data, offs, sizes, types, ids, nonces, hnon, 200 * 1024)
+    blobs = [(int(types[i]), data[int(offs[i]):int(offs[i]) + sizes[i]].tobytes(), ids[i].tobytes(),
+              nonces[i].tobytes()) for i in range(len(sizes))]
+    want = S.pack_files(keys, blobs, [hnon[k].tobytes() for k in range(len(sizes))], 200 * 1024)
+    assert len(packs) == len(want) > 3
+    order = []
+    for (o, ln, first, nb), pid, (wb, wid, wblobs) in zip(packs, pids, want):
+        assert got[o:o + ln].tobytes() == wb
+        assert pid == wid
+        order += wblobs
+        assert nb == len(wblobs)
+    assert packs[-1][0] + packs[-1][1] == sum(len(w[0]) for w in want)
+
+
+def test_restic_pack_c2_chunks(gpu):
+    """The pack stage on CDC output: a 256 MiB synthetic volume chunked and
+    hashed on the device (blob IDs), its chunks sealed into 4 MiB packs; every
+    pack and pack ID equals the oracle (libcrypto AES + Poly1305)."""
+    import torch
+    from tests import oracle_lib as O
+    from volsync_amd import DeviceChunker, TestPol
+    n = 256 << 20
+    vol = O.synth(21, 0, n)
+    t = torch.from_numpy(vol).cuda()
+    dc = DeviceChunker(TestPol)
+    nch, _ = dc.process(t.data_ptr(), n, 0, True)
+    ch = dc.chunks(0, nch)
+    dc.close()
+    sizes = [c.Length for c in ch]
+    offs = np.array([c.Start for c in ch], np.uint64)
+    ids = np.stack([np.frombuffer(c.ID, np.uint8) for c in ch])
+    rng = np.random.default_rng(5)
+    nonces = rng.integers(0, 256, (nch, 16), dtype=np.uint8)
+    hnon = rng.integers(0, 256, (nch, 16), dtype=np.uint8)
+    types = np.zeros(nch, np.uint8)
+    keys = _keys(13)
+    got, packs, pids = _pack(keys, vol, offs, sizes, types, ids, nonces, hnon, 4 << 20)
+    blobs = [(0, vol[int(offs[i]):int(offs[i]) + sizes[i]].tobytes(), ids[i].tobytes(),
+              nonces[i].tobytes()) for i in range(nch)]
+    want = S.pack_files(keys, blobs, [hnon[k].tobytes() for k in range(nch)], 4 << 20, fast=True)
+    assert [p[3] for p in packs] == [len(w[2]) for w in want]
+    for (o, ln, _, _), pid, (wb, wid, _) in zip(packs, pids, want):
+        assert pid == wid and got[o:o + ln].tobytes() == wb
+
+
+def test_open_verifies_and_decrypts(gpu):
+    """Key.Open on the device over stored records (a pack's blob records):
+    plaintext equals the original, and exactly the tampered records (one bit of
+    ciphertext, of the tag, of the nonce) are flagged -- as Open's
+    ErrUnauthenticated."""
+    import torch
+    from volsync_amd import Sealer
+    keys = _keys(14)
+    sizes = [1, 16, 17, 1000, 65_536, 333_333, 48, 12_345, 2, 70_000]
+    data, offs, types, ids, nonces, hnon = _blobs(15, sizes)
+    got, packs, _ = _pack(keys, data, offs, sizes, types, ids, nonces, hnon, 1 << 30)
+    assert len(packs) == 1
+    rec_off, o = [], 0
+    for ln in sizes:
+        rec_off.append(o)
+        o += ln + 32
+    stored = got.copy()
+    tamper = {2: rec_off[2] + 16 + 5, 5: rec_off[5] + 16 + sizes[5] + 3, 8: rec_off[8] + 7}
+    for b, pos in tamper.items():
+        stored[pos] ^= 0x10
+    for k, (b, pos) in enumerate(tamper.items()):
+        want_pt, ok = S.open_blob(keys, stored[rec_off[b]:rec_off[b] + sizes[b] + 32].tobytes())
+        assert not ok
+    d = torch.from_numpy(stored).cuda()
+    out = torch.zeros_like(d)
+    ro = torch.tensor(np.array(rec_off, np.uint64).view(np.int64), device="cuda")
+    ln = torch.tensor(np.array(sizes, np.uint32).view(np.int32), device="cuda")
+    bad = torch.zeros(len(sizes), dtype=torch.int32, device="cuda")
+    s = Sealer(*keys)
+    nbad = s.open(d.data_ptr(), ro.data_ptr(), ln.data_ptr(), len(sizes), out.data_ptr(), 0,
+                  bad.data_ptr())
+    # in place, as a restorer decrypting a downloaded pack buffer would
+    s.open(d.data_ptr(), ro.data_ptr(), ln.data_ptr(), len(sizes), d.data_ptr(), 0, bad.data_ptr())
+    torch.cuda.synchronize()
+    s.close()
+    assert nbad == len(tamper)
+    assert sorted(np.nonzero(bad.cpu().numpy())[0].tolist()) == sorted(tamper)
+    res, inplace = out.cpu().numpy(), d.cpu().numpy()
+    for b, ln_ in enumerate(sizes):
+        pt = res[rec_off[b] + 16:rec_off[b] + 16 + ln_].tobytes()
+        assert inplace[rec_off[b] + 16:rec_off[b] + 16 + ln_].tobytes() == pt
+        want_pt, ok = S.open_blob(keys, stored[rec_off[b]:rec_off[b] + ln_ + 32].tobytes())
+        assert pt == want_pt and ok == (b not in tamper)
+        if b not in tamper:
+            assert pt == data[int(offs[b]):int(offs[b]) + ln_].tobytes()

@@ -45,6 +45,10 @@ class VsMatch(ctypes.Structure):
                 ("reserved", ctypes.c_int32)]
 
 
+class VsPack(ctypes.Structure):
+    _fields_ = [("offset", c_u64), ("length", c_u64), ("first_blob", c_u32), ("n_blobs", c_u32)]
+
+
 class VsSigTable(ctypes.Structure):
     _fields_ = [("count", ctypes.c_int32), ("blength", ctypes.c_int32),
                 ("s2length", ctypes.c_int32), ("remainder", ctypes.c_int32),
@@ -131,6 +135,12 @@ def _load() -> ctypes.CDLL:
         "vs_seal_set_timing": (c_int, [vp, c_int]),
         "vs_seal_kernel_ms": (c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int)]),
         "vs_seal_close": (None, [vp]),
+        "vs_seal_records_device": (c_int, [vp, vp, vp, vp, c_size, vp, vp, vp, vp]),
+        "vs_open_run_device": (c_int, [vp, vp, vp, vp, c_size, vp, vp, vp, ctypes.POINTER(c_u64),
+                                       vp]),
+        "vs_restic_pack": (c_int, [vp, vp, vp, vp, vp, vp, vp, c_size, vp, vp, c_u64, vp, c_u64,
+                                   vp, c_size, ctypes.POINTER(c_size), ctypes.POINTER(c_u64), vp,
+                                   vp]),
         "vs_cdc_set_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_slice": (c_int, [vp, c_u32]),

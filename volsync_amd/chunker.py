@@ -383,6 +383,57 @@ class Sealer:
                                      ctypes.c_void_p(dev_out), ctypes.c_void_p(dev_macs),
                                      ctypes.c_void_p(stream or None)))
 
+    def run_records(self, dev_in: int, dev_off: int, dev_len: int, n: int, dev_nonces: int,
+                    dev_out: int, dev_ct_off: int, stream: Optional[int] = None) -> None:
+        """Key.Seal into the pack layout: nonce || ciphertext || tag around
+        dev_out + ct_off[i] (vs_seal_records_device)."""
+        check(lib.vs_seal_records_device(self._h, ctypes.c_void_p(dev_in), ctypes.c_void_p(dev_off),
+                                         ctypes.c_void_p(dev_len), n, ctypes.c_void_p(dev_nonces),
+                                         ctypes.c_void_p(dev_out), ctypes.c_void_p(dev_ct_off),
+                                         ctypes.c_void_p(stream or None)))
+
+    def open(self, dev_in: int, dev_rec_off: int, dev_len: int, n: int, dev_out: int,
+             dev_out_off: int, dev_bad: int, stream: Optional[int] = None) -> int:
+        """Key.Open over stored records (vs_open_run_device): verify each tag,
+        decrypt; returns the number of blobs whose tag did not match."""
+        nb = ctypes.c_uint64(0)
+        check(lib.vs_open_run_device(self._h, ctypes.c_void_p(dev_in), ctypes.c_void_p(dev_rec_off),
+                                     ctypes.c_void_p(dev_len), n, ctypes.c_void_p(dev_out),
+                                     ctypes.c_void_p(dev_out_off or None), ctypes.c_void_p(dev_bad),
+                                     ctypes.byref(nb), ctypes.c_void_p(stream or None)))
+        return nb.value
+
+    def pack(self, sha: "DeviceSha256", dev_in: int, offs, lens, types, ids, blob_nonces,
+             hdr_nonces, min_pack_size: int = 4 << 20, stream: Optional[int] = None):
+        """restic v0.13.1 pack files of the blobs (vs_restic_pack): returns
+        (device tensor of the packs back to back, [(offset, length, first, n)],
+        [pack id bytes]).  offs/lens/types: per blob; ids: n x 32 bytes;
+        blob_nonces: n x 16; hdr_nonces: >= n_packs x 16 (n rows suffice)."""
+        import numpy as np
+        import torch
+        from ._lib import VsPack
+        n = len(lens)
+        o = np.ascontiguousarray(offs, np.uint64)
+        ln = np.ascontiguousarray(lens, np.uint32)
+        ty = np.ascontiguousarray(types, np.uint8)
+        idb = np.ascontiguousarray(np.frombuffer(b"".join(ids), np.uint8) if isinstance(ids, list)
+                                   else ids, np.uint8)
+        bn = np.ascontiguousarray(blob_nonces, np.uint8)
+        hn = np.ascontiguousarray(hdr_nonces, np.uint8)
+        npk, olen = ctypes.c_size_t(), ctypes.c_uint64()
+        args = [self._h, sha._h, ctypes.c_void_p(dev_in), o.ctypes.data, ln.ctypes.data,
+                ty.ctypes.data, idb.ctypes.data, n, bn.ctypes.data, hn.ctypes.data, min_pack_size]
+        check(lib.vs_restic_pack(*args, None, 0, None, 0, ctypes.byref(npk), ctypes.byref(olen),
+                                 None, ctypes.c_void_p(stream or None)))
+        out = torch.zeros(max(olen.value, 16), dtype=torch.uint8, device="cuda")
+        packs = (VsPack * max(npk.value, 1))()
+        pid = np.zeros((max(npk.value, 1), 32), np.uint8)
+        check(lib.vs_restic_pack(*args, ctypes.c_void_p(out.data_ptr()), olen.value, packs,
+                                 npk.value, ctypes.byref(npk), ctypes.byref(olen), pid.ctypes.data,
+                                 ctypes.c_void_p(stream or None)))
+        return (out, [(p.offset, p.length, p.first_blob, p.n_blobs) for p in packs[:npk.value]],
+                [bytes(pid[k]) for k in range(npk.value)])
+
     def set_timing(self, on: bool) -> None:
         check(lib.vs_seal_set_timing(self._h, int(on)))
 

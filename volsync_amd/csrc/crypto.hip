@@ -357,9 +357,10 @@ __device__ __forceinline__ void aes256_tab(uint32_t (&s)[NB][4], uint32_t (&ix)[
 // per-lane search runs only for steps that straddle a blob boundary.
 // kCtrPer blocks per lane per step (ILP); two workgroups per CU (64 KiB of
 // tables each), WPE waves per SIMD
-template <int kCtrPer, int kThreads, int WPE, bool MAC = false>
+template <int kCtrPer, int kThreads, int WPE, bool MAC = false, bool OPEN = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 void seal_ctr_kernel(SealArgs a) {
+    static_assert(!OPEN || MAC, "Open verifies the MAC over its input in the same pass");
     static_assert(!MAC || kCtrPer == 1, "the fused MAC takes one block per lane per step");
     __shared__ uint32_t tab[kCtrWords];
     for (uint32_t i = threadIdx.x; i < kCtrWords; i += blockDim.x) {
@@ -393,13 +394,14 @@ void seal_ctr_kernel(SealArgs a) {
         while (a.prefix[blob + 1] <= g0) ++blob;
         const bool one = a.prefix[blob + 1] > glast;
         uint32_t s[kCtrPer][4];
-        uint64_t off[kCtrPer];
+        uint64_t off[kCtrPer], oof[kCtrPer];
         uint32_t nb[kCtrPer];
         uint64_t lb = blob, lq = 0;   // this lane's blob and block (MAC, kCtrPer == 1)
         if (one) {
             // the usual case: the whole step lies in one blob, so its
             // metadata is wave-uniform (scalar loads)
             const uint64_t pb = a.prefix[blob], ob = a.off[blob];
+            const uint64_t oo = a.out_off ? a.out_off[blob] : ob;
             const uint32_t len = a.len[blob];
             uint32_t nn[4];
             load_nonce(a.nonces, blob, nn);
@@ -408,6 +410,7 @@ void seal_ctr_kernel(SealArgs a) {
                 const uint64_t g = g0 + 64 * b + lane;
                 const uint64_t q = g - pb;
                 off[b] = ob + 16 * q;
+                oof[b] = oo + 16 * q;
                 nb[b] = g < a.total_blocks ? (uint32_t)min<uint64_t>(16, len - 16 * q) : 0;
                 ctr_block(nn, q, s[b]);
                 lq = q;
@@ -420,6 +423,7 @@ void seal_ctr_kernel(SealArgs a) {
                 const uint64_t bi = find_blob(a.prefix, a.n, gi);
                 const uint64_t q = gi - a.prefix[bi];
                 off[b] = a.off[bi] + 16 * q;
+                oof[b] = (a.out_off ? a.out_off[bi] : a.off[bi]) + 16 * q;
                 const uint32_t len = a.len[bi];
                 nb[b] = g < a.total_blocks ? (uint32_t)min<uint64_t>(16, len - 16 * q) : 0;
                 uint32_t nn[4];
@@ -439,20 +443,29 @@ void seal_ctr_kernel(SealArgs a) {
         for (int b = 0; b < (int)kCtrPer; ++b) {
             uint32_t ct[4] = {0, 0, 0, 0};   // the ciphertext block, zero-padded (MAC)
             if (nb[b] == 16) {
+                if constexpr (OPEN) {   // Open: the MAC covers the input (ciphertext)
+                    ct[0] = v[b].x;
+                    ct[1] = v[b].y;
+                    ct[2] = v[b].z;
+                    ct[3] = v[b].w;
+                }
                 v[b].x ^= s[b][0];
                 v[b].y ^= s[b][1];
                 v[b].z ^= s[b][2];
                 v[b].w ^= s[b][3];
-                __builtin_memcpy(a.out + off[b], &v[b], 16);
-                ct[0] = v[b].x;
-                ct[1] = v[b].y;
-                ct[2] = v[b].z;
-                ct[3] = v[b].w;
+                __builtin_memcpy(a.out + oof[b], &v[b], 16);
+                if constexpr (!OPEN) {
+                    ct[0] = v[b].x;
+                    ct[1] = v[b].y;
+                    ct[2] = v[b].z;
+                    ct[3] = v[b].w;
+                }
             } else {
                 for (uint32_t i = 0; i < nb[b]; ++i) {
-                    const uint8_t c = a.in[off[b] + i] ^ (uint8_t)(s[b][i >> 2] >> (8 * (i & 3)));
-                    a.out[off[b] + i] = c;
-                    ct[i >> 2] |= (uint32_t)c << (8 * (i & 3));
+                    const uint8_t x = a.in[off[b] + i];
+                    const uint8_t c = x ^ (uint8_t)(s[b][i >> 2] >> (8 * (i & 3)));
+                    a.out[oof[b] + i] = c;
+                    ct[i >> 2] |= (uint32_t)(OPEN ? x : c) << (8 * (i & 3));
                 }
             }
             if constexpr (MAC) {
@@ -492,8 +505,45 @@ __global__ __launch_bounds__(256) void seal_fin_kernel(SealArgs a) {
         uint32_t s[4];
         load_nonce(a.nonces, b, s);
         aes_encrypt(s, rk, 10, te, c);
-        poly_final(d, s, a.macs + 16 * b);
+        uint8_t tag[16];
+        poly_final(d, s, tag);
+        if (a.mode == kSealMacs) {
+            for (int i = 0; i < 16; ++i) a.macs[16 * b + i] = tag[i];
+        } else if (a.mode == kSealRecords) {
+            // the record around the ciphertext: nonce before it, tag after it
+            uint8_t *ct = a.out + a.out_off[b];
+            for (int i = 0; i < 16; ++i) ct[(uint64_t)a.len[b] + i] = tag[i];
+            for (int i = 0; i < 16; ++i) ct[i - 16] = a.nonces[16 * b + i];
+        } else {
+            uint32_t diff = 0;
+            for (int i = 0; i < 16; ++i) diff |= tag[i] ^ a.macs[16 * b + i];
+            a.bad[b] = diff != 0;
+            if (diff) atomicAdd(a.n_bad, 1ull);
+        }
     }
+}
+
+// Open's inputs gathered from stored records, one thread per blob
+__global__ __launch_bounds__(256) void open_gather_kernel(const uint8_t *in, const uint64_t *rec_off,
+                                                          const uint32_t *len, uint64_t n,
+                                                          uint8_t *nonces, uint8_t *macs,
+                                                          uint64_t *ct_off) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n) return;
+    const uint8_t *r = in + rec_off[b];
+    uint4 nn, mm;
+    __builtin_memcpy(&nn, r, 16);
+    __builtin_memcpy(&mm, r + 16 + len[b], 16);
+    *(uint4 *)(nonces + 16 * b) = nn;
+    *(uint4 *)(macs + 16 * b) = mm;
+    ct_off[b] = rec_off[b] + 16;
+}
+
+__global__ __launch_bounds__(256) void put_u32_kernel(uint8_t *out, const uint64_t *pos,
+                                                      const uint32_t *val, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    for (int k = 0; k < 4; ++k) out[pos[i] + k] = (uint8_t)(val[i] >> (8 * k));
 }
 
 __global__ __launch_bounds__(256) void seal_mac_kernel(SealArgs a) {
@@ -641,6 +691,11 @@ struct vs_seal {
     bool ran = false;
     bool timing = false;
     std::vector<hipEvent_t> ev;   // 3 per timed run: before CTR, between, after MAC
+    // Open / pack scratch
+    DevBuf o_nonce, o_mac, o_ctoff, o_cnt;
+    DevBuf p_off, p_len, p_ctoff, p_nonce, p_hdr, p_hoff, p_hlen, p_hct, p_hnonce, p_tpos, p_tval,
+        p_pack_off, p_pack_len, p_ids;
+    Stager stage;
 };
 
 VS_API int vs_seal_open(int device, const uint8_t enc_key[32], const uint8_t mac_k[16],
@@ -723,29 +778,16 @@ VS_API int vs_seal_open(int device, const uint8_t enc_key[32], const uint8_t mac
     return 0;
 }
 
-VS_API int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *dev_off,
-                              const uint32_t *dev_len, size_t n, const uint8_t *dev_nonces,
-                              uint8_t *dev_out, uint8_t *dev_macs, void *hip_stream) {
-    if (!h || (n && (!dev_in || !dev_off || !dev_len || !dev_nonces || !dev_out || !dev_macs)))
-        return fail(VS_ERR_ARG, "bad arguments");
-    if (!n) return 0;
-    if ((uintptr_t)dev_nonces & 15) return fail(VS_ERR_ARG, "nonces must be 16-byte aligned");
-    VS_TRY(enter_device(h->device));
-    const hipStream_t s = (hipStream_t)hip_stream;
-    // the previous run's CTR / MAC kernels read prefix and add into acc
+// one launch of the seal / open engine over n device blobs (a carries the
+// mode and the per-mode pointers); ordered after the handle's last run
+static int seal_run(vs_seal *h, SealArgs a, const uint32_t *dev_len, size_t n, hipStream_t s) {
     if (h->ran) VS_HIP(hipStreamWaitEvent(s, h->done, 0));
     VS_TRY(h->prefix.ensure((n + 1) * 8));
     VS_HIP(launch_seal_prefix(dev_len, n, h->prefix.as<uint64_t>(), h->pinned, s));
-    const uint64_t total = h->pinned[0];
-    SealArgs a{};
-    a.in = (const uint8_t *)dev_in;
-    a.out = dev_out;
-    a.off = dev_off;
     a.len = dev_len;
     a.n = n;
-    a.nonces = dev_nonces;
     a.prefix = h->prefix.as<uint64_t>();
-    a.total_blocks = total;
+    a.total_blocks = h->pinned[0];
     a.te0 = h->te0.as<uint32_t>();
     a.rk256 = h->rk256.as<uint32_t>();
     a.rk128 = h->rk128.as<uint32_t>();
@@ -753,7 +795,6 @@ VS_API int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *de
     a.rsq = a.rpow + 64 * 5;
     VS_TRY(h->acc.ensure(n * 5 * 8));
     a.acc = h->acc.as<unsigned long long>();
-    a.macs = dev_macs;
     hipEvent_t e[3] = {nullptr, nullptr, nullptr};
     if (h->timing) {
         for (auto &x : e) VS_HIP(hipEventCreate(&x));
@@ -762,6 +803,234 @@ VS_API int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *de
     VS_HIP(launch_seal(a, h->cus, s, e));
     VS_HIP(hipEventRecord(h->done, s));
     h->ran = true;
+    return 0;
+}
+
+VS_API int vs_seal_run_device(vs_seal *h, const void *dev_in, const uint64_t *dev_off,
+                              const uint32_t *dev_len, size_t n, const uint8_t *dev_nonces,
+                              uint8_t *dev_out, uint8_t *dev_macs, void *hip_stream) {
+    if (!h || (n && (!dev_in || !dev_off || !dev_len || !dev_nonces || !dev_out || !dev_macs)))
+        return fail(VS_ERR_ARG, "bad arguments");
+    if (!n) return 0;
+    if ((uintptr_t)dev_nonces & 15) return fail(VS_ERR_ARG, "nonces must be 16-byte aligned");
+    VS_TRY(enter_device(h->device));
+    SealArgs a{};
+    a.in = (const uint8_t *)dev_in;
+    a.out = dev_out;
+    a.off = dev_off;
+    a.nonces = dev_nonces;
+    a.macs = dev_macs;
+    a.mode = kSealMacs;
+    return seal_run(h, a, dev_len, n, (hipStream_t)hip_stream);
+}
+
+VS_API int vs_seal_records_device(vs_seal *h, const void *dev_in, const uint64_t *dev_off,
+                                  const uint32_t *dev_len, size_t n, const uint8_t *dev_nonces,
+                                  uint8_t *dev_out, const uint64_t *dev_ct_off, void *hip_stream) {
+    if (!h || (n && (!dev_in || !dev_off || !dev_len || !dev_nonces || !dev_out || !dev_ct_off)))
+        return fail(VS_ERR_ARG, "bad arguments");
+    if (!n) return 0;
+    if ((uintptr_t)dev_nonces & 15) return fail(VS_ERR_ARG, "nonces must be 16-byte aligned");
+    VS_TRY(enter_device(h->device));
+    SealArgs a{};
+    a.in = (const uint8_t *)dev_in;
+    a.out = dev_out;
+    a.off = dev_off;
+    a.out_off = dev_ct_off;
+    a.nonces = dev_nonces;
+    a.mode = kSealRecords;
+    return seal_run(h, a, dev_len, n, (hipStream_t)hip_stream);
+}
+
+VS_API int vs_open_run_device(vs_seal *h, const void *dev_in, const uint64_t *dev_rec_off,
+                              const uint32_t *dev_len, size_t n, uint8_t *dev_out,
+                              const uint64_t *dev_out_off, uint32_t *dev_bad, uint64_t *n_bad,
+                              void *hip_stream) {
+    if (n_bad) *n_bad = 0;
+    if (!h || (n && (!dev_in || !dev_rec_off || !dev_len || !dev_out || !dev_bad)))
+        return fail(VS_ERR_ARG, "bad arguments");
+    if (!n) return 0;
+    VS_TRY(enter_device(h->device));
+    const hipStream_t s = (hipStream_t)hip_stream;
+    if (h->ran) VS_HIP(hipStreamWaitEvent(s, h->done, 0));   // the scratch below
+    VS_TRY(h->o_nonce.ensure(n * 16));
+    VS_TRY(h->o_mac.ensure(n * 16));
+    VS_TRY(h->o_ctoff.ensure(n * 8));
+    VS_TRY(h->o_cnt.ensure(8));
+    VS_HIP(launch_open_gather((const uint8_t *)dev_in, dev_rec_off, dev_len, n,
+                              h->o_nonce.as<uint8_t>(), h->o_mac.as<uint8_t>(),
+                              h->o_ctoff.as<uint64_t>(), s));
+    VS_HIP(hipMemsetAsync(h->o_cnt.p, 0, 8, s));
+    SealArgs a{};
+    a.in = (const uint8_t *)dev_in;
+    a.out = dev_out;
+    a.off = h->o_ctoff.as<uint64_t>();
+    a.out_off = dev_out_off ? dev_out_off : a.off;
+    a.nonces = h->o_nonce.as<uint8_t>();
+    a.macs = h->o_mac.as<uint8_t>();
+    a.bad = dev_bad;
+    a.n_bad = h->o_cnt.as<unsigned long long>();
+    a.mode = kOpen;
+    VS_TRY(seal_run(h, a, dev_len, n, s));
+    if (n_bad) {
+        VS_HIP(hipMemcpyAsync(h->pinned + 1, h->o_cnt.p, 8, hipMemcpyDeviceToHost, s));
+        VS_HIP(hipStreamSynchronize(s));
+        *n_bad = h->pinned[1];
+    }
+    return 0;
+}
+
+// restic v0.13.1 internal/repository: one packer per blob type; a blob is
+// appended (Packer.Add) to its type's open pack, which is finalised once it
+// holds >= min_pack_size bytes; Flush finalises the data pack, then the tree
+// pack.  Finalize writes the header (per blob: type, record length, ID),
+// sealed with the pack's own nonce, and its length as a 4-byte LE trailer.
+struct PackPlan {
+    std::vector<vs_pack> packs;
+    std::vector<uint32_t> order;   // blob indices in pack order
+    std::vector<uint64_t> ct_off;  // [blob] where its ciphertext goes
+    uint64_t total = 0;
+};
+
+static void plan_packs(const uint32_t *len, const uint8_t *types, size_t n, uint64_t min_pack,
+                       PackPlan &pl) {
+    std::vector<uint32_t> cur[2];
+    uint64_t size[2] = {0, 0};
+    pl.ct_off.assign(n, 0);
+    auto close = [&](int t) {
+        if (cur[t].empty()) return;
+        vs_pack p{};
+        p.offset = pl.total;
+        p.first_blob = (uint32_t)pl.order.size();
+        p.n_blobs = (uint32_t)cur[t].size();
+        uint64_t o = pl.total;
+        for (const uint32_t i : cur[t]) {
+            pl.order.push_back(i);
+            pl.ct_off[i] = o + 16;
+            o += (uint64_t)len[i] + 32;
+        }
+        o += 37ull * cur[t].size() + 32 + 4;   // sealed header + its length
+        p.length = o - pl.total;
+        pl.total = o;
+        pl.packs.push_back(p);
+        cur[t].clear();
+        size[t] = 0;
+    };
+    for (size_t i = 0; i < n; ++i) {
+        const int t = types[i] ? 1 : 0;
+        cur[t].push_back((uint32_t)i);
+        size[t] += (uint64_t)len[i] + 32;
+        if (size[t] >= min_pack) close(t);
+    }
+    close(0);
+    close(1);
+}
+
+VS_API int vs_restic_pack(vs_seal *h, vs_sha *sha, const void *dev_in, const uint64_t *off,
+                          const uint32_t *len, const uint8_t *types, const uint8_t *ids, size_t n,
+                          const uint8_t *blob_nonces, const uint8_t *hdr_nonces,
+                          uint64_t min_pack_size, uint8_t *dev_out, uint64_t out_cap,
+                          vs_pack *packs, size_t pack_cap, size_t *n_packs, uint64_t *out_len,
+                          uint8_t *pack_ids, void *hip_stream) {
+    if (!h || !n_packs || !out_len || (n && (!off || !len || !types || !ids)))
+        return fail(VS_ERR_ARG, "bad arguments");
+    for (size_t i = 0; i < n; ++i)
+        if (types[i] > 1) return fail(VS_ERR_ARG, "blob type must be 0 (data) or 1 (tree)");
+    PackPlan pl;
+    plan_packs(len, types, n, std::max<uint64_t>(min_pack_size, 1), pl);
+    *n_packs = pl.packs.size();
+    *out_len = pl.total;
+    if (packs) memcpy(packs, pl.packs.data(), std::min(pack_cap, pl.packs.size()) * sizeof(vs_pack));
+    if (!dev_out) return 0;   // size query
+    if (!sha || !dev_in || !blob_nonces || !hdr_nonces || !pack_ids || !packs)
+        return fail(VS_ERR_ARG, "null pointer");
+    if (out_cap < pl.total) return fail(VS_ERR_ARG, "pack output buffer too small");
+    if (pack_cap < pl.packs.size()) return fail(VS_ERR_ARG, "pack descriptor array too small");
+    if (!n) return 0;
+    VS_TRY(enter_device(h->device));
+    const hipStream_t s = (hipStream_t)hip_stream;
+    if (h->ran) VS_HIP(hipStreamWaitEvent(s, h->done, 0));
+    const size_t np = pl.packs.size();
+    // 1. the blobs' records: nonce || AES-256-CTR ciphertext || Poly1305 tag
+    VS_TRY(h->p_off.ensure(n * 8));
+    VS_TRY(h->p_len.ensure(n * 4));
+    VS_TRY(h->p_ctoff.ensure(n * 8));
+    VS_TRY(h->p_nonce.ensure(n * 16));
+    VS_TRY(h->stage.h2d(h->p_off.p, off, n * 8, s));
+    VS_TRY(h->stage.h2d(h->p_len.p, len, n * 4, s));
+    VS_TRY(h->stage.h2d(h->p_ctoff.p, pl.ct_off.data(), n * 8, s));
+    VS_TRY(h->stage.h2d(h->p_nonce.p, blob_nonces, n * 16, s));
+    {
+        SealArgs a{};
+        a.in = (const uint8_t *)dev_in;
+        a.out = dev_out;
+        a.off = h->p_off.as<uint64_t>();
+        a.out_off = h->p_ctoff.as<uint64_t>();
+        a.nonces = h->p_nonce.as<uint8_t>();
+        a.mode = kSealRecords;
+        VS_TRY(seal_run(h, a, h->p_len.as<uint32_t>(), n, s));
+    }
+    // 2. the headers (pack.go makeHeader: type, Length = record length, ID),
+    // each sealed as one blob with its pack's nonce, after the records
+    std::vector<uint8_t> hdr;
+    std::vector<uint64_t> hoff(np), hct(np), tpos(np), poff(np), plen(np);
+    std::vector<uint32_t> hlen(np), tval(np);
+    for (size_t p = 0; p < np; ++p) {
+        const vs_pack &pk = pl.packs[p];
+        hoff[p] = hdr.size();
+        for (uint32_t k = 0; k < pk.n_blobs; ++k) {
+            const uint32_t i = pl.order[pk.first_blob + k];
+            const uint32_t rl = len[i] + 32;
+            hdr.push_back(types[i]);
+            for (int b = 0; b < 4; ++b) hdr.push_back((uint8_t)(rl >> (8 * b)));
+            hdr.insert(hdr.end(), ids + 32 * (size_t)i, ids + 32 * (size_t)i + 32);
+        }
+        hlen[p] = 37u * pk.n_blobs;
+        const uint64_t end = pk.offset + pk.length;
+        hct[p] = end - 4 - 16 - hlen[p];
+        tpos[p] = end - 4;
+        tval[p] = hlen[p] + 32;
+        poff[p] = pk.offset;
+        plen[p] = pk.length;
+    }
+    VS_TRY(h->p_hdr.ensure(hdr.size()));
+    VS_TRY(h->p_hoff.ensure(np * 8));
+    VS_TRY(h->p_hlen.ensure(np * 4));
+    VS_TRY(h->p_hct.ensure(np * 8));
+    VS_TRY(h->p_hnonce.ensure(np * 16));
+    VS_TRY(h->p_tpos.ensure(np * 8));
+    VS_TRY(h->p_tval.ensure(np * 4));
+    VS_TRY(h->p_pack_off.ensure(np * 8));
+    VS_TRY(h->p_pack_len.ensure(np * 4));
+    VS_TRY(h->p_ids.ensure(np * 32));
+    for (size_t p = 0; p < np; ++p)
+        if (plen[p] > 0xffffffffull) return fail(VS_ERR_ARG, "a pack over 4 GiB");
+    std::vector<uint32_t> plen32(plen.begin(), plen.end());
+    VS_TRY(h->stage.h2d(h->p_hdr.p, hdr.data(), hdr.size(), s));
+    VS_TRY(h->stage.h2d(h->p_hoff.p, hoff.data(), np * 8, s));
+    VS_TRY(h->stage.h2d(h->p_hlen.p, hlen.data(), np * 4, s));
+    VS_TRY(h->stage.h2d(h->p_hct.p, hct.data(), np * 8, s));
+    VS_TRY(h->stage.h2d(h->p_hnonce.p, hdr_nonces, np * 16, s));
+    VS_TRY(h->stage.h2d(h->p_tpos.p, tpos.data(), np * 8, s));
+    VS_TRY(h->stage.h2d(h->p_tval.p, tval.data(), np * 4, s));
+    VS_TRY(h->stage.h2d(h->p_pack_off.p, poff.data(), np * 8, s));
+    VS_TRY(h->stage.h2d(h->p_pack_len.p, plen32.data(), np * 4, s));
+    {
+        SealArgs a{};
+        a.in = h->p_hdr.as<uint8_t>();
+        a.out = dev_out;
+        a.off = h->p_hoff.as<uint64_t>();
+        a.out_off = h->p_hct.as<uint64_t>();
+        a.nonces = h->p_hnonce.as<uint8_t>();
+        a.mode = kSealRecords;
+        VS_TRY(seal_run(h, a, h->p_hlen.as<uint32_t>(), np, s));
+    }
+    VS_HIP(launch_put_u32(dev_out, h->p_tpos.as<uint64_t>(), h->p_tval.as<uint32_t>(), np, s));
+    // 3. pack IDs: SHA-256 of each whole pack file
+    VS_TRY(vs_sha256_run_device(sha, dev_out, h->p_pack_off.as<uint64_t>(),
+                                h->p_pack_len.as<uint32_t>(), np, h->p_ids.as<uint8_t>(), s));
+    VS_TRY(h->stage.d2h(pack_ids, h->p_ids.p, np * 32, s));
+    VS_HIP(hipEventRecord(h->done, s));
     return 0;
 }
 
@@ -793,7 +1062,12 @@ VS_API void vs_seal_close(vs_seal *h) {
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
     for (hipEvent_t x : h->ev) (void)hipEventDestroy(x);
-    for (DevBuf *b : {&h->te0, &h->rk256, &h->rk128, &h->rpow, &h->prefix, &h->acc}) b->release();
+    for (DevBuf *b : {&h->te0, &h->rk256, &h->rk128, &h->rpow, &h->prefix, &h->acc, &h->o_nonce,
+                      &h->o_mac, &h->o_ctoff, &h->o_cnt, &h->p_off, &h->p_len, &h->p_ctoff,
+                      &h->p_nonce, &h->p_hdr, &h->p_hoff, &h->p_hlen, &h->p_hct, &h->p_hnonce,
+                      &h->p_tpos, &h->p_tval, &h->p_pack_off, &h->p_pack_len, &h->p_ids})
+        b->release();
+    h->stage.release();
     pinned_free(h->pinned);
     if (h->done) (void)hipEventDestroy(h->done);
     delete h;
@@ -841,6 +1115,22 @@ __global__ __launch_bounds__(kScanThreads) void seal_prefix_kernel(const uint32_
 }
 }  // namespace
 
+hipError_t launch_open_gather(const uint8_t *in, const uint64_t *rec_off, const uint32_t *len,
+                              uint64_t n, uint8_t *nonces, uint8_t *macs, uint64_t *ct_off,
+                              hipStream_t s) {
+    if (!n) return hipSuccess;
+    open_gather_kernel<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(in, rec_off, len, n, nonces, macs,
+                                                                 ct_off);
+    return hipGetLastError();
+}
+
+hipError_t launch_put_u32(uint8_t *out, const uint64_t *pos, const uint32_t *val, uint64_t n,
+                          hipStream_t s) {
+    if (!n) return hipSuccess;
+    put_u32_kernel<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(out, pos, val, n);
+    return hipGetLastError();
+}
+
 // prefix[i] = blocks of blobs [0, i), prefix[n] = *total (read back: waits)
 hipError_t launch_seal_prefix(const uint32_t *len, uint64_t n, uint64_t *prefix, uint64_t *total,
                               hipStream_t s) {
@@ -857,7 +1147,7 @@ hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s, hipEvent_t *ev
     // 768-thread workgroups at 6 waves per SIMD; VSGPU_SEAL_FUSED=0 selects
     // the separate CTR + MAC kernels (A/B and tests)
     const char *fe = getenv("VSGPU_SEAL_FUSED");
-    const bool fused = !(fe && atoi(fe) == 0);
+    const bool fused = !(fe && atoi(fe) == 0) || a.mode != kSealMacs;
     if (fused) {
         hipError_t e = hipMemsetAsync(a.acc, 0, a.n * 5 * 8, s);
         if (e != hipSuccess) return e;
@@ -865,7 +1155,10 @@ hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s, hipEvent_t *ev
         if (a.total_blocks) {
             const uint64_t steps = (a.total_blocks + 63) / 64;
             const uint64_t grid = std::min<uint64_t>((steps + 11) / 12, (uint64_t)std::max(cus, 1) * 2);
-            seal_ctr_kernel<1, 768, 6, true><<<(uint32_t)grid, 768, 0, s>>>(a);
+            if (a.mode == kOpen)
+                seal_ctr_kernel<1, 768, 6, true, true><<<(uint32_t)grid, 768, 0, s>>>(a);
+            else
+                seal_ctr_kernel<1, 768, 6, true><<<(uint32_t)grid, 768, 0, s>>>(a);
         }
         if (ev[1]) (void)hipEventRecord(ev[1], s);
         const uint64_t fg = std::min<uint64_t>((a.n + 255) / 256, (uint64_t)std::max(cus, 1) * 4);

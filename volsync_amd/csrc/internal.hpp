@@ -456,12 +456,27 @@ struct SealArgs {
     const uint32_t *rpow;       // [64][5] r^1..r^64 in 26-bit limbs (MACKey.R clamped)
     const uint32_t *rsq;        // [kSealSq][5] r^(64 * 2^j) (the fused MAC's long lifts)
     unsigned long long *acc;    // [n][5] fused MAC: per-blob limb sums of the lifted partials
-    uint8_t *macs;              // [n][16]
+    uint8_t *macs;              // [n][16] (kOpen: the expected tags)
+    // where blob i's output bytes go (nullptr: off[i], i.e. in place /
+    // same layout); kSealRecords writes nonce || ciphertext || mac around it
+    const uint64_t *out_off;
+    int mode;                   // kSealMacs, kSealRecords, kOpen
+    uint32_t *bad;              // kOpen: [n] 1 where the stored tag does not match
+    unsigned long long *n_bad;  // kOpen: their count
 };
+enum { kSealMacs = 0, kSealRecords = 1, kOpen = 2 };
 constexpr int kSealSq = 24;     // r^(64 * 2^j), j < 24: lifts up to 2^30 blocks (16 GiB blobs)
 hipError_t launch_seal_prefix(const uint32_t *len, uint64_t n, uint64_t *prefix, uint64_t *total,
                               hipStream_t s);
 hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s, hipEvent_t *ev);
+// kOpen inputs from stored records (nonce || ciphertext || mac at rec_off):
+// nonces / tags gathered into 16-byte rows, ct_off = rec_off + 16
+hipError_t launch_open_gather(const uint8_t *in, const uint64_t *rec_off, const uint32_t *len,
+                              uint64_t n, uint8_t *nonces, uint8_t *macs, uint64_t *ct_off,
+                              hipStream_t s);
+// the 4-byte LE trailers of packs: out[pos[i]..+4) = val[i]
+hipError_t launch_put_u32(uint8_t *out, const uint64_t *pos, const uint32_t *val, uint64_t n,
+                          hipStream_t s);
 // adjacent-mover kernels (movers.hip)
 struct ReconPiece {
     uint64_t dst, src, len;
