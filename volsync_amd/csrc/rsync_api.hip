@@ -1305,6 +1305,7 @@ int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
         VS_HIP(hipEventRecord(j.kev[0], j.s));
         VS_HIP(launch_fs_contrib(p, j.nb, j.dC.as<uint64_t>(), j.s));
         VS_HIP(hipEventRecord(j.kev[1], j.s));
+        if (j.th.joinable()) j.th.join();   // (fs_finish joined it; never terminate())
         j.th = std::thread(fs_thread, &j, j.dC.as<const uint64_t>());
     }
     j.active = true;
@@ -1525,8 +1526,9 @@ VS_API int vs_rsync_file_sum_wait(vs_rsync *h, uint8_t out[16]) {
     if (!j.whole) return fail(VS_ERR_STATE, "the oldest checksum job is a block range");
     VS_TRY(rs_dev(h));
     h->fs_head++;
+    const int rc = fs_finish(j);   // joins the job's thread, syncs its stream
     j.active = false;
-    VS_TRY(fs_finish(j));
+    VS_TRY(rc);
     fs_account(h, j);
     memset(out, 0, 16);
     const int n = (j.csum == VS_CSUM_MD5 || j.csum == VS_CSUM_XXH3_128) ? 16 : 8;
@@ -1562,8 +1564,9 @@ VS_API int vs_rsync_file_sum_blocks_wait(vs_rsync *h, uint64_t acc_out[8]) {
     if (j.whole) return fail(VS_ERR_STATE, "the oldest checksum job is a whole file");
     VS_TRY(rs_dev(h));
     h->fs_head++;
+    const int rc = fs_finish(j);   // joins the job's thread, syncs its stream
     j.active = false;
-    VS_TRY(fs_finish(j));
+    VS_TRY(rc);
     fs_account(h, j);
     memcpy(acc_out, j.acc, 64);
     return 0;
