@@ -291,7 +291,7 @@ def rsync_main(args):
     # sum_init): device contributions + a host scramble chain on its own
     # handle.  The chain is one serial dependency per KiB of
     # the file, so file k's chain runs beside file k+1's step (two jobs in
-    # flight, each on its own host thread) and the timed region ends when the
+    # flight -- --file-sum-jobs, each on its own host thread) and the timed region ends when the
     # last one is done.  One GPU: the whole file S.  --share: the rank's whole
     # 1 KiB blocks of S from a stand-in relay state (the value rank R-1 would
     # hand over; the chain's cost does not depend on it).
@@ -310,7 +310,7 @@ def rsync_main(args):
     def fs_start():
         if not fs_on:
             return
-        if fs_inflight[0] == 2:
+        if fs_inflight[0] == args.file_sum_jobs:
             fs_wait()
         if fs_blocks is None:
             fsm.file_sum_start(ds.data_ptr(), plan.total, CSUM_XXH3_128)
@@ -390,7 +390,7 @@ def rsync_main(args):
         digests = {d for d, _ in fs_out}
         tm = fs_out[-1][1]
         fbytes = plan.total if fs_blocks is None else fs_blocks[1] * 1024
-        fsum = {"inside_step": True, "jobs_in_flight": 2,
+        fsum = {"inside_step": True, "jobs_in_flight": args.file_sum_jobs,
                 "ms_alone": round(fs_dt * 1e3, 2), "GBps_alone": round(fbytes / fs_dt / 1e9, 2),
                 "contrib_kernel_ms": round(tm["device_ms"], 2),
                 "host_chain_ms": round(tm["host_chain_ms"], 2),
@@ -964,6 +964,8 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=int, default=4)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--file-sum-jobs", type=int, default=3,
+                    help="rsync: whole-file checksums in flight (one host chain thread each)")
     ap.add_argument("--no-file-sum", action="store_true",
                     help="rsync: leave R7 (the whole-file checksum) out of the step (A/B)")
     ap.add_argument("--hash-stream", choices=["own", "main"], default="own",

@@ -1203,7 +1203,14 @@ void fs_thread(FsJob *j, const uint64_t *dC) {
 int fs_setup(FsJob &j, int device) {
     if (j.s) return 0;
     j.device = device;
-    VS_HIP(hipStreamCreateWithFlags(&j.s, hipStreamNonBlocking));
+    // the lowest priority: the contribution kernel fills what the walk and
+    // signature kernels leave free rather than taking CUs from them
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
+        (void)hipGetLastError();
+        least = 0;
+    }
+    VS_HIP(hipStreamCreateWithPriority(&j.s, hipStreamNonBlocking, least));
     VS_HIP(hipEventCreateWithFlags(&j.ev_in, hipEventDisableTiming));
     for (auto &e : j.ev) VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto &e : j.kev) VS_HIP(hipEventCreate(&e));
