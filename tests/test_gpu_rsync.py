@@ -495,7 +495,7 @@ def test_receiver_reconstruct(gpu, path):
     m.close()
 
 
-def test_c4_real_density_window_exact(gpu):
+def test_c4_real_density_window_exact(gpu, monkeypatch):
     """C4 at its real table density: the 2,097,152-block table of the 256 GiB
     destination (blength 131072, s2length 5, xxh128, checksum_seed
     0x5EED5EED) from the device signature pass -- D generated on the device
@@ -556,16 +556,19 @@ def test_c4_real_density_window_exact(gpu):
     torch.cuda.synchronize()
     assert (ds[:4096].cpu().numpy() == host[data_lo - win_lo:data_lo - win_lo + 4096]).all()
     m.load_sums_device(cnt, bl, s2l, rem, s1.data_ptr(), s2.data_ptr(), csum, seed)
-    m.match_scan(ds.data_ptr(), n, data_lo, plan.total, lo, hi)
-    gexit = m.match_stitch(e, w)
-    nm = m.match_finish()
-    got = m.matches(0, nm)
-    st = m.stats()
-    m.close()
     assert len(want) > 14000 and fa > 50000   # the density this test is for
-    assert got == want
-    assert st["false_alarms"] == fa
-    assert gexit == (wexit, wwant)
+    # the wave walk, then the cooperative walks
+    for coop in ("0", "12", "4"):
+        monkeypatch.setenv("VSGPU_WALK_COOP", coop)
+        m.match_scan(ds.data_ptr(), n, data_lo, plan.total, lo, hi)
+        gexit = m.match_stitch(e, w)
+        nm = m.match_finish()
+        got = m.matches(0, nm)
+        st = m.stats()
+        assert got == want, coop
+        assert st["false_alarms"] == fa, coop
+        assert gexit == (wexit, wwant), coop
+    m.close()
 
 
 def test_file_sum_async_overlaps_match(gpu):
@@ -674,3 +677,54 @@ def test_file_sum_jobs_fifo(gpu):
     with pytest.raises(VsError):
         m.file_sum_wait()
     m.close()
+
+
+@pytest.mark.parametrize("coop", ["12", "6", "4"])
+def test_coop_walk_exact(gpu, monkeypatch, coop):
+    """The cooperative speculative walk (VSGPU_WALK_COOP=W: W waves share one
+    segment's walk) against the C hash_search: every golden fixture, seeded
+    shifted / overwritten sources (false alarms, runs, short last blocks),
+    the C4 parameters on a 1 GiB basis, and the 4-way sharded walk."""
+    import torch
+    from volsync_amd import Matcher, SumStruct, match_sums
+    monkeypatch.setenv("VSGPU_WALK_COOP", coop)
+    for path in FIX:
+        doc, _, src = load_fixture(path)
+        p, z = doc["params"], doc["sizes"]
+        sm = SumStruct(flength=0, count=z["count"], blength=z["blength"], s2length=z["s2length"],
+                       remainder=z["remainder"], sum1=np.array(doc["sum1"], np.uint32),
+                       sum2=np.array([list(bytes.fromhex(h)) for h in doc["sum2"]],
+                                     np.uint8).reshape(z["count"], z["s2length"]))
+        assert match_sums(src, sm, p["csum_type"], p["seed"]) == [tuple(m) for m in doc["matches"]]
+    for csum_type, seed, n, frac, bs in [(R.CSUM_XXH3_128, 0x5EED5EED, 40 << 20, 0.10, 0),
+                                         (R.CSUM_XXH3_64, 7, 12 << 20, 0.30, 0),
+                                         (R.CSUM_XXH3_128, 1, 6 << 20, 0.20, 1000),
+                                         (R.CSUM_XXH3_128, 2, (5 << 20) + 777, 0.10, 0)]:
+        basis = O.synth(200 + n % 97, 0, n)
+        bl, s2l, cnt, rem = O.rsync_sizes(n, bs)
+        src = R.mutate(basis, bl, seed=n % 1000, frac=frac)
+        c1, c2 = O.rsync_signatures(basis, bl, s2l, csum_type, seed)
+        want, fa = O.rsync_match(src, c1, c2, bl, rem, csum_type, seed)
+        ds = to_dev(src)
+        m = Matcher()
+        m.load_sums(SumStruct(0, cnt, bl, s2l, rem, c1, c2), csum_type, seed)
+        got = m.match_sums(ds.data_ptr(), len(src))
+        st = m.stats()
+        m.close()
+        assert got == want and st["false_alarms"] == fa, (csum_type, n)
+    # C4 parameters, 1 GiB: the density of false alarms the coop flushes share
+    n, bl, s2l, csum, seed = 1 << 30, 131072, 5, R.CSUM_XXH3_128, 0x5EED5EED
+    basis = O.synth(4, 0, n)
+    src = R.mutate(basis, bl, seed=5, frac=0.10)
+    c1, c2 = O.rsync_signatures(basis, bl, s2l, csum, seed)
+    want, fa = O.rsync_match(src, c1, c2, bl, 0, csum, seed)
+    ds = to_dev(src)
+    m = Matcher()
+    m.load_sums(SumStruct(n, n // bl, bl, s2l, 0, c1, c2), csum, seed)
+    got = m.match_sums(ds.data_ptr(), len(src))
+    st = m.stats()
+    m.close()
+    assert got == want and st["false_alarms"] == fa
+    s = SumStruct(n, n // bl, bl, s2l, 0, c1, c2)
+    got4, fa4 = _sharded_device_match(src, s, 4, csum, seed)
+    assert got4 == want and fa4 == fa

@@ -727,6 +727,306 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
     return res;
 }
 
+// ---- the cooperative walk: W waves of a workgroup walk ONE segment -----------
+// ("cooperative walk").  At the real C4 table density a
+// wave-private walk spends most of its time hashing false-alarm windows: the
+// ~64 weak-sum collisions in the ~128 KiB literal stretch after each edit are
+// 128 KiB windows that overlap almost entirely, but each 4-window flush
+// re-streams them from the fabric because 384 walks per XCD evict each other's
+// windows from L2 between flushes.  Here the W waves of a workgroup share one
+// walk: a STEP group tests W consecutive 1024-offset batches at once (each
+// wave's start sums from the other waves' batch totals), and a flush hashes
+// up to 4 W queued windows together -- overlapping windows read by all the
+// waves of one CU at the same time, so the bytes come from the fabric about
+// once.  RUN flushes hash up to 4 W windows ahead, the depth doubling with
+// each fully matched flush (a miss costs the windows past it).  Every wave
+// runs the same control flow on the same shared results (LDS), so the
+// workgroup's barriers line up; wave 0 writes the outputs.  Results are
+// hash_search's, bit for bit, as for the wave walk.
+template <int W>
+struct CoopShared {
+    uint32_t dw[W], fw[W], nh[W];   // STEP: per-wave batch totals and hit counts
+    int64_t qoff[4 * W];            // queued hits (offset order)
+    uint32_t qsum[4 * W];
+    uint32_t wweak[4 * W];          // hashed windows
+    uint64_t wlo[4 * W], whi[4 * W];
+    uint32_t seg;                   // the segment being walked
+};
+
+template <int W>
+__device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, const uint32_t *lfilt,
+                                       uint32_t lbits, uint32_t lane, uint32_t wave, int64_t o,
+                                       int32_t want, int64_t stop, int64_t *out_off,
+                                       int32_t *out_idx, int64_t *out_fab, uint32_t cap,
+                                       const SpecView *spec, WProf &wp, CoopShared<W> &sh) {
+    constexpr uint32_t Q = 4 * W;   // windows per flush
+    const int64_t fend = min(stop, (int64_t)a.full_end);
+    const uint64_t L = a.blength;
+    const uint8_t *d = a.data;
+    const uint32_t row = lane >> 4;
+    SegResult res{0, 0xffffffffu, 0, 0, want};
+    uint64_t fa = 0;
+    uint32_t n = 0;
+    bool run = true;
+    uint32_t kahead = 1;      // RUN windows per flush: 1 at a segment start
+    uint32_t S1 = 0, S2 = 0;  // STEP: window sums at o (low 16 bits meaningful)
+    auto on_match = [&](int64_t h, int32_t i, uint64_t fa_visit) -> bool {
+        if (wave == 0 && lane == 0 && n < cap) {
+            out_off[n] = h;
+            out_idx[n] = i;
+            out_fab[n] = (int64_t)fa_visit;
+        }
+        ++n;
+        want = i + 1;
+        if (spec) {
+            uint32_t lo = 0, hi = spec->n;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if ((int64_t)uni64((uint64_t)spec->off[mid]) < h) lo = mid + 1;
+                else hi = mid;
+            }
+            const bool hitm = lo < spec->n &&
+                              uni((uint32_t)(spec->off[lo] == h && spec->idx[lo] == i)) != 0;
+            if (hitm) {
+                res.from = lo + 1;
+                fa = fa_visit + spec->fa - uni64((uint64_t)spec->fab[lo]);
+                o = spec->exit_off;
+                want = spec->exit_want;
+                return true;
+            }
+        }
+        const uint32_t li = ((uint32_t)i == a.count - 1 && a.remainder) ? a.remainder : a.blength;
+        o = h + li;
+        return false;
+    };
+    bool merged = false;
+    while (!merged && o < fend) {
+        if (run) {
+            // windows o + j L (j < k) below fend: window j on wave j / 4, row j % 4
+            const int64_t room = (fend - o + (int64_t)L - 1) / (int64_t)L;
+            const uint32_t k = (uint32_t)min<int64_t>(kahead, room);
+            uint64_t t0 = wclock(wp);
+            if (4 * wave < k) {
+                const uint32_t j = 4 * wave + row;
+                const int64_t orow = o + (int64_t)L * (int64_t)(j < k ? j : 4 * wave);
+                const RowWin w = rows_window<true>(a, rs, lane, (uint64_t)orow, L);
+                if ((lane & 15) == 0 && j < k) {
+                    sh.wweak[j] = w.weak;
+                    sh.wlo[j] = w.lo;
+                    sh.whi[j] = w.hi;
+                }
+            }
+            __syncthreads();
+            wadd(wp, kPrRun, t0);
+            bool all = true;
+            for (uint32_t j = 0; j < k; ++j) {
+                const int64_t oj = o;
+                const uint32_t wk = uni(sh.wweak[j]);
+                const uint64_t lo = uni64(sh.wlo[j]), hi = uni64(sh.whi[j]);
+                const uint64_t fa_visit = fa;
+                t0 = wclock(wp);
+                const int32_t i = unis(chain_match(a, wk, lo, hi, want, (uint32_t)L, fa));
+                wadd(wp, kPrChain, t0);
+                if (i >= 0) {
+                    merged = on_match(oj, i, fa_visit);
+                    if (merged || o != oj + (int64_t)L) {   // merged, or a short last block
+                        all = false;
+                        break;
+                    }
+                    continue;
+                }
+                const int32_t xo = sbyte(d, (uint64_t)oj);
+                const int32_t xi = (oj + 1 < fend) ? sbyte(d, (uint64_t)oj + L) : 0;
+                S1 = uni((wk & 0xffffu) - (uint32_t)xo + (uint32_t)xi);
+                S2 = uni((wk >> 16) - (uint32_t)L * (uint32_t)xo + S1);
+                o = oj + 1;
+                run = false;
+                all = false;
+                break;
+            }
+            __syncthreads();   // the window slots are read by every wave before reuse
+            kahead = all ? min(2 * k, Q) : 4u;
+            continue;
+        }
+        // ---- STEP: groups of W batches [A + 1024 w, +1024); offsets below `from` are done
+        uint64_t A = (uint64_t)o & ~15ull;
+        uint32_t T1 = S1, T2 = S2;
+        for (uint64_t u = (uint64_t)o; u > A; --u) {
+            const uint64_t v = u - 1;
+            const int32_t xo = sbyte(d, v), xi = sbyte(d, v + L);
+            T2 = T2 - T1 + (uint32_t)L * (uint32_t)xo;
+            T1 = T1 - (uint32_t)(xi - xo);
+        }
+        T1 = uni(T1);
+        T2 = uni(T2);
+        int64_t from = o;
+        bool matched = false;
+        for (;;) {
+            uint64_t tb = wclock(wp);
+            const uint64_t Aw = A + kBatch * wave;
+            const uint64_t c = Aw + 16 * (uint64_t)lane;
+            uint4 cwo, cwi;
+            batch_load(a, Aw, lane, cwo, cwi);
+            const uint32_t wo[4] = {cwo.x, cwo.y, cwo.z, cwo.w};
+            const uint32_t wi[4] = {cwi.x, cwi.y, cwi.z, cwi.w};
+            int Xo = 0, Xi = 0, Eo = 0, Ei = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                Xo = dot4(wo[k], 0x01010101u, Xo);
+                Xi = dot4(wi[k], 0x01010101u, Xi);
+                const uint32_t wt = (uint32_t)((16 - 4 * k) | ((15 - 4 * k) << 8) |
+                                               ((14 - 4 * k) << 16) | ((13 - 4 * k) << 24));
+                Eo = dot4(wo[k], wt, Eo);
+                Ei = dot4(wi[k], wt, Ei);
+            }
+            // zero-start sums of this wave's batch: s1 = T1w + P0, s2 = T2w + 16 lane T1w + Y0
+            const uint32_t D = (uint32_t)(Xi - Xo), E = (uint32_t)(Ei - Eo), X = (uint32_t)Xo;
+            const uint32_t P0 = excl_scan(D, lane);
+            const uint32_t Dl = E + 16u * P0 - (uint32_t)L * X;
+            const uint32_t Y0 = excl_scan(Dl, lane);
+            if (lane == 63) {
+                sh.dw[wave] = P0 + D;     // s1 over the batch (relative)
+                sh.fw[wave] = Y0 + Dl;    // s2 at the batch end, zero start
+            }
+            __syncthreads();
+            // this wave's start sums, and the group's end sums, from the totals
+            uint32_t t1 = T1, t2 = T2, e1 = T1, e2 = T2;
+#pragma unroll
+            for (uint32_t w2 = 0; w2 < (uint32_t)W; ++w2) {
+                const uint32_t dwv = uni(sh.dw[w2]), fwv = uni(sh.fw[w2]);
+                if (w2 < wave) {
+                    t2 = t2 + 1024u * t1 + fwv;
+                    t1 = t1 + dwv;
+                }
+                e2 = e2 + 1024u * e1 + fwv;
+                e1 = e1 + dwv;
+            }
+            uint32_t s1 = t1 + P0;
+            uint32_t s2 = t2 + 16u * lane * t1 + Y0;
+            uint32_t sums[16];
+            uint32_t valid = 0;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                sums[t] = __builtin_amdgcn_perm(s2, s1, 0x05040100u);
+                const int32_t xo = __builtin_amdgcn_sbfe((int)wo[t >> 2], 8 * (t & 3), 8);
+                const int32_t xi = __builtin_amdgcn_sbfe((int)wi[t >> 2], 8 * (t & 3), 8);
+                s1 += (uint32_t)(xi - xo);
+                s2 = s2 - (uint32_t)L * (uint32_t)xo + s1;
+                const int64_t qo = (int64_t)c + t;
+                valid |= (uint32_t)(qo >= from && qo < fend) << t;
+            }
+            uint32_t hit = valid;
+            if (lbits) {
+                uint32_t lw[16];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) lw[t] = lfilt[(sums[t] >> (32 - lbits)) >> 5];
+                uint32_t lh = 0;
+#pragma unroll
+                for (int t = 0; t < 16; ++t)
+                    lh |= ((lw[t] >> ((sums[t] >> (32 - lbits)) & 31)) & 1u) << t;
+                hit &= lh;
+            }
+            {
+                uint64_t fw[16];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const bool on = (hit >> t) & 1u;
+                    fw[t] = a.filt_b[on ? rs_bloom_word(sums[t], a.fbits) : 0u];
+                }
+                uint32_t pass = 0;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const uint64_t m = rs_bloom_mask(sums[t]);
+                    pass |= (uint32_t)((fw[t] & m) == m) << t;
+                }
+                hit &= pass;
+            }
+            for (uint32_t mm = hit; mm;) {
+                const int t = __builtin_ctz(mm);
+                mm &= mm - 1;
+                uint32_t st = sums[0];
+#pragma unroll
+                for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
+                if (!probe_full(a, st)) hit &= ~(1u << t);
+            }
+            // the group's hits in offset order: wave, lane, bit
+            const uint32_t pc = (uint32_t)__builtin_popcount(hit);
+            const uint32_t lp = excl_scan(pc, lane);
+            if (lane == 63) sh.nh[wave] = lp + pc;
+            __syncthreads();
+            uint32_t base = 0, H = 0;
+#pragma unroll
+            for (uint32_t w2 = 0; w2 < (uint32_t)W; ++w2) {
+                const uint32_t v = uni(sh.nh[w2]);
+                if (w2 < wave) base += v;
+                H += v;
+            }
+            wadd(wp, kPrStep, tb);
+            for (uint32_t r0 = 0; r0 < H && !matched && !merged; r0 += Q) {
+                // queue hits [r0, r0 + Q)
+                uint32_t g = base + lp;
+                for (uint32_t mm = hit; mm; mm &= mm - 1, ++g) {
+                    const int t = __builtin_ctz(mm);
+                    if (g >= r0 && g < r0 + Q) {
+                        uint32_t st = sums[0];
+#pragma unroll
+                        for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
+                        sh.qoff[g - r0] = (int64_t)c + t;
+                        sh.qsum[g - r0] = st;
+                    }
+                }
+                __syncthreads();
+                const uint32_t nq = min(Q, H - r0);
+                uint64_t tf = wclock(wp);
+                if (4 * wave < nq) {
+                    const uint32_t j = 4 * wave + row;
+                    const int64_t orow = sh.qoff[j < nq ? j : 4 * wave];
+                    const RowWin w = rows_window<false>(a, rs, lane, (uint64_t)orow, L);
+                    if ((lane & 15) == 0 && j < nq) {
+                        sh.wlo[j] = w.lo;
+                        sh.whi[j] = w.hi;
+                    }
+                }
+                __syncthreads();
+                wadd(wp, kPrFlush, tf);
+                for (uint32_t j = 0; j < nq; ++j) {
+                    const int64_t h = (int64_t)uni64((uint64_t)sh.qoff[j]);
+                    const uint32_t sv = uni(sh.qsum[j]);
+                    const uint64_t lo = uni64(sh.wlo[j]), hi = uni64(sh.whi[j]);
+                    const uint64_t fa_visit = fa;
+                    tf = wclock(wp);
+                    const int32_t i = unis(chain_match(a, sv, lo, hi, want, (uint32_t)L, fa));
+                    wadd(wp, kPrChain, tf);
+                    if (i >= 0) {
+                        merged = on_match(h, i, fa_visit);
+                        matched = true;
+                        break;
+                    }
+                }
+                __syncthreads();   // queue / window slots are reused
+            }
+            if (matched) break;
+            if ((int64_t)(A + kBatch * W) >= fend) {
+                o = fend;
+                break;
+            }
+            T1 = e1;
+            T2 = e2;
+            A += kBatch * W;
+            from = (int64_t)A;
+        }
+        if (matched) {
+            run = true;
+            kahead = 4;
+        }
+    }
+    res.n = n;
+    res.fa = fa;
+    res.exit_off = o;
+    res.exit_want = want;
+    return res;
+}
+
 __device__ __forceinline__ void load_prefilter(const RsWalkArgs &a, uint32_t *lfilt) {
     const uint32_t lw = a.lbits ? (1u << a.lbits) / 32 : 0;
     for (uint32_t i = threadIdx.x; i < lw; i += blockDim.x) lfilt[i] = a.filt_l[i];
@@ -794,6 +1094,64 @@ __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
         }
     }
     WPROG(a, lane, 12, 0, 0);
+}
+
+// the speculative pass with W-wave cooperative walks (walk_segment_coop):
+// W == 12 keeps the LDS prefilter (one workgroup per CU); smaller W runs
+// 12 / W workgroups per CU without it
+template <int W>
+__global__ __launch_bounds__(64 * W) void rs_walk_spec_coop_kernel(RsWalkArgs a) {
+    constexpr bool kLds = W >= 12;
+    __shared__ uint32_t lfilt[kLds ? kLdsFiltWordsW : 1];
+    __shared__ uint64_t lsec[24];
+    __shared__ CoopShared<W> sh;
+    load_secret(lsec, a.seed);
+    const uint32_t lbits = kLds ? a.lbits : 0u;
+    if (kLds) {
+        load_prefilter(a, lfilt);
+    } else {
+        __syncthreads();
+    }
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = uni(threadIdx.x >> 6);
+    const RowSec rs{lsec};
+    WProf wp{a.prof != nullptr, {}, {}};
+    for (;;) {
+        if (threadIdx.x == 0) sh.seg = atomicAdd(a.work, 1u);
+        __syncthreads();
+        const uint32_t k = uni(sh.seg);
+        __syncthreads();   // every wave has read the segment before it is overwritten
+        if (k >= a.nseg) break;
+        const uint64_t ts = wclock(wp);
+        const int64_t e = (int64_t)uni64((uint64_t)(k ? seg_lo(a, k) : a.e0));
+        const int32_t w = unis(k ? (int32_t)a.count : a.w0);
+        const uint64_t base = (uint64_t)k * a.cap;
+        const SegResult r = walk_segment_coop<W>(a, rs, lfilt, lbits, lane, wave, e, w, seg_hi(a, k),
+                                                 a.spec_off + base, a.spec_idx + base,
+                                                 a.spec_fab + base, a.cap, nullptr, wp, sh);
+        wadd(wp, kPrSeg, ts);
+        if (wave == 0 && lane == 0) {
+            a.spec_n[k] = r.n;
+            a.spec_fa[k] = r.fa;
+            a.spec_exit[k] = r.exit_off;
+            a.spec_exitw[k] = r.exit_want;
+            a.fin_entry[k] = e;
+            a.fin_entryw[k] = w;
+            a.fin_from[k] = 0xffffffffu;
+            a.fin_n[k] = 0;
+            a.fin_fa[k] = r.fa;
+            a.exit_new[k] = r.exit_off;
+            a.exitw_new[k] = r.exit_want;
+            if (r.n > a.cap) atomicOr(a.flags, 2u);
+        }
+    }
+    if (wp.on && lane == 0) {
+        uint64_t *pr = a.prof + (uint64_t)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 16;
+        for (int i = 0; i < kPrN; ++i) {
+            pr[i] = wp.cyc[i];
+            pr[8 + i] = wp.cnt[i];
+        }
+    }
 }
 
 // one stitch pass: a segment whose entry (the previous segment's exit from
@@ -871,6 +1229,24 @@ hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t
         const char *e = getenv("VSGPU_WALK_WG");
         return (e && atoi(e) == 1024) ? 1024u : kWalkThreads;
     }();
+    // VSGPU_WALK_COOP=W (4, 6 or 12; 0 = off): the speculative pass with
+    // W-wave cooperative walks (walk_segment_coop)
+    // (read at every launch: tests switch it within one process)
+    const int coop = [] {
+        const char *e = getenv("VSGPU_WALK_COOP");
+        const int v = e ? atoi(e) : 0;
+        return (v == 4 || v == 6 || v == 12) ? v : 0;
+    }();
+    if (!stitch && coop) {
+        hipError_t e = hipMemsetAsync(a.work, 0, 4, s);
+        if (e != hipSuccess) return e;
+        const uint64_t per_cu = 12 / coop;
+        const uint64_t grid = std::min<uint64_t>(a.nseg, (uint64_t)std::max(cus, 1) * per_cu);
+        if (coop == 12) rs_walk_spec_coop_kernel<12><<<(uint32_t)grid, 768, 0, s>>>(a);
+        else if (coop == 6) rs_walk_spec_coop_kernel<6><<<(uint32_t)grid, 384, 0, s>>>(a);
+        else rs_walk_spec_coop_kernel<4><<<(uint32_t)grid, 256, 0, s>>>(a);
+        return hipGetLastError();
+    }
     const uint32_t threads = stitch ? kWalkThreads : spec_threads;
     const uint32_t waves = threads / 64;
     const uint64_t grid = std::min<uint64_t>((a.nseg + waves - 1) / waves, (uint64_t)std::max(cus, 1));
