@@ -848,7 +848,10 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
             kahead = all ? min(2 * k, Q) : 4u;
             continue;
         }
-        // ---- STEP: groups of W batches [A + 1024 w, +1024); offsets below `from` are done
+        // ---- STEP: groups of W batches [A + 1024 w, +1024); offsets below
+        // `from` are done.  Hits are queued across groups until 4 W are
+        // waiting (or the region ends), so one flush hashes the overlapping
+        // false-alarm windows of an edit together.
         uint64_t A = (uint64_t)o & ~15ull;
         uint32_t T1 = S1, T2 = S2;
         for (uint64_t u = (uint64_t)o; u > A; --u) {
@@ -860,160 +863,196 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
         T1 = uni(T1);
         T2 = uni(T2);
         int64_t from = o;
-        bool matched = false;
+        bool matched = false, at_end = false;
+        uint32_t nq = 0;                 // hits queued in sh.qoff / sh.qsum
+        bool partial = false;            // the queue filled inside group (pA, pT1, pT2)
+        uint64_t pA = 0;
+        uint32_t pT1 = 0, pT2 = 0;
         for (;;) {
-            uint64_t tb = wclock(wp);
-            const uint64_t Aw = A + kBatch * wave;
-            const uint64_t c = Aw + 16 * (uint64_t)lane;
-            uint4 cwo, cwi;
-            batch_load(a, Aw, lane, cwo, cwi);
-            const uint32_t wo[4] = {cwo.x, cwo.y, cwo.z, cwo.w};
-            const uint32_t wi[4] = {cwi.x, cwi.y, cwi.z, cwi.w};
-            int Xo = 0, Xi = 0, Eo = 0, Ei = 0;
+            // ---- fill the queue
+            while (nq < Q && !at_end) {
+                uint64_t tb = wclock(wp);
+                const uint64_t Aw = A + kBatch * wave;
+                const uint64_t c = Aw + 16 * (uint64_t)lane;
+                uint4 cwo, cwi;
+                batch_load(a, Aw, lane, cwo, cwi);
+                const uint32_t wo[4] = {cwo.x, cwo.y, cwo.z, cwo.w};
+                const uint32_t wi[4] = {cwi.x, cwi.y, cwi.z, cwi.w};
+                int Xo = 0, Xi = 0, Eo = 0, Ei = 0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                Xo = dot4(wo[k], 0x01010101u, Xo);
-                Xi = dot4(wi[k], 0x01010101u, Xi);
-                const uint32_t wt = (uint32_t)((16 - 4 * k) | ((15 - 4 * k) << 8) |
-                                               ((14 - 4 * k) << 16) | ((13 - 4 * k) << 24));
-                Eo = dot4(wo[k], wt, Eo);
-                Ei = dot4(wi[k], wt, Ei);
-            }
-            // zero-start sums of this wave's batch: s1 = T1w + P0, s2 = T2w + 16 lane T1w + Y0
-            const uint32_t D = (uint32_t)(Xi - Xo), E = (uint32_t)(Ei - Eo), X = (uint32_t)Xo;
-            const uint32_t P0 = excl_scan(D, lane);
-            const uint32_t Dl = E + 16u * P0 - (uint32_t)L * X;
-            const uint32_t Y0 = excl_scan(Dl, lane);
-            if (lane == 63) {
-                sh.dw[wave] = P0 + D;     // s1 over the batch (relative)
-                sh.fw[wave] = Y0 + Dl;    // s2 at the batch end, zero start
-            }
-            __syncthreads();
-            // this wave's start sums, and the group's end sums, from the totals
-            uint32_t t1 = T1, t2 = T2, e1 = T1, e2 = T2;
-#pragma unroll
-            for (uint32_t w2 = 0; w2 < (uint32_t)W; ++w2) {
-                const uint32_t dwv = uni(sh.dw[w2]), fwv = uni(sh.fw[w2]);
-                if (w2 < wave) {
-                    t2 = t2 + 1024u * t1 + fwv;
-                    t1 = t1 + dwv;
+                for (int k = 0; k < 4; ++k) {
+                    Xo = dot4(wo[k], 0x01010101u, Xo);
+                    Xi = dot4(wi[k], 0x01010101u, Xi);
+                    const uint32_t wt = (uint32_t)((16 - 4 * k) | ((15 - 4 * k) << 8) |
+                                                   ((14 - 4 * k) << 16) | ((13 - 4 * k) << 24));
+                    Eo = dot4(wo[k], wt, Eo);
+                    Ei = dot4(wi[k], wt, Ei);
                 }
-                e2 = e2 + 1024u * e1 + fwv;
-                e1 = e1 + dwv;
-            }
-            uint32_t s1 = t1 + P0;
-            uint32_t s2 = t2 + 16u * lane * t1 + Y0;
-            uint32_t sums[16];
-            uint32_t valid = 0;
+                // zero-start sums of this wave's batch: s1 = T1w + P0, s2 = T2w + 16 lane T1w + Y0
+                const uint32_t D = (uint32_t)(Xi - Xo), E = (uint32_t)(Ei - Eo), X = (uint32_t)Xo;
+                const uint32_t P0 = excl_scan(D, lane);
+                const uint32_t Dl = E + 16u * P0 - (uint32_t)L * X;
+                const uint32_t Y0 = excl_scan(Dl, lane);
+                if (lane == 63) {
+                    sh.dw[wave] = P0 + D;
+                    sh.fw[wave] = Y0 + Dl;
+                }
+                __syncthreads();
+                uint32_t t1 = T1, t2 = T2, e1 = T1, e2 = T2;
 #pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                sums[t] = __builtin_amdgcn_perm(s2, s1, 0x05040100u);
-                const int32_t xo = __builtin_amdgcn_sbfe((int)wo[t >> 2], 8 * (t & 3), 8);
-                const int32_t xi = __builtin_amdgcn_sbfe((int)wi[t >> 2], 8 * (t & 3), 8);
-                s1 += (uint32_t)(xi - xo);
-                s2 = s2 - (uint32_t)L * (uint32_t)xo + s1;
-                const int64_t qo = (int64_t)c + t;
-                valid |= (uint32_t)(qo >= from && qo < fend) << t;
-            }
-            uint32_t hit = valid;
-            if (lbits) {
-                uint32_t lw[16];
-#pragma unroll
-                for (int t = 0; t < 16; ++t) lw[t] = lfilt[(sums[t] >> (32 - lbits)) >> 5];
-                uint32_t lh = 0;
-#pragma unroll
-                for (int t = 0; t < 16; ++t)
-                    lh |= ((lw[t] >> ((sums[t] >> (32 - lbits)) & 31)) & 1u) << t;
-                hit &= lh;
-            }
-            {
-                uint64_t fw[16];
+                for (uint32_t w2 = 0; w2 < (uint32_t)W; ++w2) {
+                    const uint32_t dwv = uni(sh.dw[w2]), fwv = uni(sh.fw[w2]);
+                    if (w2 < wave) {
+                        t2 = t2 + 1024u * t1 + fwv;
+                        t1 = t1 + dwv;
+                    }
+                    e2 = e2 + 1024u * e1 + fwv;
+                    e1 = e1 + dwv;
+                }
+                uint32_t s1 = t1 + P0;
+                uint32_t s2 = t2 + 16u * lane * t1 + Y0;
+                uint32_t sums[16];
+                uint32_t valid = 0;
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
-                    const bool on = (hit >> t) & 1u;
-                    fw[t] = a.filt_b[on ? rs_bloom_word(sums[t], a.fbits) : 0u];
+                    sums[t] = __builtin_amdgcn_perm(s2, s1, 0x05040100u);
+                    const int32_t xo = __builtin_amdgcn_sbfe((int)wo[t >> 2], 8 * (t & 3), 8);
+                    const int32_t xi = __builtin_amdgcn_sbfe((int)wi[t >> 2], 8 * (t & 3), 8);
+                    s1 += (uint32_t)(xi - xo);
+                    s2 = s2 - (uint32_t)L * (uint32_t)xo + s1;
+                    const int64_t qo = (int64_t)c + t;
+                    valid |= (uint32_t)(qo >= from && qo < fend) << t;
                 }
-                uint32_t pass = 0;
+                uint32_t hit = valid;
+                if (lbits) {
+                    uint32_t lw[16];
 #pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    const uint64_t m = rs_bloom_mask(sums[t]);
-                    pass |= (uint32_t)((fw[t] & m) == m) << t;
+                    for (int t = 0; t < 16; ++t) lw[t] = lfilt[(sums[t] >> (32 - lbits)) >> 5];
+                    uint32_t lh = 0;
+#pragma unroll
+                    for (int t = 0; t < 16; ++t)
+                        lh |= ((lw[t] >> ((sums[t] >> (32 - lbits)) & 31)) & 1u) << t;
+                    hit &= lh;
                 }
-                hit &= pass;
-            }
-            for (uint32_t mm = hit; mm;) {
-                const int t = __builtin_ctz(mm);
-                mm &= mm - 1;
-                uint32_t st = sums[0];
+                {
+                    uint64_t fw[16];
 #pragma unroll
-                for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
-                if (!probe_full(a, st)) hit &= ~(1u << t);
-            }
-            // the group's hits in offset order: wave, lane, bit
-            const uint32_t pc = (uint32_t)__builtin_popcount(hit);
-            const uint32_t lp = excl_scan(pc, lane);
-            if (lane == 63) sh.nh[wave] = lp + pc;
-            __syncthreads();
-            uint32_t base = 0, H = 0;
+                    for (int t = 0; t < 16; ++t) {
+                        const bool on = (hit >> t) & 1u;
+                        fw[t] = a.filt_b[on ? rs_bloom_word(sums[t], a.fbits) : 0u];
+                    }
+                    uint32_t pass = 0;
 #pragma unroll
-            for (uint32_t w2 = 0; w2 < (uint32_t)W; ++w2) {
-                const uint32_t v = uni(sh.nh[w2]);
-                if (w2 < wave) base += v;
-                H += v;
-            }
-            wadd(wp, kPrStep, tb);
-            for (uint32_t r0 = 0; r0 < H && !matched && !merged; r0 += Q) {
-                // queue hits [r0, r0 + Q)
-                uint32_t g = base + lp;
-                for (uint32_t mm = hit; mm; mm &= mm - 1, ++g) {
+                    for (int t = 0; t < 16; ++t) {
+                        const uint64_t m = rs_bloom_mask(sums[t]);
+                        pass |= (uint32_t)((fw[t] & m) == m) << t;
+                    }
+                    hit &= pass;
+                }
+                for (uint32_t mm = hit; mm;) {
                     const int t = __builtin_ctz(mm);
-                    if (g >= r0 && g < r0 + Q) {
-                        uint32_t st = sums[0];
+                    mm &= mm - 1;
+                    uint32_t st = sums[0];
 #pragma unroll
-                        for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
-                        sh.qoff[g - r0] = (int64_t)c + t;
-                        sh.qsum[g - r0] = st;
-                    }
+                    for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
+                    if (!probe_full(a, st)) hit &= ~(1u << t);
                 }
+                // the group's hits in offset order (wave, lane, bit), queued at nq + rank
+                const uint32_t pc = (uint32_t)__builtin_popcount(hit);
+                const uint32_t lp = excl_scan(pc, lane);
+                if (lane == 63) sh.nh[wave] = lp + pc;
                 __syncthreads();
-                const uint32_t nq = min(Q, H - r0);
-                uint64_t tf = wclock(wp);
-                if (4 * wave < nq) {
-                    const uint32_t j = 4 * wave + row;
-                    const int64_t orow = sh.qoff[j < nq ? j : 4 * wave];
-                    const RowWin w = rows_window<false>(a, rs, lane, (uint64_t)orow, L);
-                    if ((lane & 15) == 0 && j < nq) {
-                        sh.wlo[j] = w.lo;
-                        sh.whi[j] = w.hi;
+                uint32_t base = 0, H = 0;
+#pragma unroll
+                for (uint32_t w2 = 0; w2 < (uint32_t)W; ++w2) {
+                    const uint32_t v = uni(sh.nh[w2]);
+                    if (w2 < wave) base += v;
+                    H += v;
+                }
+                {
+                    uint32_t g = nq + base + lp;
+                    for (uint32_t mm = hit; mm; mm &= mm - 1, ++g) {
+                        const int t = __builtin_ctz(mm);
+                        if (g < Q) {
+                            uint32_t st = sums[0];
+#pragma unroll
+                            for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
+                            sh.qoff[g] = (int64_t)c + t;
+                            sh.qsum[g] = st;
+                        }
                     }
                 }
-                __syncthreads();
-                wadd(wp, kPrFlush, tf);
-                for (uint32_t j = 0; j < nq; ++j) {
-                    const int64_t h = (int64_t)uni64((uint64_t)sh.qoff[j]);
-                    const uint32_t sv = uni(sh.qsum[j]);
-                    const uint64_t lo = uni64(sh.wlo[j]), hi = uni64(sh.whi[j]);
-                    const uint64_t fa_visit = fa;
-                    tf = wclock(wp);
-                    const int32_t i = unis(chain_match(a, sv, lo, hi, want, (uint32_t)L, fa));
-                    wadd(wp, kPrChain, tf);
-                    if (i >= 0) {
-                        merged = on_match(h, i, fa_visit);
-                        matched = true;
-                        break;
+                wadd(wp, kPrStep, tb);
+                if (nq + H > Q) {
+                    // the queue filled inside this group: flush, then redo the
+                    // group past the last visited hit
+                    partial = true;
+                    pA = A;
+                    pT1 = T1;
+                    pT2 = T2;
+                    nq = Q;
+                } else {
+                    nq += H;
+                    if ((int64_t)(A + kBatch * W) >= fend) {
+                        at_end = true;
+                    } else {
+                        T1 = e1;
+                        T2 = e2;
+                        A += kBatch * W;
+                        from = (int64_t)A;
                     }
                 }
-                __syncthreads();   // queue / window slots are reused
+                __syncthreads();   // sh.dw / fw / nh and the queue slots
             }
-            if (matched) break;
-            if ((int64_t)(A + kBatch * W) >= fend) {
+            if (nq == 0) {   // the region ended without a hit
                 o = fend;
                 break;
             }
-            T1 = e1;
-            T2 = e2;
-            A += kBatch * W;
-            from = (int64_t)A;
+            // ---- flush: hash the queued windows together, visit them in order
+            uint64_t tf = wclock(wp);
+            if (4 * wave < nq) {
+                const uint32_t j = 4 * wave + row;
+                const int64_t orow = sh.qoff[j < nq ? j : 4 * wave];
+                const RowWin w = rows_window<false>(a, rs, lane, (uint64_t)orow, L);
+                if ((lane & 15) == 0 && j < nq) {
+                    sh.wlo[j] = w.lo;
+                    sh.whi[j] = w.hi;
+                }
+            }
+            __syncthreads();
+            wadd(wp, kPrFlush, tf);
+            int64_t hlast = 0;
+            for (uint32_t j = 0; j < nq; ++j) {
+                const int64_t h = (int64_t)uni64((uint64_t)sh.qoff[j]);
+                const uint32_t sv = uni(sh.qsum[j]);
+                const uint64_t lo = uni64(sh.wlo[j]), hi = uni64(sh.whi[j]);
+                const uint64_t fa_visit = fa;
+                tf = wclock(wp);
+                const int32_t i = unis(chain_match(a, sv, lo, hi, want, (uint32_t)L, fa));
+                wadd(wp, kPrChain, tf);
+                hlast = h;
+                if (i >= 0) {
+                    merged = on_match(h, i, fa_visit);
+                    matched = true;
+                    break;
+                }
+            }
+            __syncthreads();   // queue / window slots are reused
+            if (matched) break;
+            nq = 0;
+            if (partial) {
+                partial = false;
+                A = pA;
+                T1 = pT1;
+                T2 = pT2;
+                from = hlast + 1;
+                at_end = false;
+                continue;
+            }
+            if (at_end) {
+                o = fend;
+                break;
+            }
         }
         if (matched) {
             run = true;
