@@ -391,6 +391,38 @@ __device__ int32_t chain_match(const RsWalkArgs &a, uint32_t sum, uint64_t lo, u
     return -1;
 }
 
+// chain_match without the want_i preference: the first block in chain order
+// whose strong sum matches (or -1), false alarms counted before it -- which
+// do not depend on want_i, so queued windows can be scanned in parallel and
+// the preference applied when the walk visits them (chain_prefer).  Uniform.
+__device__ int32_t chain_scan(const RsWalkArgs &a, uint32_t sum, uint64_t lo, uint64_t hi,
+                              uint32_t klen, uint32_t &fa) {
+    const uint32_t b = sum >> (32 - a.dbits);
+    const uint32_t p0 = uni(a.dir[b]), p1 = uni(a.dir[b + 1]);
+    for (uint32_t p = p0; p < p1; ++p) {
+        const uint64_t key = uni64(a.tkey[p]);
+        const uint32_t s1 = (uint32_t)(key >> 32);
+        if (s1 < sum) continue;
+        if (s1 > sum) break;
+        const int32_t i = (int32_t)~(uint32_t)key;
+        const uint32_t li = ((uint32_t)i == a.count - 1 && a.remainder) ? a.remainder : a.blength;
+        if (li != klen) continue;
+        if (!uni((uint32_t)strong_eq(a, (uint32_t)i, lo, hi))) {
+            ++fa;
+            continue;
+        }
+        return i;
+    }
+    return -1;
+}
+__device__ __forceinline__ int32_t chain_prefer(const RsWalkArgs &a, int32_t i, uint32_t sum,
+                                                uint64_t lo, uint64_t hi, int32_t want) {
+    if (i >= 0 && i != want && want >= 0 && (uint32_t)want < a.count && uni(a.sum1[want]) == sum &&
+        uni((uint32_t)strong_eq(a, (uint32_t)want, lo, hi)))
+        return want;
+    return i;
+}
+
 // does a full-length block with sum1 == sum exist?  (the directory; the
 // filters were tested by the caller; uniform per lane, divergent across lanes)
 __device__ __forceinline__ bool probe_full(const RsWalkArgs &a, uint32_t sum) {
@@ -750,6 +782,8 @@ struct CoopShared {
     uint32_t qsum[4 * W];
     uint32_t wweak[4 * W];          // hashed windows
     uint64_t wlo[4 * W], whi[4 * W];
+    int32_t ci[4 * W];              // their chain scans (chain_scan): block or -1
+    uint32_t cfa[4 * W];            //   and false alarms before it
     uint32_t seg;                   // the segment being walked
 };
 
@@ -810,10 +844,19 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
                 const uint32_t j = 4 * wave + row;
                 const int64_t orow = o + (int64_t)L * (int64_t)(j < k ? j : 4 * wave);
                 const RowWin w = rows_window<true>(a, rs, lane, (uint64_t)orow, L);
-                if ((lane & 15) == 0 && j < k) {
-                    sh.wweak[j] = w.weak;
-                    sh.wlo[j] = w.lo;
-                    sh.whi[j] = w.hi;
+                // this wave's windows' chain scans, beside the other waves'
+                for (uint32_t r = 0; r < 4 && 4 * wave + r < k; ++r) {
+                    const uint32_t wk = (uint32_t)__builtin_amdgcn_readlane((int)w.weak, (int)(16 * r));
+                    const uint64_t lo = rdl64(w.lo, (int)(16 * r)), hi = rdl64(w.hi, (int)(16 * r));
+                    uint32_t cf = 0;
+                    const int32_t ci = unis(chain_scan(a, wk, lo, hi, (uint32_t)L, cf));
+                    if (lane == 0) {
+                        sh.wweak[4 * wave + r] = wk;
+                        sh.wlo[4 * wave + r] = lo;
+                        sh.whi[4 * wave + r] = hi;
+                        sh.ci[4 * wave + r] = ci;
+                        sh.cfa[4 * wave + r] = cf;
+                    }
                 }
             }
             __syncthreads();
@@ -825,7 +868,8 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
                 const uint64_t lo = uni64(sh.wlo[j]), hi = uni64(sh.whi[j]);
                 const uint64_t fa_visit = fa;
                 t0 = wclock(wp);
-                const int32_t i = unis(chain_match(a, wk, lo, hi, want, (uint32_t)L, fa));
+                fa += uni(sh.cfa[j]);
+                const int32_t i = unis(chain_prefer(a, unis(sh.ci[j]), wk, lo, hi, want));
                 wadd(wp, kPrChain, t0);
                 if (i >= 0) {
                     merged = on_match(oj, i, fa_visit);
@@ -869,8 +913,12 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
         uint64_t pA = 0;
         uint32_t pT1 = 0, pT2 = 0;
         for (;;) {
-            // ---- fill the queue
-            while (nq < Q && !at_end) {
+            // ---- fill the queue (until 4 W hits wait, or the scan has run a
+            // block length past the first of them: a match, which ends the
+            // STEP, is due within a block of an edit, so scanning further
+            // mostly wastes work where false alarms are sparse)
+            while (nq < Q && !at_end &&
+                   !(nq && (int64_t)A >= uni64((uint64_t)sh.qoff[0]) + (int64_t)L)) {
                 uint64_t tb = wclock(wp);
                 const uint64_t Aw = A + kBatch * wave;
                 const uint64_t c = Aw + 16 * (uint64_t)lane;
@@ -1014,9 +1062,17 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
                 const uint32_t j = 4 * wave + row;
                 const int64_t orow = sh.qoff[j < nq ? j : 4 * wave];
                 const RowWin w = rows_window<false>(a, rs, lane, (uint64_t)orow, L);
-                if ((lane & 15) == 0 && j < nq) {
-                    sh.wlo[j] = w.lo;
-                    sh.whi[j] = w.hi;
+                for (uint32_t r = 0; r < 4 && 4 * wave + r < nq; ++r) {
+                    const uint32_t sv = uni(sh.qsum[4 * wave + r]);
+                    const uint64_t lo = rdl64(w.lo, (int)(16 * r)), hi = rdl64(w.hi, (int)(16 * r));
+                    uint32_t cf = 0;
+                    const int32_t ci = unis(chain_scan(a, sv, lo, hi, (uint32_t)L, cf));
+                    if (lane == 0) {
+                        sh.wlo[4 * wave + r] = lo;
+                        sh.whi[4 * wave + r] = hi;
+                        sh.ci[4 * wave + r] = ci;
+                        sh.cfa[4 * wave + r] = cf;
+                    }
                 }
             }
             __syncthreads();
@@ -1028,7 +1084,8 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
                 const uint64_t lo = uni64(sh.wlo[j]), hi = uni64(sh.whi[j]);
                 const uint64_t fa_visit = fa;
                 tf = wclock(wp);
-                const int32_t i = unis(chain_match(a, sv, lo, hi, want, (uint32_t)L, fa));
+                fa += uni(sh.cfa[j]);
+                const int32_t i = unis(chain_prefer(a, unis(sh.ci[j]), sv, lo, hi, want));
                 wadd(wp, kPrChain, tf);
                 hlast = h;
                 if (i >= 0) {
