@@ -1320,10 +1320,13 @@ hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t
     if (!a.nseg) return hipSuccess;
     if (a.lbits > 20) return hipErrorInvalidValue;
     // VSGPU_WALK_WG=1024: the speculative pass at 16 waves per CU (128
-    // VGPRs, some spilled) instead of 12 (160 VGPRs) -- an A/B knob
+    // VGPRs, some spilled) instead of 12 (160 VGPRs); 512 / 256: 8 / 4 waves
+    // per CU (fewer walks in flight, a smaller re-fetched working set) --
+    // A/B knobs
     static const uint32_t spec_threads = [] {
         const char *e = getenv("VSGPU_WALK_WG");
-        return (e && atoi(e) == 1024) ? 1024u : kWalkThreads;
+        const int v = e ? atoi(e) : 0;
+        return (v == 1024 || v == 512 || v == 256) ? (uint32_t)v : kWalkThreads;
     }();
     // VSGPU_WALK_COOP=W (4, 6 or 12; 0 = off): the speculative pass with
     // W-wave cooperative walks (walk_segment_coop)
@@ -1352,6 +1355,10 @@ hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t
         rs_walk_stitch_kernel<<<(uint32_t)grid, kWalkThreads, 0, s>>>(a);
     else if (threads == 1024)
         rs_walk_spec_kernel<1024><<<(uint32_t)grid, 1024, 0, s>>>(a);
+    else if (threads == 512)
+        rs_walk_spec_kernel<512><<<(uint32_t)grid, 512, 0, s>>>(a);
+    else if (threads == 256)
+        rs_walk_spec_kernel<256><<<(uint32_t)grid, 256, 0, s>>>(a);
     else
         rs_walk_spec_kernel<kWalkThreads><<<(uint32_t)grid, kWalkThreads, 0, s>>>(a);
     return hipGetLastError();
