@@ -679,15 +679,18 @@ def test_file_sum_jobs_fifo(gpu):
     m.close()
 
 
-@pytest.mark.parametrize("coop", ["12", "6", "4"])
+@pytest.mark.parametrize("coop", ["12", "6", "4", "12:8", "4:8"])
 def test_coop_walk_exact(gpu, monkeypatch, coop):
     """The cooperative speculative walk (VSGPU_WALK_COOP=W: W waves share one
-    segment's walk) against the C hash_search: every golden fixture, seeded
+    segment's walk; W:k also re-syncs flush rows every k blocks,
+    VSGPU_WALK_LOCK) against the C hash_search: every golden fixture, seeded
     shifted / overwritten sources (false alarms, runs, short last blocks),
     the C4 parameters on a 1 GiB basis, and the 4-way sharded walk."""
     import torch
     from volsync_amd import Matcher, SumStruct, match_sums
-    monkeypatch.setenv("VSGPU_WALK_COOP", coop)
+    w, _, lock = coop.partition(":")
+    monkeypatch.setenv("VSGPU_WALK_COOP", w)
+    monkeypatch.setenv("VSGPU_WALK_LOCK", lock or "0")
     for path in FIX:
         doc, _, src = load_fixture(path)
         p, z = doc["params"], doc["sizes"]

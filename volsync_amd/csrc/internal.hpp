@@ -416,6 +416,7 @@ struct RsWalkArgs {
     int32_t *exitw_new;
     uint64_t *dbg;                   // debug builds: per-wave progress records (host-mapped)
     uint64_t *prof;                  // VSGPU_WALK_PROF: per-wave phase cycles/counts [waves][16]
+    uint32_t lock;                   // cooperative walk: flush rows re-sync every `lock` blocks (0: never)
 };
 hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t s);
 // the final walks' match list in order as 16-byte vs_match records (offset,

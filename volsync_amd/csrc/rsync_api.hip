@@ -897,6 +897,13 @@ int walk_scan(vs_rsync *h) {
     }
     VS_TRY(h->w_ctl.ensure(64));
     a.prof = nullptr;
+    // VSGPU_WALK_LOCK=k (even): cooperative flushes re-sync every k blocks
+    // (read per call: tests switch it within one process)
+    {
+        const char *e = getenv("VSGPU_WALK_LOCK");
+        const int v = e ? atoi(e) : 0;
+        a.lock = (v > 0 && v % 2 == 0) ? (uint32_t)v : 0u;
+    }
     a.work = h->w_ctl.as<uint32_t>();
     a.flags = h->w_ctl.as<uint32_t>() + 4;
     a.spec_off = h->w_spec_off.as<int64_t>();

@@ -259,7 +259,7 @@ struct RowWin {
 // compare both with the C oracle / libxxhash.
 template <bool WEAK>
 __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, uint64_t o,
-                              uint64_t len) {
+                              uint64_t len, uint32_t lock = 0) {
     using namespace vsstrong;
     const uint32_t q = lane & 15, sp = q >> 2, m = q & 3;
     const uint8_t *p = a.data + o + 16 * q;   // this lane's piece of each 256-byte quarter
@@ -284,11 +284,15 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = ldu16(p + (uint64_t)b * 1024 + 256 * j);
     };
-    // full blocks through a ring of kRing blocks in flight
+    // full blocks through a ring of kRing blocks in flight; with `lock`, every
+    // wave of the workgroup re-syncs every `lock` blocks (rows_window_idle
+    // holds the same barriers), so a cooperative flush's overlapping windows
+    // move through their bytes together and share them in L1 / L2
     uint4 r0[4], r1[4];
     if (nb > 0) load(r0, 0);
     if (nb > 1) load(r1, 1);
     for (uint32_t b = 0; b < nb; b += kRing) {
+        if (lock && b && b % lock == 0) __syncthreads();
         block(r0, b);
         if (b + 2 < nb) load(r0, b + 2);
         if (b + 1 >= nb) break;
@@ -354,6 +358,15 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
         r.weak = (sx & 0xffffu) | (((uint32_t)len * sx - sux) << 16);
     }
     return r;
+}
+
+// the barriers rows_window(..., lock) holds, for a wave with no window
+__device__ __forceinline__ void rows_window_idle(uint64_t len, uint32_t lock) {
+    const uint32_t nb = (uint32_t)((len - 1) / 1024);
+    for (uint32_t b = 0; b < nb; b += kRing) {
+        if (b && b % lock == 0) __syncthreads();
+        if (b + 1 >= nb) break;
+    }
 }
 
 // the first s2length bytes of (lo, hi) equal block i's sum2
@@ -1058,10 +1071,11 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
             }
             // ---- flush: hash the queued windows together, visit them in order
             uint64_t tf = wclock(wp);
+            if (a.lock && 4 * wave >= nq) rows_window_idle(L, a.lock);
             if (4 * wave < nq) {
                 const uint32_t j = 4 * wave + row;
                 const int64_t orow = sh.qoff[j < nq ? j : 4 * wave];
-                const RowWin w = rows_window<false>(a, rs, lane, (uint64_t)orow, L);
+                const RowWin w = rows_window<false>(a, rs, lane, (uint64_t)orow, L, a.lock);
                 for (uint32_t r = 0; r < 4 && 4 * wave + r < nq; ++r) {
                     const uint32_t sv = uni(sh.qsum[4 * wave + r]);
                     const uint64_t lo = rdl64(w.lo, (int)(16 * r)), hi = rdl64(w.hi, (int)(16 * r));
