@@ -772,6 +772,119 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
     return res;
 }
 
+// ---- band flushes (cooperative walk, VSGPU_WALK_BAND=1) ----------------------
+// The false-alarm windows of one edit overlap by all but a few KiB, yet a
+// flush that streams each from memory fetches every byte once per window
+// (11 B per source byte at the real C4 density).  A band flush hashes the
+// queued windows whose starts lie within kBandSpread of the first from a
+// workgroup-shared LDS ring of the source: the workgroup loads each byte of
+// [h_first, h_last + L) once, kBandChunk of every window per ring turn, and
+// the rows read their 16-byte pieces from the ring.
+constexpr uint32_t kBandR = 65536;       // ring bytes (a power of two)
+constexpr uint32_t kBandChunk = 8192;    // bytes of every window per ring turn
+constexpr int64_t kBandSpread = (int64_t)kBandR - 2 * kBandChunk - 64;
+constexpr uint32_t kBandWords = kBandR / 4 + 8;   // + a 32-byte mirror of the ring's start
+
+// 16 bytes at source offset x, any alignment: five ring words (the mirror
+// keeps them contiguous past the ring's end) and four byte-aligns
+__device__ __forceinline__ uint4 ring16(const uint32_t *ring, uint64_t x) {
+    const uint32_t i = (uint32_t)x & (kBandR - 1);
+    const uint32_t w = i >> 2, sft = i & 3;
+    const uint32_t r0 = ring[w], r1 = ring[w + 1], r2 = ring[w + 2], r3 = ring[w + 3],
+                   r4 = ring[w + 4];
+    uint4 v;
+    v.x = __builtin_amdgcn_alignbyte(r1, r0, sft);
+    v.y = __builtin_amdgcn_alignbyte(r2, r1, sft);
+    v.z = __builtin_amdgcn_alignbyte(r3, r2, sft);
+    v.w = __builtin_amdgcn_alignbyte(r4, r3, sft);
+    return v;
+}
+
+// the 16-byte granule at x (16-aligned) of the source; bytes past dlen read 0
+__device__ __forceinline__ uint4 band_granule(const RsWalkArgs &a, uint64_t x) {
+    if (x + 16 <= a.dlen) return *(const uint4 *)(a.data + x);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < 16 && x + k < a.dlen; ++k) w[k >> 2] |= (uint32_t)a.data[x + k] << (8 * (k & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ void band_put(uint32_t *ring, uint64_t x, uint4 v) {
+    const uint32_t i = (uint32_t)x & (kBandR - 1);
+    *(uint4 *)(ring + (i >> 2)) = v;
+    if (i < 32) *(uint4 *)(ring + kBandR / 4 + (i >> 2)) = v;
+}
+
+// a row's XXH3 state over a window read in pieces (rows_window's math, no
+// weak sum): blocks [b0, b1), then the partial block, last stripe and merge
+struct RowAcc {
+    uint64_t A0, A1;
+};
+__device__ __forceinline__ RowAcc row_acc_init(uint32_t lane) {
+    using namespace vsstrong;
+    const uint32_t m = lane & 3;
+    return RowAcc{(m == 0) ? P32_3 : (m == 1) ? P64_2 : (m == 2) ? P64_4 : P64_5,
+                  (m == 0) ? P64_1 : (m == 1) ? P64_3 : (m == 2) ? P32_2 : P32_1};
+}
+template <class Ld>
+__device__ __forceinline__ void row_acc_blocks(RowAcc &st, const RowSec &rs, uint32_t lane, Ld ld,
+                                               uint32_t b0, uint32_t b1) {
+    const uint32_t q = lane & 15, sp = q >> 2, m = q & 3;
+    if (b0 >= b1) return;
+    uint4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = ld((uint64_t)b0 * 1024 + 256 * j + 16 * q);
+    for (uint32_t b = b0; b < b1; ++b) {
+        uint4 nv[4];
+        const uint32_t bn = b + 1 < b1 ? b + 1 : b;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nv[j] = ld((uint64_t)bn * 1024 + 256 * j + 16 * q);
+        uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            acc16(v[j], rs.w[4 * j + sp + 2 * m], rs.w[4 * j + sp + 2 * m + 1], c0, c1);
+        st.A0 = scramble(st.A0 + row_sum_sp(c0), rs.w[16 + 2 * m]);
+        st.A1 = scramble(st.A1 + row_sum_sp(c1), rs.w[17 + 2 * m]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = nv[j];
+    }
+}
+template <class Ld>
+__device__ RowWin row_acc_finish(RowAcc &st, const RsWalkArgs &a, const RowSec &rs, uint32_t lane,
+                                 Ld ld, uint64_t len) {
+    using namespace vsstrong;
+    const uint32_t q = lane & 15, sp = q >> 2, m = q & 3;
+    const uint32_t nb = (uint32_t)((len - 1) / 1024);
+    const uint32_t ns = (uint32_t)(((len - 1) - (uint64_t)nb * 1024) / 64);
+    if (ns) {
+        uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (4 * j + sp < ns) {
+                const uint4 v = ld((uint64_t)nb * 1024 + 256 * j + 16 * q);
+                acc16(v, rs.w[4 * j + sp + 2 * m], rs.w[4 * j + sp + 2 * m + 1], c0, c1);
+            }
+        }
+        st.A0 += row_sum_sp(c0);
+        st.A1 += row_sum_sp(c1);
+    }
+    uint64_t tA = 0, tB = 0;
+    if (sp == 0) {
+        const uint4 v = ld(len - 64 + 16 * m);
+        uint64_t c0 = 0, c1 = 0;
+        acc16(v, csec_at(121 + 16 * m, a.seed), csec_at(129 + 16 * m, a.seed), c0, c1);
+        const uint64_t A0 = st.A0 + c0, A1 = st.A1 + c1;
+        tA = fold64(A0 ^ csec_at(11 + 16 * m, a.seed), A1 ^ csec_at(19 + 16 * m, a.seed));
+        if (a.csum_type == kXxh3_128)
+            tB = fold64(A0 ^ csec_at(117 + 16 * m, a.seed), A1 ^ csec_at(125 + 16 * m, a.seed));
+    }
+    tA = quad_sum(tA);
+    tB = quad_sum(tB);
+    RowWin r;
+    r.weak = 0;
+    r.lo = xxh3_aval(len * P64_1 + tA);
+    r.hi = (a.csum_type == kXxh3_128) ? xxh3_aval(~(len * P64_2) + tB) : 0;
+    return r;
+}
+
 // ---- the cooperative walk: W waves of a workgroup walk ONE segment -----------
 // ("cooperative walk").  At the real C4 table density a
 // wave-private walk spends most of its time hashing false-alarm windows: the
@@ -800,12 +913,97 @@ struct CoopShared {
     uint32_t seg;                   // the segment being walked
 };
 
+// Hash queued windows [j0, j1) (starts within kBandSpread of the first) from
+// the ring, window j0 + r on wave r / 4, row r % 4, and chain-scan them into
+// sh.wlo / whi / ci / cfa.  Every wave of the workgroup calls it (the ring
+// loads and barriers are shared); returns after a final barrier.
 template <int W>
+__device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, uint32_t wave,
+                          uint32_t *ring, CoopShared<W> &sh, uint32_t j0, uint32_t j1, uint64_t L) {
+    constexpr uint32_t kT = 64 * W;                  // threads
+    constexpr uint32_t kG = (kBandChunk + 16) / 16;  // granules of one turn's new bytes (+ rounding)
+    constexpr uint32_t kPer = (kG + kT - 1) / kT;
+    const uint32_t nw = j1 - j0, tid = threadIdx.x;
+    const uint64_t hf = uni64((uint64_t)sh.qoff[j0]), hl = uni64((uint64_t)sh.qoff[j1 - 1]);
+    const uint32_t r = 4 * wave + (lane >> 4);
+    const bool active = 4 * wave < nw;
+    const uint64_t h = (uint64_t)sh.qoff[j0 + (r < nw ? r : active ? 4 * wave : 0)];
+    // the first turn's bytes: [hf, hl + chunk)
+    {
+        const uint64_t x0 = hf & ~15ull, x1 = min(hl + kBandChunk, a.dlen);
+        for (uint64_t xb = x0 + 16ull * tid; xb < x1; xb += 16ull * kT * 8) {
+            uint4 g8[8];   // eight loads in flight before the stores
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint64_t x = xb + 16ull * kT * k;
+                if (x < x1) g8[k] = band_granule(a, x);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint64_t x = xb + 16ull * kT * k;
+                if (x < x1) band_put(ring, x, g8[k]);
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t nch = (uint32_t)((L + kBandChunk - 1) / kBandChunk);
+    const uint32_t nb = (uint32_t)((L - 1) / 1024);
+    RowAcc st = row_acc_init(lane);
+    auto ld = [&](uint64_t off) { return ring16(ring, h + off); };
+    RowWin w{0, 0, 0};
+    for (uint32_t c = 0; c < nch; ++c) {
+        // the next turn's new bytes [hl + chunk (c + 1), hl + chunk (c + 2)),
+        // loaded now, stored after this turn's reads (their ring slots are
+        // not read this turn: hl - hf <= kBandSpread)
+        uint4 g[kPer];
+        uint64_t gx0 = 0, gx1 = 0;
+        if (c + 1 < nch) {
+            gx0 = (hl + (uint64_t)kBandChunk * (c + 1)) & ~15ull;
+            gx1 = min(hl + (uint64_t)kBandChunk * (c + 2), a.dlen);
+#pragma unroll
+            for (uint32_t k = 0; k < kPer; ++k) {
+                const uint64_t x = gx0 + 16ull * (tid + k * kT);
+                if (x < gx1) g[k] = band_granule(a, x);
+            }
+        }
+        if (active) {
+            row_acc_blocks(st, rs, lane, ld, min(8 * c, nb), min(8 * c + 8, nb));
+            if (c + 1 == nch) w = row_acc_finish(st, a, rs, lane, ld, L);
+        }
+        if (c + 1 < nch) {
+#pragma unroll
+            for (uint32_t k = 0; k < kPer; ++k) {
+                const uint64_t x = gx0 + 16ull * (tid + k * kT);
+                if (x < gx1) band_put(ring, x, g[k]);
+            }
+        }
+        __syncthreads();
+    }
+    if (active) {
+        for (uint32_t rr = 0; rr < 4 && 4 * wave + rr < nw; ++rr) {
+            const uint32_t j = j0 + 4 * wave + rr;
+            const uint32_t sv = uni(sh.qsum[j]);
+            const uint64_t lo = rdl64(w.lo, (int)(16 * rr)), hi = rdl64(w.hi, (int)(16 * rr));
+            uint32_t cf = 0;
+            const int32_t ci = unis(chain_scan(a, sv, lo, hi, (uint32_t)L, cf));
+            if (lane == 0) {
+                sh.wlo[j] = lo;
+                sh.whi[j] = hi;
+                sh.ci[j] = ci;
+                sh.cfa[j] = cf;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+template <int W, bool BAND>
 __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, const uint32_t *lfilt,
                                        uint32_t lbits, uint32_t lane, uint32_t wave, int64_t o,
                                        int32_t want, int64_t stop, int64_t *out_off,
                                        int32_t *out_idx, int64_t *out_fab, uint32_t cap,
-                                       const SpecView *spec, WProf &wp, CoopShared<W> &sh) {
+                                       const SpecView *spec, WProf &wp, CoopShared<W> &sh,
+                                       uint32_t *ring) {
     constexpr uint32_t Q = 4 * W;   // windows per flush
     const int64_t fend = min(stop, (int64_t)a.full_end);
     const uint64_t L = a.blength;
@@ -1070,43 +1268,61 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
                 break;
             }
             // ---- flush: hash the queued windows together, visit them in order
-            uint64_t tf = wclock(wp);
-            if (a.lock && 4 * wave >= nq) rows_window_idle(L, a.lock);
-            if (4 * wave < nq) {
-                const uint32_t j = 4 * wave + row;
-                const int64_t orow = sh.qoff[j < nq ? j : 4 * wave];
-                const RowWin w = rows_window<false>(a, rs, lane, (uint64_t)orow, L, a.lock);
-                for (uint32_t r = 0; r < 4 && 4 * wave + r < nq; ++r) {
-                    const uint32_t sv = uni(sh.qsum[4 * wave + r]);
-                    const uint64_t lo = rdl64(w.lo, (int)(16 * r)), hi = rdl64(w.hi, (int)(16 * r));
-                    uint32_t cf = 0;
-                    const int32_t ci = unis(chain_scan(a, sv, lo, hi, (uint32_t)L, cf));
-                    if (lane == 0) {
-                        sh.wlo[4 * wave + r] = lo;
-                        sh.whi[4 * wave + r] = hi;
-                        sh.ci[4 * wave + r] = ci;
-                        sh.cfa[4 * wave + r] = cf;
+            int64_t hlast = 0;
+            // visit [jb, je): hash_search's chain walks in offset order
+            auto visit = [&](uint32_t jb, uint32_t je) {
+                for (uint32_t j = jb; j < je; ++j) {
+                    const int64_t h = (int64_t)uni64((uint64_t)sh.qoff[j]);
+                    const uint32_t sv = uni(sh.qsum[j]);
+                    const uint64_t lo = uni64(sh.wlo[j]), hi = uni64(sh.whi[j]);
+                    const uint64_t fa_visit = fa;
+                    uint64_t tc = wclock(wp);
+                    fa += uni(sh.cfa[j]);
+                    const int32_t i = unis(chain_prefer(a, unis(sh.ci[j]), sv, lo, hi, want));
+                    wadd(wp, kPrChain, tc);
+                    hlast = h;
+                    if (i >= 0) {
+                        merged = on_match(h, i, fa_visit);
+                        matched = true;
+                        return;
                     }
                 }
-            }
-            __syncthreads();
-            wadd(wp, kPrFlush, tf);
-            int64_t hlast = 0;
-            for (uint32_t j = 0; j < nq; ++j) {
-                const int64_t h = (int64_t)uni64((uint64_t)sh.qoff[j]);
-                const uint32_t sv = uni(sh.qsum[j]);
-                const uint64_t lo = uni64(sh.wlo[j]), hi = uni64(sh.whi[j]);
-                const uint64_t fa_visit = fa;
-                tf = wclock(wp);
-                fa += uni(sh.cfa[j]);
-                const int32_t i = unis(chain_prefer(a, unis(sh.ci[j]), sv, lo, hi, want));
-                wadd(wp, kPrChain, tf);
-                hlast = h;
-                if (i >= 0) {
-                    merged = on_match(h, i, fa_visit);
-                    matched = true;
-                    break;
+            };
+            if constexpr (BAND) {
+                // bands of windows starting within kBandSpread of each other
+                for (uint32_t j0 = 0; j0 < nq && !matched;) {
+                    const int64_t hf = (int64_t)uni64((uint64_t)sh.qoff[j0]);
+                    uint32_t j1 = j0 + 1;
+                    while (j1 < nq && (int64_t)uni64((uint64_t)sh.qoff[j1]) - hf <= kBandSpread) ++j1;
+                    uint64_t tf = wclock(wp);
+                    band_hash<W>(a, rs, lane, wave, ring, sh, j0, j1, L);
+                    wadd(wp, kPrFlush, tf);
+                    visit(j0, j1);
+                    j0 = j1;
                 }
+            } else {
+                uint64_t tf = wclock(wp);
+                if (a.lock && 4 * wave >= nq) rows_window_idle(L, a.lock);
+                if (4 * wave < nq) {
+                    const uint32_t j = 4 * wave + row;
+                    const int64_t orow = sh.qoff[j < nq ? j : 4 * wave];
+                    const RowWin w = rows_window<false>(a, rs, lane, (uint64_t)orow, L, a.lock);
+                    for (uint32_t r = 0; r < 4 && 4 * wave + r < nq; ++r) {
+                        const uint32_t sv = uni(sh.qsum[4 * wave + r]);
+                        const uint64_t lo = rdl64(w.lo, (int)(16 * r)), hi = rdl64(w.hi, (int)(16 * r));
+                        uint32_t cf = 0;
+                        const int32_t ci = unis(chain_scan(a, sv, lo, hi, (uint32_t)L, cf));
+                        if (lane == 0) {
+                            sh.wlo[4 * wave + r] = lo;
+                            sh.whi[4 * wave + r] = hi;
+                            sh.ci[4 * wave + r] = ci;
+                            sh.cfa[4 * wave + r] = cf;
+                        }
+                    }
+                }
+                __syncthreads();
+                wadd(wp, kPrFlush, tf);
+                visit(0, nq);
             }
             __syncthreads();   // queue / window slots are reused
             if (matched) break;
@@ -1209,10 +1425,11 @@ __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
 // the speculative pass with W-wave cooperative walks (walk_segment_coop):
 // W == 12 keeps the LDS prefilter (one workgroup per CU); smaller W runs
 // 12 / W workgroups per CU without it
-template <int W>
+template <int W, bool BAND>
 __global__ __launch_bounds__(64 * W) void rs_walk_spec_coop_kernel(RsWalkArgs a) {
     constexpr bool kLds = W >= 12;
     __shared__ uint32_t lfilt[kLds ? kLdsFiltWordsW : 1];
+    __shared__ __attribute__((aligned(16))) uint32_t ring[BAND ? kBandWords : 4];
     __shared__ uint64_t lsec[24];
     __shared__ CoopShared<W> sh;
     load_secret(lsec, a.seed);
@@ -1236,9 +1453,10 @@ __global__ __launch_bounds__(64 * W) void rs_walk_spec_coop_kernel(RsWalkArgs a)
         const int64_t e = (int64_t)uni64((uint64_t)(k ? seg_lo(a, k) : a.e0));
         const int32_t w = unis(k ? (int32_t)a.count : a.w0);
         const uint64_t base = (uint64_t)k * a.cap;
-        const SegResult r = walk_segment_coop<W>(a, rs, lfilt, lbits, lane, wave, e, w, seg_hi(a, k),
-                                                 a.spec_off + base, a.spec_idx + base,
-                                                 a.spec_fab + base, a.cap, nullptr, wp, sh);
+        const SegResult r = walk_segment_coop<W, BAND>(a, rs, lfilt, lbits, lane, wave, e, w,
+                                                       seg_hi(a, k), a.spec_off + base,
+                                                       a.spec_idx + base, a.spec_fab + base, a.cap,
+                                                       nullptr, wp, sh, ring);
         wadd(wp, kPrSeg, ts);
         if (wave == 0 && lane == 0) {
             a.spec_n[k] = r.n;
@@ -1350,14 +1568,22 @@ hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t
         const int v = e ? atoi(e) : 0;
         return (v == 4 || v == 6 || v == 12) ? v : 0;
     }();
+    // VSGPU_WALK_BAND=1 (with COOP=4): band flushes from an LDS ring (64 KiB
+    // per workgroup: two workgroups per CU)
+    const bool band = [] {
+        const char *e = getenv("VSGPU_WALK_BAND");
+        return e && atoi(e) == 1;
+    }();
     if (!stitch && coop) {
         hipError_t e = hipMemsetAsync(a.work, 0, 4, s);
         if (e != hipSuccess) return e;
-        const uint64_t per_cu = 12 / coop;
+        const bool b4 = band && coop == 4;
+        const uint64_t per_cu = b4 ? 2 : 12 / coop;
         const uint64_t grid = std::min<uint64_t>(a.nseg, (uint64_t)std::max(cus, 1) * per_cu);
-        if (coop == 12) rs_walk_spec_coop_kernel<12><<<(uint32_t)grid, 768, 0, s>>>(a);
-        else if (coop == 6) rs_walk_spec_coop_kernel<6><<<(uint32_t)grid, 384, 0, s>>>(a);
-        else rs_walk_spec_coop_kernel<4><<<(uint32_t)grid, 256, 0, s>>>(a);
+        if (coop == 12) rs_walk_spec_coop_kernel<12, false><<<(uint32_t)grid, 768, 0, s>>>(a);
+        else if (coop == 6) rs_walk_spec_coop_kernel<6, false><<<(uint32_t)grid, 384, 0, s>>>(a);
+        else if (b4) rs_walk_spec_coop_kernel<4, true><<<(uint32_t)grid, 256, 0, s>>>(a);
+        else rs_walk_spec_coop_kernel<4, false><<<(uint32_t)grid, 256, 0, s>>>(a);
         return hipGetLastError();
     }
     const uint32_t threads = stitch ? kWalkThreads : spec_threads;
