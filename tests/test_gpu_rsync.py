@@ -558,9 +558,9 @@ def test_c4_real_density_window_exact(gpu, monkeypatch):
     m.load_sums_device(cnt, bl, s2l, rem, s1.data_ptr(), s2.data_ptr(), csum, seed)
     assert len(want) > 14000 and fa > 50000   # the density this test is for
     # the wave walk, then the cooperative walks
-    for coop in ("0", "12", "4", "4b"):
-        monkeypatch.setenv("VSGPU_WALK_BAND", "1" if coop.endswith("b") else "0")
-        monkeypatch.setenv("VSGPU_WALK_COOP", coop.rstrip("b"))
+    for coop in ("0", "12", "4", "4b", "4B"):
+        monkeypatch.setenv("VSGPU_WALK_BAND", {"b": "1", "B": "2"}.get(coop[-1], "0"))
+        monkeypatch.setenv("VSGPU_WALK_COOP", coop.rstrip("bB"))
         m.match_scan(ds.data_ptr(), n, data_lo, plan.total, lo, hi)
         gexit = m.match_stitch(e, w)
         nm = m.match_finish()
@@ -680,19 +680,20 @@ def test_file_sum_jobs_fifo(gpu):
     m.close()
 
 
-@pytest.mark.parametrize("coop", ["12", "6", "4", "12:8", "4:8", "4b"])
+@pytest.mark.parametrize("coop", ["12", "6", "4", "12:8", "4:8", "4b", "4B"])
 def test_coop_walk_exact(gpu, monkeypatch, coop):
     """The cooperative speculative walk (VSGPU_WALK_COOP=W: W waves share one
     segment's walk; W:k also re-syncs flush rows every k blocks,
-    VSGPU_WALK_LOCK; 4b: band flushes from the LDS ring, VSGPU_WALK_BAND)
+    VSGPU_WALK_LOCK; 4b / 4B: band flushes from a 64 / 32 KiB LDS ring,
+    VSGPU_WALK_BAND=1 / 2)
     against the C hash_search: every golden fixture, seeded
     shifted / overwritten sources (false alarms, runs, short last blocks),
     the C4 parameters on a 1 GiB basis, and the 4-way sharded walk."""
     import torch
     from volsync_amd import Matcher, SumStruct, match_sums
     w, _, lock = coop.partition(":")
-    monkeypatch.setenv("VSGPU_WALK_BAND", "1" if w.endswith("b") else "0")
-    monkeypatch.setenv("VSGPU_WALK_COOP", w.rstrip("b"))
+    monkeypatch.setenv("VSGPU_WALK_BAND", {"b": "1", "B": "2"}.get(w[-1], "0"))
+    monkeypatch.setenv("VSGPU_WALK_COOP", w.rstrip("bB"))
     monkeypatch.setenv("VSGPU_WALK_LOCK", lock or "0")
     for path in FIX:
         doc, _, src = load_fixture(path)

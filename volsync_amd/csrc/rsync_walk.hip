@@ -772,23 +772,28 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
     return res;
 }
 
-// ---- band flushes (cooperative walk, VSGPU_WALK_BAND=1) ----------------------
+// ---- band flushes (cooperative walk, VSGPU_WALK_BAND=1|2) --------------------
 // The false-alarm windows of one edit overlap by all but a few KiB, yet a
 // flush that streams each from memory fetches every byte once per window
 // (11 B per source byte at the real C4 density).  A band flush hashes the
 // queued windows whose starts lie within kBandSpread of the first from a
 // workgroup-shared LDS ring of the source: the workgroup loads each byte of
-// [h_first, h_last + L) once, kBandChunk of every window per ring turn, and
+// [h_first, h_last + L) once, band_chunk of every window per ring turn, and
 // the rows read their 16-byte pieces from the ring.
-constexpr uint32_t kBandR = 65536;       // ring bytes (a power of two)
-constexpr uint32_t kBandChunk = 8192;    // bytes of every window per ring turn
-constexpr int64_t kBandSpread = (int64_t)kBandR - 2 * kBandChunk - 64;
-constexpr uint32_t kBandWords = kBandR / 4 + 8;   // + a 32-byte mirror of the ring's start
+// RB: ring bytes (a power of two; 64 KiB: two workgroups per CU, 32 KiB:
+// three, with bands half as wide)
+template <uint32_t RB>
+constexpr uint32_t band_chunk() { return RB / 8; }   // bytes of every window per ring turn
+template <uint32_t RB>
+constexpr int64_t band_spread() { return (int64_t)RB - 2 * band_chunk<RB>() - 64; }
+template <uint32_t RB>
+constexpr uint32_t band_words() { return RB / 4 + 8; }   // + a 32-byte mirror of the ring's start
 
 // 16 bytes at source offset x, any alignment: five ring words (the mirror
 // keeps them contiguous past the ring's end) and four byte-aligns
+template <uint32_t RB>
 __device__ __forceinline__ uint4 ring16(const uint32_t *ring, uint64_t x) {
-    const uint32_t i = (uint32_t)x & (kBandR - 1);
+    const uint32_t i = (uint32_t)x & (RB - 1);
     const uint32_t w = i >> 2, sft = i & 3;
     const uint32_t r0 = ring[w], r1 = ring[w + 1], r2 = ring[w + 2], r3 = ring[w + 3],
                    r4 = ring[w + 4];
@@ -807,10 +812,11 @@ __device__ __forceinline__ uint4 band_granule(const RsWalkArgs &a, uint64_t x) {
     for (uint32_t k = 0; k < 16 && x + k < a.dlen; ++k) w[k >> 2] |= (uint32_t)a.data[x + k] << (8 * (k & 3));
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
+template <uint32_t RB>
 __device__ __forceinline__ void band_put(uint32_t *ring, uint64_t x, uint4 v) {
-    const uint32_t i = (uint32_t)x & (kBandR - 1);
+    const uint32_t i = (uint32_t)x & (RB - 1);
     *(uint4 *)(ring + (i >> 2)) = v;
-    if (i < 32) *(uint4 *)(ring + kBandR / 4 + (i >> 2)) = v;
+    if (i < 32) *(uint4 *)(ring + RB / 4 + (i >> 2)) = v;
 }
 
 // a row's XXH3 state over a window read in pieces (rows_window's math, no
@@ -913,15 +919,16 @@ struct CoopShared {
     uint32_t seg;                   // the segment being walked
 };
 
-// Hash queued windows [j0, j1) (starts within kBandSpread of the first) from
+// Hash queued windows [j0, j1) (starts within band_spread<RB> of the first) from
 // the ring, window j0 + r on wave r / 4, row r % 4, and chain-scan them into
 // sh.wlo / whi / ci / cfa.  Every wave of the workgroup calls it (the ring
 // loads and barriers are shared); returns after a final barrier.
-template <int W>
+template <int W, uint32_t RB>
 __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, uint32_t wave,
                           uint32_t *ring, CoopShared<W> &sh, uint32_t j0, uint32_t j1, uint64_t L) {
+    constexpr uint32_t kChunk = band_chunk<RB>();
     constexpr uint32_t kT = 64 * W;                  // threads
-    constexpr uint32_t kG = (kBandChunk + 16) / 16;  // granules of one turn's new bytes (+ rounding)
+    constexpr uint32_t kG = (kChunk + 16) / 16;  // granules of one turn's new bytes (+ rounding)
     constexpr uint32_t kPer = (kG + kT - 1) / kT;
     const uint32_t nw = j1 - j0, tid = threadIdx.x;
     const uint64_t hf = uni64((uint64_t)sh.qoff[j0]), hl = uni64((uint64_t)sh.qoff[j1 - 1]);
@@ -930,7 +937,7 @@ __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, 
     const uint64_t h = (uint64_t)sh.qoff[j0 + (r < nw ? r : active ? 4 * wave : 0)];
     // the first turn's bytes: [hf, hl + chunk)
     {
-        const uint64_t x0 = hf & ~15ull, x1 = min(hl + kBandChunk, a.dlen);
+        const uint64_t x0 = hf & ~15ull, x1 = min(hl + kChunk, a.dlen);
         for (uint64_t xb = x0 + 16ull * tid; xb < x1; xb += 16ull * kT * 8) {
             uint4 g8[8];   // eight loads in flight before the stores
 #pragma unroll
@@ -941,25 +948,25 @@ __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, 
 #pragma unroll
             for (uint32_t k = 0; k < 8; ++k) {
                 const uint64_t x = xb + 16ull * kT * k;
-                if (x < x1) band_put(ring, x, g8[k]);
+                if (x < x1) band_put<RB>(ring, x, g8[k]);
             }
         }
     }
     __syncthreads();
-    const uint32_t nch = (uint32_t)((L + kBandChunk - 1) / kBandChunk);
+    const uint32_t nch = (uint32_t)((L + kChunk - 1) / kChunk);
     const uint32_t nb = (uint32_t)((L - 1) / 1024);
     RowAcc st = row_acc_init(lane);
-    auto ld = [&](uint64_t off) { return ring16(ring, h + off); };
+    auto ld = [&](uint64_t off) { return ring16<RB>(ring, h + off); };
     RowWin w{0, 0, 0};
     for (uint32_t c = 0; c < nch; ++c) {
         // the next turn's new bytes [hl + chunk (c + 1), hl + chunk (c + 2)),
         // loaded now, stored after this turn's reads (their ring slots are
-        // not read this turn: hl - hf <= kBandSpread)
+        // not read this turn: hl - hf <= band_spread<RB>)
         uint4 g[kPer];
         uint64_t gx0 = 0, gx1 = 0;
         if (c + 1 < nch) {
-            gx0 = (hl + (uint64_t)kBandChunk * (c + 1)) & ~15ull;
-            gx1 = min(hl + (uint64_t)kBandChunk * (c + 2), a.dlen);
+            gx0 = (hl + (uint64_t)kChunk * (c + 1)) & ~15ull;
+            gx1 = min(hl + (uint64_t)kChunk * (c + 2), a.dlen);
 #pragma unroll
             for (uint32_t k = 0; k < kPer; ++k) {
                 const uint64_t x = gx0 + 16ull * (tid + k * kT);
@@ -967,14 +974,15 @@ __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, 
             }
         }
         if (active) {
-            row_acc_blocks(st, rs, lane, ld, min(8 * c, nb), min(8 * c + 8, nb));
+            constexpr uint32_t kB = kChunk / 1024;   // blocks per turn
+            row_acc_blocks(st, rs, lane, ld, min(kB * c, nb), min(kB * c + kB, nb));
             if (c + 1 == nch) w = row_acc_finish(st, a, rs, lane, ld, L);
         }
         if (c + 1 < nch) {
 #pragma unroll
             for (uint32_t k = 0; k < kPer; ++k) {
                 const uint64_t x = gx0 + 16ull * (tid + k * kT);
-                if (x < gx1) band_put(ring, x, g[k]);
+                if (x < gx1) band_put<RB>(ring, x, g[k]);
             }
         }
         __syncthreads();
@@ -997,7 +1005,7 @@ __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, 
     __syncthreads();
 }
 
-template <int W, bool BAND>
+template <int W, uint32_t RB>
 __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, const uint32_t *lfilt,
                                        uint32_t lbits, uint32_t lane, uint32_t wave, int64_t o,
                                        int32_t want, int64_t stop, int64_t *out_off,
@@ -1288,14 +1296,14 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
                     }
                 }
             };
-            if constexpr (BAND) {
-                // bands of windows starting within kBandSpread of each other
+            if constexpr (RB != 0) {
+                // bands of windows starting within band_spread<RB> of each other
                 for (uint32_t j0 = 0; j0 < nq && !matched;) {
                     const int64_t hf = (int64_t)uni64((uint64_t)sh.qoff[j0]);
                     uint32_t j1 = j0 + 1;
-                    while (j1 < nq && (int64_t)uni64((uint64_t)sh.qoff[j1]) - hf <= kBandSpread) ++j1;
+                    while (j1 < nq && (int64_t)uni64((uint64_t)sh.qoff[j1]) - hf <= band_spread<RB>()) ++j1;
                     uint64_t tf = wclock(wp);
-                    band_hash<W>(a, rs, lane, wave, ring, sh, j0, j1, L);
+                    band_hash<W, RB>(a, rs, lane, wave, ring, sh, j0, j1, L);
                     wadd(wp, kPrFlush, tf);
                     visit(j0, j1);
                     j0 = j1;
@@ -1425,11 +1433,11 @@ __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
 // the speculative pass with W-wave cooperative walks (walk_segment_coop):
 // W == 12 keeps the LDS prefilter (one workgroup per CU); smaller W runs
 // 12 / W workgroups per CU without it
-template <int W, bool BAND>
+template <int W, uint32_t RB>
 __global__ __launch_bounds__(64 * W) void rs_walk_spec_coop_kernel(RsWalkArgs a) {
     constexpr bool kLds = W >= 12;
     __shared__ uint32_t lfilt[kLds ? kLdsFiltWordsW : 1];
-    __shared__ __attribute__((aligned(16))) uint32_t ring[BAND ? kBandWords : 4];
+    __shared__ __attribute__((aligned(16))) uint32_t ring[RB ? band_words<RB>() : 4];
     __shared__ uint64_t lsec[24];
     __shared__ CoopShared<W> sh;
     load_secret(lsec, a.seed);
@@ -1453,7 +1461,7 @@ __global__ __launch_bounds__(64 * W) void rs_walk_spec_coop_kernel(RsWalkArgs a)
         const int64_t e = (int64_t)uni64((uint64_t)(k ? seg_lo(a, k) : a.e0));
         const int32_t w = unis(k ? (int32_t)a.count : a.w0);
         const uint64_t base = (uint64_t)k * a.cap;
-        const SegResult r = walk_segment_coop<W, BAND>(a, rs, lfilt, lbits, lane, wave, e, w,
+        const SegResult r = walk_segment_coop<W, RB>(a, rs, lfilt, lbits, lane, wave, e, w,
                                                        seg_hi(a, k), a.spec_off + base,
                                                        a.spec_idx + base, a.spec_fab + base, a.cap,
                                                        nullptr, wp, sh, ring);
@@ -1568,22 +1576,24 @@ hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t
         const int v = e ? atoi(e) : 0;
         return (v == 4 || v == 6 || v == 12) ? v : 0;
     }();
-    // VSGPU_WALK_BAND=1 (with COOP=4): band flushes from an LDS ring (64 KiB
-    // per workgroup: two workgroups per CU)
-    const bool band = [] {
+    // VSGPU_WALK_BAND=1 / 2 (with COOP=4): band flushes from an LDS ring of
+    // 64 KiB (two workgroups per CU) / 32 KiB (three)
+    const int band = [] {
         const char *e = getenv("VSGPU_WALK_BAND");
-        return e && atoi(e) == 1;
+        const int v = e ? atoi(e) : 0;
+        return (v == 1 || v == 2) ? v : 0;
     }();
     if (!stitch && coop) {
         hipError_t e = hipMemsetAsync(a.work, 0, 4, s);
         if (e != hipSuccess) return e;
-        const bool b4 = band && coop == 4;
-        const uint64_t per_cu = b4 ? 2 : 12 / coop;
+        const int b4 = coop == 4 ? band : 0;
+        const uint64_t per_cu = b4 == 1 ? 2 : 12 / coop;
         const uint64_t grid = std::min<uint64_t>(a.nseg, (uint64_t)std::max(cus, 1) * per_cu);
-        if (coop == 12) rs_walk_spec_coop_kernel<12, false><<<(uint32_t)grid, 768, 0, s>>>(a);
-        else if (coop == 6) rs_walk_spec_coop_kernel<6, false><<<(uint32_t)grid, 384, 0, s>>>(a);
-        else if (b4) rs_walk_spec_coop_kernel<4, true><<<(uint32_t)grid, 256, 0, s>>>(a);
-        else rs_walk_spec_coop_kernel<4, false><<<(uint32_t)grid, 256, 0, s>>>(a);
+        if (coop == 12) rs_walk_spec_coop_kernel<12, 0><<<(uint32_t)grid, 768, 0, s>>>(a);
+        else if (coop == 6) rs_walk_spec_coop_kernel<6, 0><<<(uint32_t)grid, 384, 0, s>>>(a);
+        else if (b4 == 1) rs_walk_spec_coop_kernel<4, 65536><<<(uint32_t)grid, 256, 0, s>>>(a);
+        else if (b4 == 2) rs_walk_spec_coop_kernel<4, 32768><<<(uint32_t)grid, 256, 0, s>>>(a);
+        else rs_walk_spec_coop_kernel<4, 0><<<(uint32_t)grid, 256, 0, s>>>(a);
         return hipGetLastError();
     }
     const uint32_t threads = stitch ? kWalkThreads : spec_threads;
