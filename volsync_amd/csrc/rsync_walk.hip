@@ -785,7 +785,7 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
 template <uint32_t RB>
 constexpr uint32_t band_chunk() { return RB / 8; }   // bytes of every window per ring turn
 template <uint32_t RB>
-constexpr int64_t band_spread() { return (int64_t)RB - 2 * band_chunk<RB>() - 64; }
+constexpr int64_t band_spread() { return (int64_t)RB - 3 * band_chunk<RB>() - 64; }
 template <uint32_t RB>
 constexpr uint32_t band_words() { return RB / 4 + 8; }   // + a 32-byte mirror of the ring's start
 
@@ -835,22 +835,28 @@ __device__ __forceinline__ void row_acc_blocks(RowAcc &st, const RowSec &rs, uin
                                                uint32_t b0, uint32_t b1) {
     const uint32_t q = lane & 15, sp = q >> 2, m = q & 3;
     if (b0 >= b1) return;
-    uint4 v[4];
+    auto load = [&](uint4 (&v)[4], uint32_t b) {   // b clamped: every block of [b0, b1) is readable
+        b = b < b1 ? b : b1 - 1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = ld((uint64_t)b0 * 1024 + 256 * j + 16 * q);
-    for (uint32_t b = b0; b < b1; ++b) {
-        uint4 nv[4];
-        const uint32_t bn = b + 1 < b1 ? b + 1 : b;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) nv[j] = ld((uint64_t)bn * 1024 + 256 * j + 16 * q);
+        for (int j = 0; j < 4; ++j) v[j] = ld((uint64_t)b * 1024 + 256 * j + 16 * q);
+    };
+    auto block = [&](const uint4 (&v)[4]) {
         uint64_t c0 = 0, c1 = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             acc16(v[j], rs.w[4 * j + sp + 2 * m], rs.w[4 * j + sp + 2 * m + 1], c0, c1);
         st.A0 = scramble(st.A0 + row_sum_sp(c0), rs.w[16 + 2 * m]);
         st.A1 = scramble(st.A1 + row_sum_sp(c1), rs.w[17 + 2 * m]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = nv[j];
+    };
+    // two buffers, each refilled as soon as it is consumed (no register copies)
+    uint4 v0[4], v1[4];
+    load(v0, b0);
+    for (uint32_t b = b0; b < b1; b += 2) {
+        load(v1, b + 1);
+        block(v0);
+        if (b + 1 >= b1) break;
+        load(v0, b + 2);
+        block(v1);
     }
 }
 template <class Ld>
@@ -935,9 +941,9 @@ __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, 
     const uint32_t r = 4 * wave + (lane >> 4);
     const bool active = 4 * wave < nw;
     const uint64_t h = (uint64_t)sh.qoff[j0 + (r < nw ? r : active ? 4 * wave : 0)];
-    // the first turn's bytes: [hf, hl + chunk)
+    // the first two turns' bytes: [hf, hl + 2 chunk)
     {
-        const uint64_t x0 = hf & ~15ull, x1 = min(hl + kChunk, a.dlen);
+        const uint64_t x0 = hf & ~15ull, x1 = min(hl + 2 * kChunk, a.dlen);
         for (uint64_t xb = x0 + 16ull * tid; xb < x1; xb += 16ull * kT * 8) {
             uint4 g8[8];   // eight loads in flight before the stores
 #pragma unroll
@@ -952,39 +958,54 @@ __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, 
             }
         }
     }
-    __syncthreads();
     const uint32_t nch = (uint32_t)((L + kChunk - 1) / kChunk);
     const uint32_t nb = (uint32_t)((L - 1) / 1024);
+    // turn k's new bytes [hl + chunk k, hl + chunk (k + 1)) (k >= 2) are
+    // loaded at the start of turn k - 2 and stored at the end of turn k - 1:
+    // a full turn of hashing covers the load latency.  Their ring slots are
+    // not read before turn k (hl - hf <= band_spread<RB>).
+    auto load_set = [&](uint4 (&g)[kPer], uint32_t k) {
+        if (k >= nch) return;
+        const uint64_t gx0 = (hl + (uint64_t)kChunk * k) & ~15ull;
+        const uint64_t gx1 = min(hl + (uint64_t)kChunk * (k + 1), a.dlen);
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const uint64_t x = gx0 + 16ull * (tid + i * kT);
+            if (x < gx1) g[i] = band_granule(a, x);
+        }
+    };
+    auto put_set = [&](const uint4 (&g)[kPer], uint32_t k) {
+        if (k >= nch) return;
+        const uint64_t gx0 = (hl + (uint64_t)kChunk * k) & ~15ull;
+        const uint64_t gx1 = min(hl + (uint64_t)kChunk * (k + 1), a.dlen);
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const uint64_t x = gx0 + 16ull * (tid + i * kT);
+            if (x < gx1) band_put<RB>(ring, x, g[i]);
+        }
+    };
     RowAcc st = row_acc_init(lane);
     auto ld = [&](uint64_t off) { return ring16<RB>(ring, h + off); };
     RowWin w{0, 0, 0};
-    for (uint32_t c = 0; c < nch; ++c) {
-        // the next turn's new bytes [hl + chunk (c + 1), hl + chunk (c + 2)),
-        // loaded now, stored after this turn's reads (their ring slots are
-        // not read this turn: hl - hf <= band_spread<RB>)
-        uint4 g[kPer];
-        uint64_t gx0 = 0, gx1 = 0;
-        if (c + 1 < nch) {
-            gx0 = (hl + (uint64_t)kChunk * (c + 1)) & ~15ull;
-            gx1 = min(hl + (uint64_t)kChunk * (c + 2), a.dlen);
-#pragma unroll
-            for (uint32_t k = 0; k < kPer; ++k) {
-                const uint64_t x = gx0 + 16ull * (tid + k * kT);
-                if (x < gx1) g[k] = band_granule(a, x);
-            }
-        }
+    auto turn = [&](uint32_t c) {
         if (active) {
             constexpr uint32_t kB = kChunk / 1024;   // blocks per turn
             row_acc_blocks(st, rs, lane, ld, min(kB * c, nb), min(kB * c + kB, nb));
             if (c + 1 == nch) w = row_acc_finish(st, a, rs, lane, ld, L);
         }
-        if (c + 1 < nch) {
-#pragma unroll
-            for (uint32_t k = 0; k < kPer; ++k) {
-                const uint64_t x = gx0 + 16ull * (tid + k * kT);
-                if (x < gx1) band_put<RB>(ring, x, g[k]);
-            }
-        }
+    };
+    uint4 gA[kPer], gB[kPer];
+    load_set(gA, 2);
+    __syncthreads();
+    for (uint32_t c = 0; c < nch; c += 2) {
+        load_set(gB, c + 3);
+        turn(c);
+        put_set(gA, c + 2);
+        __syncthreads();
+        if (c + 1 >= nch) break;
+        load_set(gA, c + 4);
+        turn(c + 1);
+        put_set(gB, c + 3);
         __syncthreads();
     }
     if (active) {
@@ -1434,7 +1455,7 @@ __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
 // W == 12 keeps the LDS prefilter (one workgroup per CU); smaller W runs
 // 12 / W workgroups per CU without it
 template <int W, uint32_t RB>
-__global__ __launch_bounds__(64 * W) void rs_walk_spec_coop_kernel(RsWalkArgs a) {
+__global__ __launch_bounds__(64 * W, (RB == 32768 ? 3 : 1)) void rs_walk_spec_coop_kernel(RsWalkArgs a) {
     constexpr bool kLds = W >= 12;
     __shared__ uint32_t lfilt[kLds ? kLdsFiltWordsW : 1];
     __shared__ __attribute__((aligned(16))) uint32_t ring[RB ? band_words<RB>() : 4];
