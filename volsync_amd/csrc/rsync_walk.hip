@@ -1152,6 +1152,8 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
         bool partial = false;            // the queue filled inside group (pA, pT1, pT2)
         uint64_t pA = 0;
         uint32_t pT1 = 0, pT2 = 0;
+        uint4 cwo, cwi;                  // this wave's batch bytes of group pfA
+        uint64_t pfA = ~0ull;
         for (;;) {
             // ---- fill the queue (until 4 W hits wait, or the scan has run a
             // block length past the first of them: a match, which ends the
@@ -1162,10 +1164,16 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
                 uint64_t tb = wclock(wp);
                 const uint64_t Aw = A + kBatch * wave;
                 const uint64_t c = Aw + 16 * (uint64_t)lane;
-                uint4 cwo, cwi;
-                batch_load(a, Aw, lane, cwo, cwi);
+                if (pfA != A) batch_load(a, Aw, lane, cwo, cwi);
                 const uint32_t wo[4] = {cwo.x, cwo.y, cwo.z, cwo.w};
                 const uint32_t wi[4] = {cwi.x, cwi.y, cwi.z, cwi.w};
+                // the next group's bytes, in flight while this one is tested
+                if ((int64_t)(A + kBatch * W) < fend) {
+                    batch_load(a, A + kBatch * W + kBatch * wave, lane, cwo, cwi);
+                    pfA = A + kBatch * W;
+                } else {
+                    pfA = ~0ull;
+                }
                 int Xo = 0, Xi = 0, Eo = 0, Ei = 0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
