@@ -926,21 +926,43 @@ struct CoopShared {
 };
 
 // Hash queued windows [j0, j1) (starts within band_spread<RB> of the first) from
-// the ring, window j0 + r on wave r / 4, row r % 4, and chain-scan them into
-// sh.wlo / whi / ci / cfa.  Every wave of the workgroup calls it (the ring
-// loads and barriers are shared); returns after a final barrier.
+// the ring and chain-scan them into sh.wlo / whi / ci / cfa.  XXH3's block
+// contributions are independent, so a turn's (window, block) pairs are spread
+// over all 4 W rows of the workgroup, whatever the number of windows; the
+// contributions go through LDS to one lane per (window, accumulator), which
+// runs the serial scramble chain.  The partial block, last stripe and merge
+// run on row j % 4 of wave j / 4 for window j.  Every wave of the workgroup
+// calls it (ring loads and barriers are shared); returns after a barrier.
+template <uint32_t RB>
+constexpr uint32_t band_contrib_words() { return 16 * (band_chunk<RB>() / 1024) * 8 * 2; }
+__device__ __forceinline__ uint64_t xxh3_init_acc(uint32_t k) {
+    using namespace vsstrong;
+    switch (k) {
+        case 0: return P32_3;
+        case 1: return P64_1;
+        case 2: return P64_2;
+        case 3: return P64_3;
+        case 4: return P64_4;
+        case 5: return P32_2;
+        case 6: return P64_5;
+        default: return P32_1;
+    }
+}
 template <int W, uint32_t RB>
 __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, uint32_t wave,
-                          uint32_t *ring, CoopShared<W> &sh, uint32_t j0, uint32_t j1, uint64_t L) {
+                          uint32_t *ring, uint64_t *contrib, CoopShared<W> &sh, uint32_t j0,
+                          uint32_t j1, uint64_t L) {
+    static_assert(W == 4, "band flushes hold at most 16 windows");
     constexpr uint32_t kChunk = band_chunk<RB>();
+    constexpr uint32_t kB = kChunk / 1024;           // blocks per turn
     constexpr uint32_t kT = 64 * W;                  // threads
-    constexpr uint32_t kG = (kChunk + 16) / 16;  // granules of one turn's new bytes (+ rounding)
+    constexpr uint32_t kRowsW = 4 * W;               // rows of the workgroup
+    constexpr uint32_t kG = (kChunk + 16) / 16;      // granules of one turn's new bytes (+ rounding)
     constexpr uint32_t kPer = (kG + kT - 1) / kT;
     const uint32_t nw = j1 - j0, tid = threadIdx.x;
     const uint64_t hf = uni64((uint64_t)sh.qoff[j0]), hl = uni64((uint64_t)sh.qoff[j1 - 1]);
-    const uint32_t r = 4 * wave + (lane >> 4);
-    const bool active = 4 * wave < nw;
-    const uint64_t h = (uint64_t)sh.qoff[j0 + (r < nw ? r : active ? 4 * wave : 0)];
+    const uint32_t q = lane & 15, sp = q >> 2, m = q & 3;
+    const uint32_t R = 4 * wave + (lane >> 4);       // this lane's row in the workgroup
     // the first two turns' bytes: [hf, hl + 2 chunk)
     {
         const uint64_t x0 = hf & ~15ull, x1 = min(hl + 2 * kChunk, a.dlen);
@@ -961,9 +983,8 @@ __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, 
     const uint32_t nch = (uint32_t)((L + kChunk - 1) / kChunk);
     const uint32_t nb = (uint32_t)((L - 1) / 1024);
     // turn k's new bytes [hl + chunk k, hl + chunk (k + 1)) (k >= 2) are
-    // loaded at the start of turn k - 2 and stored at the end of turn k - 1:
-    // a full turn of hashing covers the load latency.  Their ring slots are
-    // not read before turn k (hl - hf <= band_spread<RB>).
+    // loaded at the start of turn k - 2 and stored at the end of turn k - 1.
+    // Their ring slots are not read before turn k (hl - hf <= band_spread<RB>).
     auto load_set = [&](uint4 (&g)[kPer], uint32_t k) {
         if (k >= nch) return;
         const uint64_t gx0 = (hl + (uint64_t)kChunk * k) & ~15ull;
@@ -984,15 +1005,37 @@ __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, 
             if (x < gx1) band_put<RB>(ring, x, g[i]);
         }
     };
-    RowAcc st = row_acc_init(lane);
-    auto ld = [&](uint64_t off) { return ring16<RB>(ring, h + off); };
-    RowWin w{0, 0, 0};
-    auto turn = [&](uint32_t c) {
-        if (active) {
-            constexpr uint32_t kB = kChunk / 1024;   // blocks per turn
-            row_acc_blocks(st, rs, lane, ld, min(kB * c, nb), min(kB * c + kB, nb));
-            if (c + 1 == nch) w = row_acc_finish(st, a, rs, lane, ld, L);
+    // chain lanes: thread t < 8 nw holds accumulator t % 8 of window t / 8
+    const bool chn = tid < 8 * nw;
+    const uint32_t ck = tid & 7, cj = tid >> 3;
+    uint64_t A = xxh3_init_acc(ck);
+    const uint64_t csec = rs.w[16 + ck];
+    // one (window, block) contribution on this row: lanes q < 4 hold accumulators 2q, 2q + 1
+    auto pair = [&](uint32_t p, uint32_t b0, uint32_t nbt) {
+        const uint32_t j = p / nbt, b = b0 + p % nbt;
+        const uint64_t h = (uint64_t)sh.qoff[j0 + j] + (uint64_t)b * 1024 + 16 * q;
+        uint4 v[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) v[jj] = ring16<RB>(ring, h + 256 * jj);
+        uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+            acc16(v[jj], rs.w[4 * jj + sp + 2 * m], rs.w[4 * jj + sp + 2 * m + 1], c0, c1);
+        c0 = row_sum_sp(c0);
+        c1 = row_sum_sp(c1);
+        if (sp == 0) {
+            uint64_t *o = contrib + (j * kB + (b - b0)) * 8 + 2 * m;
+            o[0] = c0;
+            o[1] = c1;
         }
+    };
+    auto turn = [&](uint32_t c) {
+        const uint32_t b0 = min(kB * c, nb), nbt = min(kB * c + kB, nb) - b0;
+        const uint32_t P = nw * nbt;
+        for (uint32_t p = R; p < P; p += kRowsW) pair(p, b0, nbt);
+        __syncthreads();
+        if (chn)
+            for (uint32_t b = 0; b < nbt; ++b) A = scramble(A + contrib[(cj * kB + b) * 8 + ck], csec);
     };
     uint4 gA[kPer], gB[kPer];
     load_set(gA, 2);
@@ -1008,7 +1051,16 @@ __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, 
         put_set(gB, c + 3);
         __syncthreads();
     }
+    // the chained accumulators to the finishing rows
+    if (chn) contrib[cj * 8 + ck] = A;
+    __syncthreads();
+    const bool active = 4 * wave < nw;
     if (active) {
+        const uint32_t r = R < nw ? R : 4 * wave;
+        RowAcc st{contrib[r * 8 + 2 * m], contrib[r * 8 + 2 * m + 1]};
+        const uint64_t h = (uint64_t)sh.qoff[j0 + r];
+        auto ld = [&](uint64_t off) { return ring16<RB>(ring, h + off); };
+        const RowWin w = row_acc_finish(st, a, rs, lane, ld, L);
         for (uint32_t rr = 0; rr < 4 && 4 * wave + rr < nw; ++rr) {
             const uint32_t j = j0 + 4 * wave + rr;
             const uint32_t sv = uni(sh.qsum[j]);
@@ -1332,7 +1384,8 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
                     uint32_t j1 = j0 + 1;
                     while (j1 < nq && (int64_t)uni64((uint64_t)sh.qoff[j1]) - hf <= band_spread<RB>()) ++j1;
                     uint64_t tf = wclock(wp);
-                    band_hash<W, RB>(a, rs, lane, wave, ring, sh, j0, j1, L);
+                    band_hash<W, RB>(a, rs, lane, wave, ring, (uint64_t *)(ring + band_words<RB>()),
+                                     sh, j0, j1, L);
                     wadd(wp, kPrFlush, tf);
                     visit(j0, j1);
                     j0 = j1;
@@ -1466,7 +1519,7 @@ template <int W, uint32_t RB>
 __global__ __launch_bounds__(64 * W, (RB == 32768 ? 3 : 1)) void rs_walk_spec_coop_kernel(RsWalkArgs a) {
     constexpr bool kLds = W >= 12;
     __shared__ uint32_t lfilt[kLds ? kLdsFiltWordsW : 1];
-    __shared__ __attribute__((aligned(16))) uint32_t ring[RB ? band_words<RB>() : 4];
+    __shared__ __attribute__((aligned(16))) uint32_t ring[RB ? band_words<RB>() + band_contrib_words<RB>() : 4];
     __shared__ uint64_t lsec[24];
     __shared__ CoopShared<W> sh;
     load_secret(lsec, a.seed);
