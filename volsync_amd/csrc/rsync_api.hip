@@ -955,21 +955,23 @@ int walk_scan(vs_rsync *h) {
     if (wprof) {
         std::vector<uint64_t> pr(nprof);
         VS_TRY(h->stage.d2h(pr.data(), a.prof, nprof * 8, h->stream));
-        const char *names[5] = {"run", "step", "flush", "chain", "segment"};
-        double cyc[5] = {0}, cnt[5] = {0}, mx = 0;
+        const char *names[8] = {"run", "step", "flush", "chain", "segment",
+                                "band-fill", "band-pairs", "band-chain"};
+        double cyc[8] = {0}, cnt[8] = {0}, mx = 0;
         int waves = 0;
         for (size_t w = 0; w < nprof / 16; ++w) {
             if (!pr[w * 16 + 8 + 4]) continue;
             ++waves;
-            for (int i = 0; i < 5; ++i) {
+            for (int i = 0; i < 8; ++i) {
                 cyc[i] += (double)pr[w * 16 + i];
                 cnt[i] += (double)pr[w * 16 + 8 + i];
             }
             mx = std::max(mx, (double)pr[w * 16 + 4]);
         }
         fprintf(stderr, "walk prof: %d waves; per wave:", waves);
-        for (int i = 0; i < 5; ++i)
-            fprintf(stderr, " %s %.3g cyc / %.4g calls (%.3g cyc each);", names[i],
+        for (int i = 0; i < 8; ++i)
+            if (cnt[i] > 0)
+                fprintf(stderr, " %s %.3g cyc / %.4g calls (%.3g cyc each);", names[i],
                     cyc[i] / std::max(waves, 1), cnt[i] / std::max(waves, 1),
                     cyc[i] / std::max(cnt[i], 1.0));
         fprintf(stderr, " max segment-total %.3g cyc\n", mx);

@@ -232,7 +232,10 @@ __device__ __forceinline__ void acc16(const uint4 v, uint64_t k0s, uint64_t k1s,
 
 // Optional per-wave phase timing (a.prof != nullptr; VSGPU_WALK_PROF=1):
 // s_memtime cycles and counts per phase, summed into a.prof[wave * 16 + ...]
-enum : int { kPrRun = 0, kPrStep = 1, kPrFlush = 2, kPrChain = 3, kPrSeg = 4, kPrN = 5 };
+enum : int {
+    kPrRun = 0, kPrStep = 1, kPrFlush = 2, kPrChain = 3, kPrSeg = 4,
+    kPrBandFill = 5, kPrBandPairs = 6, kPrBandChain = 7, kPrN = 8
+};
 struct WProf {
     bool on;
     uint64_t cyc[kPrN], cnt[kPrN];
@@ -951,7 +954,7 @@ __device__ __forceinline__ uint64_t xxh3_init_acc(uint32_t k) {
 template <int W, uint32_t RB>
 __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, uint32_t wave,
                           uint32_t *ring, uint64_t *contrib, CoopShared<W> &sh, uint32_t j0,
-                          uint32_t j1, uint64_t L) {
+                          uint32_t j1, uint64_t L, WProf &wp) {
     static_assert(W == 4, "band flushes hold at most 16 windows");
     constexpr uint32_t kChunk = band_chunk<RB>();
     constexpr uint32_t kB = kChunk / 1024;           // blocks per turn
@@ -964,6 +967,7 @@ __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, 
     const uint32_t q = lane & 15, sp = q >> 2, m = q & 3;
     const uint32_t R = 4 * wave + (lane >> 4);       // this lane's row in the workgroup
     // the first two turns' bytes: [hf, hl + 2 chunk)
+    uint64_t tp = wclock(wp);
     {
         const uint64_t x0 = hf & ~15ull, x1 = min(hl + 2 * kChunk, a.dlen);
         for (uint64_t xb = x0 + 16ull * tid; xb < x1; xb += 16ull * kT * 8) {
@@ -1032,14 +1036,19 @@ __device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, 
     auto turn = [&](uint32_t c) {
         const uint32_t b0 = min(kB * c, nb), nbt = min(kB * c + kB, nb) - b0;
         const uint32_t P = nw * nbt;
+        uint64_t tt = wclock(wp);
         for (uint32_t p = R; p < P; p += kRowsW) pair(p, b0, nbt);
         __syncthreads();
+        wadd(wp, kPrBandPairs, tt);
+        tt = wclock(wp);
         if (chn)
             for (uint32_t b = 0; b < nbt; ++b) A = scramble(A + contrib[(cj * kB + b) * 8 + ck], csec);
+        wadd(wp, kPrBandChain, tt);
     };
     uint4 gA[kPer], gB[kPer];
     load_set(gA, 2);
     __syncthreads();
+    wadd(wp, kPrBandFill, tp);
     for (uint32_t c = 0; c < nch; c += 2) {
         load_set(gB, c + 3);
         turn(c);
@@ -1385,7 +1394,7 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
                     while (j1 < nq && (int64_t)uni64((uint64_t)sh.qoff[j1]) - hf <= band_spread<RB>()) ++j1;
                     uint64_t tf = wclock(wp);
                     band_hash<W, RB>(a, rs, lane, wave, ring, (uint64_t *)(ring + band_words<RB>()),
-                                     sh, j0, j1, L);
+                                     sh, j0, j1, L, wp);
                     wadd(wp, kPrFlush, tf);
                     visit(j0, j1);
                     j0 = j1;
