@@ -40,6 +40,17 @@ const (
 	// upstream chunker reads 512 KiB at a time; the GPU wants large batches
 	// (the library pipelines them internally: vs_cdc_set_batch_bytes).
 	readSize = 64 * MiB
+
+	// DefaultBatchBytes is the device batch of one Chunker: one read.
+	DefaultBatchBytes = readSize
+	// DefaultMaxPending bounds the stream bytes a Chunker holds for chunks
+	// not yet returned (Chunk.Data).  At the bound Next waits for the blob
+	// IDs of batches in flight instead of reading on, so a Chunker holds at
+	// most max(maxPending, 2*batch + 2*MaxSize) + readSize bytes of the
+	// stream plus its 64 MiB read buffer: 384 MiB with the defaults
+	// (INTEGRATION.md, "Host memory per Chunker").  restic runs
+	// FileReadConcurrency (2) Chunkers per mover.
+	DefaultMaxPending = 4 * DefaultBatchBytes
 )
 
 // Chunk is one content-defined chunk of the stream (chunker.go Chunk) plus
@@ -66,10 +77,11 @@ type Chunker struct {
 	bits     int
 	err      error // sticky open/reset error, reported by Next
 
-	pending []byte // bytes read but not yet returned as Chunk.Data
-	origin  uint   // stream offset of pending[0]
-	readBuf []byte
-	eof     bool // the reader is exhausted and the final feed was sent
+	pending    []byte // bytes read but not yet returned as Chunk.Data
+	maxPending int    // at or above it, Next waits for batches in flight
+	origin     uint   // stream offset of pending[0]
+	readBuf    []byte
+	eof        bool // the reader is exhausted and the final feed was sent
 }
 
 func lastErr() error { return errors.New(C.GoString(C.vs_last_error())) }
@@ -80,7 +92,7 @@ func New(rd io.Reader, pol Pol) *Chunker { return NewWithBoundaries(rd, pol, Min
 
 // NewWithBoundaries returns a Chunker with explicit chunk size limits.
 func NewWithBoundaries(rd io.Reader, pol Pol, min, max uint) *Chunker {
-	c := &Chunker{}
+	c := &Chunker{maxPending: DefaultMaxPending}
 	c.ResetWithBoundaries(rd, pol, min, max)
 	runtime.SetFinalizer(c, (*Chunker).Close)
 	return c
@@ -119,8 +131,16 @@ func (c *Chunker) configure() {
 	}
 	if rc < 0 {
 		c.err = lastErr()
+		return
+	}
+	if C.vs_cdc_set_batch_bytes(c.h, C.uint64_t(DefaultBatchBytes)) < 0 {
+		c.err = lastErr()
 	}
 }
+
+// SetMaxPending sets the bound on stream bytes held for chunks not yet
+// returned (DefaultMaxPending); smaller values trade throughput for memory.
+func (c *Chunker) SetMaxPending(bytes int) { c.maxPending = bytes }
 
 // fill reads the next piece of the stream and copies it into the library
 // (which never retains Go pointers: cgo pointer rules).
@@ -162,7 +182,15 @@ func (c *Chunker) Next(data []byte) (Chunk, error) {
 	var out C.vs_chunk
 	var n C.size_t
 	for {
-		rc := C.vs_cdc_next(c.h, &out, 1, &n)
+		// at the bound, wait for a batch in flight rather than read more; with
+		// none in flight the held bytes belong to batches whose cuts need more
+		// input, so the stream is fed anyway
+		var rc C.int
+		if len(c.pending) >= c.maxPending {
+			rc = C.vs_cdc_next_wait(c.h, &out, 1, &n)
+		} else {
+			rc = C.vs_cdc_next(c.h, &out, 1, &n)
+		}
 		if rc == C.VS_EOF {
 			return Chunk{}, io.EOF
 		}

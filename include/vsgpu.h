@@ -91,6 +91,13 @@ int vs_cdc_feed(vs_cdc *h, const void *buf, size_t n, int final);
  * Returns VS_OK with *n_out > 0, VS_OK with *n_out == 0 when more input is
  * needed, or VS_EOF once the final chunk has been returned (io.EOF). */
 int vs_cdc_next(vs_cdc *h, vs_chunk *out, size_t cap, size_t *n_out);
+/* vs_cdc_next for a caller that bounds the stream bytes it holds: with no
+ * chunk ready it waits for the oldest batch in flight (its blob IDs) instead
+ * of returning *n_out == 0; *n_out == 0 then means no batch is in flight and
+ * the stream needs more input.  Same chunks, same order as vs_cdc_next. */
+int vs_cdc_next_wait(vs_cdc *h, vs_chunk *out, size_t cap, size_t *n_out);
+/* batches whose cuts are selected and whose blob IDs are pending */
+int vs_cdc_inflight(vs_cdc *h, uint64_t *batches);
 void vs_cdc_close(vs_cdc *h);
 /* Streaming pipeline: fed bytes are copied to the device on a
  * copy stream (pinned caller memory by DMA, waited for before the call

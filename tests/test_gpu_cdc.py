@@ -73,6 +73,29 @@ def test_stream_chunker_vs_golden(gpu, path):
     assert got == G.expected(doc)
 
 
+def test_stream_chunker_bounded_hold(gpu):
+    """A Chunker with a bound on held stream bytes (vs_cdc_next_wait, ADVICE r02:
+    the Go binding's per-Chunker memory): same chunks as the oracle, and the
+    bytes held never pass max(bound, 2 batches + 2 MaxSize) + one read."""
+    from volsync_amd import EOF, New
+    n = 160 << 20
+    data = O.synth(7, 0, n)
+    read, batch, bound = 4 << 20, 16 << 20, 20 << 20
+    ck = New(io.BytesIO(data.tobytes()), P.TEST_POL, read_size=read, batch_bytes=batch,
+             max_pending=bound)
+    got = []
+    while True:
+        try:
+            c = ck.Next()
+        except EOF:
+            break
+        got.append((c.Start, c.Length, c.Cut, c.ID.hex()))
+    held = ck.max_held
+    ck.close()
+    assert got == O.cdc_hash(data, P.TEST_POL, MIN, MAX, 20)
+    assert held <= max(bound, 2 * batch + 2 * MAX + (1 << 20)) + read, held
+
+
 def test_stream_pol_zero_error(gpu):
     import volsync_amd
     ck = volsync_amd.New(io.BytesIO(b"abc"), 0)

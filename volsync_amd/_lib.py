@@ -91,6 +91,8 @@ def _load() -> ctypes.CDLL:
         "vs_cdc_reset": (c_int, [vp, c_u64, c_u32, c_u32, c_u32]),
         "vs_cdc_feed": (c_int, [vp, vp, c_size, c_int]),
         "vs_cdc_next": (c_int, [vp, ctypes.POINTER(VsChunk), c_size, ctypes.POINTER(c_size)]),
+        "vs_cdc_next_wait": (c_int, [vp, ctypes.POINTER(VsChunk), c_size, ctypes.POINTER(c_size)]),
+        "vs_cdc_inflight": (c_int, [vp, ctypes.POINTER(c_u64)]),
         "vs_cdc_close": (None, [vp]),
         "vs_cdc_set_batch_bytes": (c_int, [vp, c_u64]),
         "vs_cdc_stream_stats": (c_int, [vp, ctypes.POINTER(ctypes.c_double)]),

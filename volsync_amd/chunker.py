@@ -76,11 +76,18 @@ class Chunker:
     on the GPU.  Not goroutine-/thread-safe (same contract as the Go type)."""
 
     def __init__(self, rd, pol: int, min_size: int = MinSize, max_size: int = MaxSize,
-                 device: int = 0, read_size: int = 64 * MiB, batch_bytes: int = 256 * MiB):
+                 device: int = 0, read_size: int = 64 * MiB, batch_bytes: int = 256 * MiB,
+                 max_pending: Optional[int] = None):
+        """max_pending bounds the stream bytes held for chunks not yet returned
+        (Chunk.Data): at or above it, Next waits for batches in flight instead
+        of reading more (vs_cdc_next_wait).  None = 4 batches.  The bytes held
+        never exceed max(max_pending, 2 * batch + 2 * MaxSize) + read_size."""
         self._h = ctypes.c_void_p()
         self._device = device
         self._read_size = read_size
         self._batch_bytes = batch_bytes
+        self._max_pending = 4 * batch_bytes if max_pending is None else int(max_pending)
+        self.max_held = 0          # high-water mark of the bytes held (tests)
         self._avg_bits = AverageBits
         self.ResetWithBoundaries(rd, pol, min_size, max_size)
 
@@ -110,7 +117,11 @@ class Chunker:
         one = (VsChunk * 1)()
         n = ctypes.c_size_t(0)
         while True:
-            rc = lib.vs_cdc_next(self._h, one, 1, ctypes.byref(n))
+            # at the bound, wait for a batch in flight rather than read more;
+            # with none in flight the bytes held belong to batches whose cuts
+            # need more input, so the stream must be fed anyway
+            nxt = lib.vs_cdc_next_wait if len(self._buf) >= self._max_pending else lib.vs_cdc_next
+            rc = nxt(self._h, one, 1, ctypes.byref(n))
             if rc == _lib.VS_EOF:
                 raise EOF()
             check(rc)
@@ -168,6 +179,7 @@ class Chunker:
             return
         block = bytes(block)
         self._buf += block
+        self.max_held = max(self.max_held, len(self._buf))
         buf = ctypes.create_string_buffer(block, len(block))
         check(lib.vs_cdc_feed(self._h, buf, len(block), 0))
 

@@ -1042,13 +1042,15 @@ VS_API int vs_cdc_feed(vs_cdc *h, const void *buf, size_t n, int final) {
     return 0;
 }
 
-VS_API int vs_cdc_next(vs_cdc *h, vs_chunk *out, size_t cap, size_t *n_out) {
+// wait_any: with no chunk ready, wait for the oldest batch in flight instead of
+// asking for more input (the caller's bound on bytes held, vs_cdc_next_wait)
+static int cdc_next(vs_cdc *h, vs_chunk *out, size_t cap, size_t *n_out, bool wait_any) {
     if (!h || (!out && cap)) return fail(VS_ERR_ARG, "bad arguments");
     if (n_out) *n_out = 0;
     if (h->streaming) {
         VS_TRY(set_dev(h));
         // after the final feed nothing else will advance the stream: wait
-        VS_TRY(collect_ready(h, h->ready.empty() && h->final_fed));
+        VS_TRY(collect_ready(h, h->ready.empty() && (h->final_fed || wait_any)));
     }
     size_t k = 0;
     while (k < cap && !h->ready.empty()) {
@@ -1057,6 +1059,20 @@ VS_API int vs_cdc_next(vs_cdc *h, vs_chunk *out, size_t cap, size_t *n_out) {
     }
     if (n_out) *n_out = k;
     if (k == 0 && h->final_fed && h->spend.empty()) return VS_EOF;
+    return 0;
+}
+
+VS_API int vs_cdc_next(vs_cdc *h, vs_chunk *out, size_t cap, size_t *n_out) {
+    return cdc_next(h, out, cap, n_out, false);
+}
+
+VS_API int vs_cdc_next_wait(vs_cdc *h, vs_chunk *out, size_t cap, size_t *n_out) {
+    return cdc_next(h, out, cap, n_out, true);
+}
+
+VS_API int vs_cdc_inflight(vs_cdc *h, uint64_t *batches) {
+    if (!h || !batches) return fail(VS_ERR_ARG, "bad arguments");
+    *batches = h->spend.size();
     return 0;
 }
 
