@@ -934,7 +934,8 @@ int walk_scan(vs_rsync *h) {
     VS_HIP(hipMemsetAsync(a.flags, 0, 4, h->stream));
     // VSGPU_WALK_PROF=1: per-wave phase cycles of the speculative pass on stderr
     static const bool wprof = getenv("VSGPU_WALK_PROF") != nullptr;
-    const size_t nprof = (size_t)std::max(h->cus, 1) * 64 * 16;
+    constexpr int kPh = 16;   // phases (rsync_walk.hip kPrN): cycles, then counts
+    const size_t nprof = (size_t)std::max(h->cus, 1) * 64 * 2 * kPh;
     if (wprof) {
         VS_TRY(h->w_prof.ensure(nprof * 8));
         VS_HIP(hipMemsetAsync(h->w_prof.p, 0, nprof * 8, h->stream));
@@ -955,21 +956,23 @@ int walk_scan(vs_rsync *h) {
     if (wprof) {
         std::vector<uint64_t> pr(nprof);
         VS_TRY(h->stage.d2h(pr.data(), a.prof, nprof * 8, h->stream));
-        const char *names[8] = {"run", "step", "flush", "chain", "segment",
-                                "band-fill", "band-pairs", "band-chain"};
-        double cyc[8] = {0}, cnt[8] = {0}, mx = 0;
+        const char *names[kPh] = {"run", "step", "flush", "chain", "segment", "band-fill",
+                                  "band-pairs", "band-chain", "step:sums", "step:lds",
+                                  "step:gather", "step:probe", "step:queue", "", "", ""};
+        double cyc[kPh] = {0}, cnt[kPh] = {0}, mx = 0;
         int waves = 0;
-        for (size_t w = 0; w < nprof / 16; ++w) {
-            if (!pr[w * 16 + 8 + 4]) continue;
+        for (size_t w = 0; w < nprof / (2 * kPh); ++w) {
+            const uint64_t *q = &pr[w * 2 * kPh];
+            if (!q[kPh + 4]) continue;
             ++waves;
-            for (int i = 0; i < 8; ++i) {
-                cyc[i] += (double)pr[w * 16 + i];
-                cnt[i] += (double)pr[w * 16 + 8 + i];
+            for (int i = 0; i < kPh; ++i) {
+                cyc[i] += (double)q[i];
+                cnt[i] += (double)q[kPh + i];
             }
-            mx = std::max(mx, (double)pr[w * 16 + 4]);
+            mx = std::max(mx, (double)q[4]);
         }
         fprintf(stderr, "walk prof: %d waves; per wave:", waves);
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < kPh; ++i)
             if (cnt[i] > 0)
                 fprintf(stderr, " %s %.3g cyc / %.4g calls (%.3g cyc each);", names[i],
                     cyc[i] / std::max(waves, 1), cnt[i] / std::max(waves, 1),

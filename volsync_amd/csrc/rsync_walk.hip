@@ -234,7 +234,11 @@ __device__ __forceinline__ void acc16(const uint4 v, uint64_t k0s, uint64_t k1s,
 // s_memtime cycles and counts per phase, summed into a.prof[wave * 16 + ...]
 enum : int {
     kPrRun = 0, kPrStep = 1, kPrFlush = 2, kPrChain = 3, kPrSeg = 4,
-    kPrBandFill = 5, kPrBandPairs = 6, kPrBandChain = 7, kPrN = 8
+    kPrBandFill = 5, kPrBandPairs = 6, kPrBandChain = 7,
+    // the wave walk's STEP batch, split: sums, LDS prefilter, blocked-filter
+    // gathers, directory probes, queueing
+    kPrStepSums = 8, kPrStepLds = 9, kPrStepGather = 10, kPrStepProbe = 11, kPrStepQueue = 12,
+    kPrN = 16
 };
 struct WProf {
     bool on;
@@ -260,7 +264,7 @@ struct RowWin {
 // Every window is a full one inside the readable data.  Restates
 // vsstrong::xxh3_long + merge and get_checksum1 (rsync.hip weak_sum); tests
 // compare both with the C oracle / libxxhash.
-template <bool WEAK>
+template <bool WEAK, uint32_t RING = kRing>
 __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, uint64_t o,
                               uint64_t len, uint32_t lock = 0) {
     using namespace vsstrong;
@@ -287,20 +291,24 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = ldu16(p + (uint64_t)b * 1024 + 256 * j);
     };
-    // full blocks through a ring of kRing blocks in flight; with `lock`, every
-    // wave of the workgroup re-syncs every `lock` blocks (rows_window_idle
-    // holds the same barriers), so a cooperative flush's overlapping windows
-    // move through their bytes together and share them in L1 / L2
-    uint4 r0[4], r1[4];
-    if (nb > 0) load(r0, 0);
-    if (nb > 1) load(r1, 1);
-    for (uint32_t b = 0; b < nb; b += kRing) {
+    // full blocks through a ring of RING blocks in flight; with `lock` (RING
+    // == kRing only), every wave of the workgroup re-syncs every `lock` blocks
+    // (rows_window_idle holds the same barriers), so a cooperative flush's
+    // overlapping windows move through their bytes together and share them in
+    // L1 / L2
+    static_assert(RING >= 2, "at least two blocks in flight");
+    uint4 ring[RING][4];
+#pragma unroll
+    for (uint32_t k = 0; k < RING; ++k)
+        if (k < nb) load(ring[k], k);
+    for (uint32_t b = 0; b < nb; b += RING) {
         if (lock && b && b % lock == 0) __syncthreads();
-        block(r0, b);
-        if (b + 2 < nb) load(r0, b + 2);
-        if (b + 1 >= nb) break;
-        block(r1, b + 1);
-        if (b + 3 < nb) load(r1, b + 3);
+#pragma unroll
+        for (uint32_t k = 0; k < RING; ++k) {
+            if (b + k >= nb) break;
+            block(ring[k], b + k);
+            if (b + k + RING < nb) load(ring[k], b + k + RING);
+        }
     }
     // the partial block: ns stripes, no scramble
     const uint32_t ns = (uint32_t)(((len - 1) - (uint64_t)nb * 1024) / 64);
@@ -518,6 +526,7 @@ __device__ __forceinline__ int64_t by_row(int64_t v, uint32_t lane, uint32_t nv)
 //         kRows at a time (rows), then visited in order.
 // Only visited windows count: a speculative window the walk does not reach
 // is dropped, so matches and false alarms are hash_search's.
+template <uint32_t RING>
 __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const uint32_t *lfilt,
                                   uint32_t lane, int64_t o, int32_t want, int64_t stop,
                                   int64_t *out_off, int32_t *out_idx, int64_t *out_fab,
@@ -572,7 +581,7 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
             const uint32_t k = ahead ? (uint32_t)min<int64_t>(kRows, room) : 1u;
             const int64_t orow = o + (int64_t)L * (int64_t)(row < k ? row : 0);
             uint64_t t0 = wclock(wp);
-            const RowWin w = rows_window<true>(a, rs, lane, (uint64_t)orow, L);
+            const RowWin w = rows_window<true, RING>(a, rs, lane, (uint64_t)orow, L);
             wadd(wp, kPrRun, t0);
             for (uint32_t j = 0; j < k; ++j) {
                 const int64_t oj = o;
@@ -661,6 +670,8 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
             // and the directory only for the few offsets that pass both
             // all 16 reads of each stage are issued before any is consumed
             // (one LDS and one L2 round trip per batch, not 16 of each)
+            wadd(wp, kPrStepSums, tb);
+            uint64_t tsub = wclock(wp);
             uint32_t hit = valid;
             if (a.lbits) {
                 uint32_t lw[16];
@@ -672,6 +683,8 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                     lh |= ((lw[t] >> ((sums[t] >> (32 - a.lbits)) & 31)) & 1u) << t;
                 hit &= lh;
             }
+            wadd(wp, kPrStepLds, tsub);
+            tsub = wclock(wp);
             {
                 uint64_t fw[16];
 #pragma unroll
@@ -687,6 +700,8 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 }
                 hit &= pass;
             }
+            wadd(wp, kPrStepGather, tsub);
+            tsub = wclock(wp);
             for (uint32_t mm = hit; mm;) {
                 const int t = __builtin_ctz(mm);
                 mm &= mm - 1;
@@ -695,6 +710,8 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
                 if (!probe_full(a, st)) hit &= ~(1u << t);
             }
+            wadd(wp, kPrStepProbe, tsub);
+            tsub = wclock(wp);
             // queue the hits in offset order (lane order, then bit order)
             uint64_t lanes = __ballot(hit != 0);
             WPROG(a, lane, 5, (int64_t)A, lanes);
@@ -715,6 +732,7 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 if (lane == hl) hit &= hit - 1;
                 lanes = __ballot(hit != 0);
             }
+            wadd(wp, kPrStepQueue, tsub);
             wadd(wp, kPrStep, tb);
             const bool more = lanes != 0;              // hits of this batch not yet queued
             const uint64_t nx = A + kBatch;
@@ -723,7 +741,7 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 // hash the queued windows together, visit them in order
                 const int64_t orow = by_row(qh, lane, nq);
                 uint64_t tf = wclock(wp);
-                const RowWin w = rows_window<false>(a, rs, lane, (uint64_t)orow, L);
+                const RowWin w = rows_window<false, RING>(a, rs, lane, (uint64_t)orow, L);
                 wadd(wp, kPrFlush, tf);
                 int64_t hlast = 0;
                 for (uint32_t j = 0; j < nq; ++j) {
@@ -1477,7 +1495,7 @@ __device__ __forceinline__ int64_t seg_hi(const RsWalkArgs &a, uint32_t k) {
 // speculative walk of every segment from its own start (segment 0 from the
 // range's speculative entry a.e0 / a.w0; the others with want_i "no
 // preference" = count)
-template <uint32_t T>
+template <uint32_t T, uint32_t RING>
 __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
     __shared__ uint32_t lfilt[kLdsFiltWordsW];
     __shared__ uint64_t lsec[24];
@@ -1492,8 +1510,9 @@ __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
         const int64_t e = (int64_t)uni64((uint64_t)(k ? seg_lo(a, k) : a.e0));
         const int32_t w = unis(k ? (int32_t)a.count : a.w0);
         const uint64_t base = (uint64_t)k * a.cap;
-        const SegResult r = walk_segment(a, rs, lfilt, lane, e, w, seg_hi(a, k), a.spec_off + base,
-                                         a.spec_idx + base, a.spec_fab + base, a.cap, nullptr, wp);
+        const SegResult r = walk_segment<RING>(a, rs, lfilt, lane, e, w, seg_hi(a, k),
+                                               a.spec_off + base, a.spec_idx + base,
+                                               a.spec_fab + base, a.cap, nullptr, wp);
         wadd(wp, kPrSeg, ts);
         if (lane == 0) {
             a.spec_n[k] = r.n;
@@ -1512,10 +1531,10 @@ __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
         WPROG(a, lane, 10, k, r.n);
     }
     if (wp.on && lane == 0) {
-        uint64_t *pr = a.prof + (uint64_t)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 16;
+        uint64_t *pr = a.prof + (uint64_t)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 2 * kPrN;
         for (int i = 0; i < kPrN; ++i) {
             pr[i] = wp.cyc[i];
-            pr[8 + i] = wp.cnt[i];
+            pr[kPrN + i] = wp.cnt[i];
         }
     }
     WPROG(a, lane, 12, 0, 0);
@@ -1573,10 +1592,10 @@ __global__ __launch_bounds__(64 * W, (RB == 32768 ? 3 : 1)) void rs_walk_spec_co
         }
     }
     if (wp.on && lane == 0) {
-        uint64_t *pr = a.prof + (uint64_t)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 16;
+        uint64_t *pr = a.prof + (uint64_t)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 2 * kPrN;
         for (int i = 0; i < kPrN; ++i) {
             pr[i] = wp.cyc[i];
-            pr[8 + i] = wp.cnt[i];
+            pr[kPrN + i] = wp.cnt[i];
         }
     }
 }
@@ -1613,8 +1632,8 @@ __global__ __launch_bounds__(kWalkThreads) void rs_walk_stitch_kernel(RsWalkArgs
             // back to the speculative entry
             r = SegResult{0, 0, sv.fa, sv.exit_off, sv.exit_want};
         } else {
-            r = walk_segment(a, rs, lfilt, lane, e, w, seg_hi(a, k), a.fin_off + base,
-                             a.fin_idx + base, a.fin_fab + base, a.cap, &sv, wp);
+            r = walk_segment<kRing>(a, rs, lfilt, lane, e, w, seg_hi(a, k), a.fin_off + base,
+                                    a.fin_idx + base, a.fin_fab + base, a.cap, &sv, wp);
         }
         if (lane == 0) {
             a.fin_entry[k] = e;
@@ -1650,14 +1669,20 @@ __global__ void rs_pad_sum2_kernel(const uint8_t *sum2, uint32_t count, uint32_t
 hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t s) {
     if (!a.nseg) return hipSuccess;
     if (a.lbits > 20) return hipErrorInvalidValue;
-    // VSGPU_WALK_WG=1024: the speculative pass at 16 waves per CU (128
-    // VGPRs, some spilled) instead of 12 (160 VGPRs); 512 / 256: 8 / 4 waves
-    // per CU (fewer walks in flight, a smaller re-fetched working set) --
-    // A/B knobs
+    // The speculative pass runs 8 waves per CU with four blocks of each window
+    // hash in flight per lane (196 VGPRs; the stitch passes keep 12 waves):
+    // one rank of the real C4 772-778 -> 799-800 GB/s, the 64 GiB shape
+    // 2011 -> 2021 (profiles/r03_walk_ring).  A/B knobs: VSGPU_WALK_WG=768 /
+    // 1024 / 256 (12 waves with two blocks in flight; 16 waves, spills; 4
+    // waves), VSGPU_WALK_RING=2 (8 waves, two blocks in flight)
     static const uint32_t spec_threads = [] {
         const char *e = getenv("VSGPU_WALK_WG");
         const int v = e ? atoi(e) : 0;
-        return (v == 1024 || v == 512 || v == 256) ? (uint32_t)v : kWalkThreads;
+        return (v == 1024 || v == 768 || v == 256) ? (uint32_t)v : 512u;
+    }();
+    static const bool ring4 = [] {
+        const char *e = getenv("VSGPU_WALK_RING");
+        return !(e && atoi(e) == 2);
     }();
     // VSGPU_WALK_COOP=W (4, 6 or 12; 0 = off): the speculative pass with
     // W-wave cooperative walks (walk_segment_coop)
@@ -1695,13 +1720,15 @@ hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t
     if (stitch)
         rs_walk_stitch_kernel<<<(uint32_t)grid, kWalkThreads, 0, s>>>(a);
     else if (threads == 1024)
-        rs_walk_spec_kernel<1024><<<(uint32_t)grid, 1024, 0, s>>>(a);
+        rs_walk_spec_kernel<1024, kRing><<<(uint32_t)grid, 1024, 0, s>>>(a);
+    else if (threads == 512 && ring4)
+        rs_walk_spec_kernel<512, 4><<<(uint32_t)grid, 512, 0, s>>>(a);
     else if (threads == 512)
-        rs_walk_spec_kernel<512><<<(uint32_t)grid, 512, 0, s>>>(a);
+        rs_walk_spec_kernel<512, kRing><<<(uint32_t)grid, 512, 0, s>>>(a);
     else if (threads == 256)
-        rs_walk_spec_kernel<256><<<(uint32_t)grid, 256, 0, s>>>(a);
+        rs_walk_spec_kernel<256, kRing><<<(uint32_t)grid, 256, 0, s>>>(a);
     else
-        rs_walk_spec_kernel<kWalkThreads><<<(uint32_t)grid, kWalkThreads, 0, s>>>(a);
+        rs_walk_spec_kernel<kWalkThreads, kRing><<<(uint32_t)grid, kWalkThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 
