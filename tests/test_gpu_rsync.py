@@ -124,6 +124,29 @@ def test_weak_collisions_and_false_alarms(gpu):
         assert st["false_alarms"] == fa
 
 
+@pytest.mark.parametrize("bbits", ["2", "10"])
+def test_membership_bucket_overflow_fallback(gpu, monkeypatch, bbits):
+    """The walk's membership buckets (one 64-byte load per probe) with so few
+    buckets that most overflow their 15 slots: the probe falls back to the
+    directory and the match list and false alarms stay hash_search's."""
+    from volsync_amd import Matcher, SumStruct
+    monkeypatch.setenv("VSGPU_RS_BBITS", bbits)
+    n, csum, seed = 24 << 20, R.CSUM_XXH3_128, 0x5EED5EED
+    basis = O.synth(31, 0, n)
+    bl, s2l, cnt, rem = O.rsync_sizes(n, 2048)
+    src = R.mutate(basis, bl, seed=3, frac=0.2)
+    c1, c2 = O.rsync_signatures(basis, bl, s2l, csum, seed)
+    want, fa = O.rsync_match(src, c1, c2, bl, rem, csum, seed)
+    ds = to_dev(src)
+    m = Matcher()
+    m.load_sums(SumStruct(0, cnt, bl, s2l, rem, c1, c2), csum, seed)
+    got = m.match_sums(ds.data_ptr(), len(src))
+    st = m.stats()
+    m.close()
+    assert cnt > 10000   # 2^10 buckets: ~12 sums each, a fifth of them overflowing
+    assert got == want and st["false_alarms"] == fa
+
+
 def test_repeated_blocks_prefer_adjacent(gpu):
     """Identical blocks: rsync's chain offers the highest index first and the
     want_i rule then prefers the block after the previous match."""

@@ -354,6 +354,19 @@ __host__ __device__ inline uint64_t rs_bloom_mask(uint32_t sum1) {
     for (int j = 0; j < VS_BLOOM_K; ++j) m |= 1ull << ((sum1 >> (6 * j)) & 63);
     return m;
 }
+// Membership buckets for the walk's probe ("is there a full-length block with
+// sum1 == s?"): 2^bbits buckets of 64 bytes -- a count, then up to 15 distinct
+// sums -- so a probe is one 64-byte load instead of the directory + sorted-key
+// round trips; a bucket whose count passed 15 falls back to those.
+constexpr uint32_t kBucketSlots = 15;
+__host__ __device__ inline uint32_t rs_bucket(uint32_t sum1, uint32_t bbits) {
+    return (sum1 * 0x85EBCA77u) >> (32 - bbits);
+}
+__host__ __device__ inline uint32_t rs_bucket_bits(uint32_t count) {
+    uint32_t lc = 0;
+    while ((1ull << lc) < (uint64_t)(count ? count : 1)) ++lc;
+    return lc < 6 ? 4 : lc - 2;   // ~4 distinct sums per bucket
+}
 // layout: filter [2^fbits bits], LDS prefilter [2^lbits bits], blocked filter [2^fbits bits]
 inline size_t rs_filter_bytes(uint32_t fbits) {
     return 2 * (((size_t)1 << fbits) / 8) + (((size_t)1 << rs_lds_filter_bits(fbits)) / 8);
@@ -386,6 +399,8 @@ struct RsWalkArgs {
     const uint32_t *dir;
     const uint32_t *filt, *filt_l;
     const uint64_t *filt_b;          // blocked filter (rs_bloom_word / rs_bloom_mask)
+    const uint32_t *bkt;             // membership buckets (rs_bucket): count, 15 sums
+    uint32_t bbits;
     uint32_t dbits, fbits, lbits;
     int64_t e0;                      // segment 0's entry (offset, want_i)
     int32_t w0;
@@ -419,6 +434,11 @@ struct RsWalkArgs {
     uint32_t lock;                   // cooperative walk: flush rows re-sync every `lock` blocks (0: never)
 };
 hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t s);
+// fill the membership buckets (zeroed by the caller) from the sorted keys:
+// each distinct sum1 of a full-length block once (the short final block,
+// index count-1 when remainder != 0, is left out)
+hipError_t launch_rs_buckets(const uint64_t *tkey, uint32_t count, uint32_t remainder,
+                             uint32_t bbits, uint32_t *bkt, hipStream_t s);
 // the final walks' match list in order as 16-byte vs_match records (offset,
 // block index, 0): cnt [nseg], pos [nseg + 1] (pos[nseg] = length),
 // partials >= nseg / 4096 + 2, out >= nseg * cap records; *fa_total = the

@@ -418,6 +418,36 @@ hipError_t launch_rs_table(const uint32_t *sum1, uint32_t count, uint64_t *keys,
     return hipGetLastError();
 }
 
+// the key at sorted position p is a full-length block
+__device__ __forceinline__ bool rs_key_full(uint64_t key, uint32_t count, uint32_t remainder) {
+    return !(remainder && ~(uint32_t)key == count - 1);
+}
+
+__global__ void rs_bucket_kernel(const uint64_t *tkey, uint32_t count, uint32_t remainder,
+                                 uint32_t bbits, uint32_t *bkt) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= count) return;
+    const uint64_t k = tkey[p];
+    if (!rs_key_full(k, count, remainder)) return;
+    const uint32_t s = (uint32_t)(k >> 32);
+    // the first full-length key of its sum's run: the run is sorted by
+    // descending index, so the short block (the largest index) leads it
+    if (p > 0 && (uint32_t)(tkey[p - 1] >> 32) == s) {
+        const bool prev_full = rs_key_full(tkey[p - 1], count, remainder);
+        if (prev_full || (p > 1 && (uint32_t)(tkey[p - 2] >> 32) == s)) return;
+    }
+    uint32_t *b = bkt + (uint64_t)rs_bucket(s, bbits) * 16;
+    const uint32_t slot = atomicAdd(&b[0], 1u);
+    if (slot < kBucketSlots) b[1 + slot] = s;
+}
+
+hipError_t launch_rs_buckets(const uint64_t *tkey, uint32_t count, uint32_t remainder,
+                             uint32_t bbits, uint32_t *bkt, hipStream_t s) {
+    if (!count) return hipSuccess;
+    rs_bucket_kernel<<<(count + 255) / 256, 256, 0, s>>>(tkey, count, remainder, bbits, bkt);
+    return hipGetLastError();
+}
+
 size_t rs_sort_tmp_bytes(uint64_t n_keys, bool pairs) {
     size_t b = 0;
     if (pairs)

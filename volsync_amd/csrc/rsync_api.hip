@@ -96,7 +96,7 @@ struct vs_rsync {
     int32_t count = 0, blength = 0, s2length = 0, remainder = 0;
     int csum_type = 0;
     uint32_t seed = 0;
-    uint32_t dbits = 0, fbits = 0;
+    uint32_t dbits = 0, fbits = 0, bbits = 0;
     // host copies for the host walk and the short-last-block tail, fetched
     // from the device table only when one of them runs (host_tables)
     bool host_ok = false;
@@ -104,7 +104,7 @@ struct vs_rsync {
     std::vector<uint8_t> sum2;
     std::vector<uint64_t> tkey_h;   // sorted (sum1 << 32 | ~i)
     std::vector<uint32_t> dir_h;
-    DevBuf d_sum1, d_keys, d_tkey, d_dir, d_filt, d_tmp;
+    DevBuf d_sum1, d_keys, d_tkey, d_dir, d_filt, d_tmp, d_bkt;
     DevBuf d_sum2p, d_sum2tmp;      // zero-padded 16-byte strong sums (device walk)
     // device walk: per-segment results and two exit buffers
     DevBuf w_spec_off, w_spec_idx, w_spec_fab, w_spec_n, w_spec_fa, w_spec_exit, w_spec_exitw;
@@ -271,6 +271,17 @@ int build_table(vs_rsync *h) {
                            h->d_tkey.as<uint64_t>(), h->d_tmp.p, h->d_tmp.cap, h->dbits,
                            h->d_dir.as<uint32_t>(), h->fbits, h->d_filt.as<uint32_t>(),
                            h->stream));
+    h->bbits = rs_bucket_bits(count);
+    {   // VSGPU_RS_BBITS=k (tests, read per load): 2^k buckets, so that small
+        // tables overflow buckets and exercise the directory fallback
+        const char *e = getenv("VSGPU_RS_BBITS");
+        const int v = e ? atoi(e) : 0;
+        if (v >= 1 && v <= 26) h->bbits = (uint32_t)v;
+    }
+    VS_TRY(h->d_bkt.ensure((64ull << h->bbits)));
+    VS_HIP(hipMemsetAsync(h->d_bkt.p, 0, 64ull << h->bbits, h->stream));
+    VS_HIP(launch_rs_buckets(h->d_tkey.as<uint64_t>(), count, (uint32_t)h->remainder, h->bbits,
+                             h->d_bkt.as<uint32_t>(), h->stream));
     VS_HIP(hipStreamSynchronize(h->stream));
     h->host_ok = false;
     h->loaded = true;
@@ -861,6 +872,8 @@ int walk_scan(vs_rsync *h) {
     a.sum1 = h->d_sum1.as<uint32_t>();
     a.tkey = h->d_tkey.as<uint64_t>();
     a.dir = h->d_dir.as<uint32_t>();
+    a.bkt = h->d_bkt.as<uint32_t>();
+    a.bbits = h->bbits;
     a.filt = h->d_filt.as<uint32_t>();
     a.fbits = h->fbits;
     a.dbits = h->dbits;
@@ -1374,7 +1387,7 @@ VS_API void vs_rsync_close(vs_rsync *h) {
     (void)hipSetDevice(h->device);
     for (FsJob &j : h->fs) fs_release(j);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    for (DevBuf *b : {&h->d_sum1, &h->d_keys, &h->d_tkey, &h->d_dir, &h->d_filt, &h->d_tmp, &h->px,
+    for (DevBuf *b : {&h->d_sum1, &h->d_keys, &h->d_tkey, &h->d_dir, &h->d_filt, &h->d_tmp, &h->d_bkt, &h->px,
                       &h->pt, &h->pxs, &h->pts, &h->partials, &h->c_off, &h->c_sum, &h->c_off2,
                       &h->c_sum2, &h->n_cand, &h->sort_tmp, &h->v_off, &h->v_len, &h->v_out,
                       &h->d_flag, &h->d_sum2p, &h->d_sum2tmp, &h->w_spec_off, &h->w_spec_idx,

@@ -463,6 +463,21 @@ __device__ __forceinline__ bool probe_full(const RsWalkArgs &a, uint32_t sum) {
     return false;
 }
 
+// probe_full through the membership buckets: one 64-byte load (four 16-byte
+// pieces of one line), the directory walk only for an overflowed bucket
+__device__ __forceinline__ bool probe_bucket(const RsWalkArgs &a, uint32_t sum) {
+    const uint4 *b = (const uint4 *)(a.bkt + (uint64_t)rs_bucket(sum, a.bbits) * 16);
+    const uint4 v0 = b[0], v1 = b[1], v2 = b[2], v3 = b[3];
+    const uint32_t w[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                            v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
+    const uint32_t n = w[0];
+    if (n > kBucketSlots) return probe_full(a, sum);
+    bool hit = false;
+#pragma unroll
+    for (uint32_t i = 0; i < kBucketSlots; ++i) hit |= (i < n) & (w[1 + i] == sum);
+    return hit;
+}
+
 __device__ __forceinline__ int32_t sbyte(const uint8_t *d, uint64_t p) {
     return (int32_t)(int8_t)d[p];
 }
@@ -708,7 +723,7 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 uint32_t st = sums[0];
 #pragma unroll
                 for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
-                if (!probe_full(a, st)) hit &= ~(1u << t);
+                if (!probe_bucket(a, st)) hit &= ~(1u << t);
             }
             wadd(wp, kPrStepProbe, tsub);
             tsub = wclock(wp);
@@ -1330,7 +1345,7 @@ __device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, co
                     uint32_t st = sums[0];
 #pragma unroll
                     for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
-                    if (!probe_full(a, st)) hit &= ~(1u << t);
+                    if (!probe_bucket(a, st)) hit &= ~(1u << t);
                 }
                 // the group's hits in offset order (wave, lane, bit), queued at nq + rank
                 const uint32_t pc = (uint32_t)__builtin_popcount(hit);
