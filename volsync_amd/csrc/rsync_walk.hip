@@ -439,6 +439,31 @@ __device__ int32_t chain_scan(const RsWalkArgs &a, uint32_t sum, uint64_t lo, ui
     }
     return -1;
 }
+// chain_scan for one window per lane (lanes diverge): the queued windows of
+// a flush resolve their chains in parallel -- one set of directory / key /
+// strong-sum round trips per flush instead of one per window, visited in
+// order afterwards (chain_prefer applies want_i where a window matched)
+__device__ int32_t chain_scan_lane(const RsWalkArgs &a, uint32_t sum, uint64_t lo, uint64_t hi,
+                                   uint32_t klen, uint32_t &fa) {
+    const uint32_t b = sum >> (32 - a.dbits);
+    const uint32_t p0 = a.dir[b], p1 = a.dir[b + 1];
+    for (uint32_t p = p0; p < p1; ++p) {
+        const uint64_t key = a.tkey[p];
+        const uint32_t s1 = (uint32_t)(key >> 32);
+        if (s1 < sum) continue;
+        if (s1 > sum) break;
+        const int32_t i = (int32_t)~(uint32_t)key;
+        const uint32_t li = ((uint32_t)i == a.count - 1 && a.remainder) ? a.remainder : a.blength;
+        if (li != klen) continue;
+        if (!strong_eq(a, (uint32_t)i, lo, hi)) {
+            ++fa;
+            continue;
+        }
+        return i;
+    }
+    return -1;
+}
+
 __device__ __forceinline__ int32_t chain_prefer(const RsWalkArgs &a, int32_t i, uint32_t sum,
                                                 uint64_t lo, uint64_t hi, int32_t want) {
     if (i >= 0 && i != want && want >= 0 && (uint32_t)want < a.count && uni(a.sum1[want]) == sum &&
@@ -759,15 +784,26 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 const RowWin w = rows_window<false, RING>(a, rs, lane, (uint64_t)orow, L);
                 wadd(wp, kPrFlush, tf);
                 int64_t hlast = 0;
+                // lane j < nq scans window j's chain (its strong sum moved
+                // from lane 16 j); the visits then only read the results
+                tf = wclock(wp);
+                const int src = (int)(16 * (lane < nq ? lane : 0));
+                const uint64_t wl = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(w.lo >> 32), src, 64) << 32) |
+                                    (uint32_t)__shfl((int)(uint32_t)w.lo, src, 64);
+                const uint64_t wh = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(w.hi >> 32), src, 64) << 32) |
+                                    (uint32_t)__shfl((int)(uint32_t)w.hi, src, 64);
+                uint32_t cfa = 0;
+                const int32_t cidx = lane < nq ? chain_scan_lane(a, qsum, wl, wh, (uint32_t)L, cfa) : -1;
+                wadd(wp, kPrChain, tf);
                 for (uint32_t j = 0; j < nq; ++j) {
                     const int64_t h = (int64_t)rdl64((uint64_t)qh, (int)j);
                     const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)qsum, (int)j);
                     const uint64_t lo = rdl64(w.lo, (int)(16 * j)), hi = rdl64(w.hi, (int)(16 * j));
                     const uint64_t fa_visit = fa;
                     WPROG(a, lane, 6, h, j);
-                    tf = wclock(wp);
-                    const int32_t i = unis(chain_match(a, sv, lo, hi, want, (uint32_t)L, fa));
-                    wadd(wp, kPrChain, tf);
+                    fa += (uint32_t)__builtin_amdgcn_readlane((int)cfa, (int)j);
+                    const int32_t ci = __builtin_amdgcn_readlane(cidx, (int)j);
+                    const int32_t i = ci >= 0 ? unis(chain_prefer(a, ci, sv, lo, hi, want)) : -1;
                     hlast = h;
                     if (i >= 0) {
                         merged = on_match(h, i, fa_visit);
