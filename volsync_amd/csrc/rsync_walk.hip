@@ -240,6 +240,11 @@ enum : int {
     kPrStepSums = 8, kPrStepLds = 9, kPrStepGather = 10, kPrStepProbe = 11, kPrStepQueue = 12,
     kPrN = 16
 };
+// The counters live in scalar registers; compiled in only with VS_WALK_PROF
+// (tools/build_variant.sh walkprof -DVS_WALK_PROF=1, run with VSGPU_LIB=...
+// and VSGPU_WALK_PROF=1): 16 phases x two u64 otherwise spill SGPRs into VGPR
+// lanes all over the production kernel.
+#ifdef VS_WALK_PROF
 struct WProf {
     bool on;
     uint64_t cyc[kPrN], cnt[kPrN];
@@ -253,6 +258,16 @@ __device__ __forceinline__ void wadd(WProf &w, int ph, uint64_t t0) {
         w.cnt[ph] += 1;
     }
 }
+#define WPROF_INIT(on_) WProf wp{(on_), {}, {}}
+#else
+struct WProf {
+    static constexpr bool on = false;
+    uint64_t cyc[kPrN], cnt[kPrN];   // never touched: `on` is a constant false
+};
+__device__ __forceinline__ uint64_t wclock(const WProf &) { return 0; }
+__device__ __forceinline__ void wadd(WProf &, int, uint64_t) {}
+#define WPROF_INIT(on_) WProf wp; (void)(on_)
+#endif
 
 struct RowWin {
     uint32_t weak;     // get_checksum1 of the row's window (WEAK only)
@@ -1554,7 +1569,7 @@ __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
     load_prefilter(a, lfilt);
     const uint32_t lane = threadIdx.x & 63;
     const RowSec rs{lsec};
-    WProf wp{a.prof != nullptr, {}, {}};
+    WPROF_INIT(a.prof != nullptr);
     for (uint32_t k = next_segment(a, lane); k < a.nseg; k = next_segment(a, lane)) {
         WPROG(a, lane, 11, k, a.nseg);
         const uint64_t ts = wclock(wp);
@@ -1611,7 +1626,7 @@ __global__ __launch_bounds__(64 * W, (RB == 32768 ? 3 : 1)) void rs_walk_spec_co
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = uni(threadIdx.x >> 6);
     const RowSec rs{lsec};
-    WProf wp{a.prof != nullptr, {}, {}};
+    WPROF_INIT(a.prof != nullptr);
     for (;;) {
         if (threadIdx.x == 0) sh.seg = atomicAdd(a.work, 1u);
         __syncthreads();
@@ -1661,7 +1676,7 @@ __global__ __launch_bounds__(kWalkThreads) void rs_walk_stitch_kernel(RsWalkArgs
     load_prefilter(a, lfilt);
     const uint32_t lane = threadIdx.x & 63;
     const RowSec rs{lsec};
-    WProf wp{false, {}, {}};
+    WPROF_INIT(false);
     for (uint32_t k = next_segment(a, lane); k < a.nseg; k = next_segment(a, lane)) {
         WPROG(a, lane, 21, k, a.nseg);
         const int64_t e = (int64_t)uni64((uint64_t)(k ? a.exit_old[k - 1] : a.e0));
