@@ -355,17 +355,18 @@ __host__ __device__ inline uint64_t rs_bloom_mask(uint32_t sum1) {
     return m;
 }
 // Membership buckets for the walk's probe ("is there a full-length block with
-// sum1 == s?"): 2^bbits buckets of 64 bytes -- a count, then up to 15 distinct
-// sums -- so a probe is one 64-byte load instead of the directory + sorted-key
-// round trips; a bucket whose count passed 15 falls back to those.
-constexpr uint32_t kBucketSlots = 15;
+// sum1 == s?"): 2^bbits buckets of 32 bytes -- a count, then up to 7 distinct
+// sums -- so a probe is one 32-byte load instead of the directory + sorted-key
+// round trips; a bucket whose count passed 7 falls back to those.
+constexpr uint32_t kBucketWords = 8;
+constexpr uint32_t kBucketSlots = kBucketWords - 1;
 __host__ __device__ inline uint32_t rs_bucket(uint32_t sum1, uint32_t bbits) {
     return (sum1 * 0x85EBCA77u) >> (32 - bbits);
 }
 __host__ __device__ inline uint32_t rs_bucket_bits(uint32_t count) {
     uint32_t lc = 0;
     while ((1ull << lc) < (uint64_t)(count ? count : 1)) ++lc;
-    return lc < 6 ? 4 : lc - 2;   // ~4 distinct sums per bucket
+    return lc < 5 ? 4 : lc - 1;   // ~2 distinct sums per bucket (P(> 7) ~ 0.1 %)
 }
 // layout: filter [2^fbits bits], LDS prefilter [2^lbits bits], blocked filter [2^fbits bits]
 inline size_t rs_filter_bytes(uint32_t fbits) {

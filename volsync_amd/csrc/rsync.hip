@@ -436,7 +436,7 @@ __global__ void rs_bucket_kernel(const uint64_t *tkey, uint32_t count, uint32_t 
         const bool prev_full = rs_key_full(tkey[p - 1], count, remainder);
         if (prev_full || (p > 1 && (uint32_t)(tkey[p - 2] >> 32) == s)) return;
     }
-    uint32_t *b = bkt + (uint64_t)rs_bucket(s, bbits) * 16;
+    uint32_t *b = bkt + (uint64_t)rs_bucket(s, bbits) * kBucketWords;
     const uint32_t slot = atomicAdd(&b[0], 1u);
     if (slot < kBucketSlots) b[1 + slot] = s;
 }

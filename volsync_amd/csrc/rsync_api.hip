@@ -278,8 +278,9 @@ int build_table(vs_rsync *h) {
         const int v = e ? atoi(e) : 0;
         if (v >= 1 && v <= 26) h->bbits = (uint32_t)v;
     }
-    VS_TRY(h->d_bkt.ensure((64ull << h->bbits)));
-    VS_HIP(hipMemsetAsync(h->d_bkt.p, 0, 64ull << h->bbits, h->stream));
+    const size_t bkt_bytes = ((size_t)kBucketWords * 4) << h->bbits;
+    VS_TRY(h->d_bkt.ensure(bkt_bytes));
+    VS_HIP(hipMemsetAsync(h->d_bkt.p, 0, bkt_bytes, h->stream));
     VS_HIP(launch_rs_buckets(h->d_tkey.as<uint64_t>(), count, (uint32_t)h->remainder, h->bbits,
                              h->d_bkt.as<uint32_t>(), h->stream));
     VS_HIP(hipStreamSynchronize(h->stream));

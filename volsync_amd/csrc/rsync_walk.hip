@@ -34,7 +34,8 @@ namespace {
 
 using vsstrong::P32_1;
 
-constexpr uint32_t kWalkThreads = 768;             // 12 waves (168 VGPRs each); the 128 KiB prefilter admits one WG/CU
+constexpr uint32_t kWalkThreads = 512;             // 8 waves (up to 256 VGPRs each); the 128 KiB prefilter admits one WG/CU
+constexpr uint32_t kWalkRing = 4;                   // window blocks in flight per lane in the wave walk
 constexpr uint32_t kLdsFiltWordsW = 1u << 15;      // 2^20-bit LDS prefilter
 constexpr uint64_t kBatch = 1024;                  // STEP offsets per wave batch (16 per lane)
 
@@ -503,19 +504,27 @@ __device__ __forceinline__ bool probe_full(const RsWalkArgs &a, uint32_t sum) {
     return false;
 }
 
-// probe_full through the membership buckets: one 64-byte load (four 16-byte
-// pieces of one line), the directory walk only for an overflowed bucket
-__device__ __forceinline__ bool probe_bucket(const RsWalkArgs &a, uint32_t sum) {
-    const uint4 *b = (const uint4 *)(a.bkt + (uint64_t)rs_bucket(sum, a.bbits) * 16);
-    const uint4 v0 = b[0], v1 = b[1], v2 = b[2], v3 = b[3];
-    const uint32_t w[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
-                            v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
-    const uint32_t n = w[0];
-    if (n > kBucketSlots) return probe_full(a, sum);
+// membership-bucket words of sum (one 32-byte load: two 16-byte pieces)
+__device__ __forceinline__ void bucket_load(const RsWalkArgs &a, uint32_t sum, uint4 &b0, uint4 &b1) {
+    const uint4 *b = (const uint4 *)(a.bkt + (uint64_t)rs_bucket(sum, a.bbits) * kBucketWords);
+    b0 = b[0];
+    b1 = b[1];
+}
+// is sum in the loaded bucket?  (the directory walk for an overflowed one)
+__device__ __forceinline__ bool bucket_has(const RsWalkArgs &a, uint32_t sum, const uint4 &b0,
+                                           const uint4 &b1) {
+    const uint32_t w[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    if (w[0] > kBucketSlots) return probe_full(a, sum);
     bool hit = false;
 #pragma unroll
-    for (uint32_t i = 0; i < kBucketSlots; ++i) hit |= (i < n) & (w[1 + i] == sum);
+    for (uint32_t i = 0; i < kBucketSlots; ++i) hit |= (i < w[0]) & (w[1 + i] == sum);
     return hit;
+}
+// probe_full through the membership buckets
+__device__ __forceinline__ bool probe_bucket(const RsWalkArgs &a, uint32_t sum) {
+    uint4 b0, b1;
+    bucket_load(a, sum, b0, b1);
+    return bucket_has(a, sum, b0, b1);
 }
 
 __device__ __forceinline__ int32_t sbyte(const uint8_t *d, uint64_t p) {
@@ -676,21 +685,37 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
         }
         T1 = uni(T1);
         T2 = uni(T2);
-        int64_t from = o;
         uint32_t nq = 0;        // queued hits: lane j < nq holds hit j (offset, weak sum)
         int64_t qh = 0;
         uint32_t qsum = 0;
         bool matched = false;
         uint4 cwo, cwi;         // the batch's leaving / entering bytes (16 per lane)
         batch_load(a, A, lane, cwo, cwi);
-        for (;;) {
+        // Stage 1 of a batch: its window sums, the LDS prefilter and the
+        // blocked filter, and the membership-bucket load of each lane's first
+        // surviving offset.  Stage 2 (probe results, queueing, flushes) of
+        // batch A runs after stage 1 of batch A + 1024, so the bucket loads of
+        // A are in flight behind A + 1024's sums and filter reads instead of
+        // stalling the wave; a match in A drops A + 1024's stage 1.  Stage 1
+        // also issues the loads of the batch after the one it tests.
+        struct Stage {
+            uint32_t hit;        // offsets passing both filters
+            uint32_t sums[16];   // (s1 & 0xffff) | (s2 << 16) per offset
+            uint32_t t1, t2;     // the sums at the next batch's first offset (uniform)
+            uint32_t pt;         // the probed offset of the lane (16: none)
+            uint4 b0, b1;        // its membership bucket
+        };
+        uint4 nwo = cwo, nwi = cwi;
+        auto stage1 = [&](uint64_t Ab, const uint4 &bo, const uint4 &bi, uint32_t t1, uint32_t t2,
+                          int64_t fromb, Stage &st) {
             uint64_t tb = wclock(wp);
-            const uint64_t c = A + 16 * (uint64_t)lane;
-            const uint32_t wo[4] = {cwo.x, cwo.y, cwo.z, cwo.w};
-            const uint32_t wi[4] = {cwi.x, cwi.y, cwi.z, cwi.w};
+            const uint64_t c = Ab + 16 * (uint64_t)lane;
+            const uint32_t wo[4] = {bo.x, bo.y, bo.z, bo.w};
+            const uint32_t wi[4] = {bi.x, bi.y, bi.z, bi.w};
             // the next batch's bytes, in flight while this one is tested
-            uint4 nwo = cwo, nwi = cwi;
-            if ((int64_t)(A + kBatch) < fend) batch_load(a, A + kBatch, lane, nwo, nwi);
+            nwo = bo;
+            nwi = bi;
+            if ((int64_t)(Ab + kBatch) < fend) batch_load(a, Ab + kBatch, lane, nwo, nwi);
             int Xo = 0, Xi = 0, Eo = 0, Ei = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -705,37 +730,36 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
             const uint32_t D = (uint32_t)(Xi - Xo), E = (uint32_t)(Ei - Eo), X = (uint32_t)Xo;
             const uint32_t P = excl_scan(D, lane);
             const uint32_t Y = excl_scan(E + 16u * P - (uint32_t)L * X, lane);
-            uint32_t s1 = T1 + P;
-            uint32_t s2 = T2 + 16u * lane * T1 + Y;
-            uint32_t sums[16];
+            uint32_t s1 = t1 + P;
+            uint32_t s2 = t2 + 16u * lane * t1 + Y;
             uint32_t valid = 0;
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
-                sums[t] = __builtin_amdgcn_perm(s2, s1, 0x05040100u);  // (s1 & 0xffff) | (s2 << 16)
+                st.sums[t] = __builtin_amdgcn_perm(s2, s1, 0x05040100u);  // (s1 & 0xffff) | (s2 << 16)
                 const int32_t xo = __builtin_amdgcn_sbfe((int)wo[t >> 2], 8 * (t & 3), 8);
                 const int32_t xi = __builtin_amdgcn_sbfe((int)wi[t >> 2], 8 * (t & 3), 8);
                 s1 += (uint32_t)(xi - xo);
                 s2 = s2 - (uint32_t)L * (uint32_t)xo + s1;
                 const int64_t qo = (int64_t)c + t;
-                valid |= (uint32_t)(qo >= from && qo < fend) << t;
+                valid |= (uint32_t)(qo >= fromb && qo < fend) << t;
             }
+            st.t1 = (uint32_t)__builtin_amdgcn_readlane((int)s1, 63);
+            st.t2 = (uint32_t)__builtin_amdgcn_readlane((int)s2, 63);
+            wadd(wp, kPrStepSums, tb);
             // membership: the LDS prefilter (top lbits of the sum), then the
             // L2-resident blocked filter for all 16 offsets at once -- offsets
-            // the prefilter rejected read word 0, so their loads coalesce --
-            // and the directory only for the few offsets that pass both
+            // the prefilter rejected read word 0, so their loads coalesce;
             // all 16 reads of each stage are issued before any is consumed
-            // (one LDS and one L2 round trip per batch, not 16 of each)
-            wadd(wp, kPrStepSums, tb);
             uint64_t tsub = wclock(wp);
             uint32_t hit = valid;
             if (a.lbits) {
                 uint32_t lw[16];
 #pragma unroll
-                for (int t = 0; t < 16; ++t) lw[t] = lfilt[(sums[t] >> (32 - a.lbits)) >> 5];
+                for (int t = 0; t < 16; ++t) lw[t] = lfilt[(st.sums[t] >> (32 - a.lbits)) >> 5];
                 uint32_t lh = 0;
 #pragma unroll
                 for (int t = 0; t < 16; ++t)
-                    lh |= ((lw[t] >> ((sums[t] >> (32 - a.lbits)) & 31)) & 1u) << t;
+                    lh |= ((lw[t] >> ((st.sums[t] >> (32 - a.lbits)) & 31)) & 1u) << t;
                 hit &= lh;
             }
             wadd(wp, kPrStepLds, tsub);
@@ -745,60 +769,89 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
                     const bool on = (hit >> t) & 1u;
-                    fw[t] = a.filt_b[on ? rs_bloom_word(sums[t], a.fbits) : 0u];
+                    fw[t] = a.filt_b[on ? rs_bloom_word(st.sums[t], a.fbits) : 0u];
                 }
                 uint32_t pass = 0;
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
-                    const uint64_t m = rs_bloom_mask(sums[t]);
+                    const uint64_t m = rs_bloom_mask(st.sums[t]);
                     pass |= (uint32_t)((fw[t] & m) == m) << t;
                 }
                 hit &= pass;
             }
+            st.hit = hit;
+            st.pt = hit ? (uint32_t)__builtin_ctz(hit) : 16u;
+            if (hit) {
+                uint32_t sv = st.sums[0];
+#pragma unroll
+                for (uint32_t k = 1; k < 16; ++k) sv = (st.pt == k) ? st.sums[k] : sv;
+                bucket_load(a, sv, st.b0, st.b1);
+            }
             wadd(wp, kPrStepGather, tsub);
-            tsub = wclock(wp);
-            for (uint32_t mm = hit; mm;) {
-                const int t = __builtin_ctz(mm);
-                mm &= mm - 1;
-                uint32_t st = sums[0];
-#pragma unroll
-                for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
-                if (!probe_bucket(a, st)) hit &= ~(1u << t);
-            }
-            wadd(wp, kPrStepProbe, tsub);
-            tsub = wclock(wp);
-            // queue the hits in offset order (lane order, then bit order)
-            uint64_t lanes = __ballot(hit != 0);
-            WPROG(a, lane, 5, (int64_t)A, lanes);
-            while (lanes && nq < kRows) {
-                const uint32_t hl = (uint32_t)__builtin_ctzll(lanes);
-                const uint32_t hm = (uint32_t)__builtin_amdgcn_readlane((int)hit, (int)hl);
-                const uint32_t t = (uint32_t)__builtin_ctz(hm);
-                uint32_t st = sums[0];
-#pragma unroll
-                for (uint32_t k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
-                const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)st, (int)hl);
-                const int64_t h = (int64_t)A + 16 * (int64_t)hl + t;
-                if (lane == nq) {
-                    qh = h;
-                    qsum = sv;
-                }
-                ++nq;
-                if (lane == hl) hit &= hit - 1;
-                lanes = __ballot(hit != 0);
-            }
-            wadd(wp, kPrStepQueue, tsub);
-            wadd(wp, kPrStep, tb);
-            const bool more = lanes != 0;              // hits of this batch not yet queued
+        };
+        Stage cur, nxt;
+        stage1(A, cwo, cwi, T1, T2, o, cur);
+        for (;;) {
+            uint64_t tb = wclock(wp);
             const uint64_t nx = A + kBatch;
             const bool last = (int64_t)nx >= fend;
-            if (nq == kRows || (!more && last && nq)) {
+            if (!last) {
+                cwo = nwo;
+                cwi = nwi;
+                stage1(nx, cwo, cwi, cur.t1, cur.t2, (int64_t)nx, nxt);
+            }
+            // stage 2 of batch A: the probe results (the preloaded bucket for
+            // the lane's first offset, the rest probed now -- rare)
+            uint64_t tsub = wclock(wp);
+            uint32_t hit = cur.hit;
+            if (hit) {
+                uint32_t sv = cur.sums[0];
+#pragma unroll
+                for (uint32_t k = 1; k < 16; ++k) sv = (cur.pt == k) ? cur.sums[k] : sv;
+                if (!bucket_has(a, sv, cur.b0, cur.b1)) hit &= ~(1u << cur.pt);
+                for (uint32_t mm = cur.hit & ~(1u << cur.pt); mm;) {
+                    const int t = __builtin_ctz(mm);
+                    mm &= mm - 1;
+                    uint32_t st = cur.sums[0];
+#pragma unroll
+                    for (int k = 1; k < 16; ++k) st = (t == k) ? cur.sums[k] : st;
+                    if (!probe_bucket(a, st)) hit &= ~(1u << t);
+                }
+            }
+            wadd(wp, kPrStepProbe, tsub);
+            // queue the hits in offset order (lane order, then bit order);
+            // a full queue is flushed and queueing goes on with the batch's
+            // remaining hits (all past the last visited one)
+            for (;;) {
+                tsub = wclock(wp);
+                uint64_t lanes = __ballot(hit != 0);
+                WPROG(a, lane, 5, (int64_t)A, lanes);
+                while (lanes && nq < kRows) {
+                    const uint32_t hl = (uint32_t)__builtin_ctzll(lanes);
+                    const uint32_t hm = (uint32_t)__builtin_amdgcn_readlane((int)hit, (int)hl);
+                    const uint32_t t = (uint32_t)__builtin_ctz(hm);
+                    uint32_t st = cur.sums[0];
+#pragma unroll
+                    for (uint32_t k = 1; k < 16; ++k) st = (t == k) ? cur.sums[k] : st;
+                    const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)st, (int)hl);
+                    const int64_t h = (int64_t)A + 16 * (int64_t)hl + t;
+                    if (lane == nq) {
+                        qh = h;
+                        qsum = sv;
+                    }
+                    ++nq;
+                    if (lane == hl) hit &= hit - 1;
+                    lanes = __ballot(hit != 0);
+                }
+                wadd(wp, kPrStepQueue, tsub);
+                const bool more = lanes != 0;              // hits of this batch not yet queued
+                if (!(nq == kRows || (!more && last && nq))) break;
                 // hash the queued windows together, visit them in order
                 const int64_t orow = by_row(qh, lane, nq);
                 uint64_t tf = wclock(wp);
-                const RowWin w = rows_window<false, RING>(a, rs, lane, (uint64_t)orow, L);
+                // (two blocks in flight here: the next batch's stage 1 is live)
+                const RowWin w = rows_window<false, kRing>(a, rs, lane, (uint64_t)orow, L);
                 wadd(wp, kPrFlush, tf);
-                int64_t hlast = 0;
                 // lane j < nq scans window j's chain (its strong sum moved
                 // from lane 16 j); the visits then only read the results
                 tf = wclock(wp);
@@ -819,7 +872,6 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                     fa += (uint32_t)__builtin_amdgcn_readlane((int)cfa, (int)j);
                     const int32_t ci = __builtin_amdgcn_readlane(cidx, (int)j);
                     const int32_t i = ci >= 0 ? unis(chain_prefer(a, ci, sv, lo, hi, want)) : -1;
-                    hlast = h;
                     if (i >= 0) {
                         merged = on_match(h, i, fa_visit);
                         matched = true;
@@ -827,24 +879,16 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                     }
                 }
                 nq = 0;
-                if (matched) break;
-                if (more) {
-                    // this batch has more hits: redo it past the last visited one
-                    from = hlast + 1;
-                    continue;
-                }
+                if (matched || !more) break;
             }
-            if (more) continue;   // not reached: the queue only stops filling when full
+            wadd(wp, kPrStep, tb);
+            if (matched) break;
             if (last) {
                 o = fend;
                 break;
             }
-            T1 = (uint32_t)__builtin_amdgcn_readlane((int)s1, 63);
-            T2 = (uint32_t)__builtin_amdgcn_readlane((int)s2, 63);
             A = nx;
-            from = (int64_t)A;
-            cwo = nwo;
-            cwi = nwi;
+            cur = nxt;
         }
         if (matched) {
             run = true;
@@ -1698,7 +1742,7 @@ __global__ __launch_bounds__(kWalkThreads) void rs_walk_stitch_kernel(RsWalkArgs
             // back to the speculative entry
             r = SegResult{0, 0, sv.fa, sv.exit_off, sv.exit_want};
         } else {
-            r = walk_segment<kRing>(a, rs, lfilt, lane, e, w, seg_hi(a, k), a.fin_off + base,
+            r = walk_segment<kWalkRing>(a, rs, lfilt, lane, e, w, seg_hi(a, k), a.fin_off + base,
                                     a.fin_idx + base, a.fin_fab + base, a.cap, &sv, wp);
         }
         if (lane == 0) {
@@ -1735,21 +1779,6 @@ __global__ void rs_pad_sum2_kernel(const uint8_t *sum2, uint32_t count, uint32_t
 hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t s) {
     if (!a.nseg) return hipSuccess;
     if (a.lbits > 20) return hipErrorInvalidValue;
-    // The speculative pass runs 8 waves per CU with four blocks of each window
-    // hash in flight per lane (196 VGPRs; the stitch passes keep 12 waves):
-    // one rank of the real C4 772-778 -> 799-800 GB/s, the 64 GiB shape
-    // 2011 -> 2021 (profiles/r03_walk_ring).  A/B knobs: VSGPU_WALK_WG=768 /
-    // 1024 / 256 (12 waves with two blocks in flight; 16 waves, spills; 4
-    // waves), VSGPU_WALK_RING=2 (8 waves, two blocks in flight)
-    static const uint32_t spec_threads = [] {
-        const char *e = getenv("VSGPU_WALK_WG");
-        const int v = e ? atoi(e) : 0;
-        return (v == 1024 || v == 768 || v == 256) ? (uint32_t)v : 512u;
-    }();
-    static const bool ring4 = [] {
-        const char *e = getenv("VSGPU_WALK_RING");
-        return !(e && atoi(e) == 2);
-    }();
     // VSGPU_WALK_COOP=W (4, 6 or 12; 0 = off): the speculative pass with
     // W-wave cooperative walks (walk_segment_coop)
     // (read at every launch: tests switch it within one process)
@@ -1778,23 +1807,18 @@ hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t
         else rs_walk_spec_coop_kernel<4, 0><<<(uint32_t)grid, 256, 0, s>>>(a);
         return hipGetLastError();
     }
-    const uint32_t threads = stitch ? kWalkThreads : spec_threads;
-    const uint32_t waves = threads / 64;
+    // both passes: 8 waves per CU, four window blocks in flight per lane,
+    // STEP batches in two stages (one rank of the real C4: 772-778 -> 840
+    // GB/s with the membership buckets and without profiling state,
+    // profiles/r03_walk_ring)
+    const uint32_t waves = kWalkThreads / 64;
     const uint64_t grid = std::min<uint64_t>((a.nseg + waves - 1) / waves, (uint64_t)std::max(cus, 1));
     hipError_t e = hipMemsetAsync(a.work, 0, 4, s);
     if (e != hipSuccess) return e;
     if (stitch)
         rs_walk_stitch_kernel<<<(uint32_t)grid, kWalkThreads, 0, s>>>(a);
-    else if (threads == 1024)
-        rs_walk_spec_kernel<1024, kRing><<<(uint32_t)grid, 1024, 0, s>>>(a);
-    else if (threads == 512 && ring4)
-        rs_walk_spec_kernel<512, 4><<<(uint32_t)grid, 512, 0, s>>>(a);
-    else if (threads == 512)
-        rs_walk_spec_kernel<512, kRing><<<(uint32_t)grid, 512, 0, s>>>(a);
-    else if (threads == 256)
-        rs_walk_spec_kernel<256, kRing><<<(uint32_t)grid, 256, 0, s>>>(a);
     else
-        rs_walk_spec_kernel<kWalkThreads, kRing><<<(uint32_t)grid, kWalkThreads, 0, s>>>(a);
+        rs_walk_spec_kernel<kWalkThreads, kWalkRing><<<(uint32_t)grid, kWalkThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 
