@@ -802,7 +802,7 @@ static int stream_copy(vs_cdc *h, uint8_t *dst, const uint8_t *src, size_t n) {
         const double t0 = now_ms();
         if (h->stage_busy[i]) VS_HIP(hipEventSynchronize(h->stage_ev[i]));
         const double t1 = now_ms();
-        memcpy(h->stage[i], src + off, k);
+        par_memcpy(h->stage[i], src + off, k);
         h->feed_stats[4] += t1 - t0;
         h->feed_stats[7] += now_ms() - t1;
         VS_HIP(hipMemcpyAsync(dst + off, h->stage[i], k, hipMemcpyHostToDevice, h->cstream));

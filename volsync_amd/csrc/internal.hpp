@@ -39,6 +39,8 @@ void *pinned_alloc(size_t bytes);   // nullptr on failure
 void pinned_free(void *p);
 // [p, p + n) lies inside one page-locked host allocation (DMA it directly)
 bool host_range_pinned(const void *p, size_t n);
+// memcpy split over a few host threads for large copies (staging)
+void par_memcpy(void *dst, const void *src, size_t n);
 
 // std::vector storage in owned pinned pages: read-back targets the DMA engine
 // writes directly (grows like any vector; every allocation is hipHostMalloc)

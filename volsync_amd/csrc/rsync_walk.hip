@@ -955,12 +955,6 @@ __device__ __forceinline__ void band_put(uint32_t *ring, uint64_t x, uint4 v) {
 struct RowAcc {
     uint64_t A0, A1;
 };
-__device__ __forceinline__ RowAcc row_acc_init(uint32_t lane) {
-    using namespace vsstrong;
-    const uint32_t m = lane & 3;
-    return RowAcc{(m == 0) ? P32_3 : (m == 1) ? P64_2 : (m == 2) ? P64_4 : P64_5,
-                  (m == 0) ? P64_1 : (m == 1) ? P64_3 : (m == 2) ? P32_2 : P32_1};
-}
 template <class Ld>
 __device__ __forceinline__ void row_acc_blocks(RowAcc &st, const RowSec &rs, uint32_t lane, Ld ld,
                                                uint32_t b0, uint32_t b1) {

@@ -10,12 +10,43 @@
 // hipHostMalloc'd by the library goes through a Stager: two owned pinned
 // buffers, the CPU memcpy of chunk k overlapping the DMA of chunk k-1.  The
 // runtime is never handed a caller pointer to pin.
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "internal.hpp"
 
 namespace vsgpu {
+
+// The staging copies are the host side of every pageable feed (the Go
+// Chunker's read buffer is pageable): one thread copies ~20 GB/s, a third of
+// what the DMA behind it moves, so large copies are split over a few threads.
+// VSGPU_COPY_THREADS (default 4, 1 = plain memcpy).
+void par_memcpy(void *dst, const void *src, size_t n) {
+    static const int threads = [] {
+        const char *e = getenv("VSGPU_COPY_THREADS");
+        const int v = e ? atoi(e) : 4;
+        return v >= 1 && v <= 16 ? v : 4;
+    }();
+    constexpr size_t kMin = 4u << 20;   // per thread
+    const int t = (int)std::min<size_t>((size_t)threads, n / kMin);
+    if (t <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const size_t part = (n / (size_t)t + 4095) & ~(size_t)4095;
+    std::vector<std::thread> pool;
+    pool.reserve((size_t)t - 1);
+    for (int i = 1; i < t; ++i) {
+        const size_t off = part * (size_t)i;
+        if (off >= n) break;
+        pool.emplace_back([=] { memcpy((char *)dst + off, (const char *)src + off, std::min(part, n - off)); });
+    }
+    memcpy(dst, src, std::min(part, n));
+    for (auto &th : pool) th.join();
+}
 
 int fail_hip(hipError_t e, const char *what, const char *file, int line) {
     (void)hipGetLastError();  // clear the runtime's last error: it is reported here
@@ -103,7 +134,7 @@ int Stager::h2d(void *dst, const void *src, size_t n, hipStream_t s) {
     for (size_t off = 0; off < n; off += kChunk) {
         const size_t k = std::min(kChunk, n - off);
         VS_TRY(wait(next));
-        memcpy(buf[next], p + off, k);
+        par_memcpy(buf[next], p + off, k);
         VS_HIP(hipMemcpyAsync(d + off, buf[next], k, hipMemcpyHostToDevice, s));
         VS_HIP(hipEventRecord(ev[next], s));
         busy[next] = true;
@@ -130,7 +161,7 @@ int Stager::d2h(void *dst, const void *src, size_t n, hipStream_t s) {
         busy[next] = true;
         if (prev >= 0) {
             VS_TRY(wait(prev));
-            memcpy(p + prev_off, buf[prev], prev_k);
+            par_memcpy(p + prev_off, buf[prev], prev_k);
         }
         prev = next;
         prev_off = off;
@@ -138,7 +169,7 @@ int Stager::d2h(void *dst, const void *src, size_t n, hipStream_t s) {
         next ^= 1;
     }
     VS_TRY(wait(prev));
-    memcpy(p + prev_off, buf[prev], prev_k);
+    par_memcpy(p + prev_off, buf[prev], prev_k);
     return 0;
 }
 
