@@ -98,8 +98,14 @@ bool host_range_pinned(const void *p, size_t n) {
             hipSuccess ||
         hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) !=
             hipSuccess) {
+        // the allocation's extent from the runtime's address-range query
         (void)hipGetLastError();
-        return false;
+        hipDeviceptr_t base = 0;
+        if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        start = (uintptr_t)base;
     }
     const uintptr_t a = (uintptr_t)p;
     return start <= a && a + n <= start + size;
