@@ -6,9 +6,11 @@ import ctypes
 import torch
 
 hip = ctypes.CDLL("libamdhip64.so")
-n = 1 << 30
+import sys
+
+n = int(float(sys.argv[1]) * (1 << 30)) if len(sys.argv) > 1 else 1 << 30
 t = torch.empty(n, dtype=torch.uint8, pin_memory=True)
-for off in (0, n // 2):
+for off in (0, n // 2, n - (64 << 20)):
     p = ctypes.c_void_p(t.data_ptr() + off)
     start = ctypes.c_uint64(0)
     size = ctypes.c_size_t(0)
