@@ -21,6 +21,8 @@ ap.add_argument("--volumes", type=int, default=4)
 ap.add_argument("--volume-bytes", type=int, default=1 << 36)
 ap.add_argument("--c4-source-bytes", type=int, default=68719492223)
 ap.add_argument("--seal-bytes", type=int, default=68718991021)
+# rank 3 of 8 of the real C4 (--mode rsync --share 3/8 --per-gpu-gib 32): its own S range
+ap.add_argument("--c4-share-source-bytes", type=int, default=34359736410)
 a = ap.parse_args()
 
 
@@ -33,7 +35,9 @@ def total(e):
     return (e["hbm_read_bytes_per_dispatch"] + e["hbm_write_bytes_per_dispatch"]) * e["calls"]
 
 
-out = {"source": a.prof, "volumes": a.volumes, "volume_bytes": a.volume_bytes}
+# sections this profile round does not hold keep their earlier source
+tj = os.path.join(os.path.dirname(a.prof.rstrip("/")), "traffic.json")
+out = json.load(open(tj)) if os.path.exists(tj) else {}
 def find(s, base, prefix=None):
     """the summary entry of kernel `base` (template arguments ignored, or
     the one whose name starts with `prefix`)"""
@@ -45,6 +49,7 @@ def find(s, base, prefix=None):
 
 s = load("c2")
 if s:
+    out.update({"source": a.prof, "volumes": a.volumes, "volume_bytes": a.volume_bytes})
     # fp_kernel<2, ...>: the FAST variant the C2 bench runs
     for stage, (k, pre) in {"fingerprint": ("fp_kernel", "fp_kernel<2"),
                             "sha256": ("sha_slice_kernel", None)}.items():
@@ -57,6 +62,14 @@ if s:
     per = e["hbm_read_bytes_per_dispatch"] + e["hbm_write_bytes_per_dispatch"]
     out["rs_walk_spec"] = {"kernel": "rs_walk_spec_kernel", "source": os.path.join(a.prof, "c4"),
                            "bytes_per_source_byte": per / a.c4_source_bytes}
+s = load("c4_share")
+if s:
+    e = find(s, "rs_walk_spec_kernel")
+    per = e["hbm_read_bytes_per_dispatch"] + e["hbm_write_bytes_per_dispatch"]
+    out["rs_walk_spec_share"] = {
+        "kernel": "rs_walk_spec_kernel", "source": os.path.join(a.prof, "c4_share"),
+        "config": "--mode rsync --share 3/8 --per-gpu-gib 32 (2 M-block table)",
+        "bytes_per_source_byte": per / a.c4_share_source_bytes}
 s = load("seal")
 if s:
     for stage, k in {"seal_ctr": "seal_ctr_kernel", "seal_mac": "seal_mac_kernel"}.items():
@@ -65,6 +78,5 @@ if s:
             per = e["hbm_read_bytes_per_dispatch"] + e["hbm_write_bytes_per_dispatch"]
             out[stage] = {"kernel": k, "source": os.path.join(a.prof, "seal"),
                           "bytes_per_plain_byte": per / a.seal_bytes}
-json.dump(out, open(os.path.join(os.path.dirname(a.prof.rstrip("/")), "traffic.json"), "w"),
-          indent=1)
+json.dump(out, open(tj, "w"), indent=1)
 print(json.dumps(out, indent=1))

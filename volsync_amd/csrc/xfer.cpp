@@ -94,10 +94,14 @@ bool host_range_pinned(const void *p, size_t n) {
     // past a registered range's end fails (hipErrorInvalidValue)
     uintptr_t start = 0;
     size_t size = 0;
+    // The range attributes report size 0 for a 64 GiB pinned allocation on
+    // ROCm 7 (tools/probe/pin_torch.py, profiles/r03_end/pin_torch64.log);
+    // hipMemGetAddressRange reports it right
     if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) !=
             hipSuccess ||
         hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) !=
-            hipSuccess) {
+            hipSuccess ||
+        size == 0) {
         // the allocation's extent from the runtime's address-range query
         (void)hipGetLastError();
         hipDeviceptr_t base = 0;
