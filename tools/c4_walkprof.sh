@@ -1,3 +1,14 @@
-cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
-VSGPU_WALK_PROF=1 timeout -k 10 300 python bench.py --mode rsync --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench_prof.log 2>&1
-rc=$?; grep "walk prof" gpurun_out/bench_prof.log | tail -2; tail -1 gpurun_out/bench_prof.log | cut -c1-400; exit $rc
+#!/bin/bash
+# Per-wave walk phase profile (s_memtime phases).  The phase
+# counters are compiled only into a profiling build; make it here first:
+#   tools/build_variant.sh walkprof -DVS_WALK_PROF=1
+# then on the box: bash tools/c4_walkprof.sh [bench.py args...]
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+mkdir -p gpurun_out
+lib=$PWD/volsync_amd/lib/var/walkprof/libvsgpu.so
+[ -f "$lib" ] || { echo "build $lib first (tools/build_variant.sh walkprof -DVS_WALK_PROF=1)" >&2; exit 2; }
+VSGPU_LIB=$lib VSGPU_WALK_PROF=1 timeout -k 10 300 python bench.py --mode rsync --steps 1 --warmup 1 \
+  --no-cpu-baseline --no-file-sum "$@" > gpurun_out/bench_walkprof.log 2>&1
+rc=$?
+grep "walk prof" gpurun_out/bench_walkprof.log | tail -1 | tr ';' '\n'
+exit $rc
