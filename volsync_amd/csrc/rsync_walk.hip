@@ -34,8 +34,17 @@ namespace {
 
 using vsstrong::P32_1;
 
-constexpr uint32_t kWalkThreads = 512;             // 8 waves (up to 256 VGPRs each); the 128 KiB prefilter admits one WG/CU
-constexpr uint32_t kWalkRing = 4;                   // window blocks in flight per lane in the wave walk
+#ifndef VS_WALK_T
+#define VS_WALK_T 512
+#endif
+#ifndef VS_WALK_RRING
+#define VS_WALK_RRING 4
+#endif
+#ifndef VS_WALK_FRING
+#define VS_WALK_FRING 2
+#endif
+constexpr uint32_t kWalkThreads = VS_WALK_T;             // 8 waves (up to 256 VGPRs each); the 128 KiB prefilter admits one WG/CU
+constexpr uint32_t kWalkRing = VS_WALK_RRING;                  // window blocks in flight per lane in the wave walk
 constexpr uint32_t kLdsFiltWordsW = 1u << 15;      // 2^20-bit LDS prefilter
 constexpr uint64_t kBatch = 1024;                  // STEP offsets per wave batch (16 per lane)
 
@@ -850,7 +859,7 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 const int64_t orow = by_row(qh, lane, nq);
                 uint64_t tf = wclock(wp);
                 // (two blocks in flight here: the next batch's stage 1 is live)
-                const RowWin w = rows_window<false, kRing>(a, rs, lane, (uint64_t)orow, L);
+                const RowWin w = rows_window<false, VS_WALK_FRING>(a, rs, lane, (uint64_t)orow, L);
                 wadd(wp, kPrFlush, tf);
                 // lane j < nq scans window j's chain (its strong sum moved
                 // from lane 16 j); the visits then only read the results
