@@ -758,3 +758,49 @@ def test_coop_walk_exact(gpu, monkeypatch, coop):
     s = SumStruct(n, n // bl, bl, s2l, 0, c1, c2)
     got4, fa4 = _sharded_device_match(src, s, 4, csum, seed)
     assert got4 == want and fa4 == fa
+
+
+def _dup_pair():
+    """A basis of 2048 identical 1 KiB blocks then 6 MiB of random bytes; the
+    source interleaves shifted runs of both with small edits, so segment
+    boundaries (1 MiB segments at blength 1024) fall inside runs of equal
+    blocks, where want_i decides the block and stitches enter the
+    speculative walks with another want_i."""
+    unit = O.synth(41, 0, 1024)
+    basis = np.concatenate([np.tile(unit, 2048), O.synth(42, 0, 6 << 20)])
+    rnd = basis[2 << 20:]
+    src = np.concatenate([O.synth(43, 0, 333), basis[: (1 << 20) + 517], rnd[:(3 << 20) + 11],
+                          O.synth(44, 0, 70_000), basis[5000:(2 << 20) - 3], rnd[1 << 20:]])
+    return basis, src
+
+
+@pytest.mark.parametrize("facap", [None, "3", "0"])
+@pytest.mark.parametrize("data", ["edits", "duplicates"])
+def test_stitch_merge_at_visited_entry(gpu, monkeypatch, facap, data):
+    """Stitch re-walks whose entry the speculative walk visited merge there
+    (same want_i) or at its next match (another want_i), with false alarms
+    from the speculative walk's recorded windows; VSGPU_WALK_FACAP shrinks
+    that record so segments with more false-alarm windows fall back to the
+    re-walk.  Every mix: hash_search's match list and false alarms."""
+    from volsync_amd import Matcher, SumStruct
+    if facap is not None:
+        monkeypatch.setenv("VSGPU_WALK_FACAP", facap)
+    csum, seed = R.CSUM_XXH3_128, 0x5EED5EED
+    if data == "edits":
+        n = 24 << 20
+        basis = O.synth(51, 0, n)
+        bl, s2l, cnt, rem = O.rsync_sizes(n, 2048)
+        src = R.mutate(basis, bl, seed=8, frac=0.25)
+    else:
+        basis, src = _dup_pair()
+        bl, s2l, cnt, rem = O.rsync_sizes(len(basis), 1024)
+    c1, c2 = O.rsync_signatures(basis, bl, s2l, csum, seed)
+    want, fa = O.rsync_match(src, c1, c2, bl, rem, csum, seed)
+    ds = to_dev(src)
+    m = Matcher()
+    m.load_sums(SumStruct(len(basis), cnt, bl, s2l, rem, c1, c2), csum, seed)
+    got = m.match_sums(ds.data_ptr(), len(src))
+    st = m.stats()
+    m.close()
+    assert len(want) > 1000
+    assert got == want and st["false_alarms"] == fa

@@ -418,6 +418,13 @@ struct RsWalkArgs {
     uint64_t *spec_fa;
     int64_t *spec_exit;
     int32_t *spec_exitw;
+    // the speculative walk's false-alarm windows (offset, running total after
+    // the window), up to facap per segment; spec_nfa[k] > facap: overflowed.
+    // A stitch whose entry the speculative walk visited merges there.
+    int64_t *spec_fao;
+    uint32_t *spec_fac;
+    uint32_t *spec_nfa;
+    uint32_t facap;
     // final walks: fin_off[0, fin_n) then spec[fin_from, spec_n) (fin_from
     // 0xffffffff: the final walk is the speculative one)
     int64_t *fin_entry;

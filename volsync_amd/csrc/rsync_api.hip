@@ -108,6 +108,7 @@ struct vs_rsync {
     DevBuf d_sum2p, d_sum2tmp;      // zero-padded 16-byte strong sums (device walk)
     // device walk: per-segment results and two exit buffers
     DevBuf w_spec_off, w_spec_idx, w_spec_fab, w_spec_n, w_spec_fa, w_spec_exit, w_spec_exitw;
+    DevBuf w_spec_fao, w_spec_fac, w_spec_nfa;
     DevBuf w_fin_entry, w_fin_entryw, w_fin_from, w_fin_n, w_fin_fa, w_fin_off, w_fin_idx,
         w_fin_fab;
     DevBuf w_exit[2], w_exitw[2], w_ctl, w_prof;
@@ -897,6 +898,18 @@ int walk_scan(vs_rsync *h) {
     VS_TRY(h->w_fin_idx.ensure(nc * 4));
     VS_TRY(h->w_fin_fab.ensure(nc * 8));
     VS_TRY(h->w_spec_n.ensure(ns * 4));
+    // false-alarm windows of the speculative walks: 1024 per segment (a 4 MiB
+    // segment of the real C4 averages ~200; more falls back to a re-walk)
+    a.facap = 1024;
+    {
+        // VSGPU_WALK_FACAP=n (tests): a smaller record, so stitches fall
+        // back to re-walks (read per call)
+        const char *e = getenv("VSGPU_WALK_FACAP");
+        if (e) a.facap = (uint32_t)std::max(0, atoi(e));
+    }
+    VS_TRY(h->w_spec_fao.ensure(ns * a.facap * 8));
+    VS_TRY(h->w_spec_fac.ensure(ns * a.facap * 4));
+    VS_TRY(h->w_spec_nfa.ensure(ns * 4));
     VS_TRY(h->w_spec_fa.ensure(ns * 8));
     VS_TRY(h->w_spec_exit.ensure(ns * 8));
     VS_TRY(h->w_spec_exitw.ensure(ns * 4));
@@ -927,6 +940,9 @@ int walk_scan(vs_rsync *h) {
     a.spec_fa = h->w_spec_fa.as<uint64_t>();
     a.spec_exit = h->w_spec_exit.as<int64_t>();
     a.spec_exitw = h->w_spec_exitw.as<int32_t>();
+    a.spec_fao = h->w_spec_fao.as<int64_t>();
+    a.spec_fac = h->w_spec_fac.as<uint32_t>();
+    a.spec_nfa = h->w_spec_nfa.as<uint32_t>();
     a.fin_entry = h->w_fin_entry.as<int64_t>();
     a.fin_entryw = h->w_fin_entryw.as<int32_t>();
     a.fin_from = h->w_fin_from.as<uint32_t>();

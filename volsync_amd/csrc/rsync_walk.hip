@@ -559,6 +559,23 @@ struct SegResult {
     int32_t exit_want;
 };
 
+// The speculative walk's false-alarm windows, recorded for the stitch: the
+// offset of each visited window with false alarms and the walk's running
+// total after it (lane 0 writes; n counts past cap on overflow)
+struct FaRec {
+    int64_t *off;
+    uint32_t *cum;
+    uint32_t cap;
+    uint32_t n;
+    __device__ __forceinline__ void add(uint32_t lane, int64_t h, uint64_t fa) {
+        if (lane == 0 && n < cap) {
+            off[n] = h;
+            cum[n] = (uint32_t)fa;
+        }
+        ++n;
+    }
+};
+
 // STEP batch [A, A + 1024): lane l's leaving bytes [A + 16 l, +16) and the
 // entering bytes one block later (A is 16-aligned); bytes past dlen read 0
 __device__ __forceinline__ void batch_load(const RsWalkArgs &a, uint64_t A, uint32_t lane,
@@ -603,7 +620,8 @@ template <uint32_t RING>
 __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const uint32_t *lfilt,
                                   uint32_t lane, int64_t o, int32_t want, int64_t stop,
                                   int64_t *out_off, int32_t *out_idx, int64_t *out_fab,
-                                  uint32_t cap, const SpecView *spec, WProf &wp) {
+                                  uint32_t cap, const SpecView *spec, WProf &wp,
+                                  FaRec *rec = nullptr) {
     const int64_t fend = min(stop, (int64_t)a.full_end);
     const uint64_t L = a.blength;
     const uint8_t *d = a.data;
@@ -663,6 +681,7 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 const uint64_t fa_visit = fa;
                 t0 = wclock(wp);
                 const int32_t i = unis(chain_match(a, wk, lo, hi, want, (uint32_t)L, fa));
+                if (rec && fa != fa_visit) rec->add(lane, oj, fa);
                 wadd(wp, kPrChain, t0);
                 WPROG(a, lane, 3, oj, i);
                 if (i >= 0) {
@@ -879,6 +898,7 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                     const uint64_t fa_visit = fa;
                     WPROG(a, lane, 6, h, j);
                     fa += (uint32_t)__builtin_amdgcn_readlane((int)cfa, (int)j);
+                    if (rec && fa != fa_visit) rec->add(lane, h, fa);
                     const int32_t ci = __builtin_amdgcn_readlane(cidx, (int)j);
                     const int32_t i = ci >= 0 ? unis(chain_prefer(a, ci, sv, lo, hi, want)) : -1;
                     if (i >= 0) {
@@ -1623,11 +1643,14 @@ __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
         const int64_t e = (int64_t)uni64((uint64_t)(k ? seg_lo(a, k) : a.e0));
         const int32_t w = unis(k ? (int32_t)a.count : a.w0);
         const uint64_t base = (uint64_t)k * a.cap;
+        FaRec rec{a.spec_fao + (uint64_t)k * a.facap, a.spec_fac + (uint64_t)k * a.facap,
+                  a.facap, 0};
         const SegResult r = walk_segment<RING>(a, rs, lfilt, lane, e, w, seg_hi(a, k),
                                                a.spec_off + base, a.spec_idx + base,
-                                               a.spec_fab + base, a.cap, nullptr, wp);
+                                               a.spec_fab + base, a.cap, nullptr, wp, &rec);
         wadd(wp, kPrSeg, ts);
         if (lane == 0) {
+            a.spec_nfa[k] = rec.n;
             a.spec_n[k] = r.n;
             a.spec_fa[k] = r.fa;
             a.spec_exit[k] = r.exit_off;
@@ -1690,6 +1713,7 @@ __global__ __launch_bounds__(64 * W, (RB == 32768 ? 3 : 1)) void rs_walk_spec_co
                                                        nullptr, wp, sh, ring);
         wadd(wp, kPrSeg, ts);
         if (wave == 0 && lane == 0) {
+            a.spec_nfa[k] = a.facap + 1;   // not recorded: stitches re-walk
             a.spec_n[k] = r.n;
             a.spec_fa[k] = r.fa;
             a.spec_exit[k] = r.exit_off;
@@ -1711,6 +1735,56 @@ __global__ __launch_bounds__(64 * W, (RB == 32768 ? 3 : 1)) void rs_walk_spec_co
             pr[kPrN + i] = wp.cnt[i];
         }
     }
+}
+
+// the speculative walk of segment k's false alarms in windows below offset x
+// (its recorded running totals; the caller checked they did not overflow)
+__device__ __forceinline__ uint64_t fa_before(const RsWalkArgs &a, uint32_t k, int64_t x) {
+    const int64_t *off = a.spec_fao + (uint64_t)k * a.facap;
+    const uint32_t *cum = a.spec_fac + (uint64_t)k * a.facap;
+    uint32_t lo = 0, hi = uni(a.spec_nfa[k]);
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((int64_t)uni64((uint64_t)off[mid]) < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo ? (uint64_t)uni(cum[lo - 1]) : 0ull;
+}
+
+// A re-walk from (e, w) that the speculative walk of segment k already
+// visited: hash_search's state is (offset, want_i), and the speculative walk
+// visits every offset of [its entry, its exit) outside its matches' blocks.
+// Same state at e: the walks agree from e on, so the final walk is the
+// speculative one from its first match at or after e, with the false alarms
+// of its windows from e on -- no re-walk.  Another want_i: they visit the
+// same offsets until that match (false alarms do not depend on want_i; only
+// the choice among equal blocks does), so r.from = 0xfffffffe asks the caller
+// to re-walk from it (r.n = its index).  False: no shortcut applies.
+__device__ __forceinline__ bool stitch_visited(const RsWalkArgs &a, uint32_t k, const SpecView &sv,
+                                               int64_t e, int32_t w, SegResult &r) {
+    const uint32_t nfa = uni(a.spec_nfa[k]);
+    const int64_t fend = min(seg_hi(a, k), (int64_t)a.full_end);
+    if (nfa > a.facap || e < seg_lo(a, k) || e >= fend || e >= sv.exit_off) return false;
+    uint32_t lo = 0, hi = sv.n;   // first speculative match at or after e
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((int64_t)uni64((uint64_t)sv.off[mid]) < e) lo = mid + 1;
+        else hi = mid;
+    }
+    int32_t wsp = k ? (int32_t)a.count : a.spec_w0;
+    if (lo) {
+        const int32_t pi = unis(sv.idx[lo - 1]);
+        const int64_t pend = (int64_t)uni64((uint64_t)sv.off[lo - 1]) +
+                             (((uint32_t)pi == a.count - 1 && a.remainder) ? a.remainder : a.blength);
+        if (e < pend) return false;   // inside a speculative match's block
+        wsp = pi + 1;
+    }
+    if (w == wsp || lo == sv.n) {
+        r = SegResult{0, lo, sv.fa - fa_before(a, k, e), sv.exit_off, lo == sv.n ? w : sv.exit_want};
+    } else {
+        r = SegResult{lo, 0xfffffffeu, 0, 0, w};
+    }
+    return true;
 }
 
 // one stitch pass: a segment whose entry (the previous segment's exit from
@@ -1741,12 +1815,23 @@ __global__ __launch_bounds__(kWalkThreads) void rs_walk_stitch_kernel(RsWalkArgs
                     uni64(a.spec_fa[k]), (int64_t)uni64((uint64_t)a.spec_exit[k]),
                     unis(a.spec_exitw[k])};
         SegResult r;
-        if (e == seg_lo(a, k) && w == (k ? (int32_t)a.count : a.spec_w0)) {
-            // back to the speculative entry
-            r = SegResult{0, 0, sv.fa, sv.exit_off, sv.exit_want};
-        } else {
-            r = walk_segment<kWalkRing>(a, rs, lfilt, lane, e, w, seg_hi(a, k), a.fin_off + base,
+        int64_t ws = e;     // where the re-walk starts
+        uint64_t fadj = 0;  // false alarms of [e, ws)
+        bool walk = true;
+        if (stitch_visited(a, k, sv, e, w, r)) {
+            walk = r.from == 0xfffffffeu;
+            if (walk) {
+                // the speculative walk visited e with another want_i: both
+                // visit the same offsets up to its next match, where want_i
+                // may choose another of equal blocks -- re-walk from there
+                ws = (int64_t)uni64((uint64_t)sv.off[r.n]);
+                fadj = fa_before(a, k, ws) - fa_before(a, k, e);
+            }
+        }
+        if (walk) {
+            r = walk_segment<kWalkRing>(a, rs, lfilt, lane, ws, w, seg_hi(a, k), a.fin_off + base,
                                     a.fin_idx + base, a.fin_fab + base, a.cap, &sv, wp);
+            r.fa += fadj;
         }
         if (lane == 0) {
             a.fin_entry[k] = e;
