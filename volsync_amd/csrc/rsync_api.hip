@@ -859,7 +859,13 @@ int walk_scan(vs_rsync *h) {
     a.full_end = F - h->blength + 1;
     a.lo = r.own_lo - r.origin;
     a.hi = r.own_hi - r.origin;
-    a.seg_len = std::max<int64_t>((int64_t)h->blength * 32, 1 << 20);
+    {
+        // VSGPU_WALK_SEGBLOCKS=n: segment length in blocks (A/B knob, read
+        // per call; default 32)
+        const char *e = getenv("VSGPU_WALK_SEGBLOCKS");
+        const int64_t sb = e && atoi(e) > 0 ? atoi(e) : 32;
+        a.seg_len = std::max<int64_t>((int64_t)h->blength * sb, 1 << 20);
+    }
     a.nseg = (uint32_t)((a.hi - a.lo + a.seg_len - 1) / a.seg_len);
     a.cap = (uint32_t)(a.seg_len / h->blength + 2);
     a.blength = (uint32_t)h->blength;
