@@ -804,3 +804,29 @@ def test_stitch_merge_at_visited_entry(gpu, monkeypatch, facap, data):
     m.close()
     assert len(want) > 1000
     assert got == want and st["false_alarms"] == fa
+
+
+@pytest.mark.parametrize("tailpct", ["30", "90"])
+def test_walk_short_tail_segments(gpu, monkeypatch, tailpct):
+    """VSGPU_WALK_TAILPCT: the last part of the range in quarter-length
+    segments (the segments the last waves pick up): the same match list and
+    false alarms as hash_search, one device and byte-range sharded."""
+    from volsync_amd import Matcher, SumStruct
+    monkeypatch.setenv("VSGPU_WALK_TAILPCT", tailpct)
+    csum, seed = R.CSUM_XXH3_128, 0x5EED5EED
+    n = 40 << 20
+    basis = O.synth(52, 0, n)
+    bl, s2l, cnt, rem = O.rsync_sizes(n, 65536)   # 2 MiB segments, 1 MiB in the tail
+    src = R.mutate(basis, bl, seed=9, frac=0.15)
+    c1, c2 = O.rsync_signatures(basis, bl, s2l, csum, seed)
+    want, fa = O.rsync_match(src, c1, c2, bl, rem, csum, seed)
+    s = SumStruct(n, cnt, bl, s2l, rem, c1, c2)
+    ds = to_dev(src)
+    m = Matcher()
+    m.load_sums(s, csum, seed)
+    got = m.match_sums(ds.data_ptr(), len(src))
+    st = m.stats()
+    m.close()
+    assert got == want and st["false_alarms"] == fa
+    got3, fa3 = _sharded_device_match(src, s, 3, csum, seed)
+    assert got3 == want and fa3 == fa

@@ -391,6 +391,8 @@ struct RsWalkArgs {
     int64_t full_end;      // offsets below it have a full window (F - blength + 1)
     int64_t lo, hi;        // the owned range
     int64_t seg_len;
+    uint32_t nseg1;        // segments [0, nseg1) are seg_len long, the rest seg_len2
+    int64_t seg_len2;
     uint32_t nseg, cap;    // segments, match capacity per segment
     uint32_t blength, count, remainder;
     int csum_type;

@@ -867,6 +867,21 @@ int walk_scan(vs_rsync *h) {
         a.seg_len = std::max<int64_t>((int64_t)h->blength * sb, 1 << 20);
     }
     a.nseg = (uint32_t)((a.hi - a.lo + a.seg_len - 1) / a.seg_len);
+    a.nseg1 = a.nseg;
+    a.seg_len2 = a.seg_len;
+    {
+        // VSGPU_WALK_TAILPCT=p: the last p % of the range in quarter-length
+        // segments, so the waves that finish last hold short segments (A/B knob)
+        const char *e = getenv("VSGPU_WALK_TAILPCT");
+        const int tp = e ? atoi(e) : 0;
+        if (tp > 0 && tp < 100) {
+            const int64_t total = a.hi - a.lo;
+            a.seg_len2 = std::max<int64_t>(a.seg_len / 4, 1 << 20);
+            a.nseg1 = (uint32_t)(total * (100 - tp) / 100 / a.seg_len);
+            const int64_t rest = total - (int64_t)a.nseg1 * a.seg_len;
+            a.nseg = a.nseg1 + (uint32_t)((rest + a.seg_len2 - 1) / a.seg_len2);
+        }
+    }
     a.cap = (uint32_t)(a.seg_len / h->blength + 2);
     a.blength = (uint32_t)h->blength;
     a.count = (uint32_t)h->count;
@@ -904,9 +919,12 @@ int walk_scan(vs_rsync *h) {
     VS_TRY(h->w_fin_idx.ensure(nc * 4));
     VS_TRY(h->w_fin_fab.ensure(nc * 8));
     VS_TRY(h->w_spec_n.ensure(ns * 4));
-    // false-alarm windows of the speculative walks: 1024 per segment (a 4 MiB
-    // segment of the real C4 averages ~200; more falls back to a re-walk)
-    a.facap = 1024;
+    // false-alarm windows of the speculative walks: up to 1024 per segment (a
+    // 4 MiB segment of the real C4 averages ~200; more falls back to a
+    // re-walk), at most 256 MiB of records per walk (small blocks, many
+    // segments)
+    a.facap = (uint32_t)std::max<uint64_t>(
+        64, std::min<uint64_t>(1024, (256ull << 20) / (12ull * std::max<uint32_t>(a.nseg, 1))));
     {
         // VSGPU_WALK_FACAP=n (tests): a smaller record, so stitches fall
         // back to re-walks (read per call)
