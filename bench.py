@@ -303,12 +303,29 @@ def rsync_main(args):
         b_lo = min(-(-sspec.own_lo // 1024), nb_file)
         b_hi = min(-(-sspec.own_hi // 1024), nb_file)
         fs_blocks = (ds.data_ptr() + b_lo * 1024 - sspec.data_lo, b_hi - b_lo)
-    fs_on = (world == 1 or share) and not args.no_file_sum
+    fs_on = not args.no_file_sum
     fs_out = []
     fs_inflight = [0]
+    relay = None
+    if fs_on and world > 1 and not share:
+        # N ranks: the XXH3 state relayed rank to rank (rsync_shard.FileSumRelay)
+        # over a gloo group of its own, one relay thread per rank; files
+        # (steps) pipeline through the ranks, so the rate is one rank's chain
+        # per step once the pipeline is full
+        from volsync_amd.rsync_shard import FileSumRelay, torch_relay_p2p
+        rg = dist.new_group(backend="gloo")
+        tail_n = min(plan.total, 1088)
+        relay = FileSumRelay(
+            fsm, sspec, ds.data_ptr(), sspec.data_lo, *torch_relay_p2p(rank, world, rg),
+            last=lambda: ds[plan.total - tail_n - sspec.data_lo:plan.total - sspec.data_lo]
+            .cpu().numpy().tobytes())
 
     def fs_start():
         if not fs_on:
+            return
+        if relay is not None:
+            relay.submit()
+            fs_inflight[0] += 1
             return
         if fs_inflight[0] == args.file_sum_jobs:
             fs_wait()
@@ -319,6 +336,11 @@ def rsync_main(args):
         fs_inflight[0] += 1
 
     def fs_wait():
+        if relay is not None:
+            for r in relay.results():
+                fs_out.append((r, fsm.file_sum_timing()))
+            fs_inflight[0] = 0
+            return
         r = fsm.file_sum_wait() if fs_blocks is None else fsm.file_sum_blocks_wait()
         fs_inflight[0] -= 1
         fs_out.append((r.hex() if isinstance(r, bytes) else
@@ -369,38 +391,85 @@ def rsync_main(args):
     dt = time.perf_counter() - t0
     kt = m.kernel_time()
     st = m.stats()
+    # exactness evidence: the last step's match list as vs_match records
+    # (SHA-256, tests/golden/make_golden_full.py), gathered in rank order
+    import hashlib
+    recs = _match_records(m, nm)
+    mine_fa = st["false_alarms"]
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=coll_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        c = torch.tensor([nm], dtype=torch.int64, device=coll_device(dev))
+        c = torch.tensor([nm, mine_fa], dtype=torch.int64, device=coll_device(dev))
         dist.all_reduce(c)
-        nm = int(c.item())
+        nm, tot_fa = int(c[0].item()), int(c[1].item())
+        parts = [None] * world if rank == 0 else None
+        dist.gather_object(recs, parts, dst=0)
+        digest = hashlib.sha256(b"".join(parts)).hexdigest() if rank == 0 else None
+    else:
+        tot_fa = mine_fa
+        digest = hashlib.sha256(recs).hexdigest()
+    exact = {"matches": nm, "false_alarms": tot_fa, "digest": digest}
+    g = _golden_rsync(dtotal)
+    if share:
+        gr = (g or {}).get("ranks", {}).get(str(sw))
+        exact = {"matches_rank": st["matches"], "false_alarms_rank": mine_fa,
+                 "digest_rank": digest}
+        if gr:
+            want = gr[sr]
+            exact["golden_entry"] = want["entry"]
+            exact["golden_match"] = (want["matches"], want["false_alarms"], want["digest"]) == \
+                (st["matches"], mine_fa, digest)
+    elif g:
+        exact["golden_match"] = (g["matches"], g["false_alarms"], g["digest"]) == \
+            (nm, tot_fa, digest)
     own_src = sspec.own_hi - sspec.own_lo
     # a --share line counts the rank's own bytes: its D blocks and S range
     value = ((n + own_src) if share else (dtotal + plan.total)) * args.steps / dt / 1e9
     fsum = None
     if fs_on:
-        # the same checksum alone, after the timed region: its latency
+        # the same checksum alone, after the timed region: its latency (the
+        # whole relay through every rank when N > 1)
         torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
         t1 = time.perf_counter()
         fs_start()
         fs_wait()
         fs_dt = time.perf_counter() - t1
         digests = {d for d, _ in fs_out}
         tm = fs_out[-1][1]
-        fbytes = plan.total if fs_blocks is None else fs_blocks[1] * 1024
-        fsum = {"inside_step": True, "jobs_in_flight": args.file_sum_jobs,
+        fbytes = (plan.total if fs_blocks is None and relay is None else
+                  relay.nblocks * 1024 if relay is not None else fs_blocks[1] * 1024)
+        digest = sorted(digests)[0]
+        if relay is not None:
+            # the file's digest comes out of the last rank
+            allv = [None] * world
+            dist.all_gather_object(allv, (digest, len(digests), relay.nblocks))
+            digest, ndig = allv[-1][0], allv[-1][1]
+            digests = set([digest]) if ndig == 1 else set(range(ndig))
+            chained = sum(v[2] for v in allv)
+            relay.close()
+        fsum = {"inside_step": True,
+                "jobs_in_flight": args.file_sum_jobs if relay is None else "relay pipeline",
                 "ms_alone": round(fs_dt * 1e3, 2), "GBps_alone": round(fbytes / fs_dt / 1e9, 2),
                 "contrib_kernel_ms": round(tm["device_ms"], 2),
                 "host_chain_ms": round(tm["host_chain_ms"], 2),
                 "host_chain_ns_per_KiB": round(tm["host_chain_ms"] * 1e6 / max(fbytes / 1024, 1), 3),
                 "gpu_steps_done_ms_per_step": round((t_gpu - t0) / args.steps * 1e3, 3),
                 "bytes": fbytes, "csum": "xxh128 (unseeded, as sum_init)",
-                "scope": ("whole file S" if fs_blocks is None else
-                          f"the rank's {fs_blocks[1]} whole 1 KiB blocks of S (stand-in relay state)"),
-                "digest" if fs_blocks is None else "state_out": sorted(digests)[0],
+                "scope": ("whole file S" if fs_blocks is None and relay is None else
+                          f"whole file S, relayed over {world} ranks ({chained} blocks chained; "
+                          f"this rank's chain: {fbytes} B)" if relay is not None else
+                          f"the rank's {fs_blocks[1]} whole 1 KiB blocks of S from a stand-in "
+                          f"relay state: the steady state of the relay pipeline, whose predecessor "
+                          f"states arrive once per step; the pipeline's fill latency (N - 1 "
+                          f"chains) is not included"),
+                "digest" if fs_blocks is None else "state_out": digest,
                 "identical_every_step": len(digests) == 1}
+        g = _golden_rsync(dtotal)
+        if g and "file_sum" in g and fs_blocks is None:
+            fsum["golden_match"] = digest == g["file_sum"]
     # the dominant kernel: rs_walk_spec_kernel, one launch per step over the
     # rank's whole source range (algorithmic bytes = those source bytes, each
     # read once by the walk: a window hash where it matches, the rolling scan
@@ -447,6 +516,7 @@ def rsync_main(args):
             "dist_backend": dist.get_backend() if world > 1 else None,
             "exchange_rounds_last_step": xst.get("exchange_rounds", 0),
             "file_sum": fsum,
+            "exact": exact,
         }
         try:
             tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
@@ -953,6 +1023,171 @@ def host_main(args):
     }), flush=True)
 
 
+def rsync_host_main(args):
+    """C4 fed from host memory through the streamed drop-in path, as rsync's
+    generator and sender read files (map_ptr windows): the destination D
+    through vs_rsync_sig_begin/feed/next (generate_and_send_sums), the sums
+    loaded (build_hash_table), the source S through vs_rsync_match_begin/
+    feed/next (match_sums), in --read-mib reads from pinned host images, the
+    device holding only a ring of 3 x 256 MiB pieces per stream.  A step = both
+    files streamed and every sum and match returned to the host.  value =
+    (|D| + |S|) / wall time, H2D included; the H2D rate
+    of the same pinned buffers is measured beside it."""
+    import ctypes
+    import hashlib
+    import numpy as np
+    import torch
+    from volsync_amd import Matcher, sum_sizes_sqroot, synth_fill_device
+    from volsync_amd._lib import VS_EOF, VsMatch, check, lib
+    from volsync_amd.rsync import CSUM_XXH3_128
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dlen = int(args.per_gpu_gib * (1 << 30))
+    hdr = sum_sizes_sqroot(dlen)
+    plan = C4Plan(dlen, hdr.blength)
+    seed = 0x5EED5EED
+    hd = torch.empty(dlen, dtype=torch.uint8, pin_memory=True)
+    hs = torch.empty(plan.total, dtype=torch.uint8, pin_memory=True)
+    piece = 4 << 30
+    tmp = torch.empty(piece, dtype=torch.uint8, device=dev)
+    for off in range(0, dlen, piece):
+        k = min(piece, dlen - off)
+        synth_fill_device(tmp.data_ptr(), C4Plan.D_SEED, off, k)
+        hd[off:off + k].copy_(tmp[:k])
+    for off in range(0, plan.total, piece):
+        k = min(piece, plan.total - off)
+        plan.fill_device(tmp.data_ptr(), off, off + k)
+        torch.cuda.synchronize(dev)
+        hs[off:off + k].copy_(tmp[:k])
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    tmp.copy_(hs[:piece], non_blocking=True)
+    torch.cuda.synchronize(dev)
+    h2d = piece / (time.perf_counter() - t) / 1e9
+    del tmp
+    torch.cuda.empty_cache()
+    m = Matcher(0)
+    read = args.read_mib << 20
+    cnt, s2l = hdr.count, hdr.s2length
+    sum1 = np.zeros(max(cnt, 1), np.uint32)
+    sum2 = np.zeros(max(cnt, 1) * s2l, np.uint8)
+    mcap = 1 << 16
+    marr = (VsMatch * mcap)()
+    got = ctypes.c_size_t(0)
+    h = m._h
+
+    def step():
+        t0 = time.perf_counter()
+        # generate_and_send_sums: D in `read` pieces, sums collected as they finish
+        check(lib.vs_rsync_sig_begin(h, dlen, hdr.blength, s2l, CSUM_XXH3_128, seed, 0, 0))
+        ns = 0
+        base = hd.data_ptr()
+        for off in range(0, dlen + read, read):
+            if off < dlen:
+                check(lib.vs_rsync_sig_feed(h, ctypes.c_void_p(base + off), min(read, dlen - off)))
+            while True:
+                rc = check(lib.vs_rsync_sig_next(h, sum1[ns:].ctypes.data,
+                                                 sum2[ns * s2l:].ctypes.data, cnt - ns,
+                                                 ctypes.byref(got)))
+                ns += got.value
+                if rc == VS_EOF or not got.value:
+                    break
+            if rc == VS_EOF:
+                break
+        assert ns == cnt, (ns, cnt)
+        t1 = time.perf_counter()
+        check(lib.vs_rsync_load_sums(h, cnt, hdr.blength, s2l, hdr.remainder, sum1.ctypes.data,
+                                     sum2.ctypes.data, CSUM_XXH3_128, seed))
+        t2 = time.perf_counter()
+        # match_sums: S in `read` pieces, matches drained after every read
+        check(lib.vs_rsync_match_begin(h, plan.total, 0, 0))
+        nm = 0
+        dig = hashlib.sha256()
+        base = hs.data_ptr()
+        off = 0
+        while True:
+            if off < plan.total:
+                check(lib.vs_rsync_match_feed(h, ctypes.c_void_p(base + off),
+                                              min(read, plan.total - off)))
+                off += read
+            rc = check(lib.vs_rsync_match_next(h, marr, mcap, ctypes.byref(got)))
+            if got.value:
+                nm += got.value
+                dig.update(ctypes.string_at(marr, got.value * 16))
+            if rc == VS_EOF:
+                break
+        nm2, fa = ctypes.c_int64(), ctypes.c_int64()
+        check(lib.vs_rsync_match_end(h, ctypes.byref(nm2), ctypes.byref(fa)))
+        assert nm2.value == nm
+        t3 = time.perf_counter()
+        return {"sig_s": t1 - t0, "load_s": t2 - t1, "match_s": t3 - t2, "matches": nm,
+                "false_alarms": fa.value, "digest": dig.hexdigest()}
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    res = []
+    for _ in range(args.steps):
+        res.append(step())
+    dt = time.perf_counter() - t0
+    st = m.match_stream_stats()
+    m.close()
+    total = dlen + plan.total
+    r = res[-1]
+    golden = _golden_rsync(dlen)
+    out = {
+        "metric": "GB/s rsync delta match (|D|+|S|), host-pinned end-to-end via the streamed "
+                  "vs_rsync_sig_* / vs_rsync_match_* path",
+        "value": round(total * args.steps / dt / 1e9, 2), "unit": "GB/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": f"synthetic (C4 destination + 10%-edited source in pinned host memory, fed in "
+                f"{args.read_mib} MiB reads)",
+        "config": {"workload": f"C4-shape streamed: {dlen >> 30} GiB destination, "
+                               f"{plan.total} B source, 1 GPU, device window 3 x 256 MiB per "
+                               f"stream (H2D included)",
+                   "blength": hdr.blength, "s2length": s2l, "count": cnt, "csum": "xxh128",
+                   "checksum_seed": hex(seed), "read_bytes": read},
+        "h2d_GBps": round(h2d, 2), "frac_of_h2d": round(total * args.steps / dt / 1e9 / h2d, 4),
+        "stages_GBps": {"signatures_stream": round(dlen / r["sig_s"] / 1e9, 2),
+                        "match_stream": round(plan.total / r["match_s"] / 1e9, 2),
+                        "load_sums_ms": round(r["load_s"] * 1e3, 2)},
+        "match_stream_stats": st,
+        "matches": r["matches"], "false_alarms": r["false_alarms"], "digest": r["digest"],
+        "identical_every_step": len({x["digest"] for x in res}) == 1,
+    }
+    if golden:
+        out["golden_match"] = (r["digest"] == golden["digest"] and r["matches"] == golden["matches"]
+                               and r["false_alarms"] == golden["false_alarms"])
+    print(json.dumps(out), flush=True)
+
+
+def _match_records(m, n: int) -> bytes:
+    """The handle's last match list as 16-byte vs_match records."""
+    import ctypes
+    from volsync_amd._lib import VsMatch, check, lib
+    arr = (VsMatch * max(n, 1))()
+    if n:
+        check(lib.vs_rsync_get_matches(m._h, 0, n, arr))
+    return ctypes.string_at(arr, n * 16) if n else b""
+
+
+def _goldens() -> dict:
+    """tests/golden/full_configs.json (tests/golden/make_golden_full.py): the
+    full-size chunk / match list digests from the C oracle, computed in the
+    build container; {} when absent."""
+    try:
+        return json.load(open(os.path.join(ROOT, "tests", "golden", "full_configs.json")))
+    except (OSError, ValueError):
+        return {}
+
+
+def _golden_rsync(dlen: int):
+    return _goldens().get("rsync", {}).get(str(dlen))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -978,10 +1213,14 @@ def main():
                          "wavefronts (0 = library default, 0xffffffff = never)")
     ap.add_argument("--wide-drain", type=int, default=0,
                     help="blocks per throughput-mode drain launch (0 = library default)")
-    ap.add_argument("--mode", choices=["cdc", "rsync", "smallfiles", "host", "seal"], default="cdc",
+    ap.add_argument("--mode", choices=["cdc", "rsync", "smallfiles", "host", "seal", "rsync-host"],
+                    default="cdc",
                     help="cdc: C2/C3 chunk+hash (the BASELINE metric); rsync: C4-shape delta "
                          "match; smallfiles: C5 per-file blob IDs; host: C2 streamed from "
-                         "pinned host memory through vs_cdc_feed/next")
+                         "pinned host memory through vs_cdc_feed/next; rsync-host: C4 streamed "
+                         "from pinned host memory through vs_rsync_sig_*/vs_rsync_match_*")
+    ap.add_argument("--read-mib", type=int, default=64,
+                    help="rsync-host: bytes per feed (the reader's read size)")
     ap.add_argument("--files", type=int, default=1_000_000, help="smallfiles: files per GPU")
     ap.add_argument("--share", default=None, metavar="R/N",
                     help="rsync: run rank R's share of the N-rank problem on this one GPU "
@@ -1009,6 +1248,8 @@ def main():
         return seal_main(args)
     if args.mode == "host":
         return host_main(args)
+    if args.mode == "rsync-host":
+        return rsync_host_main(args)
 
     import torch
     import torch.distributed as dist
@@ -1077,6 +1318,21 @@ def main():
     dc.wait()
     lat = time.perf_counter() - t1
     iso_ms, iso_launch = dc.timing(False)
+    # exactness evidence: the chunk list (this rank's chunks, gathered in rank
+    # order) as vs_chunk records, SHA-256 -> golden (tests/golden/
+    # make_golden_full.py); outside the timed region
+    import ctypes
+    import hashlib
+    from volsync_amd._lib import VsChunk, check, lib
+    arr = (VsChunk * max(nch, 1))()
+    if nch:
+        check(lib.vs_cdc_get_chunks(dc._h, 0, nch, arr))
+    recs = ctypes.string_at(arr, 56 * nch) if nch else b""
+    if world > 1:
+        parts = [None] * world if rank == 0 else None
+        dist.gather_object(recs, parts, dst=0)
+        recs = b"".join(parts) if rank == 0 else b""
+    cdigest = hashlib.sha256(recs).hexdigest()
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=coll_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1175,7 +1431,13 @@ def main():
             "single_volume": {"ms": round(lat * 1e3, 2),
                               "GBps": round(total / lat / 1e9, 2),
                               "stages_ms": iso},
+            "exact": {"chunks": nch, "digest": cdigest},
         }
+        gc = _goldens().get("cdc", {})
+        gold = (gc.get("c2") if world == 1 and seed == 2 else
+                gc.get("c3_prefix", {}).get(str(total)) if seed == 3 else None)
+        if gold and gold.get("bytes") == total and gold.get("seed") == seed:
+            out["exact"]["golden_match"] = (gold["chunks"], gold["digest"]) == (nch, cdigest)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_gib << 30, args.cpu_threads)
         print(json.dumps(out), flush=True)

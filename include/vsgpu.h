@@ -302,8 +302,10 @@ int vs_rsync_timing(vs_rsync *h, double ms_out[5]);
  * as sum_end writes it -- xxh128: LE low64 then LE high64; xxh3 / xxh64: LE
  * 64-bit value (out[8..15] zeroed); md5: the digest.  XXH3 runs as parallel
  * block contributions on the device plus one serial scramble chain on a host
- * thread; MD5 and XXH64 run the one-lane restatement.  Blocks
- * until done. */
+ * thread; MD5 and XXH64 -- serial chains with no parallel
+ * form -- are hashed on a library host thread from the file's bytes read back
+ * through the same pinned ring.  Any length.  Blocks until done; jobs other
+ * calls left in flight stay in flight (their _wait order is unchanged). */
 int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_type,
                       uint8_t out[16]);
 /* The same, asynchronous: _start queues the device part (after work queued on
@@ -311,20 +313,21 @@ int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_ty
  * runs on a library thread while the caller goes on (e.g. with the match walk
  * over the same file).  dev_src must stay valid and unchanged until its _wait.
  * Up to 4 jobs (whole files or block ranges) may be in flight per handle,
- * each with its own host thread: _wait returns the OLDEST job's digest (jobs
- * complete in start order; the _blocks_ form shares the queue).  MD5 / XXH64
- * file sums are one serial chain on one GPU lane and are refused above
- * 256 MiB (VS_ERR_ARG). */
+ * each with its own host thread and 3 pieces of device memory: _wait returns
+ * the OLDEST job's digest (jobs complete in start order; the _blocks_ form
+ * shares the queue). */
 int vs_rsync_file_sum_start(vs_rsync *h, const void *dev_src, int64_t len, int csum_type);
 int vs_rsync_file_sum_wait(vs_rsync *h, uint8_t out[16]);
 /* A file split by byte range across ranks: the XXH3 state is a
  * relay.  _blocks_start chains the nblocks whole 1 KiB blocks at dev_blocks
  * (file offset a multiple of 1024) from acc_in (NULL: the initial state,
  * vs_rsync_file_sum_init); _blocks_wait returns the state after them, which
- * the next range's owner takes as its acc_in.  The owner of the file's last
- * byte finishes with vs_rsync_file_sum_finish over the file's last
- * min(len, 1088) bytes (host memory).  XXH3 only (xxh128 and xxh3 share the
- * state; len > 240). */
+ * the next range's owner takes as its acc_in.  The ranks together must chain
+ * exactly the file's first (len - 1) / 1024 whole blocks: the block holding
+ * byte len - 1 is always the finish's partial block, even when len % 1024 ==
+ * 0.  The owner of the file's last byte finishes with
+ * vs_rsync_file_sum_finish over the file's last min(len, 1088) bytes (host
+ * memory).  XXH3 only (xxh128 and xxh3 share the state; len > 240). */
 int vs_rsync_file_sum_init(uint64_t acc[8]);
 int vs_rsync_file_sum_blocks_start(vs_rsync *h, const void *dev_blocks, int64_t nblocks,
                                    const uint64_t acc_in[8]);
@@ -350,7 +353,48 @@ int vs_rsync_reconstruct(vs_rsync *h, void *dev_out, int64_t out_len, const void
  * reset != 0 zeroes the totals after reading them. */
 int vs_rsync_kernel_time(vs_rsync *h, int which, int reset, double *ms, int64_t *launches);
 
-/* Host-memory one-shot forms: copy in, run, copy out. */
+/* ---- streamed forms: a file fed from host memory in order ---------------
+ * rsync reads files through map_ptr (fileio.c), a sliding window with an
+ * int32 length, never the whole file at once.  These entry points take the
+ * file the same way -- any number of feeds of any size, in file order -- and
+ * keep only a ring of `ring` pieces of `piece_bytes` on the device (0, 0 =
+ * 256 MiB x 3), so files far larger than HBM pass.  Fed bytes are copied
+ * before feed returns (pinned caller memory by DMA, pageable memory through
+ * the library's staging buffers).  A handle runs one stream of each kind at
+ * a time; while a match stream runs, call only its _feed / _next / _end on
+ * the handle (its walk thread uses the handle's table and buffers).
+ *
+ * Replaces match.c match_sums -> hash_search over a file of file_len bytes
+ * (the table from vs_rsync_load_sums[_device]).  Each piece is walked by a
+ * library thread from the previous piece's exit state as soon as its bytes
+ * and a blength - 1 halo are on the device, while the caller feeds the next
+ * ones.  The match list is exactly vs_rsync_match_device's over the whole
+ * file, false alarms included.
+ * _next: matches found so far, in file order (*n_out may be 0 before the
+ * last feed; after it, _next waits for the walk); VS_EOF once every match has
+ * been returned.  _end waits for the walk and gives the totals (the match
+ * list then also stays readable through vs_rsync_get_matches). */
+int vs_rsync_match_begin(vs_rsync *h, int64_t file_len, uint64_t piece_bytes, uint32_t ring);
+int vs_rsync_match_feed(vs_rsync *h, const void *buf, size_t n);
+int vs_rsync_match_next(vs_rsync *h, vs_match *out, size_t cap, size_t *n_out);
+int vs_rsync_match_end(vs_rsync *h, int64_t *n_matches, int64_t *false_alarms);
+/* [0] bytes fed from pinned memory, [1] bytes staged, [2] caller ms waiting
+ * for a free piece slot, [3] walk-thread ms walking, [4] walk-thread ms
+ * waiting for bytes, [5] pieces walked, [6] piece bytes, [7] ring */
+int vs_rsync_match_stream_stats(vs_rsync *h, double out[8]);
+/* Replaces generator.c generate_and_send_sums over a basis file of len bytes
+ * read in order: pieces of whole blocks are signed as they arrive; _next
+ * returns the sums of finished blocks in block order (sum1 [n] u32, sum2
+ * [n * s2length]), waiting for the oldest piece in flight when none is
+ * ready; VS_EOF after the last block. */
+int vs_rsync_sig_begin(vs_rsync *h, int64_t len, int32_t blength, int32_t s2length,
+                       int csum_type, uint32_t seed, uint64_t piece_bytes, uint32_t ring);
+int vs_rsync_sig_feed(vs_rsync *h, const void *buf, size_t n);
+int vs_rsync_sig_next(vs_rsync *h, uint32_t *sum1, uint8_t *sum2, size_t cap_blocks,
+                      size_t *n_blocks);
+
+/* Host-memory one-shot forms: the streamed forms above over
+ * one host buffer (the device holds at most the piece ring, whatever len is). */
 int vs_rsync_signatures(int device, const void *basis, int64_t len, int32_t blength,
                         int32_t s2length, int csum_type, uint32_t seed, uint32_t *sum1,
                         uint8_t *sum2);
@@ -424,6 +468,20 @@ int vs_restic_pack(vs_seal *h, vs_sha *sha, const void *dev_in, const uint64_t *
                    const uint8_t *blob_nonces, const uint8_t *hdr_nonces, uint64_t min_pack_size,
                    uint8_t *dev_out, uint64_t out_cap, vs_pack *packs, size_t pack_cap,
                    size_t *n_packs, uint64_t *out_len, uint8_t *pack_ids, void *hip_stream);
+/* restic v0.13.1 internal/index Index.Encode + repository.SaveUnpacked: the
+ * index file of the packs vs_restic_pack made from the same blobs (same len,
+ * types, ids, n, min_pack_size; pack_ids as it returned them).  The JSON is
+ * {"packs":[{"id":...,"blobs":[{"id":...,"type":"data"|"tree","offset":o,
+ * "length":l}...]}...]} plus a newline, l = the stored record length
+ * (plaintext + 32) and o its offset in the pack; packs in finalize order,
+ * blobs in pack order (restic's own order follows a randomly seeded hash map;
+ * its DecodeIndex reads any).  json_out (NULL: size only) receives it;
+ * file_out (NULL: JSON only) the stored file nonce || Key.Seal(JSON) || tag
+ * (*json_n + 32 bytes), file_id its SHA-256 (the name in the repository). */
+int vs_restic_index(vs_seal *h, vs_sha *sha, const uint32_t *len, const uint8_t *types,
+                    const uint8_t *ids, size_t n, uint64_t min_pack_size, const uint8_t *pack_ids,
+                    const uint8_t nonce[16], uint8_t *json_out, size_t json_cap, size_t *json_n,
+                    uint8_t *file_out, uint8_t file_id[32]);
 void vs_seal_close(vs_seal *h);
 
 /* ---- wire formats (host code, no device needed) -------
@@ -478,6 +536,33 @@ int vs_rsync_read_tokens_zstd(vs_ztok *z, const uint8_t *in, size_t n, int32_t b
  * 37 bytes per entry.  out == NULL: *n_out = the size only. */
 int vs_restic_pack_header(const uint8_t *types, const uint32_t *lengths, const uint8_t *ids,
                           size_t n, uint8_t *out, size_t cap, size_t *n_out);
+
+/* ---- options -----------------------------------------------------------
+ * The library reads no environment variables: the few settings a test or a
+ * measurement needs to change are set per handle here.  The defaults are the
+ * product settings; results are identical under every option (they change
+ * which kernels run or how work is split, never what is computed). */
+#define VS_OPT_WALK_SEGMENT_BLOCKS 1 /* rsync: device walk segment length in blocks
+                                      * (0 = automatic: 32, shorter for ranges too
+                                      * small to give every wave two segments) */
+#define VS_OPT_FILE_SUM_PIECE 2      /* rsync: file-sum read-back piece in 1 KiB blocks
+                                      * (0 = 2^18: 16 MiB of contribution rows) */
+#define VS_OPT_BUCKET_BITS 3         /* rsync: log2 of the walk's membership buckets,
+                                      * applied at the next load_sums (0 = automatic) */
+#define VS_OPT_FA_RECORD 4           /* rsync: false-alarm windows recorded per walk
+                                      * segment for stitch merges (-1 = automatic) */
+#define VS_OPT_HOST_WALK 5           /* rsync: 1 = the host walk with device
+                                      * verification for every checksum type */
+#define VS_OPT_SHA_QUAD_PCT 16       /* cdc / sha: chains within this % of the longest
+                                      * run in latency (quad) mode in the final drain
+                                      * (default 80; 0 = split mode only) */
+#define VS_OPT_FP_GENERIC 17         /* cdc: 1 = the generic fingerprint address code
+                                      * even where the FAST variant applies */
+#define VS_OPT_SEAL_FUSED 32         /* seal: 0 = separate CTR and MAC kernels (default 1) */
+int vs_rsync_set_option(vs_rsync *h, int option, int64_t value);
+int vs_cdc_set_option(vs_cdc *h, int option, int64_t value);
+int vs_sha256_set_option(vs_sha *h, int option, int64_t value);
+int vs_seal_set_option(vs_seal *h, int option, int64_t value);
 
 /* ---- device utilities for benches and tests --------------------------- */
 /* Fill dev_out[0:n] with bytes [off, off+n) of the synthetic splitmix64

@@ -512,11 +512,33 @@ int64_t ref_rsync_match(const uint8_t *src, int64_t len, int32_t count, int32_t 
  * whole source file's length.  Matches with offset in [entry, hi) are
  * emitted in order; returns #matches or -1.  Walking [0, len) from (0, 0)
  * reproduces ref_rsync_match exactly. */
+/* ref_rsync_walk_fab: the same walk; m_fab (optional, cap entries) receives
+ * the false alarms counted before each match's offset was visited -- what the
+ * full-size golden script (tests/golden/make_golden_full.py) needs to merge a
+ * walk from the true entry into a speculative one. */
+int64_t ref_rsync_walk_fab(const uint8_t *win, int64_t win_lo, int64_t len, int64_t hi,
+                           int64_t entry, int32_t entry_want, int32_t count, int32_t blength,
+                           int32_t remainder, int32_t s2length, const uint32_t *sum1,
+                           const uint8_t *sum2, int csum_type, uint32_t seed, int64_t *m_off,
+                           int32_t *m_idx, int64_t *m_fab, int64_t cap, int64_t *false_alarms,
+                           int64_t *exit_off, int32_t *exit_want);
+
 int64_t ref_rsync_walk(const uint8_t *win, int64_t win_lo, int64_t len, int64_t hi, int64_t entry,
                        int32_t entry_want, int32_t count, int32_t blength, int32_t remainder,
                        int32_t s2length, const uint32_t *sum1, const uint8_t *sum2, int csum_type,
                        uint32_t seed, int64_t *m_off, int32_t *m_idx, int64_t cap,
                        int64_t *false_alarms, int64_t *exit_off, int32_t *exit_want) {
+    return ref_rsync_walk_fab(win, win_lo, len, hi, entry, entry_want, count, blength, remainder,
+                              s2length, sum1, sum2, csum_type, seed, m_off, m_idx, NULL, cap,
+                              false_alarms, exit_off, exit_want);
+}
+
+int64_t ref_rsync_walk_fab(const uint8_t *win, int64_t win_lo, int64_t len, int64_t hi,
+                           int64_t entry, int32_t entry_want, int32_t count, int32_t blength,
+                           int32_t remainder, int32_t s2length, const uint32_t *sum1,
+                           const uint8_t *sum2, int csum_type, uint32_t seed, int64_t *m_off,
+                           int32_t *m_idx, int64_t *m_fab, int64_t cap, int64_t *false_alarms,
+                           int64_t *exit_off, int32_t *exit_want) {
     int64_t nm = 0, fa = 0;
     *exit_off = entry > hi ? entry : hi;
     *exit_want = entry_want;
@@ -547,6 +569,7 @@ int64_t ref_rsync_walk(const uint8_t *win, int64_t win_lo, int64_t len, int64_t 
     for (;;) {
         int done_csum2 = 0;
         int32_t i;
+        const int64_t fa_visit = fa;
         sum = (s1 & 0xffff) | (s2 << 16);
         uint32_t hash_entry = trad ? ((s1 + s2) & 0xffff) : sum % tablesize;
         if ((i = table[hash_entry]) < 0) goto null_hash;
@@ -569,7 +592,11 @@ int64_t ref_rsync_walk(const uint8_t *win, int64_t win_lo, int64_t len, int64_t 
                 memcmp(sum2buf, sum2 + (int64_t)want_i * s2length, (size_t)s2length) == 0)
                 i = want_i;
             want_i = i + 1;
-            if (nm < cap) { m_off[nm] = offset; m_idx[nm] = i; }
+            if (nm < cap) {
+                m_off[nm] = offset;
+                m_idx[nm] = i;
+                if (m_fab) m_fab[nm] = fa_visit;
+            }
             nm++;
             offset += BLEN(i) - 1;
             if (offset + 1 >= hi || offset + 1 >= end) {   /* next visit is past the shard */

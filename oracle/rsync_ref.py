@@ -204,3 +204,54 @@ def mutate(basis: np.ndarray, blength: int, seed: int, frac: float = 0.10, run: 
             pos = min(len(basis), at + d)
     parts.append(basis[pos:])
     return np.concatenate(parts) if parts else basis.copy()
+
+
+# ---- whole-file XXH3 as a relay of accumulator states (R7 across ranks) ----
+# The public XXH3 long-input algorithm (xxhash 0.8 XXH3_hashLong, default
+# secret, no seed -- rsync 3.2.3's sum_init seeds no xxhash file sum): eight
+# 64-bit accumulators; each 64-byte stripe n of a 1 KiB block adds its words
+# (acc[i ^ 1] += d_i) and the 32x32 products of (d_i ^ secret word n + i);
+# after the block's 16 stripes every accumulator is scrambled.  A file split
+# by byte range hands the accumulators from range to range; the ranks
+# together chain the file's (len - 1) // 1024 whole blocks (the block holding
+# the last byte is the finish's partial block even when len % 1024 == 0).
+XXH3_SECRET64 = np.array([
+    0xbe4ba423396cfeb8, 0x1cad21f72c81017c, 0xdb979083e96dd4de, 0x1f67b3b7a4a44072,
+    0x78e5c0cc4ee679cb, 0x2172ffcc7dd05a82, 0x8e2443f7744608b8, 0x4c263a81e69035e0,
+    0xcb00c391bb52283c, 0xa32e531b8b65d088, 0x4ef90da297486471, 0xd8acdea946ef1938,
+    0x3f349ce33f76faa8, 0x1d4f0bc7c7bbdcf9, 0x3159b4cd4be0518a, 0x647378d9c97e9fc8,
+    0xc3ebd33483acc5ea, 0xeb6313faffa081c5, 0x49daf0b751dd0d17, 0x9e68d429265516d3,
+    0xfca1477d58be162b, 0xce31d07ad1b8f88f, 0x280416958f3acb45, 0x7e404bbbcafbd7af],
+    dtype=np.uint64)
+_P32_1, _P32_2, _P32_3 = 0x9E3779B1, 0x85EBCA77, 0xC2B2AE3D
+_P64 = [0x9E3779B185EBCA87, 0xC2B2AE3D27D4EB4F, 0x165667B19E3779F9, 0x85EBCA77C2B2AE63,
+        0x27D4EB2F165667C5]
+
+
+def xxh3_acc_init() -> np.ndarray:
+    """XXH3_INIT_ACC."""
+    return np.array([_P32_3, _P64[0], _P64[1], _P64[2], _P64[3], _P32_2, _P64[4], _P32_1],
+                    dtype=np.uint64)
+
+
+def xxh3_acc_blocks(data, acc) -> np.ndarray:
+    """The accumulators after the whole 1 KiB blocks of `data` (a multiple of
+    1024 bytes), chained from `acc`."""
+    d = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
+    assert len(d) % 1024 == 0
+    a = np.array(acc, dtype=np.uint64)
+    if not len(d):
+        return a
+    w = np.ascontiguousarray(d).view("<u8").reshape(-1, 16, 8)          # block, stripe, lane
+    key = XXH3_SECRET64[np.arange(16)[:, None] + np.arange(8)[None, :]]  # stripe n lane i
+    dk = w ^ key
+    with np.errstate(over="ignore"):
+        prod = (dk & np.uint64(0xFFFFFFFF)) * (dk >> np.uint64(32))
+        c = prod.sum(axis=1, dtype=np.uint64)                            # [block, lane]
+        c[:, [1, 0, 3, 2, 5, 4, 7, 6]] += w.sum(axis=1, dtype=np.uint64)  # acc[i ^ 1] += d_i
+        sec = XXH3_SECRET64[16:24]
+        p = np.uint64(_P32_1)
+        for b in range(len(c)):
+            u = a + c[b]
+            a = (u ^ (u >> np.uint64(47)) ^ sec) * p
+    return a

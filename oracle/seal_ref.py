@@ -213,3 +213,31 @@ def open_blob(keys, record: bytes):
     nonce, ct, tag = record[:16], record[16:-16], record[-16:]
     ok = poly1305(ct, mr + aes128_block(mk, nonce)) == tag
     return aes256_ctr(enc, nonce, ct), ok
+
+
+def index_file(keys, blobs, packs, nonce: bytes, fast: bool = False):
+    """restic v0.13.1 internal/index Index.Encode + repository.SaveUnpacked
+    for the packs pack_files() made: the JSON document
+      {"packs":[{"id":<pack id hex>,"blobs":[{"id":<hex>,"type":"data"|"tree",
+       "offset":<record offset in the pack>,"length":<record length>}]}]}
+    as Go's json.Encoder writes it (struct field order, no spaces,
+    "supersedes" omitted when empty, a trailing newline), packs in write
+    order and blobs in pack order; the stored file = nonce || Seal(JSON); its
+    ID = SHA-256 of the file.  Returns (json bytes, file bytes, file id)."""
+    import hashlib
+    import json
+    doc = {"packs": []}
+    for _, pid, members in packs:
+        off, bl = 0, []
+        for i in members:
+            typ, plain, bid, _ = blobs[i]
+            rl = len(plain) + 32        # nonce + ciphertext + tag
+            bl.append({"id": bid.hex(), "type": "tree" if typ else "data", "offset": off,
+                       "length": rl})
+            off += rl
+        doc["packs"].append({"id": pid.hex(), "blobs": bl})
+    js = (json.dumps(doc, separators=(",", ":")) + "\n").encode()
+    enc, mk, mr = keys
+    ct, tag = (seal_fast if fast else seal)(enc, mk, mr, nonce, js)
+    f = nonce + ct + tag
+    return js, f, hashlib.sha256(f).digest()

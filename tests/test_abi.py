@@ -111,3 +111,14 @@ def test_file_sum_finish_on_host_vs_xxhash():
         acc = V.file_sum_init()
         assert V.file_sum_finish(acc, d, n, 8) == xxhash.xxh3_128(d).intdigest().to_bytes(16, "little")
         assert V.file_sum_finish(acc, d, n, 7) == xxhash.xxh3_64(d).intdigest().to_bytes(8, "little")
+
+
+def test_library_reads_no_environment():
+    """The product library takes its settings from the caller (the handle
+    options of vsgpu.h), never from the environment: a mover pod's environment
+    cannot change which kernels run.  No VSGPU_* name is in the
+    shipped object (the one getenv left is rocPRIM's, inlined by the hipcub
+    radix sorts of rsync.hip and dedup.hip)."""
+    from volsync_amd import _lib
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"VSGPU_" not in data

@@ -186,21 +186,32 @@ def test_sha256_batch_vs_hashlib(gpu):
         assert g == hashlib.sha256(buf[o:o + n]).digest()
 
 
-@pytest.mark.parametrize("pct", ["0", "1", "50", "100"])
-def test_sha256_drain_modes_vs_hashlib(gpu, monkeypatch, pct):
+@pytest.mark.parametrize("pct", [0, 1, 50, 100])
+def test_sha256_drain_modes_vs_hashlib(gpu, pct):
     """The final drain's latency (quad, 4 lanes per chain) and split tiles in one
-    launch: VSGPU_SHA_QUAD_PCT=0 is split only, 1 puts nearly every chain in
+    launch: VS_OPT_SHA_QUAD_PCT 0 is split only, 1 puts nearly every chain in
     quad tiles, 50 / 100 mix the two; every length class from 0 to 1 MiB."""
-    from volsync_amd import sha256_batch
-    monkeypatch.setenv("VSGPU_SHA_QUAD_PCT", pct)
-    rng = np.random.default_rng(int(pct) + 11)
-    buf = O.synth(71, 0, 4 << 20).tobytes()
+    import torch
+    from volsync_amd import DeviceSha256
+    from volsync_amd._lib import VS_OPT_SHA_QUAD_PCT
+    rng = np.random.default_rng(pct + 11)
+    host = O.synth(71, 0, 4 << 20)
+    buf = host.tobytes()
     lens = [int(x) for x in rng.integers(0, 200, 300)] + [55, 56, 63, 64, 65, 119, 120] + \
         [int(x) for x in rng.integers(1 << 19, 1 << 20, 40)]
     offs = [int(rng.integers(0, len(buf) - n)) for n in lens]
-    got = sha256_batch(buf, offs, lens)
+    d = torch.from_numpy(host).cuda()
+    do = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    dl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    out = torch.zeros(len(lens) * 32, dtype=torch.uint8, device="cuda")
+    sh = DeviceSha256(0)
+    sh.set_option(VS_OPT_SHA_QUAD_PCT, pct)
+    sh.run(d.data_ptr(), do.data_ptr(), dl.data_ptr(), len(lens), out.data_ptr(), None)
+    torch.cuda.synchronize()
+    sh.close()
+    got = out.cpu().numpy().reshape(-1, 32)
     for o, n, g in zip(offs, lens, got):
-        assert g == hashlib.sha256(buf[o:o + n]).digest(), n
+        assert g.tobytes() == hashlib.sha256(buf[o:o + n]).digest(), n
 
 
 def test_small_files_device_sha(gpu):

@@ -124,13 +124,14 @@ def test_weak_collisions_and_false_alarms(gpu):
         assert st["false_alarms"] == fa
 
 
-@pytest.mark.parametrize("bbits", ["2", "10"])
-def test_membership_bucket_overflow_fallback(gpu, monkeypatch, bbits):
-    """The walk's membership buckets (one 64-byte load per probe) with so few
-    buckets that most overflow their 15 slots: the probe falls back to the
-    directory and the match list and false alarms stay hash_search's."""
+@pytest.mark.parametrize("bbits", [2, 10])
+def test_membership_bucket_overflow_fallback(gpu, bbits):
+    """The walk's membership buckets (one 32-byte load per probe: a count and
+    7 sums) with so few buckets (VS_OPT_BUCKET_BITS) that most overflow: the
+    probe falls back to the directory and the match list and false alarms
+    stay hash_search's."""
     from volsync_amd import Matcher, SumStruct
-    monkeypatch.setenv("VSGPU_RS_BBITS", bbits)
+    from volsync_amd._lib import VS_OPT_BUCKET_BITS
     n, csum, seed = 24 << 20, R.CSUM_XXH3_128, 0x5EED5EED
     basis = O.synth(31, 0, n)
     bl, s2l, cnt, rem = O.rsync_sizes(n, 2048)
@@ -139,11 +140,12 @@ def test_membership_bucket_overflow_fallback(gpu, monkeypatch, bbits):
     want, fa = O.rsync_match(src, c1, c2, bl, rem, csum, seed)
     ds = to_dev(src)
     m = Matcher()
+    m.set_option(VS_OPT_BUCKET_BITS, bbits)
     m.load_sums(SumStruct(0, cnt, bl, s2l, rem, c1, c2), csum, seed)
     got = m.match_sums(ds.data_ptr(), len(src))
     st = m.stats()
     m.close()
-    assert cnt > 10000   # 2^10 buckets: ~12 sums each, a fifth of them overflowing
+    assert cnt > 10000   # 2^10 buckets: ~12 sums each, most of them overflowing
     assert got == want and st["false_alarms"] == fa
 
 
@@ -280,7 +282,7 @@ def test_block_sharded_signatures_on_device(gpu, world, n, block_size):
     assert got == O.rsync_match(src, c1, c2, hdr.blength, hdr.remainder, csum, seed)[0]
 
 
-def _sharded_device_match(src, hdr_or_sums, world, csum, seed, dev_sums=None):
+def _sharded_device_match(src, hdr_or_sums, world, csum, seed, dev_sums=None, seg_blocks=0):
     """One Matcher per "rank", each holding ONLY its source window (own range
     + blength - 1 bytes of right halo) in its own device buffer; the walk
     stitch runs in one process (run_walk_shards_local, the same Jacobi rounds
@@ -290,8 +292,10 @@ def _sharded_device_match(src, hdr_or_sums, world, csum, seed, dev_sums=None):
     s = hdr_or_sums
     specs = SourceShard.split(len(src), s.blength, world)
     hs, bufs = [], []
+    from volsync_amd._lib import VS_OPT_WALK_SEGMENT_BLOCKS
     for sp in specs:
         m = Matcher()
+        m.set_option(VS_OPT_WALK_SEGMENT_BLOCKS, seg_blocks)
         m.load_sums(s, csum, seed)
         bufs.append(to_dev(src[sp.data_lo:sp.data_hi]))
         hs.append(m)
@@ -462,21 +466,24 @@ def test_file_sum_xxh3_lengths(gpu, csum):
     m.close()
 
 
-def test_file_sum_multi_pass_and_other_types(gpu, monkeypatch):
-    """The XXH3 chain carried across contribution passes (piece size forced
-    small), and the one-lane MD5 / XXH64 restatements, on C4-fixture sources."""
+def test_file_sum_multi_pass_and_other_types(gpu):
+    """The XXH3 chain and the host MD5 / XXH64 carried across many read-back
+    pieces (VS_OPT_FILE_SUM_PIECE forced small: 1000 blocks = 62.5 KiB of
+    bytes per serial piece), and every type on C4-fixture sources."""
     from volsync_amd import Matcher
+    from volsync_amd._lib import VS_OPT_FILE_SUM_PIECE
     m = Matcher()
     data = O.synth(62, 0, (9 << 20) + 321)
     t = to_dev(data)
-    monkeypatch.setenv("VSGPU_FS_PIECE", "1000")
-    assert m.file_sum(t.data_ptr(), len(data), 8) == _file_sum_want(data.tobytes(), 8)
-    monkeypatch.delenv("VSGPU_FS_PIECE")
+    m.set_option(VS_OPT_FILE_SUM_PIECE, 1000)
+    for csum in (8, 7, 6, 5):
+        assert m.file_sum(t.data_ptr(), len(data), csum) == _file_sum_want(data.tobytes(), csum)
+    m.set_option(VS_OPT_FILE_SUM_PIECE, 0)
     for path in FIX[:6]:
         _, _, src = load_fixture(path)
         ts = to_dev(src)
         for csum in (8, 7, 6, 5):
-            n = len(src) if csum in (8, 7) else min(len(src), 1 << 20)
+            n = len(src)
             got = m.file_sum(ts.data_ptr(), n, csum)
             assert got == _file_sum_want(src[:n].tobytes(), csum), (path, csum)
     m.close()
@@ -518,7 +525,7 @@ def test_receiver_reconstruct(gpu, path):
     m.close()
 
 
-def test_c4_real_density_window_exact(gpu, monkeypatch):
+def test_c4_real_density_window_exact(gpu):
     """C4 at its real table density: the 2,097,152-block table of the 256 GiB
     destination (blength 131072, s2length 5, xxh128, checksum_seed
     0x5EED5EED) from the device signature pass -- D generated on the device
@@ -580,18 +587,16 @@ def test_c4_real_density_window_exact(gpu, monkeypatch):
     assert (ds[:4096].cpu().numpy() == host[data_lo - win_lo:data_lo - win_lo + 4096]).all()
     m.load_sums_device(cnt, bl, s2l, rem, s1.data_ptr(), s2.data_ptr(), csum, seed)
     assert len(want) > 14000 and fa > 50000   # the density this test is for
-    # the wave walk, then the cooperative walks
-    for coop in ("0", "12", "4", "4b", "4B"):
-        monkeypatch.setenv("VSGPU_WALK_BAND", {"b": "1", "B": "2"}.get(coop[-1], "0"))
-        monkeypatch.setenv("VSGPU_WALK_COOP", coop.rstrip("bB"))
-        m.match_scan(ds.data_ptr(), n, data_lo, plan.total, lo, hi)
-        gexit = m.match_stitch(e, w)
-        nm = m.match_finish()
-        got = m.matches(0, nm)
-        st = m.stats()
-        assert got == want, coop
-        assert st["false_alarms"] == fa, coop
-        assert gexit == (wexit, wwant), coop
+    # the rank's speculative walk + the stitch from the true entry, then the
+    # streamed form's walk from the true entry directly (has_entry)
+    m.match_scan(ds.data_ptr(), n, data_lo, plan.total, lo, hi)
+    gexit = m.match_stitch(e, w)
+    nm = m.match_finish()
+    got = m.matches(0, nm)
+    st = m.stats()
+    assert got == want
+    assert st["false_alarms"] == fa
+    assert gexit == (wexit, wwant)
     m.close()
 
 
@@ -669,18 +674,27 @@ def test_file_sum_64g_exact(gpu):
     print(f"64 GiB file sum: device {tm['device_ms']:.1f} ms, host chain {tm['host_chain_ms']:.1f} ms")
 
 
-def test_file_sum_serial_types_refused_when_large(gpu):
-    """MD5 / XXH64 whole-file sums are one serial chain on one GPU lane: above
-    256 MiB the library refuses them instead of running minutes."""
+def test_file_sum_serial_types_large(gpu):
+    """MD5 / XXH64 whole-file sums at C4-mode scale (MD5 as the
+    second mode): a 4 GiB + 333 B file's bytes read back through the pinned
+    ring and hashed on the library's host thread == hashlib / libxxhash."""
+    import hashlib
     import torch
-    from volsync_amd import Matcher, VsError
-    t = torch.zeros((256 << 20) + 1, dtype=torch.uint8, device="cuda")
+    import xxhash
+    from volsync_amd import Matcher, synth_fill_device
+    n = (4 << 30) + 333
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    synth_fill_device(t.data_ptr(), 65, 0, n)
+    torch.cuda.synchronize()
+    host = O.synth(65, 0, n)
     m = Matcher()
-    for csum in (5, 6):
-        with pytest.raises(VsError) as e:
-            m.file_sum(t.data_ptr(), t.numel(), csum)
-        assert e.value.code == -1 and "serial" in str(e.value)
+    got5 = m.file_sum(t.data_ptr(), n, 5)
+    got6 = m.file_sum(t.data_ptr(), n, 6)
+    tm = m.file_sum_timing()
     m.close()
+    assert got5 == hashlib.md5(host).digest()
+    assert got6 == xxhash.xxh64_intdigest(host, seed=0).to_bytes(8, "little")
+    print(f"4 GiB XXH64 file sum: host {tm['host_chain_ms']:.0f} ms")
 
 
 def test_file_sum_jobs_fifo(gpu):
@@ -691,7 +705,7 @@ def test_file_sum_jobs_fifo(gpu):
     files = [O.synth(70 + k, 0, (k + 1) * (3 << 20) + 17 * k + 241) for k in range(4)]
     devs = [to_dev(f) for f in files]
     m = Matcher()
-    for csum in (8, 7):
+    for csum in (8, 7, 5):
         for f, t in zip(files, devs):
             m.file_sum_start(t.data_ptr(), len(f), csum)
         with pytest.raises(VsError):
@@ -700,32 +714,28 @@ def test_file_sum_jobs_fifo(gpu):
             assert m.file_sum_wait() == _file_sum_want(f.tobytes(), csum)
     with pytest.raises(VsError):
         m.file_sum_wait()
+    # the blocking form beside jobs in flight: it returns its own
+    # file's digest and the pending jobs keep their order
+    m.file_sum_start(devs[0].data_ptr(), len(files[0]), 8)
+    m.file_sum_start(devs[1].data_ptr(), len(files[1]), 8)
+    assert m.file_sum(devs[2].data_ptr(), len(files[2]), 6) == _file_sum_want(files[2].tobytes(), 6)
+    m.file_sum_start(devs[3].data_ptr(), len(files[3]), 8)
+    for k in (0, 1, 3):
+        assert m.file_sum_wait() == _file_sum_want(files[k].tobytes(), 8), k
+    with pytest.raises(VsError):
+        m.file_sum_wait()
     m.close()
 
 
-@pytest.mark.parametrize("coop", ["12", "6", "4", "12:8", "4:8", "4b", "4B"])
-def test_coop_walk_exact(gpu, monkeypatch, coop):
-    """The cooperative speculative walk (VSGPU_WALK_COOP=W: W waves share one
-    segment's walk; W:k also re-syncs flush rows every k blocks,
-    VSGPU_WALK_LOCK; 4b / 4B: band flushes from a 64 / 32 KiB LDS ring,
-    VSGPU_WALK_BAND=1 / 2)
-    against the C hash_search: every golden fixture, seeded
-    shifted / overwritten sources (false alarms, runs, short last blocks),
-    the C4 parameters on a 1 GiB basis, and the 4-way sharded walk."""
-    import torch
-    from volsync_amd import Matcher, SumStruct, match_sums
-    w, _, lock = coop.partition(":")
-    monkeypatch.setenv("VSGPU_WALK_BAND", {"b": "1", "B": "2"}.get(w[-1], "0"))
-    monkeypatch.setenv("VSGPU_WALK_COOP", w.rstrip("bB"))
-    monkeypatch.setenv("VSGPU_WALK_LOCK", lock or "0")
-    for path in FIX:
-        doc, _, src = load_fixture(path)
-        p, z = doc["params"], doc["sizes"]
-        sm = SumStruct(flength=0, count=z["count"], blength=z["blength"], s2length=z["s2length"],
-                       remainder=z["remainder"], sum1=np.array(doc["sum1"], np.uint32),
-                       sum2=np.array([list(bytes.fromhex(h)) for h in doc["sum2"]],
-                                     np.uint8).reshape(z["count"], z["s2length"]))
-        assert match_sums(src, sm, p["csum_type"], p["seed"]) == [tuple(m) for m in doc["matches"]]
+@pytest.mark.parametrize("seg", [8, 16, 64])
+def test_walk_segment_lengths_exact(gpu, seg):
+    """The device walk with other segment lengths (VS_OPT_WALK_SEGMENT_BLOCKS;
+    the default is 32 blocks, shorter for small ranges): more or fewer
+    speculative segments and stitches, the same hash_search -- seeded shifted /
+    overwritten sources (false alarms, runs, short last blocks), the C4
+    parameters on a 1 GiB basis, and the 4-way sharded walk."""
+    from volsync_amd import Matcher, SumStruct
+    from volsync_amd._lib import VS_OPT_WALK_SEGMENT_BLOCKS
     for csum_type, seed, n, frac, bs in [(R.CSUM_XXH3_128, 0x5EED5EED, 40 << 20, 0.10, 0),
                                          (R.CSUM_XXH3_64, 7, 12 << 20, 0.30, 0),
                                          (R.CSUM_XXH3_128, 1, 6 << 20, 0.20, 1000),
@@ -737,6 +747,7 @@ def test_coop_walk_exact(gpu, monkeypatch, coop):
         want, fa = O.rsync_match(src, c1, c2, bl, rem, csum_type, seed)
         ds = to_dev(src)
         m = Matcher()
+        m.set_option(VS_OPT_WALK_SEGMENT_BLOCKS, seg)
         m.load_sums(SumStruct(0, cnt, bl, s2l, rem, c1, c2), csum_type, seed)
         got = m.match_sums(ds.data_ptr(), len(src))
         st = m.stats()
@@ -750,13 +761,14 @@ def test_coop_walk_exact(gpu, monkeypatch, coop):
     want, fa = O.rsync_match(src, c1, c2, bl, 0, csum, seed)
     ds = to_dev(src)
     m = Matcher()
+    m.set_option(VS_OPT_WALK_SEGMENT_BLOCKS, seg)
     m.load_sums(SumStruct(n, n // bl, bl, s2l, 0, c1, c2), csum, seed)
     got = m.match_sums(ds.data_ptr(), len(src))
     st = m.stats()
     m.close()
     assert got == want and st["false_alarms"] == fa
     s = SumStruct(n, n // bl, bl, s2l, 0, c1, c2)
-    got4, fa4 = _sharded_device_match(src, s, 4, csum, seed)
+    got4, fa4 = _sharded_device_match(src, s, 4, csum, seed, seg_blocks=seg)
     assert got4 == want and fa4 == fa
 
 
@@ -774,17 +786,16 @@ def _dup_pair():
     return basis, src
 
 
-@pytest.mark.parametrize("facap", [None, "3", "0"])
+@pytest.mark.parametrize("facap", [-1, 3, 0])
 @pytest.mark.parametrize("data", ["edits", "duplicates"])
-def test_stitch_merge_at_visited_entry(gpu, monkeypatch, facap, data):
+def test_stitch_merge_at_visited_entry(gpu, facap, data):
     """Stitch re-walks whose entry the speculative walk visited merge there
     (same want_i) or at its next match (another want_i), with false alarms
-    from the speculative walk's recorded windows; VSGPU_WALK_FACAP shrinks
+    from the speculative walk's recorded windows; VS_OPT_FA_RECORD shrinks
     that record so segments with more false-alarm windows fall back to the
     re-walk.  Every mix: hash_search's match list and false alarms."""
     from volsync_amd import Matcher, SumStruct
-    if facap is not None:
-        monkeypatch.setenv("VSGPU_WALK_FACAP", facap)
+    from volsync_amd._lib import VS_OPT_FA_RECORD
     csum, seed = R.CSUM_XXH3_128, 0x5EED5EED
     if data == "edits":
         n = 24 << 20
@@ -798,35 +809,10 @@ def test_stitch_merge_at_visited_entry(gpu, monkeypatch, facap, data):
     want, fa = O.rsync_match(src, c1, c2, bl, rem, csum, seed)
     ds = to_dev(src)
     m = Matcher()
+    m.set_option(VS_OPT_FA_RECORD, facap)
     m.load_sums(SumStruct(len(basis), cnt, bl, s2l, rem, c1, c2), csum, seed)
     got = m.match_sums(ds.data_ptr(), len(src))
     st = m.stats()
     m.close()
     assert len(want) > 1000
     assert got == want and st["false_alarms"] == fa
-
-
-@pytest.mark.parametrize("tailpct", ["30", "90"])
-def test_walk_short_tail_segments(gpu, monkeypatch, tailpct):
-    """VSGPU_WALK_TAILPCT: the last part of the range in quarter-length
-    segments (the segments the last waves pick up): the same match list and
-    false alarms as hash_search, one device and byte-range sharded."""
-    from volsync_amd import Matcher, SumStruct
-    monkeypatch.setenv("VSGPU_WALK_TAILPCT", tailpct)
-    csum, seed = R.CSUM_XXH3_128, 0x5EED5EED
-    n = 40 << 20
-    basis = O.synth(52, 0, n)
-    bl, s2l, cnt, rem = O.rsync_sizes(n, 65536)   # 2 MiB segments, 1 MiB in the tail
-    src = R.mutate(basis, bl, seed=9, frac=0.15)
-    c1, c2 = O.rsync_signatures(basis, bl, s2l, csum, seed)
-    want, fa = O.rsync_match(src, c1, c2, bl, rem, csum, seed)
-    s = SumStruct(n, cnt, bl, s2l, rem, c1, c2)
-    ds = to_dev(src)
-    m = Matcher()
-    m.load_sums(s, csum, seed)
-    got = m.match_sums(ds.data_ptr(), len(src))
-    st = m.stats()
-    m.close()
-    assert got == want and st["false_alarms"] == fa
-    got3, fa3 = _sharded_device_match(src, s, 3, csum, seed)
-    assert got3 == want and fa3 == fa

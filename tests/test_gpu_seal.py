@@ -17,8 +17,17 @@ pytestmark = pytest.mark.gpu
 def seal_variant(request, monkeypatch):
     """Every test runs on both launch paths: the MAC fused into the CTR pass
     (default: per-lane Horner sums lifted by r^e and added per blob) and the
-    separate CTR + one-wave-per-blob MAC kernels (VSGPU_SEAL_FUSED=0)."""
-    monkeypatch.setenv("VSGPU_SEAL_FUSED", "1" if request.param == "fused" else "0")
+    separate CTR + one-wave-per-blob MAC kernels (VS_OPT_SEAL_FUSED = 0 on
+    every Sealer the test opens)."""
+    import volsync_amd.chunker as C
+    from volsync_amd._lib import VS_OPT_SEAL_FUSED
+    orig = C.Sealer.__init__
+    fused = 1 if request.param == "fused" else 0
+
+    def init(self, *a, **k):
+        orig(self, *a, **k)
+        self.set_option(VS_OPT_SEAL_FUSED, fused)
+    monkeypatch.setattr(C.Sealer, "__init__", init)
     return request.param
 
 
@@ -194,6 +203,49 @@ def test_restic_pack_files_vs_oracle(gpu):
         order += wblobs
         assert nb == len(wblobs)
     assert packs[-1][0] + packs[-1][1] == sum(len(w[0]) for w in want)
+
+
+def test_restic_index_vs_oracle(gpu):
+    """vs_restic_index ((f)3, restic's index file): the JSON of the packs
+    vs_restic_pack built -- pack IDs, per blob its ID, type, record offset in
+    the pack and stored length -- equals the v0.13.1 Index.Encode
+    restatement byte for byte; the stored file (nonce || sealed JSON || tag)
+    and its ID equal the oracle's Key.Seal + SHA-256; Key.Open of the file
+    gives the JSON back and every entry points at its blob's record in the
+    pack bytes (the round trip a restore's LoadIndex + LoadBlob makes)."""
+    import json
+    import torch
+    from volsync_amd import DeviceSha256, Sealer
+    keys = _keys(16)
+    sizes = [1, 15, 16, 17, 1000, 70_000, 33, 200_000, 5, 150_000, 64, 100_000, 3000, 90_000,
+             120_000, 7, 16 * 1024, 250_000, 1, 99_999]
+    data, offs, types, ids, nonces, hnon = _blobs(17, sizes, tree_every=3)
+    got, packs, pids = _pack(keys, data, offs, sizes, types, ids, nonces, hnon, 200 * 1024)
+    nonce = bytes(range(16, 32))
+    s, sha = Sealer(*keys), DeviceSha256()
+    js, f, fid = s.index(sha, sizes, types, ids, pids, nonce, 200 * 1024)
+    torch.cuda.synchronize()
+    s.close()
+    sha.close()
+    blobs = [(int(types[i]), data[int(offs[i]):int(offs[i]) + sizes[i]].tobytes(), ids[i].tobytes(),
+              nonces[i].tobytes()) for i in range(len(sizes))]
+    want_packs = S.pack_files(keys, blobs, [hnon[k].tobytes() for k in range(len(sizes))],
+                              200 * 1024)
+    wjs, wf, wid = S.index_file(keys, blobs, want_packs, nonce)
+    assert js == wjs and f == wf and fid == wid
+    plain, ok = S.open_blob(keys, f)
+    assert ok and plain == js
+    doc = json.loads(plain)
+    assert [p["id"] for p in doc["packs"]] == [p.hex() for p in pids]
+    seen = set()
+    for (po, pl, _, _), pk in zip(packs, doc["packs"]):
+        for b in pk["blobs"]:
+            i = next(k for k in range(len(sizes)) if ids[k].tobytes().hex() == b["id"])
+            rec = got[po + b["offset"]:po + b["offset"] + b["length"]].tobytes()
+            pt, ok = S.open_blob(keys, rec)
+            assert ok and pt == blobs[i][1] and b["type"] == ("tree" if types[i] else "data")
+            seen.add(i)
+    assert seen == set(range(len(sizes)))
 
 
 def test_restic_pack_c2_chunks(gpu):

@@ -124,3 +124,70 @@ def test_sharded_walk_local_dup_blocks(world):
     want, fa = O.rsync_match(src, c1, c2, bl, rem, R.CSUM_XXH3_128, 77)
     assert got == want
     assert sum(h.fa for h in hs) == fa
+
+
+class OracleChain:
+    """file_sum_blocks_start / _wait, as volsync_amd.Matcher, over the rank's
+    own host bytes with the numpy XXH3 restatement (oracle/rsync_ref.py)."""
+
+    def __init__(self, window, data_lo):
+        self.w, self.lo = window, data_lo
+
+    def file_sum_blocks_start(self, addr, nblocks, acc):
+        off = addr - self.lo   # the relay passes ptr + b_lo * 1024 - data_lo with ptr = data_lo
+        self.acc = R.xxh3_acc_blocks(self.w[off:off + nblocks * 1024], acc)
+
+    def file_sum_blocks_wait(self):
+        return self.acc
+
+
+def _relay_worker(rank, world, port, args, outdir):
+    import torch.distributed as dist
+    from volsync_amd.rsync_shard import FileSumRelay, SourceShard, torch_relay_p2p
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, bl, files = args
+    g = dist.new_group(backend="gloo")           # the relay's own group (own thread)
+    data = O.synth(58, 0, n)
+    spec = SourceShard.for_rank(n, bl, world, rank)
+    win = data[spec.data_lo:spec.data_hi].copy()  # only the rank's bytes
+    fs = FileSumRelay(OracleChain(win, spec.data_lo), spec, spec.data_lo, spec.data_lo,
+                      *torch_relay_p2p(rank, world, g),
+                      last=lambda: win[len(win) - min(n, 1088):].tobytes(),
+                      init=R.xxh3_acc_init)
+    for _ in range(files):
+        fs.submit()
+        dist.barrier()                            # the main thread's collectives go on
+    out = {"r": fs.results(), "nb": fs.nblocks}
+    fs.close()
+    allr = [None] * world
+    dist.all_gather_object(allr, out)
+    if rank == 0:
+        with open(os.path.join(outdir, "relay.json"), "w") as f:
+            json.dump(allr, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,args", [
+    (2, ((3 << 20) + 777, 131072, 3)),
+    (3, (3 << 20, 65536, 2)),          # len % 1024 == 0: the last whole block is the finish's
+    (5, (700 << 10, 8192, 2)),
+])
+def test_file_sum_relay_gloo(world, args):
+    """R7 across ranks (rsync_shard.FileSumRelay): each rank chains its own
+    whole 1 KiB blocks from its predecessor's accumulators (point-to-point on
+    a gloo group of the relay's own, beside the main thread's collectives),
+    several files in flight; the last rank's digest is libxxhash's XXH3-128 of
+    the whole file, and the ranks chain exactly (len - 1) // 1024 blocks."""
+    import torch.multiprocessing as mp
+    import xxhash
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_relay_worker, args=(world, _free_port(), args, d), nprocs=world,
+                           join=True, start_method="spawn")
+        res = json.load(open(os.path.join(d, "relay.json")))
+    n, _, files = args
+    data = O.synth(58, 0, n)
+    want = xxhash.xxh3_128_intdigest(data.tobytes()).to_bytes(16, "little").hex()
+    assert res[-1]["r"] == [want] * files
+    assert sum(r["nb"] for r in res) == (n - 1) // 1024

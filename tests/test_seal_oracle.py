@@ -58,3 +58,22 @@ def test_seal_into_equals_seal():
     dst = ctypes.create_string_buffer(len(pt))
     mac = S.seal_into(*keys, nonce, ctypes.addressof(src), len(pt), ctypes.addressof(dst))
     assert (dst.raw, mac) == S.seal(*keys, nonce, pt)
+
+
+def test_index_file_restatement_format():
+    """The index restatement writes what v0.13.1's json.Encoder writes for
+    jsonIndex / packJSON / blobJSON: fields in struct order, no spaces,
+    "supersedes" omitted when empty, IDs as hex, BlobType as "data" / "tree",
+    Offset / Length of the record in the pack (plaintext + 32), a trailing
+    newline -- and the stored file opens back to it."""
+    keys = (bytes(range(32)), bytes(range(16)), bytes(range(16, 32)))
+    blobs = [(0, b"a" * 10, bytes([1] * 32), bytes(16)), (1, b"b" * 5, bytes([2] * 32), bytes(16)),
+             (0, b"c" * 7, bytes([3] * 32), bytes(16))]
+    packs = S.pack_files(keys, blobs, [bytes(16)] * 3, 1 << 20)
+    js, f, fid = S.index_file(keys, blobs, packs, bytes(range(16)))
+    p0, p1 = packs[0][1].hex(), packs[1][1].hex()
+    want = ('{"packs":[{"id":"%s","blobs":[{"id":"%s","type":"data","offset":0,"length":42},'
+            '{"id":"%s","type":"data","offset":42,"length":39}]},{"id":"%s","blobs":[{"id":"%s",'
+            '"type":"tree","offset":0,"length":37}]}]}\n') % (p0, "01" * 32, "03" * 32, p1, "02" * 32)
+    assert js.decode() == want
+    assert len(f) == len(js) + 32 and S.open_blob(keys, f) == (js, True)

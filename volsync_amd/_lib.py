@@ -22,6 +22,16 @@ VS_ERR_NOMEM = -4
 VS_ERR_STATE = -5
 VS_ERR_HIP = -6
 
+# handle options (vsgpu.h "options"): tests and measurement only
+VS_OPT_WALK_SEGMENT_BLOCKS = 1
+VS_OPT_FILE_SUM_PIECE = 2
+VS_OPT_BUCKET_BITS = 3
+VS_OPT_FA_RECORD = 4
+VS_OPT_HOST_WALK = 5
+VS_OPT_SHA_QUAD_PCT = 16
+VS_OPT_FP_GENERIC = 17
+VS_OPT_SEAL_FUSED = 32
+
 u8p = ctypes.POINTER(ctypes.c_uint8)
 u32p = ctypes.POINTER(ctypes.c_uint32)
 u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -143,6 +153,8 @@ def _load() -> ctypes.CDLL:
         "vs_restic_pack": (c_int, [vp, vp, vp, vp, vp, vp, vp, c_size, vp, vp, c_u64, vp, c_u64,
                                    vp, c_size, ctypes.POINTER(c_size), ctypes.POINTER(c_u64), vp,
                                    vp]),
+        "vs_restic_index": (c_int, [vp, vp, vp, vp, vp, c_size, c_u64, vp, vp, vp, c_size,
+                                    ctypes.POINTER(c_size), vp, vp]),
         "vs_cdc_set_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_stream": (c_int, [vp, vp]),
         "vs_cdc_set_hash_slice": (c_int, [vp, c_u32]),
@@ -177,6 +189,18 @@ def _load() -> ctypes.CDLL:
         "vs_rsync_stats": (c_int, [vp, i64p, i64p, i64p, i32p]),
         "vs_rsync_timing": (c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
         "vs_rsync_kernel_time": (c_int, [vp, c_int, c_int, ctypes.POINTER(ctypes.c_double), i64p]),
+        "vs_rsync_match_begin": (c_int, [vp, i64, c_u64, c_u32]),
+        "vs_rsync_match_feed": (c_int, [vp, vp, c_size]),
+        "vs_rsync_match_next": (c_int, [vp, ctypes.POINTER(VsMatch), c_size, ctypes.POINTER(c_size)]),
+        "vs_rsync_match_end": (c_int, [vp, i64p, i64p]),
+        "vs_rsync_match_stream_stats": (c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
+        "vs_rsync_sig_begin": (c_int, [vp, i64, i32, i32, c_int, c_u32, c_u64, c_u32]),
+        "vs_rsync_sig_feed": (c_int, [vp, vp, c_size]),
+        "vs_rsync_sig_next": (c_int, [vp, vp, vp, c_size, ctypes.POINTER(c_size)]),
+        "vs_rsync_set_option": (c_int, [vp, c_int, i64]),
+        "vs_cdc_set_option": (c_int, [vp, c_int, i64]),
+        "vs_sha256_set_option": (c_int, [vp, c_int, i64]),
+        "vs_seal_set_option": (c_int, [vp, c_int, i64]),
         "vs_rsync_signatures": (c_int, [c_int, vp, i64, i32, i32, c_int, c_u32, vp, vp]),
         "vs_rsync_match": (c_int, [c_int, vp, i64, ctypes.POINTER(VsSigTable), c_int, c_u32,
                                    ctypes.POINTER(VsMatch), c_size, ctypes.POINTER(c_size)]),

@@ -229,6 +229,10 @@ class DeviceChunker:
         (0 = default, 0xffffffff = never); drain_blocks per drain launch."""
         check(lib.vs_cdc_set_hash_wide(self._h, int(min_chains), int(drain_blocks)))
 
+    def set_option(self, option: int, value: int) -> None:
+        """vs_cdc_set_option (volsync_amd._lib VS_OPT_*)."""
+        check(lib.vs_cdc_set_option(self._h, option, value))
+
     def batches(self):
         """(batches finished so far, batches the ring keeps)."""
         f = ctypes.c_uint64(0)
@@ -335,6 +339,9 @@ class DeviceSha256:
     def set_wide(self, min_chains: int = 0, drain_blocks: int = 0) -> None:
         """Throughput mode from min_chains active blobs (0 = default, 0xffffffff = never)."""
         check(lib.vs_sha256_set_wide(self._h, int(min_chains), int(drain_blocks)))
+
+    def set_option(self, option: int, value: int) -> None:
+        check(lib.vs_sha256_set_option(self._h, option, value))
 
     def blocks(self, dev_buf: int, length: int, block_size: int, dev_out: int,
                stream: Optional[int] = None) -> int:
@@ -446,8 +453,34 @@ class Sealer:
         return (out, [(p.offset, p.length, p.first_blob, p.n_blobs) for p in packs[:npk.value]],
                 [bytes(pid[k]) for k in range(npk.value)])
 
+    def index(self, sha: "DeviceSha256", lens, types, ids, pack_ids, nonce: bytes,
+              min_pack_size: int = 4 << 20):
+        """restic v0.13.1's index file of the packs pack() made from the same
+        blobs (vs_restic_index): (index JSON bytes, stored file bytes =
+        nonce || sealed JSON || tag, file ID)."""
+        import numpy as np
+        n = len(lens)
+        ln = np.ascontiguousarray(lens, np.uint32)
+        ty = np.ascontiguousarray(types, np.uint8)
+        idb = np.ascontiguousarray(np.frombuffer(b"".join(ids), np.uint8) if isinstance(ids, list)
+                                   else ids, np.uint8)
+        pk = np.ascontiguousarray(np.frombuffer(b"".join(pack_ids), np.uint8) if pack_ids
+                                  else np.zeros(32, np.uint8))
+        nj = ctypes.c_size_t()
+        args = [self._h, sha._h, ln.ctypes.data, ty.ctypes.data, idb.ctypes.data, n, min_pack_size,
+                pk.ctypes.data, nonce]
+        check(lib.vs_restic_index(*args, None, 0, ctypes.byref(nj), None, None))
+        js = ctypes.create_string_buffer(max(nj.value, 1))
+        fo = ctypes.create_string_buffer(nj.value + 32)
+        fid = ctypes.create_string_buffer(32)
+        check(lib.vs_restic_index(*args, js, nj.value, ctypes.byref(nj), fo, fid))
+        return js.raw[:nj.value], fo.raw[:nj.value + 32], fid.raw
+
     def set_timing(self, on: bool) -> None:
         check(lib.vs_seal_set_timing(self._h, int(on)))
+
+    def set_option(self, option: int, value: int) -> None:
+        check(lib.vs_seal_set_option(self._h, option, value))
 
     def kernel_ms(self):
         """(ctr_ms, mac_ms, runs) summed over the timed runs since the last call."""

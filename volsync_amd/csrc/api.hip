@@ -77,6 +77,9 @@ struct vs_cdc {
     int last = -1;                // slot of the last finished batch
     uint64_t n_chunks = 0;
     DevBuf n_out;
+    // VS_OPT_FP_GENERIC: the generic fingerprint variant even where the FAST
+    // one applies (A/B measurements; results are identical)
+    bool fp_generic = false;
     // SHA-256: time-sliced engine on its own stream (hstream)
     ShaEngine sha;
     uint32_t hash_budget = 512;   // blocks per chain per slice (0xffffffff: unbounded)
@@ -200,15 +203,6 @@ static int sync_stream(vs_cdc *h, bool all = false) {
     return 0;
 }
 
-// VSGPU_FP_FAST=0 selects the generic fingerprint variant even where the
-// FAST one applies (A/B measurements; results are identical)
-static bool fast_fp_enabled() {
-    static const bool on = [] {
-        const char *e = getenv("VSGPU_FP_FAST");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
 
 // one slice of the hash engine on the hash stream, followed by its event.
 // Flow control: before slice i reuses event slot i % kSliceEv the host waits
@@ -382,7 +376,7 @@ static int run_scan_kernels(vs_cdc *h) {
         a.k_hi = k_hi;
         a.n_edge = k_lo + (h->nstrips - k_hi);
         a.work = h->flags.as<uint32_t>() + 3;  // zeroed with the flags above
-        const bool fast = !wide && h->idx_shift >= 8 && fast_fp_enabled();
+        const bool fast = !wide && h->idx_shift >= 8 && !h->fp_generic;
         // a fed stream's hash slices hold up to a few hundred workgroups for
         // ~10 ms on the masked half of the CUs: a persistent grid of one
         // workgroup per CU would wait for them before it could complete, so
@@ -975,7 +969,11 @@ VS_API int vs_cdc_reset(vs_cdc *h, uint64_t pol, uint32_t min_size, uint32_t max
         if (h->own_hm && h->hstream == h->own_hm) h->hstream = h->own_h;
     }
     VS_TRY(set_params(h, pol, min_size, max_size, avg_bits));
-    static const bool trace = getenv("VSGPU_STREAM_TRACE") != nullptr;
+#ifdef VS_STREAM_TRACE
+    constexpr bool trace = true;   // debug builds: host time split of a stream
+#else
+    constexpr bool trace = false;
+#endif
     if (trace && h->streaming)
         fprintf(stderr, "stream: host ms stitch %.1f finish %.1f scan %.1f\n", h->dbg_ms[0],
                 h->dbg_ms[1], h->dbg_ms[2]);
@@ -1354,6 +1352,31 @@ VS_API int vs_blob_dedup(vs_sha *h, const uint8_t *dev_ids, size_t n, uint32_t *
         *n_unique = h->dd_pinned[0];
     }
     return 0;
+}
+
+// the options a vs_cdc / vs_sha handle takes (vsgpu.h); the engine's quad
+// (latency-mode) share of the final drain: 0 = split mode only
+static int sha_option(ShaEngine &e, int option, int64_t value) {
+    if (option != VS_OPT_SHA_QUAD_PCT) return fail(VS_ERR_ARG, "unknown option " + std::to_string(option));
+    if (value < 0 || value > 1000) return fail(VS_ERR_ARG, "quad share out of range");
+    e.quad_pct = (uint32_t)value;
+    return 0;
+}
+
+VS_API int vs_cdc_set_option(vs_cdc *h, int option, int64_t value) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    VS_TRY(cdc_wait(h));
+    if (option == VS_OPT_FP_GENERIC) {
+        h->fp_generic = value != 0;
+        return 0;
+    }
+    return sha_option(h->sha, option, value);
+}
+
+VS_API int vs_sha256_set_option(vs_sha *h, int option, int64_t value) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    if (h->ran) VS_HIP(hipEventSynchronize(h->done));
+    return sha_option(h->eng, option, value);
 }
 
 VS_API int vs_sha256_set_wide(vs_sha *h, uint32_t min_chains, uint32_t drain_blocks) {

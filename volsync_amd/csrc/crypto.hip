@@ -690,11 +690,13 @@ struct vs_seal {
     hipEvent_t done = nullptr;
     bool ran = false;
     bool timing = false;
+    bool fused = true;            // VS_OPT_SEAL_FUSED
     std::vector<hipEvent_t> ev;   // 3 per timed run: before CTR, between, after MAC
     // Open / pack scratch
     DevBuf o_nonce, o_mac, o_ctoff, o_cnt;
     DevBuf p_off, p_len, p_ctoff, p_nonce, p_hdr, p_hoff, p_hlen, p_hct, p_hnonce, p_tpos, p_tval,
         p_pack_off, p_pack_len, p_ids;
+    DevBuf i_json, i_file;        // the index file (vs_restic_index)
     Stager stage;
 };
 
@@ -793,6 +795,7 @@ static int seal_run(vs_seal *h, SealArgs a, const uint32_t *dev_len, size_t n, h
     a.rk128 = h->rk128.as<uint32_t>();
     a.rpow = h->rpow.as<uint32_t>();
     a.rsq = a.rpow + 64 * 5;
+    a.fused = h->fused;
     VS_TRY(h->acc.ensure(n * 5 * 8));
     a.acc = h->acc.as<unsigned long long>();
     hipEvent_t e[3] = {nullptr, nullptr, nullptr};
@@ -1034,6 +1037,117 @@ VS_API int vs_restic_pack(vs_seal *h, vs_sha *sha, const void *dev_in, const uin
     return 0;
 }
 
+// restic v0.13.1 internal/index Index.Encode (json.NewEncoder(w).Encode of
+// jsonIndex{Packs: []packJSON{ID, Blobs: []blobJSON{ID, Type, Offset,
+// Length}}}, "supersedes" omitted when empty): blob offsets and lengths are
+// those of the records in the pack (Length = plaintext + 32, the stored
+// length), types marshal as "data" / "tree", IDs as lower-case hex.  restic
+// lists blobs in its index hash map's order, which a per-process random seed
+// shuffles; this writes packs in finalize order and blobs in pack order, one
+// of the orders restic's DecodeIndex reads back the same.
+static void index_json(const PackPlan &pl, const uint32_t *len, const uint8_t *types,
+                       const uint8_t *ids, const uint8_t *pack_ids, std::string &js) {
+    static const char *hex = "0123456789abcdef";
+    auto put_id = [&](const uint8_t *id) {
+        js += '"';
+        for (int b = 0; b < 32; ++b) {
+            js += hex[id[b] >> 4];
+            js += hex[id[b] & 15];
+        }
+        js += '"';
+    };
+    js = "{\"packs\":[";
+    for (size_t p = 0; p < pl.packs.size(); ++p) {
+        const vs_pack &pk = pl.packs[p];
+        if (p) js += ',';
+        js += "{\"id\":";
+        put_id(pack_ids + 32 * p);
+        js += ",\"blobs\":[";
+        uint64_t off = 0;
+        for (uint32_t k = 0; k < pk.n_blobs; ++k) {
+            const uint32_t i = pl.order[pk.first_blob + k];
+            const uint64_t rl = (uint64_t)len[i] + 32;
+            if (k) js += ',';
+            js += "{\"id\":";
+            put_id(ids + 32 * (size_t)i);
+            js += types[i] ? ",\"type\":\"tree\"" : ",\"type\":\"data\"";
+            js += ",\"offset\":" + std::to_string(off) + ",\"length\":" + std::to_string(rl) + "}";
+            off += rl;
+        }
+        js += "]}";
+    }
+    js += "]}\n";
+}
+
+VS_API int vs_restic_index(vs_seal *h, vs_sha *sha, const uint32_t *len, const uint8_t *types,
+                           const uint8_t *ids, size_t n, uint64_t min_pack_size,
+                           const uint8_t *pack_ids, const uint8_t nonce[16], uint8_t *json_out,
+                           size_t json_cap, size_t *json_n, uint8_t *file_out, uint8_t file_id[32]) {
+    if (!json_n || (n && (!len || !types || !ids || !pack_ids)))
+        return fail(VS_ERR_ARG, "bad arguments");
+    for (size_t i = 0; i < n; ++i)
+        if (types[i] > 1) return fail(VS_ERR_ARG, "blob type must be 0 (data) or 1 (tree)");
+    PackPlan pl;
+    plan_packs(len, types, n, std::max<uint64_t>(min_pack_size, 1), pl);
+    std::string js;
+    index_json(pl, len, types, ids, pack_ids, js);
+    *json_n = js.size();
+    if (json_out) {
+        if (json_cap < js.size()) return fail(VS_ERR_ARG, "index JSON buffer too small");
+        memcpy(json_out, js.data(), js.size());
+    }
+    if (!file_out) return 0;   // the plaintext only
+    if (!h || !sha || !nonce || !file_id) return fail(VS_ERR_ARG, "null handle or output");
+    if (js.size() > 0xffffffffull - 32) return fail(VS_ERR_ARG, "index over 4 GiB");
+    // repository.SaveUnpacked: Key.Seal(nonce) -> nonce || ciphertext || tag,
+    // stored under the SHA-256 of those bytes
+    VS_TRY(enter_device(h->device));
+    const hipStream_t s = nullptr;
+    if (h->ran) VS_HIP(hipStreamWaitEvent(s, h->done, 0));
+    const uint64_t flen = js.size() + 32;
+    VS_TRY(h->i_json.ensure(js.size() + 16));
+    VS_TRY(h->i_file.ensure(flen + 16));
+    VS_TRY(h->p_hoff.ensure(8));
+    VS_TRY(h->p_hlen.ensure(4));
+    VS_TRY(h->p_hct.ensure(8));
+    VS_TRY(h->p_hnonce.ensure(16));
+    VS_TRY(h->p_ids.ensure(32));
+    const uint64_t zero = 0, ct = 16;
+    const uint32_t jl = (uint32_t)js.size(), fl = (uint32_t)flen;
+    VS_TRY(h->stage.h2d(h->i_json.p, js.data(), js.size(), s));
+    VS_TRY(h->stage.h2d(h->p_hoff.p, &zero, 8, s));
+    VS_TRY(h->stage.h2d(h->p_hlen.p, &jl, 4, s));
+    VS_TRY(h->stage.h2d(h->p_hct.p, &ct, 8, s));
+    VS_TRY(h->stage.h2d(h->p_hnonce.p, nonce, 16, s));
+    {
+        SealArgs a{};
+        a.in = h->i_json.as<uint8_t>();
+        a.out = h->i_file.as<uint8_t>();
+        a.off = h->p_hoff.as<uint64_t>();
+        a.out_off = h->p_hct.as<uint64_t>();
+        a.nonces = h->p_hnonce.as<uint8_t>();
+        a.mode = kSealRecords;
+        VS_TRY(seal_run(h, a, h->p_hlen.as<uint32_t>(), 1, s));
+    }
+    // the file's ID by the SHA-256 engine (offset 0, flen bytes)
+    VS_TRY(h->p_pack_len.ensure(4));
+    VS_TRY(h->stage.h2d(h->p_pack_len.p, &fl, 4, s));
+    VS_TRY(vs_sha256_run_device(sha, h->i_file.p, h->p_hoff.as<uint64_t>(),
+                                h->p_pack_len.as<uint32_t>(), 1, h->p_ids.as<uint8_t>(), s));
+    VS_TRY(h->stage.d2h(file_out, h->i_file.p, flen, s));
+    VS_TRY(h->stage.d2h(file_id, h->p_ids.p, 32, s));
+    VS_HIP(hipEventRecord(h->done, s));
+    return 0;
+}
+
+VS_API int vs_seal_set_option(vs_seal *h, int option, int64_t value) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    if (option != VS_OPT_SEAL_FUSED) return fail(VS_ERR_ARG, "unknown vs_seal option");
+    if (h->ran) VS_HIP(hipEventSynchronize(h->done));
+    h->fused = value != 0;
+    return 0;
+}
+
 VS_API int vs_seal_set_timing(vs_seal *h, int on) {
     if (!h) return fail(VS_ERR_ARG, "bad arguments");
     h->timing = on != 0;
@@ -1144,10 +1258,9 @@ hipError_t launch_seal_prefix(const uint32_t *len, uint64_t n, uint64_t *prefix,
 
 hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s, hipEvent_t *ev) {
     // default: the MAC fused into the CTR pass (no re-read of the ciphertext),
-    // 768-thread workgroups at 6 waves per SIMD; VSGPU_SEAL_FUSED=0 selects
+    // 768-thread workgroups at 6 waves per SIMD; VS_OPT_SEAL_FUSED = 0 selects
     // the separate CTR + MAC kernels (A/B and tests)
-    const char *fe = getenv("VSGPU_SEAL_FUSED");
-    const bool fused = !(fe && atoi(fe) == 0) || a.mode != kSealMacs;
+    const bool fused = a.fused || a.mode != kSealMacs;
     if (fused) {
         hipError_t e = hipMemsetAsync(a.acc, 0, a.n * 5 * 8, s);
         if (e != hipSuccess) return e;
@@ -1168,24 +1281,13 @@ hipError_t launch_seal(const SealArgs &a, int cus, hipStream_t s, hipEvent_t *ev
     }
     if (ev[0]) (void)hipEventRecord(ev[0], s);
     if (a.total_blocks) {
-        // variants (VSGPU_SEAL_CTR, for measurement; 16 GiB of blobs, r02):
-        // 1 (default) = 1 block per lane, 1024 threads, 8 waves per SIMD:
-        // 22.0 ms; 0 = 2 blocks per lane, 512 threads: 22.6 ms; 2 = 3 blocks,
-        // 512 threads: 22.8 ms.  LDS-issue bound (2 cycles per ds_read_b32,
-        // 224 lookups per block): SQ_LDS_IDX_ACTIVE is ~65 % of the cycles.
-        static const int variant = [] {
-            const char *e = getenv("VSGPU_SEAL_CTR");
-            return e ? atoi(e) : 1;
-        }();
-        const int per = variant == 1 ? 1 : variant == 2 ? 3 : 2;
-        const int threads = variant == 1 ? 1024 : 512;
-        const uint64_t steps = (a.total_blocks + 64 * per - 1) / (64 * per);
-        const uint64_t wg_waves = threads / 64;
-        const uint64_t grid = std::min<uint64_t>((steps + wg_waves - 1) / wg_waves,
-                                                 (uint64_t)std::max(cus, 1) * 2);
-        if (variant == 1) seal_ctr_kernel<1, 1024, 8><<<(uint32_t)grid, 1024, 0, s>>>(a);
-        else if (variant == 2) seal_ctr_kernel<3, 512, 4><<<(uint32_t)grid, 512, 0, s>>>(a);
-        else seal_ctr_kernel<2, 512, 4><<<(uint32_t)grid, 512, 0, s>>>(a);
+        // 1 block per lane, 1024 threads, 8 waves per SIMD: 22.0 ms per 16 GiB
+        // of blobs against 22.6 / 22.8 ms for 2 / 3 blocks per lane at 512
+        // threads (r02).  LDS-issue bound (2 cycles per ds_read_b32, 224
+        // lookups per block): SQ_LDS_IDX_ACTIVE is ~65 % of the cycles.
+        const uint64_t steps = (a.total_blocks + 63) / 64;
+        const uint64_t grid = std::min<uint64_t>((steps + 15) / 16, (uint64_t)std::max(cus, 1) * 2);
+        seal_ctr_kernel<1, 1024, 8><<<(uint32_t)grid, 1024, 0, s>>>(a);
     }
     if (ev[1]) (void)hipEventRecord(ev[1], s);
     const uint64_t mg = std::min<uint64_t>((a.n + 3) / 4, (uint64_t)std::max(cus, 1) * 8);

@@ -12,9 +12,9 @@
 // -- add, xor-shift, multiply, no algebra to split it -- which a host core
 // runs ~20x faster than any GPU wave (a dependent op every cycle or so
 // against one every 4+ cycles), so it runs there (filesum_host.cpp, fed by
-// the contributions read back in pieces).  Other types and
-// short files run the one-lane restatement (strong.hpp checksum2), serial by
-// construction.
+// the contributions read back in pieces).  MD5, XXH64 and
+// XXH3 of <= 240 bytes are serial chains with no parallel form: the host
+// thread hashes the file's bytes as they are read back (filesum_host.cpp).
 #include "internal.hpp"
 #include "strong.hpp"
 
@@ -58,26 +58,12 @@ __global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint6
     *(uint4 *)(C + b * 8 + 2 * m) = o;
 }
 
-// the one-lane restatement (short XXH3, XXH64, MD5): serial by construction
-__global__ void fs_serial_kernel(const uint8_t *p, uint64_t len, int csum_type, uint8_t *out) {
-    if (threadIdx.x || blockIdx.x) return;
-    uint8_t o[16];
-    checksum2(p, len, csum_type, 0, o);
-    for (int i = 0; i < 16; ++i) out[i] = o[i];
-}
-
 }  // namespace
 
 hipError_t launch_fs_contrib(const uint8_t *p, uint64_t nb, uint64_t *C, hipStream_t s) {
     if (!nb) return hipSuccess;
     const uint64_t waves = (nb + 15) / 16;
     fs_contrib_kernel<<<(uint32_t)((waves + 3) / 4), 256, 0, s>>>(p, nb, C);
-    return hipGetLastError();
-}
-
-hipError_t launch_fs_serial(const uint8_t *p, uint64_t len, int csum_type, uint8_t *out,
-                            hipStream_t s) {
-    fs_serial_kernel<<<1, 64, 0, s>>>(p, len, csum_type, out);
     return hipGetLastError();
 }
 

@@ -414,16 +414,6 @@ hipError_t launch_fingerprint(const FpArgs &a, bool wide, bool fast, int cus, hi
     if (units == 0 && a.n_edge == 0) return hipSuccess;
     const uint64_t grid =
         std::max<uint64_t>(1, std::min<uint64_t>(units, (uint64_t)std::max(cus, 1)));
-    // VSGPU_FP_WG=512: 8 fingerprint waves per CU instead of 12, which leaves
-    // registers (and, with the 32 KiB hash kernel, LDS) for a SHA-256
-    // workgroup on every CU beside the pass
-    const char *e = getenv("VSGPU_FP_WG");
-    if (e && atoi(e) == 512) {
-        if (wide) fp_kernel<kFpWide, 512><<<(uint32_t)grid, 512, 0, s>>>(a);
-        else if (fast) fp_kernel<kFpFast, 512><<<(uint32_t)grid, 512, 0, s>>>(a);
-        else fp_kernel<kFpNarrow, 512><<<(uint32_t)grid, 512, 0, s>>>(a);
-        return hipGetLastError();
-    }
     if (wide)
         fp_kernel<kFpWide, kFpThreads><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
     else if (fast)

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/vsgpu.h"
+#include "filesum.hpp"
 
 namespace vsgpu {
 
@@ -391,8 +392,6 @@ struct RsWalkArgs {
     int64_t full_end;      // offsets below it have a full window (F - blength + 1)
     int64_t lo, hi;        // the owned range
     int64_t seg_len;
-    uint32_t nseg1;        // segments [0, nseg1) are seg_len long, the rest seg_len2
-    int64_t seg_len2;
     uint32_t nseg, cap;    // segments, match capacity per segment
     uint32_t blength, count, remainder;
     int csum_type;
@@ -404,7 +403,7 @@ struct RsWalkArgs {
     const uint32_t *dir;
     const uint32_t *filt, *filt_l;
     const uint64_t *filt_b;          // blocked filter (rs_bloom_word / rs_bloom_mask)
-    const uint32_t *bkt;             // membership buckets (rs_bucket): count, 15 sums
+    const uint32_t *bkt;             // membership buckets (rs_bucket): 32 B, a count + 7 sums
     uint32_t bbits;
     uint32_t dbits, fbits, lbits;
     int64_t e0;                      // segment 0's entry (offset, want_i)
@@ -442,8 +441,7 @@ struct RsWalkArgs {
     int64_t *exit_new;
     int32_t *exitw_new;
     uint64_t *dbg;                   // debug builds: per-wave progress records (host-mapped)
-    uint64_t *prof;                  // VSGPU_WALK_PROF: per-wave phase cycles/counts [waves][16]
-    uint32_t lock;                   // cooperative walk: flush rows re-sync every `lock` blocks (0: never)
+    uint64_t *prof;                  // VS_WALK_PROF builds: per-wave phase cycles/counts [waves][16]
 };
 hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t s);
 // fill the membership buckets (zeroed by the caller) from the sorted keys:
@@ -462,17 +460,8 @@ hipError_t launch_rs_pad_sum2(const uint8_t *sum2, uint32_t count, uint32_t s2le
 // whole-file checksum (filesum.hip + filesum_host.cpp):
 // contributions of nb whole 1 KiB blocks -> C[nb][8] (block-major)
 hipError_t launch_fs_contrib(const uint8_t *p, uint64_t nb, uint64_t *C, hipStream_t s);
-// the one-lane digest (MD5, XXH64, XXH3 of <= 240 bytes) -> out[16]
-hipError_t launch_fs_serial(const uint8_t *p, uint64_t len, int csum_type, uint8_t *out,
-                            hipStream_t s);
-// host: the XXH3 scramble chain over nb contribution rows (AVX-512 when the
-// CPU has it); the last partial block, last stripe and merge from the file's
-// last min(len, 1088) bytes -> sum_end's 16 bytes
-void xxh3_init_acc(uint64_t acc[8]);
-void xxh3_chain_rows(const uint64_t *C, uint64_t nb, uint64_t acc[8]);
-void xxh3_file_finish(const uint8_t *last, uint64_t len, const uint64_t acc[8], int csum_type,
-                      uint8_t out[16]);
-const char *xxh3_chain_isa();
+
+
 // restic Key.Seal (crypto.hip)
 struct SealArgs {
     const uint8_t *in;
@@ -494,6 +483,7 @@ struct SealArgs {
     // same layout); kSealRecords writes nonce || ciphertext || mac around it
     const uint64_t *out_off;
     int mode;                   // kSealMacs, kSealRecords, kOpen
+    bool fused;                 // kSealMacs: the MAC inside the CTR pass (else two kernels)
     uint32_t *bad;              // kOpen: [n] 1 where the stored tag does not match
     unsigned long long *n_bad;  // kOpen: their count
 };

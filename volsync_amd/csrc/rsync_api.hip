@@ -18,7 +18,9 @@
 //      walk repeats.  The final walk found every strong sum it needed, so it
 //      made exactly rsync's decisions.
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -58,26 +60,87 @@ struct RsRun {
     int64_t tail_fa = 0;
 };
 
-// One whole-file checksum in flight (R7): the block
-// contributions on the device (one launch, HBM-bound), read back piece by
-// piece into a pinned ring on the job's own stream -- the copy engine runs
-// beside the walk's kernels -- and chained on a host thread as each piece
-// lands.  XXH3 of <= 240 bytes, XXH64 and MD5 run the one-lane kernel.
+// One whole-file checksum in flight (R7).  XXH3 of a long
+// file: the block contributions are computed on the device one piece at a
+// time into a 3-deep device ring, read back into a pinned ring on the job's
+// own stream -- the copy engine runs beside the walk's kernels -- and chained
+// on a host thread as each piece lands.  MD5, XXH64 and XXH3 of <= 240 bytes
+// are serial chains: the file's bytes come back through the same ring and
+// are hashed on the host thread.  Device memory per job: 3 pieces.
 struct FsJob {
     static constexpr int kRing = 3;
-    uint64_t piece = 1ull << 18;          // blocks per read-back piece (16 MiB of rows)
+    uint64_t piece = 1ull << 18;          // blocks per piece (16 MiB of rows; serial: of bytes)
     hipStream_t s = nullptr;
-    hipEvent_t ev[kRing] = {}, ev_in = nullptr, kev[2] = {};
-    uint64_t *hC[kRing] = {};             // pinned ring
-    uint8_t *hlast = nullptr;             // pinned: the file's last <= 1088 bytes / the digest
-    DevBuf dC, dout;
+    hipEvent_t ev[kRing] = {}, ev_in = nullptr, kev[kRing][2] = {};
+    uint8_t *hC[kRing] = {};              // pinned ring (piece * 64 bytes each)
+    uint8_t *hlast = nullptr;             // pinned: the file's last <= 1088 bytes
+    DevBuf dC;                            // device ring of contribution rows
+    const uint8_t *src = nullptr;
     std::thread th;
-    bool active = false, whole = false, serial = false;
+    bool active = false, whole = false, serial = false, consumed = false;
     int device = 0, csum = 0, rc = 0;
     std::string err;
     uint64_t len = 0, nb = 0;
     uint64_t acc[8] = {};
+    uint8_t digest[16] = {};
     double host_ms = 0, dev_ms = 0;
+};
+
+// ---- streamed forms: a file fed from host memory in order -------------------
+// The sender's source (match_sums) and the generator's basis
+// (generate_and_send_sums) reach rsync through map_ptr's sliding window, one
+// read at a time: the library receives them piece by piece and keeps only a
+// small ring of pieces on the device, so a file may be far larger than HBM.
+//
+// MatchStream: piece k owns the walk's visits to [k P, (k+1) P) and needs its
+// bytes plus a blength - 1 halo (the first bytes of piece k+1, copied on the
+// device when they arrive).  The walk is sequential, so each piece is walked
+// from its TRUE entry -- the previous piece's exit -- with no speculation
+// between pieces; inside a piece the segment walk of DESIGN.md 3.4 runs as
+// usual.  Pieces are walked by a library thread while the caller feeds the
+// next ones: the H2D copies (copy stream) overlap the walks (handle stream).
+struct MatchStream {
+    static constexpr uint32_t kMaxRing = 8;
+    int64_t flen = 0, piece = 0, halo = 0, np = 0;
+    uint32_t ring = 0;
+    vsgpu::DevBuf slot[kMaxRing];
+    hipEvent_t ev[kMaxRing] = {};     // piece k's bytes and halo are on the device
+    hipStream_t cs = nullptr;          // copies of fed bytes
+    vsgpu::Stager stage;               // pageable feeds (the walk thread uses the handle's)
+    int64_t fed = 0, queued = 0;       // bytes received; pieces whose bytes are all queued
+    uint64_t pinned_bytes = 0, staged_bytes = 0;
+    double feed_wait_ms = 0;           // caller time waiting for a free slot
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    int64_t complete = 0, walked = 0;  // (under mu) pieces queued / walked
+    bool stop = false;
+    int rc = 0;
+    std::string err;
+    std::vector<vs_match> out;         // (under mu) matches found, [head, size) not yet returned
+    size_t head = 0;
+    int64_t fa = 0, hashed = 0;        // (under mu)
+    double walk_ms = 0, idle_ms = 0;   // (under mu) worker time walking / waiting for bytes
+};
+
+// SigStream: pieces are whole blocks; each is signed as soon as its bytes are
+// on the device, and the sums are read back into pinned host arrays in block
+// order for vs_rsync_sig_next.
+struct SigStream {
+    static constexpr uint32_t kMaxRing = 8;
+    int64_t len = 0, piece = 0, count = 0, np = 0;
+    int32_t blength = 0, s2length = 0, remainder = 0;
+    int csum = 0;
+    uint32_t seed = 0, ring = 0;
+    vsgpu::DevBuf slot[kMaxRing], d1, d2;
+    hipEvent_t ev_in[kMaxRing] = {}, ev_done[kMaxRing] = {};
+    hipStream_t cs = nullptr;
+    vsgpu::Stager stage;
+    uint32_t *h1 = nullptr;            // pinned [count]
+    uint8_t *h2 = nullptr;             // pinned [count * s2length]
+    int64_t fed = 0, launched = 0, done = 0;   // bytes; pieces signed; pieces read back
+    int64_t returned = 0;              // blocks handed to the caller
+    uint64_t pinned_bytes = 0, staged_bytes = 0;
 };
 
 struct vs_rsync {
@@ -139,6 +202,15 @@ struct vs_rsync {
     RsRun run;
     int64_t st_cand = 0, st_fa = 0, st_hashed = 0;
     int32_t st_rounds = 0;
+    // options (vs_rsync_set_option; tests and measurement)
+    uint32_t seg_blocks = 0;        // walk segment length in blocks (0: automatic)
+    uint32_t opt_bbits = 0;         // membership bucket bits (0: automatic)
+    int32_t opt_facap = -1;         // false-alarm windows recorded per segment (-1: automatic)
+    bool opt_host_walk = false;     // the host walk for every checksum type
+    uint64_t fs_piece = 0;          // file-sum piece in 1 KiB blocks (0: 2^18)
+    // streamed forms (host-fed files): see the MatchStream / SigStream section
+    MatchStream *mst = nullptr;
+    SigStream *sst = nullptr;
     double ms[5] = {0, 0, 0, 0, 0};
     uint64_t *pinned = nullptr;
     // device walk's compacted match list (walk_collect)
@@ -250,17 +322,9 @@ int build_table(vs_rsync *h) {
     // so the walk's gathers stay L2-resident.  At C4's 2 M blocks the cap
     // (16 bits per key) measured 745 -> 775-787 GB/s per rank; at 524 K
     // blocks 32 and 16 bits per key are within 1 % and 8 bits per key loses
-    // 5 % (profiles/r02_walk_ab).  VSGPU_RS_FBITS_ADD=k: 2^k bits per key,
-    // uncapped (A/B knob).
-    static const int fadd = [] {
-        const char *e = getenv("VSGPU_RS_FBITS_ADD");
-        const int v = e ? atoi(e) : 0;
-        return v >= 2 && v <= 7 ? v : 0;
-    }();
+    // 5 % (profiles/r02_walk_ab).
     const uint32_t lc = ceil_log2(std::max<uint32_t>(count, 1));
-    h->fbits = std::min<uint32_t>(std::max<uint32_t>(fadd ? lc + (uint32_t)fadd : std::min(lc + 5, 25u),
-                                                     10),
-                                  28);
+    h->fbits = std::min<uint32_t>(std::max<uint32_t>(std::min(lc + 5, 25u), 10), 28);
     const size_t n = std::max<uint32_t>(count, 1);
     VS_TRY(h->d_keys.ensure(n * 8));
     VS_TRY(h->d_tkey.ensure(n * 8));
@@ -272,13 +336,9 @@ int build_table(vs_rsync *h) {
                            h->d_tkey.as<uint64_t>(), h->d_tmp.p, h->d_tmp.cap, h->dbits,
                            h->d_dir.as<uint32_t>(), h->fbits, h->d_filt.as<uint32_t>(),
                            h->stream));
-    h->bbits = rs_bucket_bits(count);
-    {   // VSGPU_RS_BBITS=k (tests, read per load): 2^k buckets, so that small
-        // tables overflow buckets and exercise the directory fallback
-        const char *e = getenv("VSGPU_RS_BBITS");
-        const int v = e ? atoi(e) : 0;
-        if (v >= 1 && v <= 26) h->bbits = (uint32_t)v;
-    }
+    // VS_OPT_BUCKET_BITS (tests): 2^k buckets, so that small tables overflow
+    // buckets and exercise the directory fallback
+    h->bbits = h->opt_bbits ? h->opt_bbits : rs_bucket_bits(count);
     const size_t bkt_bytes = ((size_t)kBucketWords * 4) << h->bbits;
     VS_TRY(h->d_bkt.ensure(bkt_bytes));
     VS_HIP(hipMemsetAsync(h->d_bkt.p, 0, bkt_bytes, h->stream));
@@ -590,7 +650,11 @@ int scan_candidates(vs_rsync *h, std::vector<uint64_t> &batch) {
     const int64_t dlen = r.dlen;
     const int64_t F = r.flen - r.origin;
     const int64_t lo = r.own_lo - r.origin, hi = r.own_hi - r.origin;
-    static const bool trace = getenv("VSGPU_RS_TRACE") != nullptr;
+#ifdef VS_RS_TRACE
+    constexpr bool trace = true;   // debug builds: stage times on stderr
+#else
+    constexpr bool trace = false;
+#endif
     const double t0 = now_ms();
     // 1. coarse prefixes of the data
     const uint64_t nblk = ((uint64_t)dlen + kRsG - 1) / kRsG;
@@ -704,7 +768,7 @@ namespace {
 uint64_t *g_walk_dbg = nullptr;
 std::atomic<int> g_walk_gen{0};
 void walk_watch_arm(vs_rsync *h, RsWalkArgs &a) {
-    const char *e = getenv("VSGPU_WALK_WATCH");
+    const char *e = getenv("VSGPU_WALK_WATCH");   // VS_WALK_DEBUG builds only
     if (!e) return;
     if (!g_walk_dbg && hipHostMalloc((void **)&g_walk_dbg, 4096 * 32, hipHostMallocMapped) != hipSuccess)
         return;
@@ -732,8 +796,8 @@ inline void walk_watch_arm(vs_rsync *, RsWalkArgs &) {}
 inline void walk_watch_done() {}
 #endif
 bool walk_eligible(const vs_rsync *h) {
-    static const bool host_only = getenv("VSGPU_RS_HOSTWALK") != nullptr;
-    return !host_only && (h->csum_type == VS_CSUM_XXH3_128 || h->csum_type == VS_CSUM_XXH3_64) &&
+    return !h->opt_host_walk &&
+           (h->csum_type == VS_CSUM_XXH3_128 || h->csum_type == VS_CSUM_XXH3_64) &&
            h->blength > 240;
 }
 
@@ -793,7 +857,11 @@ int walk_tail(vs_rsync *h, int64_t x, int32_t xw, int64_t *exit_off, int32_t *ex
     int64_t o = x;
     int32_t want = xw;
     const int64_t t = F - h->remainder;
-    static const bool trace = getenv("VSGPU_RS_TRACE") != nullptr;
+#ifdef VS_RS_TRACE
+    constexpr bool trace = true;   // debug builds: stage times on stderr
+#else
+    constexpr bool trace = false;
+#endif
     if (trace)
         fprintf(stderr, "rs: walk tail: device exit %lld want %d, tail offset %lld, range end %lld\n",
                 (long long)x, xw, (long long)t, (long long)hi);
@@ -860,28 +928,19 @@ int walk_scan(vs_rsync *h) {
     a.lo = r.own_lo - r.origin;
     a.hi = r.own_hi - r.origin;
     {
-        // VSGPU_WALK_SEGBLOCKS=n: segment length in blocks (A/B knob, read
-        // per call; default 32)
-        const char *e = getenv("VSGPU_WALK_SEGBLOCKS");
-        const int64_t sb = e && atoi(e) > 0 ? atoi(e) : 32;
-        a.seg_len = std::max<int64_t>((int64_t)h->blength * sb, 1 << 20);
+        // segment length: 32 blocks (4 MiB at C4; 16 measured slower, 64
+        // within noise), shorter -- down to 1 MiB -- when the
+        // range is too small to give every wave of the grid two segments (a
+        // streamed piece of 256 MiB: 256 segments instead of 64 idle-heavy
+        // ones).  vs_rsync_set_walk_segment overrides it.
+        const int64_t range = std::max<int64_t>(a.hi - a.lo, 1);
+        const int64_t waves = (int64_t)std::max(h->cus, 1) * 8;
+        int64_t sl = (int64_t)h->blength * (h->seg_blocks ? h->seg_blocks : 32);
+        if (!h->seg_blocks && range / sl < 2 * waves)
+            sl = std::max<int64_t>(range / (2 * waves), h->blength);
+        a.seg_len = std::max<int64_t>(sl, 1 << 20);
     }
     a.nseg = (uint32_t)((a.hi - a.lo + a.seg_len - 1) / a.seg_len);
-    a.nseg1 = a.nseg;
-    a.seg_len2 = a.seg_len;
-    {
-        // VSGPU_WALK_TAILPCT=p: the last p % of the range in quarter-length
-        // segments, so the waves that finish last hold short segments (A/B knob)
-        const char *e = getenv("VSGPU_WALK_TAILPCT");
-        const int tp = e ? atoi(e) : 0;
-        if (tp > 0 && tp < 100) {
-            const int64_t total = a.hi - a.lo;
-            a.seg_len2 = std::max<int64_t>(a.seg_len / 4, 1 << 20);
-            a.nseg1 = (uint32_t)(total * (100 - tp) / 100 / a.seg_len);
-            const int64_t rest = total - (int64_t)a.nseg1 * a.seg_len;
-            a.nseg = a.nseg1 + (uint32_t)((rest + a.seg_len2 - 1) / a.seg_len2);
-        }
-    }
     a.cap = (uint32_t)(a.seg_len / h->blength + 2);
     a.blength = (uint32_t)h->blength;
     a.count = (uint32_t)h->count;
@@ -903,14 +962,6 @@ int walk_scan(vs_rsync *h) {
     a.lbits = rs_lds_filter_bits(h->fbits);
     a.filt_l = h->d_filt.as<uint32_t>() + ((1ull << h->fbits) / 32);
     a.filt_b = (const uint64_t *)(a.filt_l + ((1ull << a.lbits) / 32));
-    // VSGPU_WALK_LBITS=0: the walk skips the LDS prefilter (A/B knob)
-    {
-        static const int lb = [] {
-            const char *e = getenv("VSGPU_WALK_LBITS");
-            return e ? atoi(e) : -1;
-        }();
-        if (lb == 0) a.lbits = 0;
-    }
     const size_t ns = std::max<uint32_t>(a.nseg, 1), nc = ns * a.cap;
     VS_TRY(h->w_spec_off.ensure(nc * 8));
     VS_TRY(h->w_spec_idx.ensure(nc * 4));
@@ -925,12 +976,8 @@ int walk_scan(vs_rsync *h) {
     // segments)
     a.facap = (uint32_t)std::max<uint64_t>(
         64, std::min<uint64_t>(1024, (256ull << 20) / (12ull * std::max<uint32_t>(a.nseg, 1))));
-    {
-        // VSGPU_WALK_FACAP=n (tests): a smaller record, so stitches fall
-        // back to re-walks (read per call)
-        const char *e = getenv("VSGPU_WALK_FACAP");
-        if (e) a.facap = (uint32_t)std::max(0, atoi(e));
-    }
+    // VS_OPT_FA_RECORD (tests): a smaller record, so stitches fall back to re-walks
+    if (h->opt_facap >= 0) a.facap = (uint32_t)h->opt_facap;
     VS_TRY(h->w_spec_fao.ensure(ns * a.facap * 8));
     VS_TRY(h->w_spec_fac.ensure(ns * a.facap * 4));
     VS_TRY(h->w_spec_nfa.ensure(ns * 4));
@@ -948,13 +995,6 @@ int walk_scan(vs_rsync *h) {
     }
     VS_TRY(h->w_ctl.ensure(64));
     a.prof = nullptr;
-    // VSGPU_WALK_LOCK=k (even): cooperative flushes re-sync every k blocks
-    // (read per call: tests switch it within one process)
-    {
-        const char *e = getenv("VSGPU_WALK_LOCK");
-        const int v = e ? atoi(e) : 0;
-        a.lock = (v > 0 && v % 2 == 0) ? (uint32_t)v : 0u;
-    }
     a.work = h->w_ctl.as<uint32_t>();
     a.flags = h->w_ctl.as<uint32_t>() + 4;
     a.spec_off = h->w_spec_off.as<int64_t>();
@@ -986,8 +1026,13 @@ int walk_scan(vs_rsync *h) {
     a.exitw_new = h->w_exitw[0].as<int32_t>();
     const double t0 = now_ms();
     VS_HIP(hipMemsetAsync(a.flags, 0, 4, h->stream));
-    // VSGPU_WALK_PROF=1: per-wave phase cycles of the speculative pass on stderr
-    static const bool wprof = getenv("VSGPU_WALK_PROF") != nullptr;
+    // profiling builds (-DVS_WALK_PROF): per-wave phase cycles of the
+    // speculative pass on stderr
+#ifdef VS_WALK_PROF
+    constexpr bool wprof = true;
+#else
+    constexpr bool wprof = false;
+#endif
     constexpr int kPh = 16;   // phases (rsync_walk.hip kPrN): cycles, then counts
     const size_t nprof = (size_t)std::max(h->cus, 1) * 64 * 2 * kPh;
     if (wprof) {
@@ -1095,8 +1140,13 @@ int walk_collect(vs_rsync *h, std::vector<vs_match> &out, int64_t *fa) {
 }
 
 // ---- sharded match_sums: scan + speculative walk, stitch, finish
+// entry / want: where the range's own walk starts -- the true entry when the
+// caller knows it (the streamed walk: the previous piece's exit), else
+// (has_entry false) hash_search's start at offset 0 or "no preference" (the
+// speculative entry of a shard, stitched later)
 int match_scan(vs_rsync *h, const void *dev_src, int64_t dlen, int64_t origin, int64_t flen,
-               int64_t own_lo, int64_t own_hi, int64_t *exit_off, int32_t *exit_want) {
+               int64_t own_lo, int64_t own_hi, int64_t *exit_off, int32_t *exit_want,
+               bool has_entry = false, int64_t entry = 0, int32_t want = 0) {
     if (!h->loaded) return fail(VS_ERR_STATE, "vs_rsync_match_scan before vs_rsync_load_sums");
     if (dlen < 0 || (dlen && !dev_src) || origin < 0 || flen < origin + dlen || own_lo < origin ||
         own_hi < own_lo || own_hi > flen)
@@ -1118,13 +1168,14 @@ int match_scan(vs_rsync *h, const void *dev_src, int64_t dlen, int64_t origin, i
     for (int i = 2; i < 5; ++i) h->ms[i] = 0;
     // the speculative entry: hash_search's own start at offset 0, else
     // want_i = count ("no preference": want_i < count fails)
-    r.spec_entry = own_lo;
-    r.spec_want = own_lo == 0 ? 0 : h->count;
+    if (has_entry && (entry < own_lo || want < 0))
+        return fail(VS_ERR_ARG, "entry before the owned range or negative want_i");
+    r.spec_entry = has_entry ? entry : own_lo;
+    r.spec_want = has_entry ? want : (own_lo == 0 ? 0 : h->count);
     r.state = 1;
-    const int64_t rel_hi = own_hi - origin;
-    if (own_hi == own_lo || flen == 0 || h->count == 0) {
+    if (own_hi <= r.spec_entry || flen == 0 || h->count == 0) {
         // match_sums: no sums (or no owned offsets) -> all literal
-        r.spec_exit = std::max(own_lo, own_hi);
+        r.spec_exit = std::max(r.spec_entry, own_hi);
         r.spec_exit_want = r.spec_want;
     } else if (walk_eligible(h)) {
         if (((uintptr_t)dev_src & 15) != 0)
@@ -1141,12 +1192,11 @@ int match_scan(vs_rsync *h, const void *dev_src, int64_t dlen, int64_t origin, i
         std::vector<uint64_t> &batch = h->h_batch;
         VS_TRY(scan_candidates(h, batch));
         WalkState ws;
-        VS_TRY(run_walk(h, own_lo - origin, r.spec_want, nullptr, batch, r.spec, r.spec_fa_before,
-                        ws));
+        VS_TRY(run_walk(h, r.spec_entry - origin, r.spec_want, nullptr, batch, r.spec,
+                        r.spec_fa_before, ws));
         r.spec_fa = ws.false_alarms;
         r.spec_exit = ws.exit_off + origin;
         r.spec_exit_want = ws.exit_want;
-        (void)rel_hi;
     }
     r.fin_exit = r.spec_exit;
     r.fin_exit_want = r.spec_exit_want;
@@ -1231,39 +1281,66 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
 }
 
 // ---- whole-file checksum jobs (FsJob) ----------------------------------------
-constexpr uint64_t kFsSerialMax = 256ull << 20;
-
-void fs_thread(FsJob *j, const uint64_t *dC) {
-    const uint64_t np = (j->nb + j->piece - 1) / j->piece;
-    const double t0 = now_ms();
-    double chain = 0;
+// The job's thread: piece i = contributions of blocks [i P, (i+1) P) into
+// device slot i % R, read back into pinned slot i % R (serial types: the
+// bytes themselves, P * 64 at a time), then chained / hashed on the host.
+// Stream order on j->s keeps a device slot until its read-back is done; a
+// pinned slot is refilled only after the host consumed it.
+void fs_thread(FsJob *j) {
+    const bool serial = j->serial;
+    const uint64_t unit = serial ? 1 : 1024;             // source bytes per item
+    const uint64_t items = serial ? j->len : j->nb;       // bytes or blocks
+    const uint64_t per = serial ? j->piece * 64 : j->piece;
+    const uint64_t np = (items + per - 1) / per;
+    double chain = 0, kms = 0;
     auto fail_here = [&](hipError_t e, const char *what) {
         j->rc = VS_ERR_HIP;
         j->err = std::string(what) + ": " + hipGetErrorName(e);
         (void)hipGetLastError();
     };
     if (hipSetDevice(j->device) != hipSuccess) return fail_here(hipGetLastError(), "hipSetDevice");
+    SerialSum ss;
+    if (serial) serial_sum_init(ss, j->csum);
     auto issue = [&](uint64_t i) -> bool {
-        const uint64_t b0 = i * j->piece, n = std::min(j->piece, j->nb - b0);
-        hipError_t e = hipMemcpyAsync(j->hC[i % FsJob::kRing], dC + b0 * 8, n * 64,
-                                      hipMemcpyDeviceToHost, j->s);
-        if (e == hipSuccess) e = hipEventRecord(j->ev[i % FsJob::kRing], j->s);
-        if (e != hipSuccess) fail_here(e, "contribution read-back");
+        const int r = (int)(i % FsJob::kRing);
+        const uint64_t i0 = i * per, n = std::min(per, items - i0);
+        hipError_t e = hipSuccess;
+        if (serial) {
+            e = hipMemcpyAsync(j->hC[r], j->src + i0, n, hipMemcpyDeviceToHost, j->s);
+        } else {
+            uint64_t *dc = j->dC.as<uint64_t>() + (uint64_t)r * j->piece * 8;
+            e = hipEventRecord(j->kev[r][0], j->s);
+            if (e == hipSuccess) e = launch_fs_contrib(j->src + i0 * unit, n, dc, j->s);
+            if (e == hipSuccess) e = hipEventRecord(j->kev[r][1], j->s);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(j->hC[r], dc, n * 64, hipMemcpyDeviceToHost, j->s);
+        }
+        if (e == hipSuccess) e = hipEventRecord(j->ev[r], j->s);
+        if (e != hipSuccess) fail_here(e, "file-sum piece");
         return e == hipSuccess;
     };
     for (uint64_t i = 0; i < std::min<uint64_t>(np, FsJob::kRing); ++i)
         if (!issue(i)) return;
     for (uint64_t i = 0; i < np; ++i) {
-        const hipError_t e = hipEventSynchronize(j->ev[i % FsJob::kRing]);
-        if (e != hipSuccess) return fail_here(e, "contribution read-back wait");
-        const uint64_t b0 = i * j->piece, n = std::min(j->piece, j->nb - b0);
+        const int r = (int)(i % FsJob::kRing);
+        const hipError_t e = hipEventSynchronize(j->ev[r]);
+        if (e != hipSuccess) return fail_here(e, "file-sum piece wait");
+        const uint64_t i0 = i * per, n = std::min(per, items - i0);
         const double c0 = now_ms();
-        xxh3_chain_rows(j->hC[i % FsJob::kRing], n, j->acc);
+        if (serial) {
+            serial_sum_update(ss, j->hC[r], n);
+        } else {
+            xxh3_chain_rows((const uint64_t *)j->hC[r], n, j->acc);
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, j->kev[r][0], j->kev[r][1]) == hipSuccess) kms += ms;
+            (void)hipGetLastError();
+        }
         chain += now_ms() - c0;
         if (i + FsJob::kRing < np && !issue(i + FsJob::kRing)) return;
     }
+    if (serial) serial_sum_final(ss, j->digest);
     j->host_ms = chain;
-    (void)t0;
+    j->dev_ms = kms;
 }
 
 int fs_setup(FsJob &j, int device) {
@@ -1279,14 +1356,22 @@ int fs_setup(FsJob &j, int device) {
     VS_HIP(hipStreamCreateWithPriority(&j.s, hipStreamNonBlocking, least));
     VS_HIP(hipEventCreateWithFlags(&j.ev_in, hipEventDisableTiming));
     for (auto &e : j.ev) VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (auto &e : j.kev) VS_HIP(hipEventCreate(&e));
+    for (auto &k : j.kev)
+        for (auto &e : k) VS_HIP(hipEventCreate(&e));
     if (!(j.hlast = (uint8_t *)pinned_alloc(2048))) return fail(VS_ERR_NOMEM, "pinned tail buffer");
-    const char *pe = getenv("VSGPU_FS_PIECE");   // tests: many ring turns on small files
-    if (pe && strtoull(pe, nullptr, 10)) j.piece = strtoull(pe, nullptr, 10);
-    for (auto &p : j.hC)
-        if (!(p = (uint64_t *)pinned_alloc(j.piece * 64)))
-            return fail(VS_ERR_NOMEM, "pinned contribution ring");
     return 0;
+}
+
+// the job's rings, sized for its piece length (kept across jobs)
+int fs_rings(FsJob &j, uint64_t piece) {
+    if (piece != j.piece || !j.hC[0]) {
+        for (auto &p : j.hC) pinned_free(p), p = nullptr;
+        j.piece = piece;
+        for (auto &p : j.hC)
+            if (!(p = (uint8_t *)pinned_alloc(j.piece * 64)))
+                return fail(VS_ERR_NOMEM, "pinned file-sum ring");
+    }
+    return j.dC.ensure((size_t)FsJob::kRing * j.piece * 64);
 }
 
 // waits for the job (if any); the job's status becomes the return value
@@ -1294,8 +1379,6 @@ int fs_finish(FsJob &j) {
     if (!j.active) return 0;
     if (j.th.joinable()) j.th.join();
     const hipError_t e = hipStreamSynchronize(j.s);
-    float ms = 0;
-    if (!j.serial && j.nb && hipEventElapsedTime(&ms, j.kev[0], j.kev[1]) == hipSuccess) j.dev_ms = ms;
     (void)hipGetLastError();
     if (j.rc < 0) {
         const int rc = j.rc;
@@ -1317,11 +1400,11 @@ void fs_release(FsJob &j) {
     pinned_free(j.hlast);
     j.hlast = nullptr;
     j.dC.release();
-    j.dout.release();
     for (auto &e : j.ev)
         if (e) (void)hipEventDestroy(e), e = nullptr;
-    for (auto &e : j.kev)
-        if (e) (void)hipEventDestroy(e), e = nullptr;
+    for (auto &k : j.kev)
+        for (auto &e : k)
+            if (e) (void)hipEventDestroy(e), e = nullptr;
     if (j.ev_in) (void)hipEventDestroy(j.ev_in), j.ev_in = nullptr;
     if (j.s) (void)hipStreamDestroy(j.s), j.s = nullptr;
     j.active = false;
@@ -1334,6 +1417,15 @@ void fs_account(vs_rsync *h, const FsJob &j) {
     h->fs_host_ms = j.host_ms;
 }
 
+// jobs whose result a blocking vs_rsync_file_sum already took leave the FIFO
+// once everything older has been waited for
+void fs_pop_consumed(vs_rsync *h) {
+    while (h->fs_head != h->fs_tail && h->fs[h->fs_head % vs_rsync::kFsJobs].consumed) {
+        h->fs[h->fs_head % vs_rsync::kFsJobs].consumed = false;
+        h->fs_head++;
+    }
+}
+
 // whole: the digest of the file p[0, len); else the accumulators after the
 // whole blocks p[0, len) (len a multiple of 1024) chained from acc_in
 int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
@@ -1342,47 +1434,428 @@ int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
         return fail(VS_ERR_STATE, "4 whole-file checksums in flight: wait for one first");
     FsJob &j = h->fs[h->fs_tail % vs_rsync::kFsJobs];
     VS_TRY(fs_setup(j, h->device));
+    VS_TRY(fs_rings(j, h->fs_piece ? h->fs_piece : (1ull << 18)));
     j.whole = whole;
     j.csum = csum;
     j.len = len;
+    j.src = p;
     j.rc = 0;
     j.err.clear();
     j.host_ms = j.dev_ms = 0;
+    j.consumed = false;
     const bool xxh3 = csum == VS_CSUM_XXH3_64 || csum == VS_CSUM_XXH3_128;
     j.serial = whole && (!xxh3 || len <= 240);
     // after the caller's null-stream work and this handle's queued work
     VS_HIP(hipEventRecord(j.ev_in, h->stream));
     VS_HIP(hipStreamWaitEvent(j.s, j.ev_in, 0));
     if (j.serial) {
-        VS_TRY(j.dout.ensure(16));
-        VS_HIP(launch_fs_serial(p, len, csum, j.dout.as<uint8_t>(), j.s));
-        VS_HIP(hipMemcpyAsync(j.hlast, j.dout.p, 16, hipMemcpyDeviceToHost, j.s));
         j.nb = 0;
-        j.active = true;
-        h->fs_tail++;
-        return 0;
-    }
-    j.nb = whole ? (len - 1) / 1024 : len / 1024;
-    if (whole) {
-        xxh3_init_acc(j.acc);
     } else {
-        if (acc_in) memcpy(j.acc, acc_in, 64);
-        else xxh3_init_acc(j.acc);
+        j.nb = whole ? (len - 1) / 1024 : len / 1024;
+        if (whole || !acc_in) xxh3_init_acc(j.acc);
+        else memcpy(j.acc, acc_in, 64);
+        if (whole) {   // the last partial block, last stripe: read back for the finish
+            const uint64_t keep = std::min<uint64_t>(len, 1088);
+            VS_HIP(hipMemcpyAsync(j.hlast, p + len - keep, keep, hipMemcpyDeviceToHost, j.s));
+        }
     }
-    if (whole) {   // the last partial block, last stripe: read back for the finish
-        const uint64_t keep = std::min<uint64_t>(len, 1088);
-        VS_HIP(hipMemcpyAsync(j.hlast, p + len - keep, keep, hipMemcpyDeviceToHost, j.s));
-    }
-    if (j.nb) {
-        VS_TRY(j.dC.ensure(j.nb * 64));
-        VS_HIP(hipEventRecord(j.kev[0], j.s));
-        VS_HIP(launch_fs_contrib(p, j.nb, j.dC.as<uint64_t>(), j.s));
-        VS_HIP(hipEventRecord(j.kev[1], j.s));
-        if (j.th.joinable()) j.th.join();   // (fs_finish joined it; never terminate())
-        j.th = std::thread(fs_thread, &j, j.dC.as<const uint64_t>());
+    if (j.th.joinable()) j.th.join();   // (fs_finish joined it; never terminate())
+    if (j.serial ? len > 0 : j.nb > 0) {
+        j.th = std::thread(fs_thread, &j);
+    } else if (j.serial) {   // an empty file: nothing to read back
+        SerialSum ss;
+        serial_sum_init(ss, csum);
+        serial_sum_final(ss, j.digest);
     }
     j.active = true;
     h->fs_tail++;
+    return 0;
+}
+
+// the finished job's digest (whole files)
+void fs_digest(const FsJob &j, uint8_t out[16]) {
+    memset(out, 0, 16);
+    const int n = (j.csum == VS_CSUM_MD5 || j.csum == VS_CSUM_XXH3_128) ? 16 : 8;
+    if (j.serial) {
+        memcpy(out, j.digest, (size_t)n);
+    } else {
+        uint8_t o[16];
+        xxh3_file_finish(j.hlast, j.len, j.acc, j.csum, o);
+        memcpy(out, o, (size_t)n);
+    }
+}
+
+// ---- streamed forms (MatchStream / SigStream) --------------------------------
+// n caller bytes to device dst on copy stream cs: pinned caller memory by DMA
+// (*dma set: the call waits for it before returning -- the caller owns the
+// buffer), pageable memory through the stream's own staging buffers
+int feed_copy(Stager &st, hipStream_t cs, uint8_t *dst, const uint8_t *src, size_t n, bool *dma,
+              uint64_t *pinned_bytes, uint64_t *staged_bytes) {
+    if (!n) return 0;
+    if (host_range_pinned(src, n)) {
+        VS_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, cs));
+        *dma = true;
+        *pinned_bytes += n;
+        return 0;
+    }
+    *staged_bytes += n;
+    return st.h2d(dst, src, n, cs);
+}
+
+int stream_mk(hipStream_t *cs, hipEvent_t *ev, uint32_t nev) {
+    if (!*cs) VS_HIP(hipStreamCreateWithFlags(cs, hipStreamNonBlocking));
+    for (uint32_t i = 0; i < nev; ++i)
+        if (!ev[i]) VS_HIP(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    return 0;
+}
+
+void ms_release(vs_rsync *h) {
+    MatchStream *m = h->mst;
+    if (!m) return;
+    {
+        std::lock_guard<std::mutex> lk(m->mu);
+        m->stop = true;
+    }
+    m->cv.notify_all();
+    if (m->th.joinable()) m->th.join();
+    if (m->cs) (void)hipStreamSynchronize(m->cs);
+    for (auto &b : m->slot) b.release();
+    for (auto &e : m->ev)
+        if (e) (void)hipEventDestroy(e);
+    m->stage.release();
+    if (m->cs) (void)hipStreamDestroy(m->cs);
+    delete m;
+    h->mst = nullptr;
+}
+
+// the walk thread: piece k from the previous piece's exit, as its bytes arrive
+void ms_worker(vs_rsync *h, MatchStream *m) {
+    int64_t entry = 0;
+    int32_t want = 0;
+    for (int64_t k = 0; k < m->np; ++k) {
+        {
+            const double t0 = now_ms();
+            std::unique_lock<std::mutex> lk(m->mu);
+            m->cv.wait(lk, [&] { return m->stop || m->complete > k; });
+            m->idle_ms += now_ms() - t0;
+            if (m->stop) return;
+        }
+        const double t0 = now_ms();
+        const int64_t lo = k * m->piece, hi = std::min(lo + m->piece, m->flen);
+        const int64_t dhi = std::min(hi + m->halo, m->flen);
+        int rc = 0;
+        int64_t nm = 0, fa = 0, hashed = 0;
+        if (entry < hi) {
+            int64_t x = 0;
+            int32_t xw = 0;
+            rc = rs_dev(h);
+            if (!rc && hipStreamWaitEvent(h->stream, m->ev[k % m->ring], 0) != hipSuccess)
+                rc = fail_hip(hipGetLastError(), "hipStreamWaitEvent (streamed piece)", __FILE__,
+                              __LINE__);
+            if (!rc)
+                rc = match_scan(h, m->slot[k % m->ring].p, dhi - lo, lo, m->flen, lo, hi, &x, &xw,
+                                true, entry, want);
+            if (!rc) rc = match_finish(h, &nm);
+            if (!rc) {
+                fa = h->st_fa;
+                hashed = h->st_hashed;
+                entry = x;
+                want = xw;
+            }
+        }
+        std::lock_guard<std::mutex> lk(m->mu);
+        if (rc < 0) {
+            m->rc = rc;
+            m->err = vs_last_error();
+            m->stop = true;
+            m->cv.notify_all();
+            return;
+        }
+        if (nm) m->out.insert(m->out.end(), h->matches.begin(), h->matches.begin() + nm);
+        m->fa += fa;
+        m->hashed += hashed;
+        m->walked = k + 1;
+        m->walk_ms += now_ms() - t0;
+        m->cv.notify_all();
+    }
+}
+
+int ms_error(MatchStream *m) {
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (m->rc < 0) return fail(m->rc, "streamed match walk: " + m->err);
+    return 0;
+}
+
+int ms_begin(vs_rsync *h, int64_t flen, uint64_t piece, uint32_t ring) {
+    if (!h->loaded) return fail(VS_ERR_STATE, "vs_rsync_match_begin before vs_rsync_load_sums");
+    if (flen < 0) return fail(VS_ERR_ARG, "negative file length");
+    if (!piece) piece = 256ull << 20;
+    if (!ring) ring = 3;
+    if (ring < 2 || ring > MatchStream::kMaxRing || piece < (1u << 20) || (piece & 15))
+        return fail(VS_ERR_ARG, "piece must be >= 1 MiB and a multiple of 16, ring 2..8");
+    VS_TRY(rs_dev(h));
+    ms_release(h);
+    MatchStream *m = new MatchStream();
+    h->mst = m;
+    m->flen = flen;
+    m->halo = h->blength - 1;
+    // a piece never shorter than the walk's halo; small files get one slot's worth
+    m->piece = (int64_t)std::max<uint64_t>(piece, ((uint64_t)h->blength + 15) & ~15ull);
+    m->np = flen ? (flen + m->piece - 1) / m->piece : 0;
+    m->ring = ring;
+    // slots k % ring for the pieces there are (a small file: one)
+    const uint32_t nslot = (uint32_t)std::min<int64_t>(ring, std::max<int64_t>(m->np, 1));
+    const size_t sb = (size_t)std::min<int64_t>(m->piece + m->halo, std::max<int64_t>(flen, 16)) + 16;
+    VS_TRY(stream_mk(&m->cs, m->ev, nslot));
+    for (uint32_t i = 0; i < nslot; ++i) VS_TRY(m->slot[i].ensure(sb));
+    h->matches.clear();
+    h->st_cand = h->st_fa = h->st_hashed = 0;
+    h->st_rounds = 0;
+    if (m->np) m->th = std::thread(ms_worker, h, m);
+    return 0;
+}
+
+int ms_feed(vs_rsync *h, const uint8_t *p, size_t n) {
+    MatchStream *m = h->mst;
+    if (!m) return fail(VS_ERR_STATE, "vs_rsync_match_feed before vs_rsync_match_begin");
+    VS_TRY(ms_error(m));
+    if (n && !p) return fail(VS_ERR_ARG, "null buffer");
+    if ((int64_t)n > m->flen - m->fed) return fail(VS_ERR_ARG, "fed past the file length given to begin");
+    VS_TRY(rs_dev(h));
+    bool dma = false;
+    while (n) {
+        const int64_t k = m->fed / m->piece, off = m->fed - k * m->piece;
+        const size_t take = (size_t)std::min<int64_t>((int64_t)n, m->piece - off);
+        if (k >= m->ring) {   // slot k % ring: free once piece k - ring is walked
+            const double t0 = now_ms();
+            std::unique_lock<std::mutex> lk(m->mu);
+            m->cv.wait(lk, [&] { return m->stop || m->walked > k - m->ring; });
+            m->feed_wait_ms += now_ms() - t0;
+            if (m->stop) {
+                lk.unlock();
+                VS_TRY(ms_error(m));
+                return fail(VS_ERR_STATE, "streamed match stopped");
+            }
+        }
+        uint8_t *dst = m->slot[k % m->ring].as<uint8_t>() + off;
+        VS_TRY(feed_copy(m->stage, m->cs, dst, p, take, &dma, &m->pinned_bytes, &m->staged_bytes));
+        if (k > 0 && off < m->halo) {   // also piece k-1's halo
+            const size_t hn = (size_t)std::min<int64_t>((int64_t)take, m->halo - off);
+            VS_HIP(hipMemcpyAsync(m->slot[(k - 1) % m->ring].as<uint8_t>() + m->piece + off, dst, hn,
+                                  hipMemcpyDeviceToDevice, m->cs));
+        }
+        m->fed += (int64_t)take;
+        p += take;
+        n -= take;
+        // pieces whose bytes and halo are now all queued
+        int64_t q = m->queued;
+        while (q < m->np && m->fed >= std::min((q + 1) * m->piece + m->halo, m->flen)) {
+            VS_HIP(hipEventRecord(m->ev[q % m->ring], m->cs));
+            ++q;
+        }
+        if (q != m->queued) {
+            m->queued = q;
+            {
+                std::lock_guard<std::mutex> lk(m->mu);
+                m->complete = q;
+            }
+            m->cv.notify_all();
+        }
+    }
+    if (dma) VS_HIP(hipStreamSynchronize(m->cs));   // the caller's pinned bytes are copied
+    return 0;
+}
+
+// matches found so far, in order; with wait: blocks until at least one is
+// found or the walk is over.  VS_EOF once the last has been returned.
+int ms_next(vs_rsync *h, vs_match *out, size_t cap, size_t *n_out, bool wait) {
+    MatchStream *m = h->mst;
+    *n_out = 0;
+    if (!m) return fail(VS_ERR_STATE, "vs_rsync_match_next before vs_rsync_match_begin");
+    std::unique_lock<std::mutex> lk(m->mu);
+    if (wait)
+        m->cv.wait(lk, [&] { return m->stop || m->head < m->out.size() || m->walked == m->np; });
+    if (m->rc < 0) {
+        lk.unlock();
+        return ms_error(m);
+    }
+    const size_t n = std::min(cap, m->out.size() - m->head);
+    if (n) memcpy(out, m->out.data() + m->head, n * sizeof(vs_match));
+    m->head += n;
+    *n_out = n;
+    if (!n && m->walked == m->np && m->fed == m->flen) return VS_EOF;
+    return 0;
+}
+
+int ms_end(vs_rsync *h, int64_t *n_matches, int64_t *false_alarms) {
+    MatchStream *m = h->mst;
+    if (!m) return fail(VS_ERR_STATE, "vs_rsync_match_end before vs_rsync_match_begin");
+    if (m->fed != m->flen)
+        return fail(VS_ERR_STATE, "vs_rsync_match_end after " + std::to_string(m->fed) + " of " +
+                                      std::to_string(m->flen) + " bytes");
+    {
+        std::unique_lock<std::mutex> lk(m->mu);
+        m->cv.wait(lk, [&] { return m->stop || m->walked == m->np; });
+    }
+    if (m->th.joinable()) m->th.join();
+    VS_TRY(ms_error(m));
+    std::lock_guard<std::mutex> lk(m->mu);
+    // the handle's counters and match list describe the whole file now
+    h->st_fa = m->fa;
+    h->st_hashed = m->hashed;
+    h->matches.assign(m->out.begin(), m->out.end());
+    if (n_matches) *n_matches = (int64_t)m->out.size();
+    if (false_alarms) *false_alarms = m->fa;
+    return 0;
+}
+
+void ss_release(vs_rsync *h) {
+    SigStream *s = h->sst;
+    if (!s) return;
+    if (s->cs) (void)hipStreamSynchronize(s->cs);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (auto &b : s->slot) b.release();
+    s->d1.release();
+    s->d2.release();
+    for (auto &e : s->ev_in)
+        if (e) (void)hipEventDestroy(e);
+    for (auto &e : s->ev_done)
+        if (e) (void)hipEventDestroy(e);
+    pinned_free(s->h1);
+    pinned_free(s->h2);
+    s->stage.release();
+    if (s->cs) (void)hipStreamDestroy(s->cs);
+    delete s;
+    h->sst = nullptr;
+}
+
+int ss_begin(vs_rsync *h, int64_t len, int32_t blength, int32_t s2length, int csum, uint32_t seed,
+             uint64_t piece, uint32_t ring) {
+    VS_TRY(check_csum(csum));
+    if (len < 0 || blength <= 0 || s2length < 1 || s2length > 16)
+        return fail(VS_ERR_ARG, "bad length, blength or s2length");
+    if (!piece) piece = 256ull << 20;
+    if (!ring) ring = 3;
+    if (ring < 2 || ring > SigStream::kMaxRing) return fail(VS_ERR_ARG, "ring must be 2..8");
+    const int64_t count = len / blength + (len % blength != 0);
+    if (count > INT32_MAX) return fail(VS_ERR_ARG, "block count overflows int32");
+    VS_TRY(rs_dev(h));
+    ss_release(h);
+    SigStream *s = new SigStream();
+    h->sst = s;
+    s->len = len;
+    s->blength = blength;
+    s->s2length = s2length;
+    s->remainder = (int32_t)(len % blength);
+    s->csum = csum;
+    s->seed = seed;
+    s->count = count;
+    s->piece = std::max<int64_t>((int64_t)piece / blength, 1) * blength;
+    s->np = len ? (len + s->piece - 1) / s->piece : 0;
+    s->ring = ring;
+    const uint32_t nslot = (uint32_t)std::min<int64_t>(ring, std::max<int64_t>(s->np, 1));
+    VS_TRY(stream_mk(&s->cs, s->ev_in, nslot));
+    VS_TRY(stream_mk(&s->cs, s->ev_done, nslot));
+    const size_t sb = (size_t)std::min<int64_t>(s->piece, std::max<int64_t>(len, 16)) + 16;
+    for (uint32_t i = 0; i < nslot; ++i) VS_TRY(s->slot[i].ensure(sb));
+    const size_t c = (size_t)std::max<int64_t>(count, 1);
+    VS_TRY(s->d1.ensure(c * 4));
+    VS_TRY(s->d2.ensure(c * s2length));
+    if (!(s->h1 = (uint32_t *)pinned_alloc(c * 4)) || !(s->h2 = (uint8_t *)pinned_alloc(c * s2length)))
+        return fail(VS_ERR_NOMEM, "pinned signature read-back arrays");
+    return 0;
+}
+
+// piece k's bytes are queued: sign it on the handle's stream, read its sums back
+int ss_launch(vs_rsync *h, SigStream *s, int64_t k) {
+    const int64_t lo = k * s->piece, hi = std::min(lo + s->piece, s->len);
+    const int64_t b0 = lo / s->blength;
+    RsSigArgs a{};
+    a.data = s->slot[k % s->ring].as<uint8_t>();
+    a.len = (uint64_t)(hi - lo);
+    a.count = (uint64_t)((hi - lo + s->blength - 1) / s->blength);
+    a.blength = (uint32_t)s->blength;
+    a.remainder = (uint32_t)((hi - lo) % s->blength);
+    a.s2length = (uint32_t)s->s2length;
+    a.csum_type = s->csum;
+    a.seed = s->seed;
+    a.sum1 = s->d1.as<uint32_t>() + b0;
+    a.sum2 = s->d2.as<uint8_t>() + b0 * s->s2length;
+    VS_HIP(hipEventRecord(s->ev_in[k % s->ring], s->cs));
+    VS_HIP(hipStreamWaitEvent(h->stream, s->ev_in[k % s->ring], 0));
+    VS_HIP(launch_rs_signatures(a, h->stream));
+    VS_HIP(hipMemcpyAsync(s->h1 + b0, a.sum1, a.count * 4, hipMemcpyDeviceToHost, h->stream));
+    VS_HIP(hipMemcpyAsync(s->h2 + b0 * s->s2length, a.sum2, a.count * s->s2length,
+                          hipMemcpyDeviceToHost, h->stream));
+    VS_HIP(hipEventRecord(s->ev_done[k % s->ring], h->stream));
+    return 0;
+}
+
+// pieces whose sums are on the host: without wait, those that are done now
+int ss_collect(SigStream *s, bool wait) {
+    while (s->done < s->launched) {
+        hipEvent_t e = s->ev_done[s->done % s->ring];
+        if (wait) {
+            VS_HIP(hipEventSynchronize(e));
+        } else {
+            const hipError_t q = hipEventQuery(e);
+            if (q == hipErrorNotReady) {
+                (void)hipGetLastError();
+                break;
+            }
+            if (q != hipSuccess) return fail_hip(q, "signature piece", __FILE__, __LINE__);
+        }
+        ++s->done;
+        if (wait) break;   // one piece per wait
+    }
+    return 0;
+}
+
+int ss_feed(vs_rsync *h, const uint8_t *p, size_t n) {
+    SigStream *s = h->sst;
+    if (!s) return fail(VS_ERR_STATE, "vs_rsync_sig_feed before vs_rsync_sig_begin");
+    if (n && !p) return fail(VS_ERR_ARG, "null buffer");
+    if ((int64_t)n > s->len - s->fed) return fail(VS_ERR_ARG, "fed past the length given to begin");
+    VS_TRY(rs_dev(h));
+    bool dma = false;
+    while (n) {
+        const int64_t k = s->fed / s->piece, off = s->fed - k * s->piece;
+        const size_t take = (size_t)std::min<int64_t>((int64_t)n, s->piece - off);
+        while (k >= s->done + s->ring) VS_TRY(ss_collect(s, true));   // slot k % ring is free
+        VS_TRY(feed_copy(s->stage, s->cs, s->slot[k % s->ring].as<uint8_t>() + off, p, take, &dma,
+                         &s->pinned_bytes, &s->staged_bytes));
+        s->fed += (int64_t)take;
+        p += take;
+        n -= take;
+        if (s->fed == std::min((k + 1) * s->piece, s->len)) {
+            VS_TRY(ss_launch(h, s, k));
+            s->launched = k + 1;
+        }
+    }
+    if (dma) VS_HIP(hipStreamSynchronize(s->cs));
+    return 0;
+}
+
+int ss_next(vs_rsync *h, uint32_t *sum1, uint8_t *sum2, size_t cap, size_t *n_out) {
+    SigStream *s = h->sst;
+    *n_out = 0;
+    if (!s) return fail(VS_ERR_STATE, "vs_rsync_sig_next before vs_rsync_sig_begin");
+    VS_TRY(rs_dev(h));
+    VS_TRY(ss_collect(s, false));
+    const int64_t per = s->piece / s->blength;
+    // nothing ready but a piece in flight: wait for the oldest (with none in
+    // flight, more input is needed first)
+    if (std::min(s->done * per, s->count) == s->returned && s->done < s->launched)
+        VS_TRY(ss_collect(s, true));
+    const int64_t avail = std::min(s->done * per, s->count) - s->returned;
+    const size_t n = (size_t)std::min<int64_t>((int64_t)cap, avail);
+    if (n) {
+        memcpy(sum1, s->h1 + s->returned, n * 4);
+        memcpy(sum2, s->h2 + s->returned * s->s2length, n * (size_t)s->s2length);
+        s->returned += (int64_t)n;
+    }
+    *n_out = n;
+    if (!n && s->returned == s->count && s->fed == s->len) return VS_EOF;
     return 0;
 }
 
@@ -1426,6 +1899,8 @@ VS_API int vs_rsync_set_stream(vs_rsync *h, void *hip_stream) {
 VS_API void vs_rsync_close(vs_rsync *h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    ms_release(h);
+    ss_release(h);
     for (FsJob &j : h->fs) fs_release(j);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (DevBuf *b : {&h->d_sum1, &h->d_keys, &h->d_tkey, &h->d_dir, &h->d_filt, &h->d_tmp, &h->d_bkt, &h->px,
@@ -1582,11 +2057,6 @@ VS_API int vs_rsync_file_sum_start(vs_rsync *h, const void *dev_src, int64_t len
     if (csum_type != VS_CSUM_MD5 && csum_type != VS_CSUM_XXH64 && csum_type != VS_CSUM_XXH3_64 &&
         csum_type != VS_CSUM_XXH3_128)
         return fail(VS_ERR_ARG, "unsupported checksum type");
-    const bool xxh3 = csum_type == VS_CSUM_XXH3_64 || csum_type == VS_CSUM_XXH3_128;
-    if (!xxh3 && len > kFsSerialMax)
-        return fail(VS_ERR_ARG, "whole-file MD5 / XXH64 is one serial chain (one GPU lane, "
-                                "~0.1 GB/s): refused above " + std::to_string(kFsSerialMax) +
-                                " bytes -- negotiate xxh128 (DESIGN.md 3.4)");
     VS_TRY(rs_dev(h));
     VS_TRY(order_after_null(h));
     return fs_start(h, (const uint8_t *)dev_src, (uint64_t)len, csum_type, true, nullptr);
@@ -1601,24 +2071,28 @@ VS_API int vs_rsync_file_sum_wait(vs_rsync *h, uint8_t out[16]) {
     h->fs_head++;
     const int rc = fs_finish(j);   // joins the job's thread, syncs its stream
     j.active = false;
+    fs_pop_consumed(h);
     VS_TRY(rc);
     fs_account(h, j);
-    memset(out, 0, 16);
-    const int n = (j.csum == VS_CSUM_MD5 || j.csum == VS_CSUM_XXH3_128) ? 16 : 8;
-    if (j.serial) {
-        memcpy(out, j.hlast, (size_t)n);
-    } else {
-        uint8_t o[16];
-        xxh3_file_finish(j.hlast, j.len, j.acc, j.csum, o);
-        memcpy(out, o, (size_t)n);
-    }
+    fs_digest(j, out);
     return 0;
 }
 
+// the blocking form waits for its own job only: jobs the caller already has in
+// flight keep their FIFO order (the slot is skipped when they are waited for)
 VS_API int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_type,
                              uint8_t out[16]) {
+    if (!out) return fail(VS_ERR_ARG, "bad arguments");
     VS_TRY(vs_rsync_file_sum_start(h, dev_src, len, csum_type));
-    return vs_rsync_file_sum_wait(h, out);
+    FsJob &j = h->fs[(h->fs_tail - 1) % vs_rsync::kFsJobs];
+    const int rc = fs_finish(j);
+    j.active = false;
+    j.consumed = true;
+    fs_pop_consumed(h);
+    VS_TRY(rc);
+    fs_account(h, j);
+    fs_digest(j, out);
+    return 0;
 }
 
 VS_API int vs_rsync_file_sum_blocks_start(vs_rsync *h, const void *dev_blocks, int64_t nblocks,
@@ -1639,6 +2113,7 @@ VS_API int vs_rsync_file_sum_blocks_wait(vs_rsync *h, uint64_t acc_out[8]) {
     h->fs_head++;
     const int rc = fs_finish(j);   // joins the job's thread, syncs its stream
     j.active = false;
+    fs_pop_consumed(h);
     VS_TRY(rc);
     fs_account(h, j);
     memcpy(acc_out, j.acc, 64);
@@ -1725,6 +2200,94 @@ VS_API int vs_rsync_kernel_time(vs_rsync *h, int which, int reset, double *ms,
     return 0;
 }
 
+VS_API int vs_rsync_set_option(vs_rsync *h, int option, int64_t value) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    switch (option) {
+        case VS_OPT_WALK_SEGMENT_BLOCKS:
+            if (value < 0 || value > (1 << 20)) return fail(VS_ERR_ARG, "segment length out of range");
+            h->seg_blocks = (uint32_t)value;
+            return 0;
+        case VS_OPT_FILE_SUM_PIECE:
+            if (value < 0 || value > (1 << 24)) return fail(VS_ERR_ARG, "file-sum piece out of range");
+            for (const FsJob &j : h->fs)
+                if (j.active) return fail(VS_ERR_STATE, "file-sum jobs in flight");
+            h->fs_piece = (uint64_t)value;
+            return 0;
+        case VS_OPT_BUCKET_BITS:
+            if (value < 0 || value > 26) return fail(VS_ERR_ARG, "bucket bits out of range");
+            h->opt_bbits = (uint32_t)value;   // applies to the next load_sums
+            return 0;
+        case VS_OPT_FA_RECORD:
+            if (value < -1 || value > 4096) return fail(VS_ERR_ARG, "false-alarm record out of range");
+            h->opt_facap = (int32_t)value;
+            return 0;
+        case VS_OPT_HOST_WALK:
+            h->opt_host_walk = value != 0;
+            return 0;
+        default:
+            return fail(VS_ERR_ARG, "unknown vs_rsync option " + std::to_string(option));
+    }
+}
+
+VS_API int vs_rsync_match_begin(vs_rsync *h, int64_t file_len, uint64_t piece_bytes,
+                                uint32_t ring) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    return ms_begin(h, file_len, piece_bytes, ring);
+}
+
+VS_API int vs_rsync_match_feed(vs_rsync *h, const void *buf, size_t n) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    return ms_feed(h, (const uint8_t *)buf, n);
+}
+
+VS_API int vs_rsync_match_next(vs_rsync *h, vs_match *out, size_t cap, size_t *n_out) {
+    if (!h || !n_out || (cap && !out)) return fail(VS_ERR_ARG, "bad arguments");
+    // once every byte is fed the caller can only wait for the walk
+    const bool all = h->mst && h->mst->fed == h->mst->flen;
+    return ms_next(h, out, cap, n_out, all);
+}
+
+VS_API int vs_rsync_match_end(vs_rsync *h, int64_t *n_matches, int64_t *false_alarms) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    return ms_end(h, n_matches, false_alarms);
+}
+
+VS_API int vs_rsync_match_stream_stats(vs_rsync *h, double out[8]) {
+    if (!h || !out) return fail(VS_ERR_ARG, "bad arguments");
+    for (int i = 0; i < 8; ++i) out[i] = 0;
+    MatchStream *m = h->mst;
+    if (!m) return 0;
+    std::lock_guard<std::mutex> lk(m->mu);
+    out[0] = (double)m->pinned_bytes;
+    out[1] = (double)m->staged_bytes;
+    out[2] = m->feed_wait_ms;
+    out[3] = m->walk_ms;
+    out[4] = m->idle_ms;
+    out[5] = (double)m->walked;
+    out[6] = (double)m->piece;
+    out[7] = (double)m->ring;
+    return 0;
+}
+
+VS_API int vs_rsync_sig_begin(vs_rsync *h, int64_t len, int32_t blength, int32_t s2length,
+                              int csum_type, uint32_t seed, uint64_t piece_bytes, uint32_t ring) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    return ss_begin(h, len, blength, s2length, csum_type, seed, piece_bytes, ring);
+}
+
+VS_API int vs_rsync_sig_feed(vs_rsync *h, const void *buf, size_t n) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    return ss_feed(h, (const uint8_t *)buf, n);
+}
+
+VS_API int vs_rsync_sig_next(vs_rsync *h, uint32_t *sum1, uint8_t *sum2, size_t cap_blocks,
+                             size_t *n_blocks) {
+    if (!h || !n_blocks || (cap_blocks && (!sum1 || !sum2))) return fail(VS_ERR_ARG, "bad arguments");
+    return ss_next(h, sum1, sum2, cap_blocks, n_blocks);
+}
+
+// The host one-shot forms run the streamed paths: a file of any size passes
+// through a bounded device ring (SURVEY.md 8(b) signatures).
 VS_API int vs_rsync_signatures(int device, const void *basis, int64_t len, int32_t blength,
                                int32_t s2length, int csum_type, uint32_t seed, uint32_t *sum1,
                                uint8_t *sum2) {
@@ -1733,25 +2296,15 @@ VS_API int vs_rsync_signatures(int device, const void *basis, int64_t len, int32
     if (count && (!sum1 || !sum2)) return fail(VS_ERR_ARG, "null outputs");
     vs_rsync *h = nullptr;
     VS_TRY(vs_rsync_open(device, &h));
-    DevBuf d, s1, s2;
-    int r = 0;
-    if ((r = d.ensure((size_t)std::max<int64_t>(len, 16))) < 0 ||
-        (r = s1.ensure((size_t)std::max<int64_t>(count, 1) * 4)) < 0 ||
-        (r = s2.ensure((size_t)std::max<int64_t>(count, 1) * s2length)) < 0) {
-        vs_rsync_close(h);
-        return r;
+    int r = vs_rsync_sig_begin(h, len, blength, s2length, csum_type, seed, 0, 0);
+    if (!r && len) r = vs_rsync_sig_feed(h, basis, (size_t)len);
+    int64_t got = 0;
+    while (!r) {
+        size_t n = 0;
+        r = vs_rsync_sig_next(h, sum1 + got, sum2 + got * s2length, (size_t)(count - got), &n);
+        got += (int64_t)n;
     }
-    // the caller's buffers are staged through the handle's own pinned chunks
-    // (xfer.cpp): the runtime is never asked to pin caller memory
-    if (len) r = h->stage.h2d(d.p, basis, (size_t)len, h->stream);
-    if (!r)
-        r = vs_rsync_signatures_device(h, d.p, len, blength, s2length, csum_type, seed,
-                                       s1.as<uint32_t>(), s2.as<uint8_t>());
-    if (!r && count) r = h->stage.d2h(sum1, s1.p, (size_t)count * 4, h->stream);
-    if (!r && count) r = h->stage.d2h(sum2, s2.p, (size_t)count * s2length, h->stream);
-    d.release();
-    s1.release();
-    s2.release();
+    if (r == VS_EOF) r = got == count ? 0 : fail(VS_ERR_STATE, "signature stream ended early");
     vs_rsync_close(h);
     return r;
 }
@@ -1765,11 +2318,10 @@ VS_API int vs_rsync_match(int device, const void *src, int64_t len, const vs_sig
     VS_TRY(vs_rsync_open(device, &h));
     int r = vs_rsync_load_sums(h, t->count, t->blength, t->s2length, t->remainder, t->sum1,
                                t->sum2, csum_type, seed);
-    DevBuf d;
+    if (!r) r = vs_rsync_match_begin(h, len, 0, 0);
+    if (!r && len) r = vs_rsync_match_feed(h, src, (size_t)len);
     int64_t nm = 0;
-    if (!r) r = d.ensure((size_t)std::max<int64_t>(len, 16));
-    if (!r && len) r = h->stage.h2d(d.p, src, (size_t)len, h->stream);
-    if (!r) r = vs_rsync_match_device(h, d.p, len, &nm);
+    if (!r) r = vs_rsync_match_end(h, &nm, nullptr);
     if (!r) {
         *n_out = (size_t)nm;
         if ((size_t)nm > cap)
@@ -1777,7 +2329,6 @@ VS_API int vs_rsync_match(int device, const void *src, int64_t len, const vs_sig
         else
             r = vs_rsync_get_matches(h, 0, nm, out);
     }
-    d.release();
     vs_rsync_close(h);
     return r;
 }

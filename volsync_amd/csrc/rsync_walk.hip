@@ -291,7 +291,7 @@ struct RowWin {
 // compare both with the C oracle / libxxhash.
 template <bool WEAK, uint32_t RING = kRing>
 __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, uint64_t o,
-                              uint64_t len, uint32_t lock = 0) {
+                              uint64_t len) {
     using namespace vsstrong;
     const uint32_t q = lane & 15, sp = q >> 2, m = q & 3;
     const uint8_t *p = a.data + o + 16 * q;   // this lane's piece of each 256-byte quarter
@@ -316,18 +316,13 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = ldu16(p + (uint64_t)b * 1024 + 256 * j);
     };
-    // full blocks through a ring of RING blocks in flight; with `lock` (RING
-    // == kRing only), every wave of the workgroup re-syncs every `lock` blocks
-    // (rows_window_idle holds the same barriers), so a cooperative flush's
-    // overlapping windows move through their bytes together and share them in
-    // L1 / L2
+    // full blocks through a ring of RING blocks in flight
     static_assert(RING >= 2, "at least two blocks in flight");
     uint4 ring[RING][4];
 #pragma unroll
     for (uint32_t k = 0; k < RING; ++k)
         if (k < nb) load(ring[k], k);
     for (uint32_t b = 0; b < nb; b += RING) {
-        if (lock && b && b % lock == 0) __syncthreads();
 #pragma unroll
         for (uint32_t k = 0; k < RING; ++k) {
             if (b + k >= nb) break;
@@ -396,15 +391,6 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
     return r;
 }
 
-// the barriers rows_window(..., lock) holds, for a wave with no window
-__device__ __forceinline__ void rows_window_idle(uint64_t len, uint32_t lock) {
-    const uint32_t nb = (uint32_t)((len - 1) / 1024);
-    for (uint32_t b = 0; b < nb; b += kRing) {
-        if (b && b % lock == 0) __syncthreads();
-        if (b + 1 >= nb) break;
-    }
-}
-
 // the first s2length bytes of (lo, hi) equal block i's sum2
 __device__ __forceinline__ bool strong_eq(const RsWalkArgs &a, uint32_t i, uint64_t lo,
                                           uint64_t hi) {
@@ -440,31 +426,7 @@ __device__ int32_t chain_match(const RsWalkArgs &a, uint32_t sum, uint64_t lo, u
     return -1;
 }
 
-// chain_match without the want_i preference: the first block in chain order
-// whose strong sum matches (or -1), false alarms counted before it -- which
-// do not depend on want_i, so queued windows can be scanned in parallel and
-// the preference applied when the walk visits them (chain_prefer).  Uniform.
-__device__ int32_t chain_scan(const RsWalkArgs &a, uint32_t sum, uint64_t lo, uint64_t hi,
-                              uint32_t klen, uint32_t &fa) {
-    const uint32_t b = sum >> (32 - a.dbits);
-    const uint32_t p0 = uni(a.dir[b]), p1 = uni(a.dir[b + 1]);
-    for (uint32_t p = p0; p < p1; ++p) {
-        const uint64_t key = uni64(a.tkey[p]);
-        const uint32_t s1 = (uint32_t)(key >> 32);
-        if (s1 < sum) continue;
-        if (s1 > sum) break;
-        const int32_t i = (int32_t)~(uint32_t)key;
-        const uint32_t li = ((uint32_t)i == a.count - 1 && a.remainder) ? a.remainder : a.blength;
-        if (li != klen) continue;
-        if (!uni((uint32_t)strong_eq(a, (uint32_t)i, lo, hi))) {
-            ++fa;
-            continue;
-        }
-        return i;
-    }
-    return -1;
-}
-// chain_scan for one window per lane (lanes diverge): the queued windows of
+// chain_match without the want_i preference, one window per lane (lanes diverge): the queued windows of
 // a flush resolve their chains in parallel -- one set of directory / key /
 // strong-sum round trips per flush instead of one per window, visited in
 // order afterwards (chain_prefer applies want_i where a window matched)
@@ -932,677 +894,6 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
     return res;
 }
 
-// ---- band flushes (cooperative walk, VSGPU_WALK_BAND=1|2) --------------------
-// The false-alarm windows of one edit overlap by all but a few KiB, yet a
-// flush that streams each from memory fetches every byte once per window
-// (11 B per source byte at the real C4 density).  A band flush hashes the
-// queued windows whose starts lie within kBandSpread of the first from a
-// workgroup-shared LDS ring of the source: the workgroup loads each byte of
-// [h_first, h_last + L) once, band_chunk of every window per ring turn, and
-// the rows read their 16-byte pieces from the ring.
-// RB: ring bytes (a power of two; 64 KiB: two workgroups per CU, 32 KiB:
-// three, with bands half as wide)
-template <uint32_t RB>
-constexpr uint32_t band_chunk() { return RB / 8; }   // bytes of every window per ring turn
-template <uint32_t RB>
-constexpr int64_t band_spread() { return (int64_t)RB - 3 * band_chunk<RB>() - 64; }
-template <uint32_t RB>
-constexpr uint32_t band_words() { return RB / 4 + 8; }   // + a 32-byte mirror of the ring's start
-
-// 16 bytes at source offset x, any alignment: five ring words (the mirror
-// keeps them contiguous past the ring's end) and four byte-aligns
-template <uint32_t RB>
-__device__ __forceinline__ uint4 ring16(const uint32_t *ring, uint64_t x) {
-    const uint32_t i = (uint32_t)x & (RB - 1);
-    const uint32_t w = i >> 2, sft = i & 3;
-    const uint32_t r0 = ring[w], r1 = ring[w + 1], r2 = ring[w + 2], r3 = ring[w + 3],
-                   r4 = ring[w + 4];
-    uint4 v;
-    v.x = __builtin_amdgcn_alignbyte(r1, r0, sft);
-    v.y = __builtin_amdgcn_alignbyte(r2, r1, sft);
-    v.z = __builtin_amdgcn_alignbyte(r3, r2, sft);
-    v.w = __builtin_amdgcn_alignbyte(r4, r3, sft);
-    return v;
-}
-
-// the 16-byte granule at x (16-aligned) of the source; bytes past dlen read 0
-__device__ __forceinline__ uint4 band_granule(const RsWalkArgs &a, uint64_t x) {
-    if (x + 16 <= a.dlen) return *(const uint4 *)(a.data + x);
-    uint32_t w[4] = {0, 0, 0, 0};
-    for (uint32_t k = 0; k < 16 && x + k < a.dlen; ++k) w[k >> 2] |= (uint32_t)a.data[x + k] << (8 * (k & 3));
-    return make_uint4(w[0], w[1], w[2], w[3]);
-}
-template <uint32_t RB>
-__device__ __forceinline__ void band_put(uint32_t *ring, uint64_t x, uint4 v) {
-    const uint32_t i = (uint32_t)x & (RB - 1);
-    *(uint4 *)(ring + (i >> 2)) = v;
-    if (i < 32) *(uint4 *)(ring + RB / 4 + (i >> 2)) = v;
-}
-
-// a row's XXH3 state over a window read in pieces (rows_window's math, no
-// weak sum): blocks [b0, b1), then the partial block, last stripe and merge
-struct RowAcc {
-    uint64_t A0, A1;
-};
-template <class Ld>
-__device__ __forceinline__ void row_acc_blocks(RowAcc &st, const RowSec &rs, uint32_t lane, Ld ld,
-                                               uint32_t b0, uint32_t b1) {
-    const uint32_t q = lane & 15, sp = q >> 2, m = q & 3;
-    if (b0 >= b1) return;
-    auto load = [&](uint4 (&v)[4], uint32_t b) {   // b clamped: every block of [b0, b1) is readable
-        b = b < b1 ? b : b1 - 1;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = ld((uint64_t)b * 1024 + 256 * j + 16 * q);
-    };
-    auto block = [&](const uint4 (&v)[4]) {
-        uint64_t c0 = 0, c1 = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            acc16(v[j], rs.w[4 * j + sp + 2 * m], rs.w[4 * j + sp + 2 * m + 1], c0, c1);
-        st.A0 = scramble(st.A0 + row_sum_sp(c0), rs.w[16 + 2 * m]);
-        st.A1 = scramble(st.A1 + row_sum_sp(c1), rs.w[17 + 2 * m]);
-    };
-    // two buffers, each refilled as soon as it is consumed (no register copies)
-    uint4 v0[4], v1[4];
-    load(v0, b0);
-    for (uint32_t b = b0; b < b1; b += 2) {
-        load(v1, b + 1);
-        block(v0);
-        if (b + 1 >= b1) break;
-        load(v0, b + 2);
-        block(v1);
-    }
-}
-template <class Ld>
-__device__ RowWin row_acc_finish(RowAcc &st, const RsWalkArgs &a, const RowSec &rs, uint32_t lane,
-                                 Ld ld, uint64_t len) {
-    using namespace vsstrong;
-    const uint32_t q = lane & 15, sp = q >> 2, m = q & 3;
-    const uint32_t nb = (uint32_t)((len - 1) / 1024);
-    const uint32_t ns = (uint32_t)(((len - 1) - (uint64_t)nb * 1024) / 64);
-    if (ns) {
-        uint64_t c0 = 0, c1 = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (4 * j + sp < ns) {
-                const uint4 v = ld((uint64_t)nb * 1024 + 256 * j + 16 * q);
-                acc16(v, rs.w[4 * j + sp + 2 * m], rs.w[4 * j + sp + 2 * m + 1], c0, c1);
-            }
-        }
-        st.A0 += row_sum_sp(c0);
-        st.A1 += row_sum_sp(c1);
-    }
-    uint64_t tA = 0, tB = 0;
-    if (sp == 0) {
-        const uint4 v = ld(len - 64 + 16 * m);
-        uint64_t c0 = 0, c1 = 0;
-        acc16(v, csec_at(121 + 16 * m, a.seed), csec_at(129 + 16 * m, a.seed), c0, c1);
-        const uint64_t A0 = st.A0 + c0, A1 = st.A1 + c1;
-        tA = fold64(A0 ^ csec_at(11 + 16 * m, a.seed), A1 ^ csec_at(19 + 16 * m, a.seed));
-        if (a.csum_type == kXxh3_128)
-            tB = fold64(A0 ^ csec_at(117 + 16 * m, a.seed), A1 ^ csec_at(125 + 16 * m, a.seed));
-    }
-    tA = quad_sum(tA);
-    tB = quad_sum(tB);
-    RowWin r;
-    r.weak = 0;
-    r.lo = xxh3_aval(len * P64_1 + tA);
-    r.hi = (a.csum_type == kXxh3_128) ? xxh3_aval(~(len * P64_2) + tB) : 0;
-    return r;
-}
-
-// ---- the cooperative walk: W waves of a workgroup walk ONE segment -----------
-// ("cooperative walk").  At the real C4 table density a
-// wave-private walk spends most of its time hashing false-alarm windows: the
-// ~64 weak-sum collisions in the ~128 KiB literal stretch after each edit are
-// 128 KiB windows that overlap almost entirely, but each 4-window flush
-// re-streams them from the fabric because 384 walks per XCD evict each other's
-// windows from L2 between flushes.  Here the W waves of a workgroup share one
-// walk: a STEP group tests W consecutive 1024-offset batches at once (each
-// wave's start sums from the other waves' batch totals), and a flush hashes
-// up to 4 W queued windows together -- overlapping windows read by all the
-// waves of one CU at the same time, so the bytes come from the fabric about
-// once.  RUN flushes hash up to 4 W windows ahead, the depth doubling with
-// each fully matched flush (a miss costs the windows past it).  Every wave
-// runs the same control flow on the same shared results (LDS), so the
-// workgroup's barriers line up; wave 0 writes the outputs.  Results are
-// hash_search's, bit for bit, as for the wave walk.
-template <int W>
-struct CoopShared {
-    uint32_t dw[W], fw[W], nh[W];   // STEP: per-wave batch totals and hit counts
-    int64_t qoff[4 * W];            // queued hits (offset order)
-    uint32_t qsum[4 * W];
-    uint32_t wweak[4 * W];          // hashed windows
-    uint64_t wlo[4 * W], whi[4 * W];
-    int32_t ci[4 * W];              // their chain scans (chain_scan): block or -1
-    uint32_t cfa[4 * W];            //   and false alarms before it
-    uint32_t seg;                   // the segment being walked
-};
-
-// Hash queued windows [j0, j1) (starts within band_spread<RB> of the first) from
-// the ring and chain-scan them into sh.wlo / whi / ci / cfa.  XXH3's block
-// contributions are independent, so a turn's (window, block) pairs are spread
-// over all 4 W rows of the workgroup, whatever the number of windows; the
-// contributions go through LDS to one lane per (window, accumulator), which
-// runs the serial scramble chain.  The partial block, last stripe and merge
-// run on row j % 4 of wave j / 4 for window j.  Every wave of the workgroup
-// calls it (ring loads and barriers are shared); returns after a barrier.
-template <uint32_t RB>
-constexpr uint32_t band_contrib_words() { return 16 * (band_chunk<RB>() / 1024) * 8 * 2; }
-__device__ __forceinline__ uint64_t xxh3_init_acc(uint32_t k) {
-    using namespace vsstrong;
-    switch (k) {
-        case 0: return P32_3;
-        case 1: return P64_1;
-        case 2: return P64_2;
-        case 3: return P64_3;
-        case 4: return P64_4;
-        case 5: return P32_2;
-        case 6: return P64_5;
-        default: return P32_1;
-    }
-}
-template <int W, uint32_t RB>
-__device__ void band_hash(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, uint32_t wave,
-                          uint32_t *ring, uint64_t *contrib, CoopShared<W> &sh, uint32_t j0,
-                          uint32_t j1, uint64_t L, WProf &wp) {
-    static_assert(W == 4, "band flushes hold at most 16 windows");
-    constexpr uint32_t kChunk = band_chunk<RB>();
-    constexpr uint32_t kB = kChunk / 1024;           // blocks per turn
-    constexpr uint32_t kT = 64 * W;                  // threads
-    constexpr uint32_t kRowsW = 4 * W;               // rows of the workgroup
-    constexpr uint32_t kG = (kChunk + 16) / 16;      // granules of one turn's new bytes (+ rounding)
-    constexpr uint32_t kPer = (kG + kT - 1) / kT;
-    const uint32_t nw = j1 - j0, tid = threadIdx.x;
-    const uint64_t hf = uni64((uint64_t)sh.qoff[j0]), hl = uni64((uint64_t)sh.qoff[j1 - 1]);
-    const uint32_t q = lane & 15, sp = q >> 2, m = q & 3;
-    const uint32_t R = 4 * wave + (lane >> 4);       // this lane's row in the workgroup
-    // the first two turns' bytes: [hf, hl + 2 chunk)
-    uint64_t tp = wclock(wp);
-    {
-        const uint64_t x0 = hf & ~15ull, x1 = min(hl + 2 * kChunk, a.dlen);
-        for (uint64_t xb = x0 + 16ull * tid; xb < x1; xb += 16ull * kT * 8) {
-            uint4 g8[8];   // eight loads in flight before the stores
-#pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) {
-                const uint64_t x = xb + 16ull * kT * k;
-                if (x < x1) g8[k] = band_granule(a, x);
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) {
-                const uint64_t x = xb + 16ull * kT * k;
-                if (x < x1) band_put<RB>(ring, x, g8[k]);
-            }
-        }
-    }
-    const uint32_t nch = (uint32_t)((L + kChunk - 1) / kChunk);
-    const uint32_t nb = (uint32_t)((L - 1) / 1024);
-    // turn k's new bytes [hl + chunk k, hl + chunk (k + 1)) (k >= 2) are
-    // loaded at the start of turn k - 2 and stored at the end of turn k - 1.
-    // Their ring slots are not read before turn k (hl - hf <= band_spread<RB>).
-    auto load_set = [&](uint4 (&g)[kPer], uint32_t k) {
-        if (k >= nch) return;
-        const uint64_t gx0 = (hl + (uint64_t)kChunk * k) & ~15ull;
-        const uint64_t gx1 = min(hl + (uint64_t)kChunk * (k + 1), a.dlen);
-#pragma unroll
-        for (uint32_t i = 0; i < kPer; ++i) {
-            const uint64_t x = gx0 + 16ull * (tid + i * kT);
-            if (x < gx1) g[i] = band_granule(a, x);
-        }
-    };
-    auto put_set = [&](const uint4 (&g)[kPer], uint32_t k) {
-        if (k >= nch) return;
-        const uint64_t gx0 = (hl + (uint64_t)kChunk * k) & ~15ull;
-        const uint64_t gx1 = min(hl + (uint64_t)kChunk * (k + 1), a.dlen);
-#pragma unroll
-        for (uint32_t i = 0; i < kPer; ++i) {
-            const uint64_t x = gx0 + 16ull * (tid + i * kT);
-            if (x < gx1) band_put<RB>(ring, x, g[i]);
-        }
-    };
-    // chain lanes: thread t < 8 nw holds accumulator t % 8 of window t / 8
-    const bool chn = tid < 8 * nw;
-    const uint32_t ck = tid & 7, cj = tid >> 3;
-    uint64_t A = xxh3_init_acc(ck);
-    const uint64_t csec = rs.w[16 + ck];
-    // one (window, block) contribution on this row: lanes q < 4 hold accumulators 2q, 2q + 1
-    auto pair = [&](uint32_t p, uint32_t b0, uint32_t nbt) {
-        const uint32_t j = p / nbt, b = b0 + p % nbt;
-        const uint64_t h = (uint64_t)sh.qoff[j0 + j] + (uint64_t)b * 1024 + 16 * q;
-        uint4 v[4];
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) v[jj] = ring16<RB>(ring, h + 256 * jj);
-        uint64_t c0 = 0, c1 = 0;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-            acc16(v[jj], rs.w[4 * jj + sp + 2 * m], rs.w[4 * jj + sp + 2 * m + 1], c0, c1);
-        c0 = row_sum_sp(c0);
-        c1 = row_sum_sp(c1);
-        if (sp == 0) {
-            uint64_t *o = contrib + (j * kB + (b - b0)) * 8 + 2 * m;
-            o[0] = c0;
-            o[1] = c1;
-        }
-    };
-    auto turn = [&](uint32_t c) {
-        const uint32_t b0 = min(kB * c, nb), nbt = min(kB * c + kB, nb) - b0;
-        const uint32_t P = nw * nbt;
-        uint64_t tt = wclock(wp);
-        for (uint32_t p = R; p < P; p += kRowsW) pair(p, b0, nbt);
-        __syncthreads();
-        wadd(wp, kPrBandPairs, tt);
-        tt = wclock(wp);
-        if (chn)
-            for (uint32_t b = 0; b < nbt; ++b) A = scramble(A + contrib[(cj * kB + b) * 8 + ck], csec);
-        wadd(wp, kPrBandChain, tt);
-    };
-    uint4 gA[kPer], gB[kPer];
-    load_set(gA, 2);
-    __syncthreads();
-    wadd(wp, kPrBandFill, tp);
-    for (uint32_t c = 0; c < nch; c += 2) {
-        load_set(gB, c + 3);
-        turn(c);
-        put_set(gA, c + 2);
-        __syncthreads();
-        if (c + 1 >= nch) break;
-        load_set(gA, c + 4);
-        turn(c + 1);
-        put_set(gB, c + 3);
-        __syncthreads();
-    }
-    // the chained accumulators to the finishing rows
-    if (chn) contrib[cj * 8 + ck] = A;
-    __syncthreads();
-    const bool active = 4 * wave < nw;
-    if (active) {
-        const uint32_t r = R < nw ? R : 4 * wave;
-        RowAcc st{contrib[r * 8 + 2 * m], contrib[r * 8 + 2 * m + 1]};
-        const uint64_t h = (uint64_t)sh.qoff[j0 + r];
-        auto ld = [&](uint64_t off) { return ring16<RB>(ring, h + off); };
-        const RowWin w = row_acc_finish(st, a, rs, lane, ld, L);
-        for (uint32_t rr = 0; rr < 4 && 4 * wave + rr < nw; ++rr) {
-            const uint32_t j = j0 + 4 * wave + rr;
-            const uint32_t sv = uni(sh.qsum[j]);
-            const uint64_t lo = rdl64(w.lo, (int)(16 * rr)), hi = rdl64(w.hi, (int)(16 * rr));
-            uint32_t cf = 0;
-            const int32_t ci = unis(chain_scan(a, sv, lo, hi, (uint32_t)L, cf));
-            if (lane == 0) {
-                sh.wlo[j] = lo;
-                sh.whi[j] = hi;
-                sh.ci[j] = ci;
-                sh.cfa[j] = cf;
-            }
-        }
-    }
-    __syncthreads();
-}
-
-template <int W, uint32_t RB>
-__device__ SegResult walk_segment_coop(const RsWalkArgs &a, const RowSec &rs, const uint32_t *lfilt,
-                                       uint32_t lbits, uint32_t lane, uint32_t wave, int64_t o,
-                                       int32_t want, int64_t stop, int64_t *out_off,
-                                       int32_t *out_idx, int64_t *out_fab, uint32_t cap,
-                                       const SpecView *spec, WProf &wp, CoopShared<W> &sh,
-                                       uint32_t *ring) {
-    constexpr uint32_t Q = 4 * W;   // windows per flush
-    const int64_t fend = min(stop, (int64_t)a.full_end);
-    const uint64_t L = a.blength;
-    const uint8_t *d = a.data;
-    const uint32_t row = lane >> 4;
-    SegResult res{0, 0xffffffffu, 0, 0, want};
-    uint64_t fa = 0;
-    uint32_t n = 0;
-    bool run = true;
-    uint32_t kahead = 1;      // RUN windows per flush: 1 at a segment start
-    uint32_t S1 = 0, S2 = 0;  // STEP: window sums at o (low 16 bits meaningful)
-    auto on_match = [&](int64_t h, int32_t i, uint64_t fa_visit) -> bool {
-        if (wave == 0 && lane == 0 && n < cap) {
-            out_off[n] = h;
-            out_idx[n] = i;
-            out_fab[n] = (int64_t)fa_visit;
-        }
-        ++n;
-        want = i + 1;
-        if (spec) {
-            uint32_t lo = 0, hi = spec->n;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if ((int64_t)uni64((uint64_t)spec->off[mid]) < h) lo = mid + 1;
-                else hi = mid;
-            }
-            const bool hitm = lo < spec->n &&
-                              uni((uint32_t)(spec->off[lo] == h && spec->idx[lo] == i)) != 0;
-            if (hitm) {
-                res.from = lo + 1;
-                fa = fa_visit + spec->fa - uni64((uint64_t)spec->fab[lo]);
-                o = spec->exit_off;
-                want = spec->exit_want;
-                return true;
-            }
-        }
-        const uint32_t li = ((uint32_t)i == a.count - 1 && a.remainder) ? a.remainder : a.blength;
-        o = h + li;
-        return false;
-    };
-    bool merged = false;
-    while (!merged && o < fend) {
-        if (run) {
-            // windows o + j L (j < k) below fend: window j on wave j / 4, row j % 4
-            const int64_t room = (fend - o + (int64_t)L - 1) / (int64_t)L;
-            const uint32_t k = (uint32_t)min<int64_t>(kahead, room);
-            uint64_t t0 = wclock(wp);
-            if (4 * wave < k) {
-                const uint32_t j = 4 * wave + row;
-                const int64_t orow = o + (int64_t)L * (int64_t)(j < k ? j : 4 * wave);
-                const RowWin w = rows_window<true>(a, rs, lane, (uint64_t)orow, L);
-                // this wave's windows' chain scans, beside the other waves'
-                for (uint32_t r = 0; r < 4 && 4 * wave + r < k; ++r) {
-                    const uint32_t wk = (uint32_t)__builtin_amdgcn_readlane((int)w.weak, (int)(16 * r));
-                    const uint64_t lo = rdl64(w.lo, (int)(16 * r)), hi = rdl64(w.hi, (int)(16 * r));
-                    uint32_t cf = 0;
-                    const int32_t ci = unis(chain_scan(a, wk, lo, hi, (uint32_t)L, cf));
-                    if (lane == 0) {
-                        sh.wweak[4 * wave + r] = wk;
-                        sh.wlo[4 * wave + r] = lo;
-                        sh.whi[4 * wave + r] = hi;
-                        sh.ci[4 * wave + r] = ci;
-                        sh.cfa[4 * wave + r] = cf;
-                    }
-                }
-            }
-            __syncthreads();
-            wadd(wp, kPrRun, t0);
-            bool all = true;
-            for (uint32_t j = 0; j < k; ++j) {
-                const int64_t oj = o;
-                const uint32_t wk = uni(sh.wweak[j]);
-                const uint64_t lo = uni64(sh.wlo[j]), hi = uni64(sh.whi[j]);
-                const uint64_t fa_visit = fa;
-                t0 = wclock(wp);
-                fa += uni(sh.cfa[j]);
-                const int32_t i = unis(chain_prefer(a, unis(sh.ci[j]), wk, lo, hi, want));
-                wadd(wp, kPrChain, t0);
-                if (i >= 0) {
-                    merged = on_match(oj, i, fa_visit);
-                    if (merged || o != oj + (int64_t)L) {   // merged, or a short last block
-                        all = false;
-                        break;
-                    }
-                    continue;
-                }
-                const int32_t xo = sbyte(d, (uint64_t)oj);
-                const int32_t xi = (oj + 1 < fend) ? sbyte(d, (uint64_t)oj + L) : 0;
-                S1 = uni((wk & 0xffffu) - (uint32_t)xo + (uint32_t)xi);
-                S2 = uni((wk >> 16) - (uint32_t)L * (uint32_t)xo + S1);
-                o = oj + 1;
-                run = false;
-                all = false;
-                break;
-            }
-            __syncthreads();   // the window slots are read by every wave before reuse
-            kahead = all ? min(2 * k, Q) : 4u;
-            continue;
-        }
-        // ---- STEP: groups of W batches [A + 1024 w, +1024); offsets below
-        // `from` are done.  Hits are queued across groups until 4 W are
-        // waiting (or the region ends), so one flush hashes the overlapping
-        // false-alarm windows of an edit together.
-        uint64_t A = (uint64_t)o & ~15ull;
-        uint32_t T1 = S1, T2 = S2;
-        for (uint64_t u = (uint64_t)o; u > A; --u) {
-            const uint64_t v = u - 1;
-            const int32_t xo = sbyte(d, v), xi = sbyte(d, v + L);
-            T2 = T2 - T1 + (uint32_t)L * (uint32_t)xo;
-            T1 = T1 - (uint32_t)(xi - xo);
-        }
-        T1 = uni(T1);
-        T2 = uni(T2);
-        int64_t from = o;
-        bool matched = false, at_end = false;
-        uint32_t nq = 0;                 // hits queued in sh.qoff / sh.qsum
-        bool partial = false;            // the queue filled inside group (pA, pT1, pT2)
-        uint64_t pA = 0;
-        uint32_t pT1 = 0, pT2 = 0;
-        uint4 cwo, cwi;                  // this wave's batch bytes of group pfA
-        uint64_t pfA = ~0ull;
-        for (;;) {
-            // ---- fill the queue (until 4 W hits wait, or the scan has run a
-            // block length past the first of them: a match, which ends the
-            // STEP, is due within a block of an edit, so scanning further
-            // mostly wastes work where false alarms are sparse)
-            while (nq < Q && !at_end &&
-                   !(nq && (int64_t)A >= uni64((uint64_t)sh.qoff[0]) + (int64_t)L)) {
-                uint64_t tb = wclock(wp);
-                const uint64_t Aw = A + kBatch * wave;
-                const uint64_t c = Aw + 16 * (uint64_t)lane;
-                if (pfA != A) batch_load(a, Aw, lane, cwo, cwi);
-                const uint32_t wo[4] = {cwo.x, cwo.y, cwo.z, cwo.w};
-                const uint32_t wi[4] = {cwi.x, cwi.y, cwi.z, cwi.w};
-                // the next group's bytes, in flight while this one is tested
-                if ((int64_t)(A + kBatch * W) < fend) {
-                    batch_load(a, A + kBatch * W + kBatch * wave, lane, cwo, cwi);
-                    pfA = A + kBatch * W;
-                } else {
-                    pfA = ~0ull;
-                }
-                int Xo = 0, Xi = 0, Eo = 0, Ei = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    Xo = dot4(wo[k], 0x01010101u, Xo);
-                    Xi = dot4(wi[k], 0x01010101u, Xi);
-                    const uint32_t wt = (uint32_t)((16 - 4 * k) | ((15 - 4 * k) << 8) |
-                                                   ((14 - 4 * k) << 16) | ((13 - 4 * k) << 24));
-                    Eo = dot4(wo[k], wt, Eo);
-                    Ei = dot4(wi[k], wt, Ei);
-                }
-                // zero-start sums of this wave's batch: s1 = T1w + P0, s2 = T2w + 16 lane T1w + Y0
-                const uint32_t D = (uint32_t)(Xi - Xo), E = (uint32_t)(Ei - Eo), X = (uint32_t)Xo;
-                const uint32_t P0 = excl_scan(D, lane);
-                const uint32_t Dl = E + 16u * P0 - (uint32_t)L * X;
-                const uint32_t Y0 = excl_scan(Dl, lane);
-                if (lane == 63) {
-                    sh.dw[wave] = P0 + D;
-                    sh.fw[wave] = Y0 + Dl;
-                }
-                __syncthreads();
-                uint32_t t1 = T1, t2 = T2, e1 = T1, e2 = T2;
-#pragma unroll
-                for (uint32_t w2 = 0; w2 < (uint32_t)W; ++w2) {
-                    const uint32_t dwv = uni(sh.dw[w2]), fwv = uni(sh.fw[w2]);
-                    if (w2 < wave) {
-                        t2 = t2 + 1024u * t1 + fwv;
-                        t1 = t1 + dwv;
-                    }
-                    e2 = e2 + 1024u * e1 + fwv;
-                    e1 = e1 + dwv;
-                }
-                uint32_t s1 = t1 + P0;
-                uint32_t s2 = t2 + 16u * lane * t1 + Y0;
-                uint32_t sums[16];
-                uint32_t valid = 0;
-#pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    sums[t] = __builtin_amdgcn_perm(s2, s1, 0x05040100u);
-                    const int32_t xo = __builtin_amdgcn_sbfe((int)wo[t >> 2], 8 * (t & 3), 8);
-                    const int32_t xi = __builtin_amdgcn_sbfe((int)wi[t >> 2], 8 * (t & 3), 8);
-                    s1 += (uint32_t)(xi - xo);
-                    s2 = s2 - (uint32_t)L * (uint32_t)xo + s1;
-                    const int64_t qo = (int64_t)c + t;
-                    valid |= (uint32_t)(qo >= from && qo < fend) << t;
-                }
-                uint32_t hit = valid;
-                if (lbits) {
-                    uint32_t lw[16];
-#pragma unroll
-                    for (int t = 0; t < 16; ++t) lw[t] = lfilt[(sums[t] >> (32 - lbits)) >> 5];
-                    uint32_t lh = 0;
-#pragma unroll
-                    for (int t = 0; t < 16; ++t)
-                        lh |= ((lw[t] >> ((sums[t] >> (32 - lbits)) & 31)) & 1u) << t;
-                    hit &= lh;
-                }
-                {
-                    uint64_t fw[16];
-#pragma unroll
-                    for (int t = 0; t < 16; ++t) {
-                        const bool on = (hit >> t) & 1u;
-                        fw[t] = a.filt_b[on ? rs_bloom_word(sums[t], a.fbits) : 0u];
-                    }
-                    uint32_t pass = 0;
-#pragma unroll
-                    for (int t = 0; t < 16; ++t) {
-                        const uint64_t m = rs_bloom_mask(sums[t]);
-                        pass |= (uint32_t)((fw[t] & m) == m) << t;
-                    }
-                    hit &= pass;
-                }
-                for (uint32_t mm = hit; mm;) {
-                    const int t = __builtin_ctz(mm);
-                    mm &= mm - 1;
-                    uint32_t st = sums[0];
-#pragma unroll
-                    for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
-                    if (!probe_bucket(a, st)) hit &= ~(1u << t);
-                }
-                // the group's hits in offset order (wave, lane, bit), queued at nq + rank
-                const uint32_t pc = (uint32_t)__builtin_popcount(hit);
-                const uint32_t lp = excl_scan(pc, lane);
-                if (lane == 63) sh.nh[wave] = lp + pc;
-                __syncthreads();
-                uint32_t base = 0, H = 0;
-#pragma unroll
-                for (uint32_t w2 = 0; w2 < (uint32_t)W; ++w2) {
-                    const uint32_t v = uni(sh.nh[w2]);
-                    if (w2 < wave) base += v;
-                    H += v;
-                }
-                {
-                    uint32_t g = nq + base + lp;
-                    for (uint32_t mm = hit; mm; mm &= mm - 1, ++g) {
-                        const int t = __builtin_ctz(mm);
-                        if (g < Q) {
-                            uint32_t st = sums[0];
-#pragma unroll
-                            for (int k = 1; k < 16; ++k) st = (t == k) ? sums[k] : st;
-                            sh.qoff[g] = (int64_t)c + t;
-                            sh.qsum[g] = st;
-                        }
-                    }
-                }
-                wadd(wp, kPrStep, tb);
-                if (nq + H > Q) {
-                    // the queue filled inside this group: flush, then redo the
-                    // group past the last visited hit
-                    partial = true;
-                    pA = A;
-                    pT1 = T1;
-                    pT2 = T2;
-                    nq = Q;
-                } else {
-                    nq += H;
-                    if ((int64_t)(A + kBatch * W) >= fend) {
-                        at_end = true;
-                    } else {
-                        T1 = e1;
-                        T2 = e2;
-                        A += kBatch * W;
-                        from = (int64_t)A;
-                    }
-                }
-                __syncthreads();   // sh.dw / fw / nh and the queue slots
-            }
-            if (nq == 0) {   // the region ended without a hit
-                o = fend;
-                break;
-            }
-            // ---- flush: hash the queued windows together, visit them in order
-            int64_t hlast = 0;
-            // visit [jb, je): hash_search's chain walks in offset order
-            auto visit = [&](uint32_t jb, uint32_t je) {
-                for (uint32_t j = jb; j < je; ++j) {
-                    const int64_t h = (int64_t)uni64((uint64_t)sh.qoff[j]);
-                    const uint32_t sv = uni(sh.qsum[j]);
-                    const uint64_t lo = uni64(sh.wlo[j]), hi = uni64(sh.whi[j]);
-                    const uint64_t fa_visit = fa;
-                    uint64_t tc = wclock(wp);
-                    fa += uni(sh.cfa[j]);
-                    const int32_t i = unis(chain_prefer(a, unis(sh.ci[j]), sv, lo, hi, want));
-                    wadd(wp, kPrChain, tc);
-                    hlast = h;
-                    if (i >= 0) {
-                        merged = on_match(h, i, fa_visit);
-                        matched = true;
-                        return;
-                    }
-                }
-            };
-            if constexpr (RB != 0) {
-                // bands of windows starting within band_spread<RB> of each other
-                for (uint32_t j0 = 0; j0 < nq && !matched;) {
-                    const int64_t hf = (int64_t)uni64((uint64_t)sh.qoff[j0]);
-                    uint32_t j1 = j0 + 1;
-                    while (j1 < nq && (int64_t)uni64((uint64_t)sh.qoff[j1]) - hf <= band_spread<RB>()) ++j1;
-                    uint64_t tf = wclock(wp);
-                    band_hash<W, RB>(a, rs, lane, wave, ring, (uint64_t *)(ring + band_words<RB>()),
-                                     sh, j0, j1, L, wp);
-                    wadd(wp, kPrFlush, tf);
-                    visit(j0, j1);
-                    j0 = j1;
-                }
-            } else {
-                uint64_t tf = wclock(wp);
-                if (a.lock && 4 * wave >= nq) rows_window_idle(L, a.lock);
-                if (4 * wave < nq) {
-                    const uint32_t j = 4 * wave + row;
-                    const int64_t orow = sh.qoff[j < nq ? j : 4 * wave];
-                    const RowWin w = rows_window<false>(a, rs, lane, (uint64_t)orow, L, a.lock);
-                    for (uint32_t r = 0; r < 4 && 4 * wave + r < nq; ++r) {
-                        const uint32_t sv = uni(sh.qsum[4 * wave + r]);
-                        const uint64_t lo = rdl64(w.lo, (int)(16 * r)), hi = rdl64(w.hi, (int)(16 * r));
-                        uint32_t cf = 0;
-                        const int32_t ci = unis(chain_scan(a, sv, lo, hi, (uint32_t)L, cf));
-                        if (lane == 0) {
-                            sh.wlo[4 * wave + r] = lo;
-                            sh.whi[4 * wave + r] = hi;
-                            sh.ci[4 * wave + r] = ci;
-                            sh.cfa[4 * wave + r] = cf;
-                        }
-                    }
-                }
-                __syncthreads();
-                wadd(wp, kPrFlush, tf);
-                visit(0, nq);
-            }
-            __syncthreads();   // queue / window slots are reused
-            if (matched) break;
-            nq = 0;
-            if (partial) {
-                partial = false;
-                A = pA;
-                T1 = pT1;
-                T2 = pT2;
-                from = hlast + 1;
-                at_end = false;
-                continue;
-            }
-            if (at_end) {
-                o = fend;
-                break;
-            }
-        }
-        if (matched) {
-            run = true;
-            kahead = 4;
-        }
-    }
-    res.n = n;
-    res.fa = fa;
-    res.exit_off = o;
-    res.exit_want = want;
-    return res;
-}
-
 __device__ __forceinline__ void load_prefilter(const RsWalkArgs &a, uint32_t *lfilt) {
     const uint32_t lw = a.lbits ? (1u << a.lbits) / 32 : 0;
     for (uint32_t i = threadIdx.x; i < lw; i += blockDim.x) lfilt[i] = a.filt_l[i];
@@ -1619,8 +910,7 @@ __device__ __forceinline__ uint32_t next_segment(const RsWalkArgs &a, uint32_t l
 }
 
 __device__ __forceinline__ int64_t seg_lo(const RsWalkArgs &a, uint32_t k) {
-    return k <= a.nseg1 ? a.lo + (int64_t)k * a.seg_len
-                        : a.lo + (int64_t)a.nseg1 * a.seg_len + (int64_t)(k - a.nseg1) * a.seg_len2;
+    return a.lo + (int64_t)k * a.seg_len;
 }
 __device__ __forceinline__ int64_t seg_hi(const RsWalkArgs &a, uint32_t k) {
     return min(seg_lo(a, k + 1), a.hi);
@@ -1675,67 +965,6 @@ __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
         }
     }
     WPROG(a, lane, 12, 0, 0);
-}
-
-// the speculative pass with W-wave cooperative walks (walk_segment_coop):
-// W == 12 keeps the LDS prefilter (one workgroup per CU); smaller W runs
-// 12 / W workgroups per CU without it
-template <int W, uint32_t RB>
-__global__ __launch_bounds__(64 * W, (RB == 32768 ? 3 : 1)) void rs_walk_spec_coop_kernel(RsWalkArgs a) {
-    constexpr bool kLds = W >= 12;
-    __shared__ uint32_t lfilt[kLds ? kLdsFiltWordsW : 1];
-    __shared__ __attribute__((aligned(16))) uint32_t ring[RB ? band_words<RB>() + band_contrib_words<RB>() : 4];
-    __shared__ uint64_t lsec[24];
-    __shared__ CoopShared<W> sh;
-    load_secret(lsec, a.seed);
-    const uint32_t lbits = kLds ? a.lbits : 0u;
-    if (kLds) {
-        load_prefilter(a, lfilt);
-    } else {
-        __syncthreads();
-    }
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = uni(threadIdx.x >> 6);
-    const RowSec rs{lsec};
-    WPROF_INIT(a.prof != nullptr);
-    for (;;) {
-        if (threadIdx.x == 0) sh.seg = atomicAdd(a.work, 1u);
-        __syncthreads();
-        const uint32_t k = uni(sh.seg);
-        __syncthreads();   // every wave has read the segment before it is overwritten
-        if (k >= a.nseg) break;
-        const uint64_t ts = wclock(wp);
-        const int64_t e = (int64_t)uni64((uint64_t)(k ? seg_lo(a, k) : a.e0));
-        const int32_t w = unis(k ? (int32_t)a.count : a.w0);
-        const uint64_t base = (uint64_t)k * a.cap;
-        const SegResult r = walk_segment_coop<W, RB>(a, rs, lfilt, lbits, lane, wave, e, w,
-                                                       seg_hi(a, k), a.spec_off + base,
-                                                       a.spec_idx + base, a.spec_fab + base, a.cap,
-                                                       nullptr, wp, sh, ring);
-        wadd(wp, kPrSeg, ts);
-        if (wave == 0 && lane == 0) {
-            a.spec_nfa[k] = a.facap + 1;   // not recorded: stitches re-walk
-            a.spec_n[k] = r.n;
-            a.spec_fa[k] = r.fa;
-            a.spec_exit[k] = r.exit_off;
-            a.spec_exitw[k] = r.exit_want;
-            a.fin_entry[k] = e;
-            a.fin_entryw[k] = w;
-            a.fin_from[k] = 0xffffffffu;
-            a.fin_n[k] = 0;
-            a.fin_fa[k] = r.fa;
-            a.exit_new[k] = r.exit_off;
-            a.exitw_new[k] = r.exit_want;
-            if (r.n > a.cap) atomicOr(a.flags, 2u);
-        }
-    }
-    if (wp.on && lane == 0) {
-        uint64_t *pr = a.prof + (uint64_t)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 2 * kPrN;
-        for (int i = 0; i < kPrN; ++i) {
-            pr[i] = wp.cyc[i];
-            pr[kPrN + i] = wp.cnt[i];
-        }
-    }
 }
 
 // the speculative walk of segment k's false alarms in windows below offset x
@@ -1868,34 +1097,6 @@ __global__ void rs_pad_sum2_kernel(const uint8_t *sum2, uint32_t count, uint32_t
 hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t s) {
     if (!a.nseg) return hipSuccess;
     if (a.lbits > 20) return hipErrorInvalidValue;
-    // VSGPU_WALK_COOP=W (4, 6 or 12; 0 = off): the speculative pass with
-    // W-wave cooperative walks (walk_segment_coop)
-    // (read at every launch: tests switch it within one process)
-    const int coop = [] {
-        const char *e = getenv("VSGPU_WALK_COOP");
-        const int v = e ? atoi(e) : 0;
-        return (v == 4 || v == 6 || v == 12) ? v : 0;
-    }();
-    // VSGPU_WALK_BAND=1 / 2 (with COOP=4): band flushes from an LDS ring of
-    // 64 KiB (two workgroups per CU) / 32 KiB (three)
-    const int band = [] {
-        const char *e = getenv("VSGPU_WALK_BAND");
-        const int v = e ? atoi(e) : 0;
-        return (v == 1 || v == 2) ? v : 0;
-    }();
-    if (!stitch && coop) {
-        hipError_t e = hipMemsetAsync(a.work, 0, 4, s);
-        if (e != hipSuccess) return e;
-        const int b4 = coop == 4 ? band : 0;
-        const uint64_t per_cu = b4 == 1 ? 2 : 12 / coop;
-        const uint64_t grid = std::min<uint64_t>(a.nseg, (uint64_t)std::max(cus, 1) * per_cu);
-        if (coop == 12) rs_walk_spec_coop_kernel<12, 0><<<(uint32_t)grid, 768, 0, s>>>(a);
-        else if (coop == 6) rs_walk_spec_coop_kernel<6, 0><<<(uint32_t)grid, 384, 0, s>>>(a);
-        else if (b4 == 1) rs_walk_spec_coop_kernel<4, 65536><<<(uint32_t)grid, 256, 0, s>>>(a);
-        else if (b4 == 2) rs_walk_spec_coop_kernel<4, 32768><<<(uint32_t)grid, 256, 0, s>>>(a);
-        else rs_walk_spec_coop_kernel<4, 0><<<(uint32_t)grid, 256, 0, s>>>(a);
-        return hipGetLastError();
-    }
     // both passes: 8 waves per CU, four window blocks in flight per lane,
     // STEP batches in two stages (one rank of the real C4: 772-778 -> 840
     // GB/s with the membership buckets and without profiling state,

@@ -674,7 +674,6 @@ static uint64_t bucket_blocks(uint32_t k) {
 
 int ShaEngine::init(int dev) {
     device = dev;
-    if (const char *q = getenv("VSGPU_SHA_QUAD_PCT")) quad_pct = (uint32_t)strtoul(q, nullptr, 0);
     if (!hist_h) VS_HIP(hipHostMalloc((void **)&hist_h, kShaBuckets * 4, hipHostMallocDefault));
     VS_TRY(ctl.ensure(64));
     VS_TRY(hist.ensure((2 * kShaBuckets + 16) * 4));

@@ -333,7 +333,9 @@ int send_zstd_token(vs_ztok *z, int32_t token, const uint8_t *data, int32_t nb) 
                 z->out.insert(z->out.end(), z->obuf, z->obuf + n + 2);
                 z->zout.size = 0;
             }
-        } while (in.pos < in.size || (flush == kZFlush && r != 0));
+            // token.c: loop while the input is not consumed or the internal
+            // state is not fully written out (in every flush mode)
+        } while (in.pos < in.size || r > 0);
         z->flush_pending = token == -2;
     }
     if (token == -1) w_byte(z, kEndFlag);

@@ -22,14 +22,9 @@ namespace vsgpu {
 
 // The staging copies are the host side of every pageable feed (the Go
 // Chunker's read buffer is pageable): one thread copies ~20 GB/s, a third of
-// what the DMA behind it moves, so large copies are split over a few threads.
-// VSGPU_COPY_THREADS (default 4, 1 = plain memcpy).
+// what the DMA behind it moves, so large copies are split over four threads.
 void par_memcpy(void *dst, const void *src, size_t n) {
-    static const int threads = [] {
-        const char *e = getenv("VSGPU_COPY_THREADS");
-        const int v = e ? atoi(e) : 4;
-        return v >= 1 && v <= 16 ? v : 4;
-    }();
+    constexpr int threads = 4;
     constexpr size_t kMin = 4u << 20;   // per thread
     const int t = (int)std::min<size_t>((size_t)threads, n / kMin);
     if (t <= 1) {

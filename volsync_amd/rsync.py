@@ -229,6 +229,74 @@ class Matcher:
     def match_sums(self, dev_src: int, length: int) -> List[Tuple[int, int]]:
         return self.matches(0, self.match_device(dev_src, length))
 
+    # ---- streamed forms: a file fed from host memory (vs_rsync_match_* / sig_*) ----
+    def match_begin(self, file_len: int, piece: int = 0, ring: int = 0) -> None:
+        """match_sums over a file of file_len bytes that arrives by feed();
+        the device holds at most `ring` pieces of `piece` bytes."""
+        check(lib.vs_rsync_match_begin(self._h, file_len, piece, ring))
+
+    def match_feed(self, buf, n: Optional[int] = None) -> None:
+        """Next bytes of the file: a host address with n, or a buffer."""
+        if n is None:
+            b = _host_bytes(buf)
+            check(lib.vs_rsync_match_feed(self._h, b.ctypes.data if len(b) else None, len(b)))
+        else:
+            check(lib.vs_rsync_match_feed(self._h, ctypes.c_void_p(buf or None), n))
+
+    def match_next(self, cap: int = 65536) -> Optional[List[Tuple[int, int]]]:
+        """Matches found so far, in order; None at the end of the list."""
+        arr = (VsMatch * max(cap, 1))()
+        n = ctypes.c_size_t(0)
+        rc = check(lib.vs_rsync_match_next(self._h, arr, cap, ctypes.byref(n)))
+        if rc == 1 and n.value == 0:
+            return None
+        return [(arr[i].offset, arr[i].block_index) for i in range(n.value)]
+
+    def match_end(self) -> Tuple[int, int]:
+        """Waits for the walk: (matches, false alarms) of the whole file."""
+        nm, fa = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(lib.vs_rsync_match_end(self._h, ctypes.byref(nm), ctypes.byref(fa)))
+        self._last_n = nm.value
+        return nm.value, fa.value
+
+    def match_stream_stats(self) -> dict:
+        st = (ctypes.c_double * 8)()
+        check(lib.vs_rsync_match_stream_stats(self._h, st))
+        return {"pinned_bytes": st[0], "staged_bytes": st[1], "feed_wait_ms": st[2],
+                "walk_ms": st[3], "walk_idle_ms": st[4], "pieces": int(st[5]),
+                "piece_bytes": int(st[6]), "ring": int(st[7])}
+
+    def sig_begin(self, length: int, blength: int, s2length: int, csum_type: int, seed: int,
+                  piece: int = 0, ring: int = 0) -> None:
+        check(lib.vs_rsync_sig_begin(self._h, length, blength, s2length, csum_type,
+                                     seed & 0xFFFFFFFF, piece, ring))
+        self._sig_s2 = s2length
+
+    def sig_feed(self, buf, n: Optional[int] = None) -> None:
+        if n is None:
+            b = _host_bytes(buf)
+            check(lib.vs_rsync_sig_feed(self._h, b.ctypes.data if len(b) else None, len(b)))
+        else:
+            check(lib.vs_rsync_sig_feed(self._h, ctypes.c_void_p(buf or None), n))
+
+    def sig_next(self, cap: int = 1 << 16):
+        """(sum1 [n] u32, sum2 [n, s2length]) of the next finished blocks, or
+        None after the last."""
+        s1 = np.zeros(max(cap, 1), np.uint32)
+        s2 = np.zeros((max(cap, 1), self._sig_s2), np.uint8)
+        n = ctypes.c_size_t(0)
+        rc = check(lib.vs_rsync_sig_next(self._h, s1.ctypes.data, s2.ctypes.data, cap,
+                                         ctypes.byref(n)))
+        if rc == 1 and n.value == 0:
+            return None
+        return s1[: n.value], s2[: n.value]
+
+    def set_option(self, option: int, value: int) -> None:
+        """vs_rsync_set_option (volsync_amd._lib VS_OPT_*)."""
+        check(lib.vs_rsync_set_option(self._h, option, value))
+
+    _sig_s2 = 2
+
     _last_n = 0
 
 

@@ -188,3 +188,107 @@ def run_walk_shards_local(handles: Sequence, specs: Sequence[SourceShard], ptrs:
     for h in handles:
         out.extend(h.matches(0, h.match_finish()))
     return out
+
+
+# ---- R7 across ranks: the whole-file XXH3 as a relay -------------------------
+#
+# match.c matched() streams every source byte into the file checksum
+# (checksum.c sum_update), one serial XXH3 scramble chain per 1 KiB block.  A
+# file split by byte range therefore relays the 64-byte accumulator state:
+# rank r chains its whole blocks [b_lo, b_hi) from rank r-1's state
+# (vs_rsync_file_sum_blocks_start / _wait: device contributions, host chain)
+# and hands the result to rank r+1; the last rank finishes with the file's
+# last min(len, 1088) bytes (vs_rsync_file_sum_finish).  The ranks together
+# chain exactly (len - 1) // 1024 blocks.  The relay is serial per file
+# (len / 1 KiB chain steps, ~2.1 ns each on the host), but files are
+# independent, so a relay thread per rank runs file k's chain while its
+# successor runs file k-1's: a systolic pipeline whose rate is one rank's
+# chain per file, with a fill latency of world - 1 chains.
+class FileSumRelay:
+    """One rank's relay thread.  fsm: a Matcher (or a test double with
+    file_sum_blocks_start / _wait); ptr: address of file offset data_lo in
+    the rank's copy of its bytes; send(acc) / recv() -> acc move the 8 u64
+    accumulators to the next rank / from the previous one (rank 0 starts
+    from the initial state); last(): the file's last min(len, 1088) bytes
+    (the last rank only).  submit() queues one file, results() waits for all
+    queued files and returns the last rank's digests (others: the states
+    they handed on)."""
+
+    def __init__(self, fsm, spec: SourceShard, ptr: int, data_lo: int, send, recv, last,
+                 csum: int = 8, init=None, finish=None):
+        import queue
+        import threading
+        nb_file = (spec.length - 1) // 1024 if spec.length else 0
+        self.b_lo = min(-(-spec.own_lo // 1024), nb_file)
+        self.b_hi = min(-(-spec.own_hi // 1024), nb_file)
+        if spec.rank == spec.world - 1:
+            self.b_hi = nb_file
+        self.spec, self.fsm, self.csum = spec, fsm, csum
+        self.addr = ptr + self.b_lo * 1024 - data_lo
+        self.send, self.recv, self.last = send, recv, last
+        if init is None or finish is None:
+            from .rsync import file_sum_finish, file_sum_init
+            init, finish = init or file_sum_init, finish or file_sum_finish
+        self._init, self._finish = init, finish
+        self._q = queue.Queue()
+        self._out, self._err = [], []
+        self._th = threading.Thread(target=self._run, daemon=True)
+        self._th.start()
+
+    @property
+    def nblocks(self) -> int:
+        return self.b_hi - self.b_lo
+
+    def _run(self):
+        while True:
+            job = self._q.get()
+            if job is None:
+                return
+            try:
+                spec = self.spec
+                acc = self._init() if spec.rank == 0 else self.recv()
+                self.fsm.file_sum_blocks_start(self.addr, self.nblocks, acc)
+                acc = self.fsm.file_sum_blocks_wait()
+                if spec.rank < spec.world - 1:
+                    self.send(acc)
+                    self._out.append("".join(f"{int(x):016x}" for x in acc))
+                else:
+                    self._out.append(self._finish(acc, self.last(), spec.length, self.csum).hex())
+            except Exception as e:  # reported by results()
+                self._err.append(e)
+            finally:
+                self._q.task_done()
+
+    def submit(self) -> None:
+        self._q.put(1)
+
+    def results(self):
+        self._q.join()
+        if self._err:
+            raise self._err[0]
+        out, self._out = self._out, []
+        return out
+
+    def close(self) -> None:
+        self._q.put(None)
+        self._th.join()
+
+
+def torch_relay_p2p(rank: int, world: int, group=None):
+    """(send, recv) of the 8 accumulators to the next / from the previous rank
+    over torch.distributed point-to-point on CPU tensors (a gloo group of its
+    own: the relay thread runs beside the main thread's collectives)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    def send(acc):
+        t = torch.from_numpy(np.ascontiguousarray(acc, np.uint64).view(np.int64).copy())
+        dist.send(t, dst=rank + 1, group=group)
+
+    def recv():
+        t = torch.zeros(8, dtype=torch.int64)
+        dist.recv(t, src=rank - 1, group=group)
+        return t.numpy().view(np.uint64).copy()
+
+    return send, recv
