@@ -1101,7 +1101,7 @@ def rsync_host_main(args):
                                      sum2.ctypes.data, CSUM_XXH3_128, seed))
         t2 = time.perf_counter()
         # match_sums: S in `read` pieces, matches drained after every read
-        check(lib.vs_rsync_match_begin(h, plan.total, 0, 0))
+        check(lib.vs_rsync_match_begin(h, plan.total, CSUM_XXH3_128, 0, 0))
         nm = 0
         dig = hashlib.sha256()
         base = hs.data_ptr()
@@ -1118,11 +1118,12 @@ def rsync_host_main(args):
             if rc == VS_EOF:
                 break
         nm2, fa = ctypes.c_int64(), ctypes.c_int64()
-        check(lib.vs_rsync_match_end(h, ctypes.byref(nm2), ctypes.byref(fa)))
+        fsum = ctypes.create_string_buffer(16)
+        check(lib.vs_rsync_match_end(h, ctypes.byref(nm2), ctypes.byref(fa), fsum))
         assert nm2.value == nm
         t3 = time.perf_counter()
         return {"sig_s": t1 - t0, "load_s": t2 - t1, "match_s": t3 - t2, "matches": nm,
-                "false_alarms": fa.value, "digest": dig.hexdigest()}
+                "false_alarms": fa.value, "digest": dig.hexdigest(), "file_sum": fsum.raw.hex()}
 
     for _ in range(args.warmup):
         step()
@@ -1156,11 +1157,14 @@ def rsync_host_main(args):
                         "load_sums_ms": round(r["load_s"] * 1e3, 2)},
         "match_stream_stats": st,
         "matches": r["matches"], "false_alarms": r["false_alarms"], "digest": r["digest"],
-        "identical_every_step": len({x["digest"] for x in res}) == 1,
+        "file_sum": {"csum": "xxh128 (R7, computed as S streamed through)", "digest": r["file_sum"]},
+        "identical_every_step": len({(x["digest"], x["file_sum"]) for x in res}) == 1,
     }
     if golden:
         out["golden_match"] = (r["digest"] == golden["digest"] and r["matches"] == golden["matches"]
                                and r["false_alarms"] == golden["false_alarms"])
+        if "file_sum" in golden:
+            out["file_sum"]["golden_match"] = r["file_sum"] == golden["file_sum"]
     print(json.dumps(out), flush=True)
 
 

@@ -374,14 +374,24 @@ int vs_rsync_kernel_time(vs_rsync *h, int which, int reset, double *ms, int64_t 
  * last feed; after it, _next waits for the walk); VS_EOF once every match has
  * been returned.  _end waits for the walk and gives the totals (the match
  * list then also stays readable through vs_rsync_get_matches). */
-int vs_rsync_match_begin(vs_rsync *h, int64_t file_len, uint64_t piece_bytes, uint32_t ring);
+/* file_csum (0 = none): the negotiated xfersum whose whole-file checksum
+ * (R7: sum_update over every byte, which matched() does in match.c) the
+ * stream also computes as the file passes -- XXH3 from each piece's block
+ * contributions on the device, chained by the walk thread; MD5 / XXH64 on the
+ * caller's thread from the fed bytes -- returned by _end in file_sum (as
+ * vs_rsync_file_sum writes it; NULL: not wanted).  piece_bytes: a multiple of
+ * 1024, >= 1 MiB. */
+int vs_rsync_match_begin(vs_rsync *h, int64_t file_len, int file_csum, uint64_t piece_bytes,
+                         uint32_t ring);
 int vs_rsync_match_feed(vs_rsync *h, const void *buf, size_t n);
 int vs_rsync_match_next(vs_rsync *h, vs_match *out, size_t cap, size_t *n_out);
-int vs_rsync_match_end(vs_rsync *h, int64_t *n_matches, int64_t *false_alarms);
+int vs_rsync_match_end(vs_rsync *h, int64_t *n_matches, int64_t *false_alarms,
+                       uint8_t file_sum[16]);
 /* [0] bytes fed from pinned memory, [1] bytes staged, [2] caller ms waiting
  * for a free piece slot, [3] walk-thread ms walking, [4] walk-thread ms
- * waiting for bytes, [5] pieces walked, [6] piece bytes, [7] ring */
-int vs_rsync_match_stream_stats(vs_rsync *h, double out[8]);
+ * waiting for bytes, [5] pieces walked, [6] piece bytes, [7] ring, [8]
+ * walk-thread ms on the XXH3 file checksum, [9] file_csum */
+int vs_rsync_match_stream_stats(vs_rsync *h, double out[10]);
 /* Replaces generator.c generate_and_send_sums over a basis file of len bytes
  * read in order: pieces of whole blocks are signed as they arrive; _next
  * returns the sums of finished blocks in block order (sum1 [n] u32, sum2

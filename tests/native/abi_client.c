@@ -23,8 +23,9 @@
  *       generated read_size bytes at a time into one host buffer and fed:
  *       vs_rsync_sig_begin/feed/next (sums collected after every read), then
  *       vs_rsync_load_sums + vs_rsync_match_begin/feed/next (matches drained
- *       after every read, as matched() would be called).  Prints "sizes ...",
- *       "offset block" per match, then "false_alarms N".
+ *       after every read, as matched() would be called; the whole-file
+ *       checksum computed as the source passes).  Prints "sizes ...",
+ *       "offset block" per match, "file_sum <hex>", then "false_alarms N".
  */
 #include <inttypes.h>
 #include <stdint.h>
@@ -193,7 +194,7 @@ static int run_rsync_plan(const char *path, uint64_t read_size, uint64_t piece, 
     /* match_sums: the table, then the source read in order */
     if ((rc = vs_rsync_load_sums(h, count, bl, s2, rem, sum1, sum2, csum, seed)))
         return die("vs_rsync_load_sums", rc);
-    if ((rc = vs_rsync_match_begin(h, slen, piece, ring))) return die("vs_rsync_match_begin", rc);
+    if ((rc = vs_rsync_match_begin(h, slen, csum, piece, ring))) return die("vs_rsync_match_begin", rc);
     printf("sizes %d %d %d %d\n", bl, s2, count, rem);
     vs_match m[256];
     int64_t nm = 0;
@@ -214,9 +215,12 @@ static int run_rsync_plan(const char *path, uint64_t read_size, uint64_t piece, 
         pos += take;
     }
     int64_t total = 0, fa = 0;
-    if ((rc = vs_rsync_match_end(h, &total, &fa))) return die("vs_rsync_match_end", rc);
+    uint8_t fsum[16];
+    if ((rc = vs_rsync_match_end(h, &total, &fa, fsum))) return die("vs_rsync_match_end", rc);
     if (total != nm) return die("match count", -1);
-    printf("false_alarms %" PRId64 "\n", fa);
+    printf("file_sum ");
+    for (int b = 0; b < 16; ++b) printf("%02x", fsum[b]);
+    printf("\nfalse_alarms %" PRId64 "\n", fa);
     fprintf(stderr, "rsync-plan: %" PRId64 " matches, %" PRId64 " false alarms over %" PRId64 " bytes\n",
             nm, fa, slen);
     vs_rsync_close(h);

@@ -50,10 +50,25 @@ def c4plan_3g():
             "want": want, "fa": fa}
 
 
-def _stream_match(m, data, feeds, piece, ring):
+def _file_sum_want(data, csum: int) -> bytes:
+    """checksum.c sum_end of the whole file (no seed), by libxxhash / hashlib."""
+    import hashlib
+    import xxhash
+    b = data if isinstance(data, (bytes, memoryview)) else np.ascontiguousarray(data)
+    if csum == 8:
+        return xxhash.xxh3_128_intdigest(b).to_bytes(16, "little")
+    if csum == 7:
+        return xxhash.xxh3_64_intdigest(b).to_bytes(8, "little")
+    if csum == 6:
+        return xxhash.xxh64_intdigest(b, seed=0).to_bytes(8, "little")
+    return hashlib.md5(b).digest()
+
+
+def _stream_match(m, data, feeds, piece, ring, file_csum=0):
     """feed `data` in the given feed sizes, draining matches after each feed
-    (as matched() would be called); returns (matches, false alarms)."""
-    m.match_begin(len(data), piece, ring)
+    (as matched() would be called); returns (matches, false alarms[, file
+    checksum])."""
+    m.match_begin(len(data), piece, ring, file_csum)
     got, pos = [], 0
     base = data.ctypes.data if isinstance(data, np.ndarray) else data.data_ptr()
     for n in feeds:
@@ -70,9 +85,9 @@ def _stream_match(m, data, feeds, piece, ring):
         if r is None:
             break
         got.extend(r)
-    nm, fa = m.match_end()
-    assert nm == len(got)
-    return got, fa
+    r = m.match_end()
+    assert r[0] == len(got)
+    return (got,) + tuple(r[1:])
 
 
 def _stream_sigs(m, data, feeds, hdr, csum, seed, piece=0, ring=0):
@@ -113,12 +128,13 @@ def test_stream_c4plan_3g_pageable_exact(gpu, c4plan_3g):
     src = c["src"]
     piece = 256 << 20
     feeds = [min(piece, len(src) - o) for o in range(0, len(src), piece)]
-    got, fa = _stream_match(m, src, feeds, piece, 3)
+    got, fa, fsum = _stream_match(m, src, feeds, piece, 3, file_csum=8)
     used = free0 - torch.cuda.mem_get_info()[0]
     st = m.match_stream_stats()
     m.close()
     assert got == c["want"]
     assert fa == c["fa"]
+    assert fsum == _file_sum_want(src, 8)   # R7 as the file passed
     assert st["piece_bytes"] * st["ring"] <= 1 << 30 and st["staged_bytes"] == len(src)
     # ring slots (3 x (256 MiB + halo)) + walk scratch; never the file
     assert used < (1 << 30) + (256 << 20), used
@@ -152,10 +168,11 @@ def test_stream_c4plan_3g_c_client(gpu, c4plan_3g):
     assert r.returncode == 0, r.stderr
     lines = [ln for ln in r.stdout.split("\n") if ln]
     assert lines[0].split()[1:] == [str(bl), str(s2l), str(cnt), str(rem)]
-    assert lines[-1].startswith("false_alarms ")
-    got = [tuple(int(x) for x in ln.split()) for ln in lines[1:-1]]
+    assert lines[-1].startswith("false_alarms ") and lines[-2].startswith("file_sum ")
+    got = [tuple(int(x) for x in ln.split()) for ln in lines[1:-2]]
     assert got == c["want"]
     assert int(lines[-1].split()[1]) == c["fa"]
+    assert lines[-2].split()[1] == _file_sum_want(c["src"], 8).hex()
 
 
 def test_stream_signatures_3g(gpu, c4plan_3g):
@@ -224,10 +241,13 @@ def test_stream_ragged_feeds(gpu, csum, seed):
     assert np.array_equal(g1, c1) and np.array_equal(g2, c2)
     m.load_sums(SumStruct(n, hdr.count, hdr.blength, hdr.s2length, hdr.remainder, c1, c2), csum,
                 seed)
-    got, gfa = _stream_match(m, src, feeds, 1 << 20, 2)
+    got, gfa, fsum = _stream_match(m, src, feeds, 1 << 20, 2, file_csum=csum)
+    # the other XXH3 width through the device-contribution path too
+    got2, _, fsum2 = _stream_match(m, src, feeds[::-1], 1 << 20, 3, file_csum=7)
     m.close()
-    assert got == want
+    assert got == want and got2 == want
     assert gfa == fa
+    assert fsum == _file_sum_want(src, csum) and fsum2 == _file_sum_want(src, 7)
 
 
 @pytest.mark.parametrize("slen", [0, 1, 5000, (1 << 20) - 1, 1 << 20, (1 << 20) + 1, (2 << 20) + 77])
@@ -251,16 +271,17 @@ def test_stream_edge_lengths(gpu, slen):
         pin[:slen].copy_(torch.from_numpy(src))
     m = Matcher()
     m.load_sums(s, R.CSUM_XXH3_128, SEED)
-    m.match_begin(slen, 1 << 20, 2)
+    m.match_begin(slen, 1 << 20, 2, 8)
     if slen:
         m.match_feed(pin.data_ptr(), slen)
     got = []
     while (r := m.match_next()) is not None:
         got.extend(r)
-    nm, gfa = m.match_end()
+    nm, gfa, fsum = m.match_end()
     st = m.match_stream_stats()
     m.close()
     assert got == want and nm == len(want) and gfa == fa
+    assert fsum == _file_sum_want(src, 8)   # 0, <= 240 and long files
     assert st["pinned_bytes"] == slen
     assert match_sums(src, s, R.CSUM_XXH3_128, SEED) == want
 

@@ -189,10 +189,10 @@ def _load() -> ctypes.CDLL:
         "vs_rsync_stats": (c_int, [vp, i64p, i64p, i64p, i32p]),
         "vs_rsync_timing": (c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
         "vs_rsync_kernel_time": (c_int, [vp, c_int, c_int, ctypes.POINTER(ctypes.c_double), i64p]),
-        "vs_rsync_match_begin": (c_int, [vp, i64, c_u64, c_u32]),
+        "vs_rsync_match_begin": (c_int, [vp, i64, c_int, c_u64, c_u32]),
         "vs_rsync_match_feed": (c_int, [vp, vp, c_size]),
         "vs_rsync_match_next": (c_int, [vp, ctypes.POINTER(VsMatch), c_size, ctypes.POINTER(c_size)]),
-        "vs_rsync_match_end": (c_int, [vp, i64p, i64p]),
+        "vs_rsync_match_end": (c_int, [vp, i64p, i64p, vp]),
         "vs_rsync_match_stream_stats": (c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
         "vs_rsync_sig_begin": (c_int, [vp, i64, i32, i32, c_int, c_u32, c_u64, c_u32]),
         "vs_rsync_sig_feed": (c_int, [vp, vp, c_size]),

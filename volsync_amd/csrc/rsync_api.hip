@@ -121,6 +121,18 @@ struct MatchStream {
     size_t head = 0;
     int64_t fa = 0, hashed = 0;        // (under mu)
     double walk_ms = 0, idle_ms = 0;   // (under mu) worker time walking / waiting for bytes
+    // R7 as the file passes (file_csum != 0): XXH3 of a long file from each
+    // piece's block contributions on the device, chained by the walk thread;
+    // MD5 / XXH64 / short XXH3 on the host from the fed bytes; the file's
+    // last <= 1088 bytes kept for the XXH3 finish
+    int fcsum = 0;
+    bool fs_xxh3 = false;
+    uint64_t acc[8] = {};
+    vsgpu::SerialSum ss{};
+    vsgpu::DevBuf dC;
+    uint64_t *hC = nullptr;            // pinned: one piece's contribution rows
+    uint8_t last[1088] = {};
+    double fs_ms = 0;                  // (under mu) walk-thread contributions + chain
 };
 
 // SigStream: pieces are whole blocks; each is signed as soon as its bytes are
@@ -1523,6 +1535,8 @@ void ms_release(vs_rsync *h) {
     for (auto &e : m->ev)
         if (e) (void)hipEventDestroy(e);
     m->stage.release();
+    m->dC.release();
+    pinned_free(m->hC);
     if (m->cs) (void)hipStreamDestroy(m->cs);
     delete m;
     h->mst = nullptr;
@@ -1543,15 +1557,31 @@ void ms_worker(vs_rsync *h, MatchStream *m) {
         const double t0 = now_ms();
         const int64_t lo = k * m->piece, hi = std::min(lo + m->piece, m->flen);
         const int64_t dhi = std::min(hi + m->halo, m->flen);
-        int rc = 0;
+        int rc = rs_dev(h);
         int64_t nm = 0, fa = 0, hashed = 0;
-        if (entry < hi) {
+        if (!rc && hipStreamWaitEvent(h->stream, m->ev[k % m->ring], 0) != hipSuccess)
+            rc = fail_hip(hipGetLastError(), "hipStreamWaitEvent (streamed piece)", __FILE__,
+                          __LINE__);
+        double fms = 0;
+        if (!rc && m->fs_xxh3) {   // R7: this piece's whole blocks of the file
+            const double f0 = now_ms();
+            const uint64_t nbf = (uint64_t)(m->flen - 1) / 1024;
+            const uint64_t b0 = (uint64_t)lo / 1024, b1 = std::min<uint64_t>((uint64_t)hi / 1024, nbf);
+            if (b1 > b0) {
+                hipError_t e = launch_fs_contrib(m->slot[k % m->ring].as<uint8_t>(), b1 - b0,
+                                                 m->dC.as<uint64_t>(), h->stream);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(m->hC, m->dC.p, (b1 - b0) * 64, hipMemcpyDeviceToHost,
+                                       h->stream);
+                if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+                if (e != hipSuccess) rc = fail_hip(e, "streamed file-sum piece", __FILE__, __LINE__);
+                else xxh3_chain_rows(m->hC, b1 - b0, m->acc);
+            }
+            fms = now_ms() - f0;
+        }
+        if (!rc && entry < hi) {
             int64_t x = 0;
             int32_t xw = 0;
-            rc = rs_dev(h);
-            if (!rc && hipStreamWaitEvent(h->stream, m->ev[k % m->ring], 0) != hipSuccess)
-                rc = fail_hip(hipGetLastError(), "hipStreamWaitEvent (streamed piece)", __FILE__,
-                              __LINE__);
             if (!rc)
                 rc = match_scan(h, m->slot[k % m->ring].p, dhi - lo, lo, m->flen, lo, hi, &x, &xw,
                                 true, entry, want);
@@ -1575,7 +1605,8 @@ void ms_worker(vs_rsync *h, MatchStream *m) {
         m->fa += fa;
         m->hashed += hashed;
         m->walked = k + 1;
-        m->walk_ms += now_ms() - t0;
+        m->walk_ms += now_ms() - t0 - fms;
+        m->fs_ms += fms;
         m->cv.notify_all();
     }
 }
@@ -1586,13 +1617,14 @@ int ms_error(MatchStream *m) {
     return 0;
 }
 
-int ms_begin(vs_rsync *h, int64_t flen, uint64_t piece, uint32_t ring) {
+int ms_begin(vs_rsync *h, int64_t flen, int fcsum, uint64_t piece, uint32_t ring) {
     if (!h->loaded) return fail(VS_ERR_STATE, "vs_rsync_match_begin before vs_rsync_load_sums");
     if (flen < 0) return fail(VS_ERR_ARG, "negative file length");
+    if (fcsum) VS_TRY(check_csum(fcsum));
     if (!piece) piece = 256ull << 20;
     if (!ring) ring = 3;
-    if (ring < 2 || ring > MatchStream::kMaxRing || piece < (1u << 20) || (piece & 15))
-        return fail(VS_ERR_ARG, "piece must be >= 1 MiB and a multiple of 16, ring 2..8");
+    if (ring < 2 || ring > MatchStream::kMaxRing || piece < (1u << 20) || (piece & 1023))
+        return fail(VS_ERR_ARG, "piece must be >= 1 MiB and a multiple of 1024, ring 2..8");
     VS_TRY(rs_dev(h));
     ms_release(h);
     MatchStream *m = new MatchStream();
@@ -1600,7 +1632,7 @@ int ms_begin(vs_rsync *h, int64_t flen, uint64_t piece, uint32_t ring) {
     m->flen = flen;
     m->halo = h->blength - 1;
     // a piece never shorter than the walk's halo; small files get one slot's worth
-    m->piece = (int64_t)std::max<uint64_t>(piece, ((uint64_t)h->blength + 15) & ~15ull);
+    m->piece = (int64_t)std::max<uint64_t>(piece, ((uint64_t)h->blength + 1023) & ~1023ull);
     m->np = flen ? (flen + m->piece - 1) / m->piece : 0;
     m->ring = ring;
     // slots k % ring for the pieces there are (a small file: one)
@@ -1608,6 +1640,17 @@ int ms_begin(vs_rsync *h, int64_t flen, uint64_t piece, uint32_t ring) {
     const size_t sb = (size_t)std::min<int64_t>(m->piece + m->halo, std::max<int64_t>(flen, 16)) + 16;
     VS_TRY(stream_mk(&m->cs, m->ev, nslot));
     for (uint32_t i = 0; i < nslot; ++i) VS_TRY(m->slot[i].ensure(sb));
+    m->fcsum = fcsum;
+    m->fs_xxh3 = (fcsum == VS_CSUM_XXH3_64 || fcsum == VS_CSUM_XXH3_128) && flen > 240;
+    if (m->fs_xxh3) {
+        xxh3_init_acc(m->acc);
+        const uint64_t rows = (uint64_t)m->piece / 1024;
+        VS_TRY(m->dC.ensure(rows * 64));
+        if (!(m->hC = (uint64_t *)pinned_alloc(rows * 64)))
+            return fail(VS_ERR_NOMEM, "pinned file-sum rows");
+    } else if (fcsum) {
+        serial_sum_init(m->ss, fcsum);
+    }
     h->matches.clear();
     h->st_cand = h->st_fa = h->st_hashed = 0;
     h->st_rounds = 0;
@@ -1639,6 +1682,12 @@ int ms_feed(vs_rsync *h, const uint8_t *p, size_t n) {
         }
         uint8_t *dst = m->slot[k % m->ring].as<uint8_t>() + off;
         VS_TRY(feed_copy(m->stage, m->cs, dst, p, take, &dma, &m->pinned_bytes, &m->staged_bytes));
+        if (m->fcsum && !m->fs_xxh3) serial_sum_update(m->ss, p, take);
+        const int64_t keep = std::min<int64_t>(m->flen, 1088), t0 = m->flen - keep;
+        if (m->fs_xxh3 && m->fed + (int64_t)take > t0) {   // the file's last bytes, for the finish
+            const int64_t a = std::max(m->fed, t0);
+            memcpy(m->last + (a - t0), p + (a - m->fed), (size_t)(m->fed + (int64_t)take - a));
+        }
         if (k > 0 && off < m->halo) {   // also piece k-1's halo
             const size_t hn = (size_t)std::min<int64_t>((int64_t)take, m->halo - off);
             VS_HIP(hipMemcpyAsync(m->slot[(k - 1) % m->ring].as<uint8_t>() + m->piece + off, dst, hn,
@@ -1687,7 +1736,7 @@ int ms_next(vs_rsync *h, vs_match *out, size_t cap, size_t *n_out, bool wait) {
     return 0;
 }
 
-int ms_end(vs_rsync *h, int64_t *n_matches, int64_t *false_alarms) {
+int ms_end(vs_rsync *h, int64_t *n_matches, int64_t *false_alarms, uint8_t *file_sum) {
     MatchStream *m = h->mst;
     if (!m) return fail(VS_ERR_STATE, "vs_rsync_match_end before vs_rsync_match_begin");
     if (m->fed != m->flen)
@@ -1706,6 +1755,18 @@ int ms_end(vs_rsync *h, int64_t *n_matches, int64_t *false_alarms) {
     h->matches.assign(m->out.begin(), m->out.end());
     if (n_matches) *n_matches = (int64_t)m->out.size();
     if (false_alarms) *false_alarms = m->fa;
+    if (file_sum) {
+        memset(file_sum, 0, 16);
+        if (!m->fcsum) return fail(VS_ERR_STATE, "the stream was begun without a file checksum");
+        uint8_t o[16];
+        if (m->fs_xxh3) {
+            xxh3_file_finish(m->last, (uint64_t)m->flen, m->acc, m->fcsum, o);
+        } else {
+            SerialSum ss = m->ss;   // _end may be called again
+            serial_sum_final(ss, o);
+        }
+        memcpy(file_sum, o, (m->fcsum == VS_CSUM_MD5 || m->fcsum == VS_CSUM_XXH3_128) ? 16 : 8);
+    }
     return 0;
 }
 
@@ -2229,10 +2290,10 @@ VS_API int vs_rsync_set_option(vs_rsync *h, int option, int64_t value) {
     }
 }
 
-VS_API int vs_rsync_match_begin(vs_rsync *h, int64_t file_len, uint64_t piece_bytes,
-                                uint32_t ring) {
+VS_API int vs_rsync_match_begin(vs_rsync *h, int64_t file_len, int file_csum,
+                                uint64_t piece_bytes, uint32_t ring) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
-    return ms_begin(h, file_len, piece_bytes, ring);
+    return ms_begin(h, file_len, file_csum, piece_bytes, ring);
 }
 
 VS_API int vs_rsync_match_feed(vs_rsync *h, const void *buf, size_t n) {
@@ -2247,14 +2308,15 @@ VS_API int vs_rsync_match_next(vs_rsync *h, vs_match *out, size_t cap, size_t *n
     return ms_next(h, out, cap, n_out, all);
 }
 
-VS_API int vs_rsync_match_end(vs_rsync *h, int64_t *n_matches, int64_t *false_alarms) {
+VS_API int vs_rsync_match_end(vs_rsync *h, int64_t *n_matches, int64_t *false_alarms,
+                              uint8_t file_sum[16]) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
-    return ms_end(h, n_matches, false_alarms);
+    return ms_end(h, n_matches, false_alarms, file_sum);
 }
 
-VS_API int vs_rsync_match_stream_stats(vs_rsync *h, double out[8]) {
+VS_API int vs_rsync_match_stream_stats(vs_rsync *h, double out[10]) {
     if (!h || !out) return fail(VS_ERR_ARG, "bad arguments");
-    for (int i = 0; i < 8; ++i) out[i] = 0;
+    for (int i = 0; i < 10; ++i) out[i] = 0;
     MatchStream *m = h->mst;
     if (!m) return 0;
     std::lock_guard<std::mutex> lk(m->mu);
@@ -2266,6 +2328,8 @@ VS_API int vs_rsync_match_stream_stats(vs_rsync *h, double out[8]) {
     out[5] = (double)m->walked;
     out[6] = (double)m->piece;
     out[7] = (double)m->ring;
+    out[8] = m->fs_ms;
+    out[9] = (double)m->fcsum;
     return 0;
 }
 
@@ -2318,10 +2382,10 @@ VS_API int vs_rsync_match(int device, const void *src, int64_t len, const vs_sig
     VS_TRY(vs_rsync_open(device, &h));
     int r = vs_rsync_load_sums(h, t->count, t->blength, t->s2length, t->remainder, t->sum1,
                                t->sum2, csum_type, seed);
-    if (!r) r = vs_rsync_match_begin(h, len, 0, 0);
+    if (!r) r = vs_rsync_match_begin(h, len, 0, 0, 0);
     if (!r && len) r = vs_rsync_match_feed(h, src, (size_t)len);
     int64_t nm = 0;
-    if (!r) r = vs_rsync_match_end(h, &nm, nullptr);
+    if (!r) r = vs_rsync_match_end(h, &nm, nullptr, nullptr);
     if (!r) {
         *n_out = (size_t)nm;
         if ((size_t)nm > cap)

@@ -230,10 +230,12 @@ class Matcher:
         return self.matches(0, self.match_device(dev_src, length))
 
     # ---- streamed forms: a file fed from host memory (vs_rsync_match_* / sig_*) ----
-    def match_begin(self, file_len: int, piece: int = 0, ring: int = 0) -> None:
+    def match_begin(self, file_len: int, piece: int = 0, ring: int = 0, file_csum: int = 0) -> None:
         """match_sums over a file of file_len bytes that arrives by feed();
-        the device holds at most `ring` pieces of `piece` bytes."""
-        check(lib.vs_rsync_match_begin(self._h, file_len, piece, ring))
+        the device holds at most `ring` pieces of `piece` bytes; file_csum:
+        also the whole-file checksum of that type (match_end returns it)."""
+        check(lib.vs_rsync_match_begin(self._h, file_len, file_csum, piece, ring))
+        self._ms_csum = file_csum
 
     def match_feed(self, buf, n: Optional[int] = None) -> None:
         """Next bytes of the file: a host address with n, or a buffer."""
@@ -252,19 +254,26 @@ class Matcher:
             return None
         return [(arr[i].offset, arr[i].block_index) for i in range(n.value)]
 
-    def match_end(self) -> Tuple[int, int]:
-        """Waits for the walk: (matches, false alarms) of the whole file."""
+    def match_end(self):
+        """Waits for the walk: (matches, false alarms) of the whole file, plus
+        the whole-file checksum when the stream was begun with file_csum."""
         nm, fa = ctypes.c_int64(0), ctypes.c_int64(0)
-        check(lib.vs_rsync_match_end(self._h, ctypes.byref(nm), ctypes.byref(fa)))
+        fs = ctypes.create_string_buffer(16) if self._ms_csum else None
+        check(lib.vs_rsync_match_end(self._h, ctypes.byref(nm), ctypes.byref(fa), fs))
         self._last_n = nm.value
-        return nm.value, fa.value
+        if fs is None:
+            return nm.value, fa.value
+        return nm.value, fa.value, fs.raw[: 16 if self._ms_csum in (CSUM_MD5, CSUM_XXH3_128) else 8]
+
+    _ms_csum = 0
 
     def match_stream_stats(self) -> dict:
-        st = (ctypes.c_double * 8)()
+        st = (ctypes.c_double * 10)()
         check(lib.vs_rsync_match_stream_stats(self._h, st))
         return {"pinned_bytes": st[0], "staged_bytes": st[1], "feed_wait_ms": st[2],
                 "walk_ms": st[3], "walk_idle_ms": st[4], "pieces": int(st[5]),
-                "piece_bytes": int(st[6]), "ring": int(st[7])}
+                "piece_bytes": int(st[6]), "ring": int(st[7]), "file_sum_ms": st[8],
+                "file_csum": int(st[9])}
 
     def sig_begin(self, length: int, blength: int, s2length: int, csum_type: int, seed: int,
                   piece: int = 0, ring: int = 0) -> None:
