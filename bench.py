@@ -224,7 +224,9 @@ def rsync_main(args):
     import torch
     import torch.distributed as dist
     from volsync_amd import Matcher, sum_sizes_sqroot, synth_fill_device
-    from volsync_amd.rsync import CSUM_XXH3_128
+    from volsync_amd.rsync import CSUM_MD5, CSUM_XXH3_64, CSUM_XXH3_128, CSUM_XXH64
+    CSUM = {"xxh128": CSUM_XXH3_128, "xxh3": CSUM_XXH3_64, "xxh64": CSUM_XXH64,
+            "md5": CSUM_MD5}[args.csum]
     from volsync_amd.rsync_shard import (BlockShard, SourceShard, gather_sums, run_walk_shard,
                                          torch_pair_collectives)
 
@@ -270,7 +272,7 @@ def rsync_main(args):
             synth_fill_device(db.data_ptr(), C4Plan.D_SEED, p.byte_lo, p.byte_hi - p.byte_lo,
                               device=local, stream=stream)
             m.signatures_device(db.data_ptr(), p.byte_hi - p.byte_lo, hdr.blength, hdr.s2length,
-                                CSUM_XXH3_128, seed, full1[p.b_lo:].data_ptr(),
+                                CSUM, seed, full1[p.b_lo:].data_ptr(),
                                 full2[p.b_lo * hdr.s2length:].data_ptr())
         torch.cuda.synchronize(dev)
         if prev is not None:
@@ -278,7 +280,7 @@ def rsync_main(args):
             plan.fill_device(ds.data_ptr(), prev.data_lo, prev.data_hi, device=local,
                              stream=stream)
             m.load_sums_device(hdr.count, hdr.blength, hdr.s2length, hdr.remainder,
-                               full1.data_ptr(), full2.data_ptr(), CSUM_XXH3_128, seed)
+                               full1.data_ptr(), full2.data_ptr(), CSUM, seed)
             share_entry = m.match_scan(ds.data_ptr(), prev.data_hi - prev.data_lo, prev.data_lo,
                                        prev.length, prev.own_lo, prev.own_hi)
             m.match_finish()
@@ -303,7 +305,9 @@ def rsync_main(args):
         b_lo = min(-(-sspec.own_lo // 1024), nb_file)
         b_hi = min(-(-sspec.own_hi // 1024), nb_file)
         fs_blocks = (ds.data_ptr() + b_lo * 1024 - sspec.data_lo, b_hi - b_lo)
-    fs_on = not args.no_file_sum
+    # R7 across ranks relays the XXH3 accumulators; an MD5 / XXH64 file sum
+    # is one host chain over the whole file (not relayed here)
+    fs_on = not args.no_file_sum and (world == 1 or share or args.csum in ("xxh128", "xxh3"))
     fs_out = []
     fs_inflight = [0]
     relay = None
@@ -330,7 +334,7 @@ def rsync_main(args):
         if fs_inflight[0] == args.file_sum_jobs:
             fs_wait()
         if fs_blocks is None:
-            fsm.file_sum_start(ds.data_ptr(), plan.total, CSUM_XXH3_128)
+            fsm.file_sum_start(ds.data_ptr(), plan.total, CSUM)
         else:
             fsm.file_sum_blocks_start(fs_blocks[0], fs_blocks[1], None)
         fs_inflight[0] += 1
@@ -348,7 +352,7 @@ def rsync_main(args):
 
     def step():
         fs_start()
-        m.signatures_device(db.data_ptr(), n, hdr.blength, hdr.s2length, CSUM_XXH3_128, seed,
+        m.signatures_device(db.data_ptr(), n, hdr.blength, hdr.s2length, CSUM, seed,
                             s1.data_ptr(), s2.data_ptr())
         f1, f2 = s1, s2
         if share:
@@ -356,7 +360,7 @@ def rsync_main(args):
         elif world > 1:
             f1, f2 = gather_sums(s1, s2, shard, hdr.s2length, all_gather_any)
         m.load_sums_device(hdr.count, hdr.blength, hdr.s2length, hdr.remainder, f1.data_ptr(),
-                           f2.data_ptr(), CSUM_XXH3_128, seed)
+                           f2.data_ptr(), CSUM, seed)
         if share:
             m.match_scan(ds.data_ptr(), sspec.data_hi - sspec.data_lo, sspec.data_lo,
                          sspec.length, sspec.own_lo, sspec.own_hi)
@@ -410,7 +414,7 @@ def rsync_main(args):
         tot_fa = mine_fa
         digest = hashlib.sha256(recs).hexdigest()
     exact = {"matches": nm, "false_alarms": tot_fa, "digest": digest}
-    g = _golden_rsync(dtotal)
+    g = _golden_rsync(dtotal) if args.csum == "xxh128" else None
     if share:
         gr = (g or {}).get("ranks", {}).get(str(sw))
         exact = {"matches_rank": st["matches"], "false_alarms_rank": mine_fa,
@@ -457,7 +461,7 @@ def rsync_main(args):
                 "host_chain_ms": round(tm["host_chain_ms"], 2),
                 "host_chain_ns_per_KiB": round(tm["host_chain_ms"] * 1e6 / max(fbytes / 1024, 1), 3),
                 "gpu_steps_done_ms_per_step": round((t_gpu - t0) / args.steps * 1e3, 3),
-                "bytes": fbytes, "csum": "xxh128 (unseeded, as sum_init)",
+                "bytes": fbytes, "csum": f"{args.csum} (unseeded, as sum_init)",
                 "scope": ("whole file S" if fs_blocks is None and relay is None else
                           f"whole file S, relayed over {world} ranks ({chained} blocks chained; "
                           f"this rank's chain: {fbytes} B)" if relay is not None else
@@ -467,7 +471,7 @@ def rsync_main(args):
                           f"chains) is not included"),
                 "digest" if fs_blocks is None else "state_out": digest,
                 "identical_every_step": len(digests) == 1}
-        g = _golden_rsync(dtotal)
+        g = _golden_rsync(dtotal) if args.csum == "xxh128" else None
         if g and "file_sum" in g and fs_blocks is None:
             fsum["golden_match"] = digest == g["file_sum"]
     # the dominant kernel: rs_walk_spec_kernel, one launch per step over the
@@ -496,7 +500,7 @@ def rsync_main(args):
                                       f"({per >> 30} GiB of D per GPU; sums all-gathered, walks "
                                       f"stitched over RCCL)" if world > 1 else "1 GPU"),
                        "blength": hdr.blength, "s2length": hdr.s2length, "count": hdr.count,
-                       "source_bytes": plan.total, "csum": "xxh128", "checksum_seed": hex(seed),
+                       "source_bytes": plan.total, "csum": args.csum, "checksum_seed": hex(seed),
                        "matches": nm},
             "roofline": {"bound": "hbm", "achieved": round(scan_gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(scan_gbs / HBM_PEAK_GBS, 4),
@@ -1223,6 +1227,9 @@ def main():
                          "match; smallfiles: C5 per-file blob IDs; host: C2 streamed from "
                          "pinned host memory through vs_cdc_feed/next; rsync-host: C4 streamed "
                          "from pinned host memory through vs_rsync_sig_*/vs_rsync_match_*")
+    ap.add_argument("--csum", choices=["xxh128", "xxh3", "xxh64", "md5"], default="xxh128",
+                    help="rsync: the negotiated strong / whole-file checksum (rsync 3.2.3 peers: "
+                         "xxh128; md5 against peers without xxhash -- the host walk)")
     ap.add_argument("--read-mib", type=int, default=64,
                     help="rsync-host: bytes per feed (the reader's read size)")
     ap.add_argument("--files", type=int, default=1_000_000, help="smallfiles: files per GPU")
@@ -1437,9 +1444,7 @@ def main():
                               "stages_ms": iso},
             "exact": {"chunks": nch, "digest": cdigest},
         }
-        gc = _goldens().get("cdc", {})
-        gold = (gc.get("c2") if world == 1 and seed == 2 else
-                gc.get("c3_prefix", {}).get(str(total)) if seed == 3 else None)
+        gold = _goldens().get("cdc", {}).get(str(seed), {}).get(str(total))
         if gold and gold.get("bytes") == total and gold.get("seed") == seed:
             out["exact"]["golden_match"] = (gold["chunks"], gold["digest"]) == (nch, cdigest)
         if world == 1 and not args.no_cpu_baseline:

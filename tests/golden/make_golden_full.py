@@ -17,7 +17,7 @@ share: the N-rank bench runs N x 128 GiB of it as one final stream, and a
 prefix's chunk list is the full list's chunks that end inside it plus one EOF
 chunk, so one 1 TiB pass gives N = 1, 2, 4, 8.
 
-rsync (C4, bench.py C4Plan): destinations of 64, 128 and 256 GiB (seed 4,
+rsync (C4, bench.py C4Plan): destinations of 8, 16, 64, 128 and 256 GiB (seed 4,
 xxh128, checksum_seed 0x5EED5EED), each against its 10 %-edited source.  The
 source is walked in 1 GiB ranges in parallel from speculative entries, then
 stitched in order: the walk from each range's true entry runs to the first
@@ -26,7 +26,8 @@ the false alarms before the merge are the speculative record's `fab`), else
 the range is re-walked whole.  256 GiB also gets the 8-rank split of the real
 C4 (SourceShard), per rank: its own matches, false alarms and true entry.
 
-usage: python tests/golden/make_golden_full.py [cdc|rsync|all] [--threads T]
+usage: python tests/golden/make_golden_full.py [cdc|rsync|filesum|all] [--threads T]
+       [--rsync-gib G ...] [--skip-c3]
 writes tests/golden/full_configs.json (merged with what is there).
 """
 from __future__ import annotations
@@ -255,16 +256,24 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("what", nargs="?", default="all", choices=["cdc", "rsync", "filesum", "all"])
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
-    ap.add_argument("--rsync-gib", type=int, nargs="*", default=[64, 128, 256])
+    ap.add_argument("--rsync-gib", type=int, nargs="*", default=[8, 16, 64, 128, 256])
+    ap.add_argument("--skip-c3", action="store_true", help="cdc: keep the 1 TiB entries")
     a = ap.parse_args()
     data = json.load(open(OUT)) if os.path.exists(OUT) else {}
     data["_about"] = ("tests/golden/make_golden_full.py: full-size chunk / match list digests "
                       "(vs_chunk / vs_match records, SHA-256) from the C oracle")
     if a.what in ("cdc", "all"):
-        data.setdefault("cdc", {})
-        data["cdc"]["c2"] = cdc_golden(2, 64 * GiB, [64 * GiB], a.threads)[str(64 * GiB)]
-        c3 = cdc_golden(3, 1024 * GiB, [128 * GiB, 256 * GiB, 512 * GiB, 1024 * GiB], a.threads)
-        data["cdc"]["c3_prefix"] = c3
+        # data["cdc"][seed][length]: the chunk list of the stream's first
+        # `length` bytes as one final stream (C2 = seed 2 at 64 GiB and its
+        # power-of-two prefixes, for the shared-GPU rehearsals; C3 = seed 3
+        # at N x 128 GiB)
+        cdc = data.setdefault("cdc", {})
+        cdc.setdefault("2", {}).update(
+            cdc_golden(2, 64 * GiB, [(1 << k) * GiB for k in range(7)], a.threads))
+        json.dump(data, open(OUT, "w"), indent=1)
+        if not a.skip_c3:
+            cdc.setdefault("3", {}).update(
+                cdc_golden(3, 1024 * GiB, [128 * GiB, 256 * GiB, 512 * GiB, 1024 * GiB], a.threads))
         json.dump(data, open(OUT, "w"), indent=1)
     if a.what in ("rsync", "all"):
         data.setdefault("rsync", {})
