@@ -260,6 +260,12 @@ def rsync_main(args):
     s2 = torch.zeros(max(shard.blocks, 1) * hdr.s2length, dtype=torch.uint8, device=dev)
     m = Matcher(local)
     m.set_stream(stream)
+    if args.walk_opt:
+        # A/B: --walk-opt NAME=V[,NAME=V] (volsync_amd._lib VS_OPT_* without the prefix)
+        from volsync_amd import _lib
+        for kv in args.walk_opt.split(","):
+            k, v = kv.split("=")
+            m.set_option(getattr(_lib, "VS_OPT_" + k.upper()), int(v))
     seed = 0x5EED5EED
     full1 = full2 = None
     share_entry = None
@@ -1230,6 +1236,8 @@ def main():
     ap.add_argument("--csum", choices=["xxh128", "xxh3", "xxh64", "md5"], default="xxh128",
                     help="rsync: the negotiated strong / whole-file checksum (rsync 3.2.3 peers: "
                          "xxh128; md5 against peers without xxhash -- the host walk)")
+    ap.add_argument("--walk-opt", default="",
+                    help="rsync A/B: handle options, e.g. walk_prefilter=0,walk_segment_blocks=64")
     ap.add_argument("--read-mib", type=int, default=64,
                     help="rsync-host: bytes per feed (the reader's read size)")
     ap.add_argument("--files", type=int, default=1_000_000, help="smallfiles: files per GPU")

@@ -563,6 +563,8 @@ int vs_restic_pack_header(const uint8_t *types, const uint32_t *lengths, const u
                                       * segment for stitch merges (-1 = automatic) */
 #define VS_OPT_HOST_WALK 5           /* rsync: 1 = the host walk with device
                                       * verification for every checksum type */
+#define VS_OPT_WALK_PREFILTER 6      /* rsync: 0 = the device walk without its LDS
+                                      * prefilter (default 1) */
 #define VS_OPT_SHA_QUAD_PCT 16       /* cdc / sha: chains within this % of the longest
                                       * run in latency (quad) mode in the final drain
                                       * (default 80; 0 = split mode only) */

@@ -727,15 +727,16 @@ def test_file_sum_jobs_fifo(gpu):
     m.close()
 
 
-@pytest.mark.parametrize("seg", [8, 16, 64])
-def test_walk_segment_lengths_exact(gpu, seg):
+@pytest.mark.parametrize("seg,prefilter", [(8, 1), (16, 1), (64, 1), (0, 0)])
+def test_walk_segment_lengths_exact(gpu, seg, prefilter):
     """The device walk with other segment lengths (VS_OPT_WALK_SEGMENT_BLOCKS;
-    the default is 32 blocks, shorter for small ranges): more or fewer
-    speculative segments and stitches, the same hash_search -- seeded shifted /
-    overwritten sources (false alarms, runs, short last blocks), the C4
-    parameters on a 1 GiB basis, and the 4-way sharded walk."""
+    the default 0 is 32 blocks, shorter for small ranges) and without the LDS
+    prefilter (VS_OPT_WALK_PREFILTER 0): more or fewer speculative segments
+    and stitches, the same hash_search -- seeded shifted / overwritten sources
+    (false alarms, runs, short last blocks), the C4 parameters on a 1 GiB
+    basis, and the 4-way sharded walk."""
     from volsync_amd import Matcher, SumStruct
-    from volsync_amd._lib import VS_OPT_WALK_SEGMENT_BLOCKS
+    from volsync_amd._lib import VS_OPT_WALK_PREFILTER, VS_OPT_WALK_SEGMENT_BLOCKS
     for csum_type, seed, n, frac, bs in [(R.CSUM_XXH3_128, 0x5EED5EED, 40 << 20, 0.10, 0),
                                          (R.CSUM_XXH3_64, 7, 12 << 20, 0.30, 0),
                                          (R.CSUM_XXH3_128, 1, 6 << 20, 0.20, 1000),
@@ -748,6 +749,7 @@ def test_walk_segment_lengths_exact(gpu, seg):
         ds = to_dev(src)
         m = Matcher()
         m.set_option(VS_OPT_WALK_SEGMENT_BLOCKS, seg)
+        m.set_option(VS_OPT_WALK_PREFILTER, prefilter)
         m.load_sums(SumStruct(0, cnt, bl, s2l, rem, c1, c2), csum_type, seed)
         got = m.match_sums(ds.data_ptr(), len(src))
         st = m.stats()
@@ -762,6 +764,7 @@ def test_walk_segment_lengths_exact(gpu, seg):
     ds = to_dev(src)
     m = Matcher()
     m.set_option(VS_OPT_WALK_SEGMENT_BLOCKS, seg)
+    m.set_option(VS_OPT_WALK_PREFILTER, prefilter)
     m.load_sums(SumStruct(n, n // bl, bl, s2l, 0, c1, c2), csum, seed)
     got = m.match_sums(ds.data_ptr(), len(src))
     st = m.stats()

@@ -219,6 +219,7 @@ struct vs_rsync {
     uint32_t opt_bbits = 0;         // membership bucket bits (0: automatic)
     int32_t opt_facap = -1;         // false-alarm windows recorded per segment (-1: automatic)
     bool opt_host_walk = false;     // the host walk for every checksum type
+    bool opt_prefilter = true;      // the walk's LDS prefilter
     uint64_t fs_piece = 0;          // file-sum piece in 1 KiB blocks (0: 2^18)
     // streamed forms (host-fed files): see the MatchStream / SigStream section
     MatchStream *mst = nullptr;
@@ -974,6 +975,7 @@ int walk_scan(vs_rsync *h) {
     a.lbits = rs_lds_filter_bits(h->fbits);
     a.filt_l = h->d_filt.as<uint32_t>() + ((1ull << h->fbits) / 32);
     a.filt_b = (const uint64_t *)(a.filt_l + ((1ull << a.lbits) / 32));
+    if (!h->opt_prefilter) a.lbits = 0;   // VS_OPT_WALK_PREFILTER 0: no LDS prefilter
     const size_t ns = std::max<uint32_t>(a.nseg, 1), nc = ns * a.cap;
     VS_TRY(h->w_spec_off.ensure(nc * 8));
     VS_TRY(h->w_spec_idx.ensure(nc * 4));
@@ -2284,6 +2286,9 @@ VS_API int vs_rsync_set_option(vs_rsync *h, int option, int64_t value) {
             return 0;
         case VS_OPT_HOST_WALK:
             h->opt_host_walk = value != 0;
+            return 0;
+        case VS_OPT_WALK_PREFILTER:
+            h->opt_prefilter = value != 0;
             return 0;
         default:
             return fail(VS_ERR_ARG, "unknown vs_rsync option " + std::to_string(option));
