@@ -1242,9 +1242,10 @@ def main():
                     help="rsync-host: bytes per feed (the reader's read size)")
     ap.add_argument("--files", type=int, default=1_000_000, help="smallfiles: files per GPU")
     ap.add_argument("--share", default=None, metavar="R/N",
-                    help="rsync: run rank R's share of the N-rank problem on this one GPU "
-                         "(full table, its D blocks and S range; e.g. 3/8 with --per-gpu-gib 32 "
-                         "is one rank of C4)")
+                    help="run rank R's share of the N-rank problem on this one GPU; rsync: "
+                         "the full table, its D blocks and S range (3/8 with --per-gpu-gib 32 "
+                         "is one rank of C4); cdc: its 128 GiB of C3's 1 TiB, cut from its true "
+                         "entry")
     ap.add_argument("--dry", action="store_true",
                     help="CPU/gloo rehearsal of the multi-rank protocol (no GPU; value null)")
     args = ap.parse_args()
@@ -1277,12 +1278,23 @@ def main():
 
     world, rank, local, dev = dist_setup()
 
+    # --share R/N: rank R's work of the N-rank C3 on this one GPU -- its
+    # byte range scanned, its chunks cut from its true entry (the exit of
+    # rank R-1, from the golden) and hashed; the per-rank golden digest checks it
+    share = None
+    if args.share:
+        share = tuple(int(x) for x in args.share.split("/"))
+        assert world == 1 and len(share) == 2 and 0 <= share[0] < share[1], args.share
+    sw, sr = (share[1], share[0]) if share else (world, rank)
     per = int(args.per_gpu_gib * (1 << 30))
     seed = 2                      # C2's stream
-    if world > 1 and args.c3_default:
+    if sw > 1 and args.c3_default:
         per, seed = 128 << 30, 3  # C3's per-GPU share of its 1 TiB stream
-    total = per * world
-    spec = ShardSpec.for_rank(total, world, rank, MaxSize)
+    total = per * sw
+    spec = ShardSpec.for_rank(total, sw, sr, MaxSize)
+    gold_all = _goldens().get("cdc", {}).get(str(seed), {}).get(str(total))
+    gold_rank = (gold_all or {}).get("ranks", [None] * sw)[sr] if share else None
+    share_entry = (gold_rank["entry"] if gold_rank else spec.own_lo) if share else None
     dlen = spec.data_hi - spec.data_lo
     buf = torch.empty(dlen, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -1305,7 +1317,11 @@ def main():
         # stream; its chunks join the time-sliced SHA-256 engine on the hash
         # stream, which keeps hashing them while the next volume is chunked
         # (DESIGN.md 3.4).  wait() hashes everything still queued.
-        if world == 1:
+        if share:
+            dc.scan(buf.data_ptr(), dlen, spec.data_lo, spec.own_lo, spec.own_hi, spec.final)
+            dc.stitch(share_entry)
+            n = dc.finish()
+        elif world == 1:
             n, _ = dc.process(buf.data_ptr(), dlen, 0, True)
         else:
             n = run_shard(dc, spec, buf.data_ptr(), *coll, stats=xst)
@@ -1409,7 +1425,8 @@ def main():
     roofline = dict(roof[dom_name])
     roofline["kernel"] = dom_name
 
-    value = total * args.steps / dt / 1e9
+    # a --share line counts the rank's own bytes
+    value = (own_bytes if share else total) * args.steps / dt / 1e9
     if rank == 0:
         out = {
             "metric": "GB/s chunked+SHA-256 (restic CDC)",
@@ -1424,7 +1441,11 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 volume image, device-resident)",
-            "config": {"workload": (f"C2: {total >> 30} GiB volume, restic CDC + SHA-256, 1 GPU"
+            "config": {"workload": (f"C3 rank {sr} of {sw}: its {own_bytes >> 30} GiB share of the "
+                                    f"{total >> 30} GiB seed-{seed} volume on one GPU (scan, stitch "
+                                    f"from the true entry, finish; exit exchange not included)"
+                                    if share else
+                                    f"C2: {total >> 30} GiB volume, restic CDC + SHA-256, 1 GPU"
                                     if world == 1 else
                                     f"{'C3' if total == 1 << 40 else 'C3-shape'}: {total >> 30} GiB "
                                     f"volume (seed {seed}) byte-range sharded over {world} GPUs "
@@ -1452,10 +1473,16 @@ def main():
                               "stages_ms": iso},
             "exact": {"chunks": nch, "digest": cdigest},
         }
-        gold = _goldens().get("cdc", {}).get(str(seed), {}).get(str(total))
-        if gold and gold.get("bytes") == total and gold.get("seed") == seed:
+        gold = gold_all
+        if share:
+            out["exact"]["entry"] = share_entry
+            out["exact"]["entry_source"] = "golden" if gold_rank else "speculative (no golden)"
+            if gold_rank:
+                out["exact"]["golden_match"] = ((gold_rank["chunks"], gold_rank["digest"])
+                                                == (nch, cdigest))
+        elif gold and gold.get("bytes") == total and gold.get("seed") == seed:
             out["exact"]["golden_match"] = (gold["chunks"], gold["digest"]) == (nch, cdigest)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not share:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_gib << 30, args.cpu_threads)
         print(json.dumps(out), flush=True)
     dc.close()

@@ -565,6 +565,12 @@ int vs_restic_pack_header(const uint8_t *types, const uint32_t *lengths, const u
                                       * verification for every checksum type */
 #define VS_OPT_WALK_PREFILTER 6      /* rsync: 0 = the device walk without its LDS
                                       * prefilter (default 1) */
+#define VS_OPT_WALK_FLUSH_WINDOWS 7  /* rsync: STEP weak hits hashed per flush: 16 =
+                                      * address-lockstep passes over the resync span
+                                      * (blocks > 1 KiB; default), 4 = four windows
+                                      * per pass */
+#define VS_OPT_WALK_FLUSH_SPAN 8     /* rsync: flush once the scan is this many bytes
+                                      * past the first queued hit (0 = no bound; default) */
 #define VS_OPT_SHA_QUAD_PCT 16       /* cdc / sha: chains within this % of the longest
                                       * run in latency (quad) mode in the final drain
                                       * (default 80; 0 = split mode only) */

@@ -26,7 +26,7 @@ the false alarms before the merge are the speculative record's `fab`), else
 the range is re-walked whole.  256 GiB also gets the 8-rank split of the real
 C4 (SourceShard), per rank: its own matches, false alarms and true entry.
 
-usage: python tests/golden/make_golden_full.py [cdc|rsync|filesum|all] [--threads T]
+usage: python tests/golden/make_golden_full.py [cdc|c3|rsync|filesum|all] [--threads T]
        [--rsync-gib G ...] [--skip-c3]
 writes tests/golden/full_configs.json (merged with what is there).
 """
@@ -84,7 +84,7 @@ def eof_chunk(seed: int, s: int, end: int):
     return s, end - s, ch[0][2], bytes.fromhex(ch[0][3])
 
 
-def cdc_golden(seed: int, length: int, prefixes, threads: int) -> dict:
+def cdc_golden(seed: int, length: int, prefixes, threads: int, per_rank: int = 0) -> dict:
     t0 = time.time()
     s, ln, c, ids = O.cdc_synth_mt(seed, length, POL, MN, MX, AVG, threads)
     print(f"cdc seed {seed}: {length >> 30} GiB, {len(s)} chunks in {time.time() - t0:.0f} s",
@@ -101,6 +101,21 @@ def cdc_golden(seed: int, length: int, prefixes, threads: int) -> dict:
         out[str(L)] = {"seed": seed, "bytes": L, "chunks": int(len(rec)), "digest": digest(rec),
                        "first": [int(rec[0, :8].view(np.uint64)[0]), int(rec[0, 8:16].view(np.uint64)[0])],
                        "pol": hex(POL), "min": MN, "max": MX, "avg_bits": AVG}
+        if per_rank and L % per_rank == 0 and L > per_rank:
+            # the W-rank byte-range split of this prefix (volsync_amd/shard.py
+            # ShardSpec): rank r's chunks are those starting in [own_lo, own_hi),
+            # its true entry the first chunk start at or after own_lo
+            W = L // per_rank
+            st = rec[:, 0:8].copy().view(np.uint64).ravel()
+            ranks = []
+            for r in range(W):
+                lo, hi = L * r // W, L * (r + 1) // W
+                a = int(np.searchsorted(st, lo, side="left"))
+                b = int(np.searchsorted(st, hi, side="left"))
+                ranks.append({"rank": r, "own_lo": lo, "own_hi": hi,
+                              "entry": int(st[a]) if a < len(st) else L,
+                              "chunks": b - a, "digest": digest(rec[a:b])})
+            out[str(L)]["ranks"] = ranks
     return out
 
 
@@ -254,7 +269,7 @@ def file_sum_golden(dlen: int, threads: int) -> str:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="?", default="all", choices=["cdc", "rsync", "filesum", "all"])
+    ap.add_argument("what", nargs="?", default="all", choices=["cdc", "c3", "rsync", "filesum", "all"])
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     ap.add_argument("--rsync-gib", type=int, nargs="*", default=[8, 16, 64, 128, 256])
     ap.add_argument("--skip-c3", action="store_true", help="cdc: keep the 1 TiB entries")
@@ -271,9 +286,12 @@ def main():
         cdc.setdefault("2", {}).update(
             cdc_golden(2, 64 * GiB, [(1 << k) * GiB for k in range(7)], a.threads))
         json.dump(data, open(OUT, "w"), indent=1)
+    if a.what in ("cdc", "c3", "all"):
+        cdc = data.setdefault("cdc", {})
         if not a.skip_c3:
             cdc.setdefault("3", {}).update(
-                cdc_golden(3, 1024 * GiB, [128 * GiB, 256 * GiB, 512 * GiB, 1024 * GiB], a.threads))
+                cdc_golden(3, 1024 * GiB, [128 * GiB, 256 * GiB, 512 * GiB, 1024 * GiB], a.threads,
+                           per_rank=128 * GiB))
         json.dump(data, open(OUT, "w"), indent=1)
     if a.what in ("rsync", "all"):
         data.setdefault("rsync", {})

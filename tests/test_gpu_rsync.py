@@ -727,16 +727,27 @@ def test_file_sum_jobs_fifo(gpu):
     m.close()
 
 
-@pytest.mark.parametrize("seg,prefilter", [(8, 1), (16, 1), (64, 1), (0, 0)])
-def test_walk_segment_lengths_exact(gpu, seg, prefilter):
+@pytest.mark.parametrize("seg,prefilter,flushq,span", [(8, 1, 16, 0), (16, 1, 4, 0),
+                                                       (64, 1, 16, 8192), (0, 0, 16, 0),
+                                                       (0, 1, 16, 40000), (0, 1, 4, 3000)])
+def test_walk_segment_lengths_exact(gpu, seg, prefilter, flushq, span):
     """The device walk with other segment lengths (VS_OPT_WALK_SEGMENT_BLOCKS;
-    the default 0 is 32 blocks, shorter for small ranges) and without the LDS
-    prefilter (VS_OPT_WALK_PREFILTER 0): more or fewer speculative segments
-    and stitches, the same hash_search -- seeded shifted / overwritten sources
-    (false alarms, runs, short last blocks), the C4 parameters on a 1 GiB
-    basis, and the 4-way sharded walk."""
+    the default 0 is 32 blocks, shorter for small ranges), without the LDS
+    prefilter (VS_OPT_WALK_PREFILTER 0), with four-window flushes in place of
+    the wide address-lockstep ones (VS_OPT_WALK_FLUSH_WINDOWS) and with flushes
+    bounded by a span (VS_OPT_WALK_FLUSH_SPAN): more or fewer speculative
+    segments, stitches and flushes, the same hash_search -- seeded shifted /
+    overwritten sources (false alarms, runs, short last blocks), the C4
+    parameters on a 1 GiB basis, and the 4-way sharded walk."""
     from volsync_amd import Matcher, SumStruct
-    from volsync_amd._lib import VS_OPT_WALK_PREFILTER, VS_OPT_WALK_SEGMENT_BLOCKS
+    from volsync_amd._lib import (VS_OPT_WALK_FLUSH_SPAN, VS_OPT_WALK_FLUSH_WINDOWS,
+                                  VS_OPT_WALK_PREFILTER, VS_OPT_WALK_SEGMENT_BLOCKS)
+
+    def opts(m):
+        m.set_option(VS_OPT_WALK_SEGMENT_BLOCKS, seg)
+        m.set_option(VS_OPT_WALK_PREFILTER, prefilter)
+        m.set_option(VS_OPT_WALK_FLUSH_WINDOWS, flushq)
+        m.set_option(VS_OPT_WALK_FLUSH_SPAN, span)
     for csum_type, seed, n, frac, bs in [(R.CSUM_XXH3_128, 0x5EED5EED, 40 << 20, 0.10, 0),
                                          (R.CSUM_XXH3_64, 7, 12 << 20, 0.30, 0),
                                          (R.CSUM_XXH3_128, 1, 6 << 20, 0.20, 1000),
@@ -748,8 +759,7 @@ def test_walk_segment_lengths_exact(gpu, seg, prefilter):
         want, fa = O.rsync_match(src, c1, c2, bl, rem, csum_type, seed)
         ds = to_dev(src)
         m = Matcher()
-        m.set_option(VS_OPT_WALK_SEGMENT_BLOCKS, seg)
-        m.set_option(VS_OPT_WALK_PREFILTER, prefilter)
+        opts(m)
         m.load_sums(SumStruct(0, cnt, bl, s2l, rem, c1, c2), csum_type, seed)
         got = m.match_sums(ds.data_ptr(), len(src))
         st = m.stats()
@@ -763,8 +773,7 @@ def test_walk_segment_lengths_exact(gpu, seg, prefilter):
     want, fa = O.rsync_match(src, c1, c2, bl, 0, csum, seed)
     ds = to_dev(src)
     m = Matcher()
-    m.set_option(VS_OPT_WALK_SEGMENT_BLOCKS, seg)
-    m.set_option(VS_OPT_WALK_PREFILTER, prefilter)
+    opts(m)
     m.load_sums(SumStruct(n, n // bl, bl, s2l, 0, c1, c2), csum, seed)
     got = m.match_sums(ds.data_ptr(), len(src))
     st = m.stats()

@@ -440,6 +440,8 @@ struct RsWalkArgs {
     const int32_t *exitw_old;
     int64_t *exit_new;
     int32_t *exitw_new;
+    uint32_t flushq;                 // STEP hits queued per flush: 4 (rows) or 16 (wide)
+    uint32_t flushspan;              // flush once the scan ran this far past the first hit (0: no bound)
     uint64_t *dbg;                   // debug builds: per-wave progress records (host-mapped)
     uint64_t *prof;                  // VS_WALK_PROF builds: per-wave phase cycles/counts [waves][16]
 };

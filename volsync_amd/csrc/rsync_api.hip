@@ -220,6 +220,8 @@ struct vs_rsync {
     int32_t opt_facap = -1;         // false-alarm windows recorded per segment (-1: automatic)
     bool opt_host_walk = false;     // the host walk for every checksum type
     bool opt_prefilter = true;      // the walk's LDS prefilter
+    uint32_t opt_flushq = 16;       // STEP hits per flush (4: rows only; 16: wide passes)
+    uint32_t opt_flushspan = 0;     // flush once the scan is this far past the first hit (0: none)
     uint64_t fs_piece = 0;          // file-sum piece in 1 KiB blocks (0: 2^18)
     // streamed forms (host-fed files): see the MatchStream / SigStream section
     MatchStream *mst = nullptr;
@@ -976,6 +978,8 @@ int walk_scan(vs_rsync *h) {
     a.filt_l = h->d_filt.as<uint32_t>() + ((1ull << h->fbits) / 32);
     a.filt_b = (const uint64_t *)(a.filt_l + ((1ull << a.lbits) / 32));
     if (!h->opt_prefilter) a.lbits = 0;   // VS_OPT_WALK_PREFILTER 0: no LDS prefilter
+    a.flushq = h->opt_flushq;
+    a.flushspan = h->opt_flushspan;
     const size_t ns = std::max<uint32_t>(a.nseg, 1), nc = ns * a.cap;
     VS_TRY(h->w_spec_off.ensure(nc * 8));
     VS_TRY(h->w_spec_idx.ensure(nc * 4));
@@ -2286,6 +2290,14 @@ VS_API int vs_rsync_set_option(vs_rsync *h, int option, int64_t value) {
             return 0;
         case VS_OPT_HOST_WALK:
             h->opt_host_walk = value != 0;
+            return 0;
+        case VS_OPT_WALK_FLUSH_WINDOWS:
+            if (value != 4 && value != 16) return fail(VS_ERR_ARG, "flush windows: 4 or 16");
+            h->opt_flushq = (uint32_t)value;
+            return 0;
+        case VS_OPT_WALK_FLUSH_SPAN:
+            if (value < 0 || value > (1ll << 30)) return fail(VS_ERR_ARG, "flush span out of range");
+            h->opt_flushspan = (uint32_t)value;
             return 0;
         case VS_OPT_WALK_PREFILTER:
             h->opt_prefilter = value != 0;

@@ -391,6 +391,97 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
     return r;
 }
 
+// ---- wide flushes: up to 16 windows, address-lockstep ----------------------
+// At real C4 density a resync after an edit visits ~64 false-alarm windows of
+// one block length within ~2 block lengths of source; hashed four at a time
+// (rows_window) every flush re-streams the whole span, and with every wave of
+// the chip doing the same the spans do not stay in L2.  Here window j (lanes
+// 4j .. 4j+3, lane k owning accumulators 2k, 2k+1 and reading bytes
+// [16k, 16k + 16) of every stripe -- the signature pass's layout) hashes its
+// block b = t - tau_j in iteration t, tau_j = (h_j - h_0) >> 10, so every
+// window of the wave reads inside [h_0 + 1024 t, h_0 + 1024 t + 2048): the
+// wave's loads walk the span once, as one sliding 2 KiB, and the 16 windows
+// share each line.  Windows not yet started or already finished compute on a
+// clamped block and keep their accumulators.  Same XXH3 as rows_window; the
+// results of window j sit in lanes 4j .. 4j+3.
+constexpr uint32_t kWideQ = 16;
+constexpr uint32_t kWideRing = 8;   // stripes in flight per lane
+
+// (not inlined: the call keeps the walk's own register allocation at its
+// four-window spill count, 37 VGPRs against 81 inlined)
+__device__ __noinline__ RowWin wide_windows(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, int64_t qh,
+                               uint32_t nq, uint64_t len) {
+    using namespace vsstrong;
+    const uint32_t j = lane >> 2, k = lane & 3;
+    const int64_t h0 = (int64_t)rdl64((uint64_t)qh, 0);
+    const int64_t hl = (int64_t)rdl64((uint64_t)qh, (int)(nq - 1));
+    const int64_t hj = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)qh >> 32),
+                                                             (int)(j < nq ? j : 0), 64) << 32) |
+                                 (uint32_t)__shfl((int)(uint32_t)qh, (int)(j < nq ? j : 0), 64));
+    const uint32_t tau = (uint32_t)((hj - h0) >> 10);
+    const uint32_t nb = (uint32_t)((len - 1) / 1024);
+    const uint32_t T = uni((uint32_t)((hl - h0) >> 10)) + nb;
+    const uint8_t *p = a.data + hj + 16 * k;
+    uint64_t a0 = (k == 0) ? P32_3 : (k == 1) ? P64_2 : (k == 2) ? P64_4 : P64_5;
+    uint64_t a1 = (k == 0) ? P64_1 : (k == 1) ? P64_3 : (k == 2) ? P32_2 : P32_1;
+    const uint64_t scr0 = rs.w[16 + 2 * k], scr1 = rs.w[17 + 2 * k];
+    // stripe s of iteration t: p + 1024 * clamp(t - tau, 0, nb - 1) + 64 s
+    auto addr = [&](uint32_t t) -> const uint8_t * {
+        const uint32_t b = t < tau ? 0u : min(t - tau, nb - 1);
+        return p + (uint64_t)b * 1024;
+    };
+    uint4 v[kWideRing];
+    {
+        const uint8_t *q = addr(0);
+#pragma unroll
+        for (uint32_t s = 0; s < kWideRing; ++s) v[s] = ldu16(q + 64 * s);
+    }
+    for (uint32_t t = 0; t < T; ++t) {
+        const uint8_t *q = addr(t), *qn = addr(t + 1);
+        // the secret words are re-read from LDS every iteration (ds_read2_b64
+        // per stripe) rather than hoisted into 64 registers
+        const uint64_t *sw = rs.w;
+        asm volatile("" : "+v"(sw));
+        uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+        for (uint32_t s = 0; s < 16; ++s) {
+            const uint4 x = v[s % kWideRing];
+            // refill: stripe s + kWideRing of this iteration, or of the next
+            v[s % kWideRing] = (s + kWideRing < 16) ? ldu16(q + 64 * (s + kWideRing))
+                                                    : ldu16(qn + 64 * (s + kWideRing - 16));
+            acc16(x, sw[s + 2 * k], sw[s + 2 * k + 1], c0, c1);
+        }
+        const bool on = t >= tau && t - tau < nb;
+        const uint64_t n0 = scramble(a0 + c0, scr0), n1 = scramble(a1 + c1, scr1);
+        a0 = on ? n0 : a0;
+        a1 = on ? n1 : a1;
+    }
+    // the partial block (ns stripes, no scramble) and the last stripe
+    const uint32_t ns = (uint32_t)(((len - 1) - (uint64_t)nb * 1024) / 64);
+    {
+        uint64_t c0 = 0, c1 = 0;
+        const uint8_t *q = p + (uint64_t)nb * 1024;
+#pragma unroll
+        for (uint32_t s = 0; s < 16; ++s)
+            if (s < ns) acc16(ldu16(q + 64 * s), rs.w[s + 2 * k], rs.w[s + 2 * k + 1], c0, c1);
+        acc16(ldu16(a.data + hj + len - 64 + 16 * k), csec_at(121 + 16 * k, a.seed),
+              csec_at(129 + 16 * k, a.seed), c0, c1);
+        a0 += c0;
+        a1 += c1;
+    }
+    uint64_t tA = fold64(a0 ^ csec_at(11 + 16 * k, a.seed), a1 ^ csec_at(19 + 16 * k, a.seed));
+    uint64_t tB = (a.csum_type == kXxh3_128)
+                      ? fold64(a0 ^ csec_at(117 + 16 * k, a.seed), a1 ^ csec_at(125 + 16 * k, a.seed))
+                      : 0;
+    tA = quad_sum(tA);
+    tB = quad_sum(tB);
+    RowWin r;
+    r.weak = 0;
+    r.lo = xxh3_aval(len * P64_1 + tA);
+    r.hi = (a.csum_type == kXxh3_128) ? xxh3_aval(~(len * P64_2) + tB) : 0;
+    return r;
+}
+
 // the first s2length bytes of (lo, hi) equal block i's sum2
 __device__ __forceinline__ bool strong_eq(const RsWalkArgs &a, uint32_t i, uint64_t lo,
                                           uint64_t hi) {
@@ -586,6 +677,8 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                                   FaRec *rec = nullptr) {
     const int64_t fend = min(stop, (int64_t)a.full_end);
     const uint64_t L = a.blength;
+    // STEP hits per flush: kWideQ (wide passes) needs windows of whole blocks
+    const uint32_t fq = (a.flushq > kRows && L > 1024) ? kWideQ : kRows;
     const uint8_t *d = a.data;
     const uint32_t row = lane >> 4;
     SegResult res{0, 0xffffffffu, 0, 0, want};
@@ -816,7 +909,7 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 tsub = wclock(wp);
                 uint64_t lanes = __ballot(hit != 0);
                 WPROG(a, lane, 5, (int64_t)A, lanes);
-                while (lanes && nq < kRows) {
+                while (lanes && nq < fq) {
                     const uint32_t hl = (uint32_t)__builtin_ctzll(lanes);
                     const uint32_t hm = (uint32_t)__builtin_amdgcn_readlane((int)hit, (int)hl);
                     const uint32_t t = (uint32_t)__builtin_ctz(hm);
@@ -835,17 +928,31 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 }
                 wadd(wp, kPrStepQueue, tsub);
                 const bool more = lanes != 0;              // hits of this batch not yet queued
-                if (!(nq == kRows || (!more && last && nq))) break;
-                // hash the queued windows together, visit them in order
-                const int64_t orow = by_row(qh, lane, nq);
+                // flush: a full queue, the scan's end, or (a.flushspan) the
+                // scan ran that far past the first queued hit
+                const bool span = a.flushspan && nq &&
+                                  (int64_t)(A + kBatch) - (int64_t)rdl64((uint64_t)qh, 0) >=
+                                      (int64_t)a.flushspan;
+                if (!(nq == fq || (!more && last && nq) || span)) break;
+                // hash the queued windows together, visit them in order: more
+                // than kRows in one address-lockstep pass, else one per row
+                const bool wide = nq > kRows;
                 uint64_t tf = wclock(wp);
-                // (two blocks in flight here: the next batch's stage 1 is live)
-                const RowWin w = rows_window<false, VS_WALK_FRING>(a, rs, lane, (uint64_t)orow, L);
+                RowWin w;
+                if (wide) {
+                    w = wide_windows(a, rs, lane, qh, nq, L);
+                } else {
+                    const int64_t orow = by_row(qh, lane, nq);
+                    // (two blocks in flight here: the next batch's stage 1 is live)
+                    w = rows_window<false, VS_WALK_FRING>(a, rs, lane, (uint64_t)orow, L);
+                }
                 wadd(wp, kPrFlush, tf);
                 // lane j < nq scans window j's chain (its strong sum moved
-                // from lane 16 j); the visits then only read the results
+                // from lane 16 j, or 4 j after a wide pass); the visits then
+                // only read the results
                 tf = wclock(wp);
-                const int src = (int)(16 * (lane < nq ? lane : 0));
+                const uint32_t wstride = wide ? 4u : 16u;
+                const int src = (int)(wstride * (lane < nq ? lane : 0));
                 const uint64_t wl = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(w.lo >> 32), src, 64) << 32) |
                                     (uint32_t)__shfl((int)(uint32_t)w.lo, src, 64);
                 const uint64_t wh = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(w.hi >> 32), src, 64) << 32) |
@@ -856,7 +963,7 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 for (uint32_t j = 0; j < nq; ++j) {
                     const int64_t h = (int64_t)rdl64((uint64_t)qh, (int)j);
                     const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)qsum, (int)j);
-                    const uint64_t lo = rdl64(w.lo, (int)(16 * j)), hi = rdl64(w.hi, (int)(16 * j));
+                    const uint64_t lo = rdl64(w.lo, (int)(wstride * j)), hi = rdl64(w.hi, (int)(wstride * j));
                     const uint64_t fa_visit = fa;
                     WPROG(a, lane, 6, h, j);
                     fa += (uint32_t)__builtin_amdgcn_readlane((int)cfa, (int)j);
