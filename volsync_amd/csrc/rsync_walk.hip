@@ -405,13 +405,33 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
 // clamped block and keep their accumulators.  Same XXH3 as rows_window; the
 // results of window j sit in lanes 4j .. 4j+3.
 constexpr uint32_t kWideQ = 16;
-constexpr uint32_t kWideRing = 8;   // stripes in flight per lane
 
-// (not inlined: the call keeps the walk's own register allocation at its
-// four-window spill count, 37 VGPRs against 81 inlined)
-__device__ __noinline__ RowWin wide_windows(const RsWalkArgs &a, const RowSec &rs, uint32_t lane, int64_t qh,
-                               uint32_t nq, uint64_t len) {
+// Not inlined: inlined, its registers and the STEP state live across a flush
+// spill 75 VGPRs of the walk (26 without it); called, 33.
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
+typedef __attribute__((address_space(3))) const uint64_t l_u64;
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const u64x2 g_u64x2;
+// 16 bytes at any byte address (one global_load_dwordx4: gfx950 unaligned mode)
+__device__ __forceinline__ u64x2 gld2(g_u8 *p) {
+    return *(g_u64x2 *)p;
+}
+__device__ __forceinline__ void acc2(const u64x2 d, uint64_t k0s, uint64_t k1s, uint64_t &c0,
+                                     uint64_t &c1) {
+    const uint64_t k0 = d.x ^ k0s, k1 = d.y ^ k1s;
+    c0 += (uint64_t)(uint32_t)k0 * (k0 >> 32) + d.y;
+    c1 += (uint64_t)(uint32_t)k1 * (k1 >> 32) + d.x;
+}
+
+// (typed pointers and uniform scalars: a call boundary would otherwise turn
+// every load into a flat one and the block loop into a divergent one)
+__device__ __noinline__ RowWin wide_windows(g_u8 *data, l_u64 *sw0, uint64_t seed, int csum_type,
+                                            uint32_t lane, int64_t qh, uint32_t nq, uint64_t len) {
     using namespace vsstrong;
+    nq = uni(nq);
+    len = uni64(len);
+    seed = uni64(seed);
+    csum_type = unis(csum_type);
     const uint32_t j = lane >> 2, k = lane & 3;
     const int64_t h0 = (int64_t)rdl64((uint64_t)qh, 0);
     const int64_t hl = (int64_t)rdl64((uint64_t)qh, (int)(nq - 1));
@@ -421,36 +441,41 @@ __device__ __noinline__ RowWin wide_windows(const RsWalkArgs &a, const RowSec &r
     const uint32_t tau = (uint32_t)((hj - h0) >> 10);
     const uint32_t nb = (uint32_t)((len - 1) / 1024);
     const uint32_t T = uni((uint32_t)((hl - h0) >> 10)) + nb;
-    const uint8_t *p = a.data + hj + 16 * k;
+    g_u8 *p = data + hj + 16 * k;
     uint64_t a0 = (k == 0) ? P32_3 : (k == 1) ? P64_2 : (k == 2) ? P64_4 : P64_5;
     uint64_t a1 = (k == 0) ? P64_1 : (k == 1) ? P64_3 : (k == 2) ? P32_2 : P32_1;
-    const uint64_t scr0 = rs.w[16 + 2 * k], scr1 = rs.w[17 + 2 * k];
-    // stripe s of iteration t: p + 1024 * clamp(t - tau, 0, nb - 1) + 64 s
-    auto addr = [&](uint32_t t) -> const uint8_t * {
+    const uint64_t scr0 = sw0[16 + 2 * k], scr1 = sw0[17 + 2 * k];
+    // block of iteration t: clamp(t - tau, 0, nb - 1)
+    auto addr = [&](uint32_t t) -> g_u8 * {
         const uint32_t b = t < tau ? 0u : min(t - tau, nb - 1);
         return p + (uint64_t)b * 1024;
     };
-    uint4 v[kWideRing];
+    // stripes 0..7 (lo) and 8..15 (hi) of an iteration; each half is loaded
+    // while the other is hashed
+    u64x2 lo[8], hi[8];
     {
-        const uint8_t *q = addr(0);
+        g_u8 *q = addr(0);
 #pragma unroll
-        for (uint32_t s = 0; s < kWideRing; ++s) v[s] = ldu16(q + 64 * s);
+        for (uint32_t s = 0; s < 8; ++s) lo[s] = gld2(q + 64 * s);
     }
     for (uint32_t t = 0; t < T; ++t) {
-        const uint8_t *q = addr(t), *qn = addr(t + 1);
+        g_u8 *q = addr(t), *qn = addr(t + 1);
         // the secret words are re-read from LDS every iteration (ds_read2_b64
-        // per stripe) rather than hoisted into 64 registers
-        const uint64_t *sw = rs.w;
+        // per stripe) rather than held in 64 registers
+        l_u64 *sw = sw0;
         asm volatile("" : "+v"(sw));
         uint64_t c0 = 0, c1 = 0;
 #pragma unroll
-        for (uint32_t s = 0; s < 16; ++s) {
-            const uint4 x = v[s % kWideRing];
-            // refill: stripe s + kWideRing of this iteration, or of the next
-            v[s % kWideRing] = (s + kWideRing < 16) ? ldu16(q + 64 * (s + kWideRing))
-                                                    : ldu16(qn + 64 * (s + kWideRing - 16));
-            acc16(x, sw[s + 2 * k], sw[s + 2 * k + 1], c0, c1);
-        }
+        for (uint32_t s = 0; s < 8; ++s) hi[s] = gld2(q + 512 + 64 * s);
+        __builtin_amdgcn_sched_barrier(6);   // (ALU may cross; the loads stay ahead of the other half's hashing)
+#pragma unroll
+        for (uint32_t s = 0; s < 8; ++s) acc2(lo[s], sw[s + 2 * k], sw[s + 2 * k + 1], c0, c1);
+#pragma unroll
+        for (uint32_t s = 0; s < 8; ++s) lo[s] = gld2(qn + 64 * s);
+        __builtin_amdgcn_sched_barrier(6);
+#pragma unroll
+        for (uint32_t s = 0; s < 8; ++s)
+            acc2(hi[s], sw[8 + s + 2 * k], sw[8 + s + 2 * k + 1], c0, c1);
         const bool on = t >= tau && t - tau < nb;
         const uint64_t n0 = scramble(a0 + c0, scr0), n1 = scramble(a1 + c1, scr1);
         a0 = on ? n0 : a0;
@@ -460,25 +485,25 @@ __device__ __noinline__ RowWin wide_windows(const RsWalkArgs &a, const RowSec &r
     const uint32_t ns = (uint32_t)(((len - 1) - (uint64_t)nb * 1024) / 64);
     {
         uint64_t c0 = 0, c1 = 0;
-        const uint8_t *q = p + (uint64_t)nb * 1024;
+        g_u8 *q = p + (uint64_t)nb * 1024;
 #pragma unroll
         for (uint32_t s = 0; s < 16; ++s)
-            if (s < ns) acc16(ldu16(q + 64 * s), rs.w[s + 2 * k], rs.w[s + 2 * k + 1], c0, c1);
-        acc16(ldu16(a.data + hj + len - 64 + 16 * k), csec_at(121 + 16 * k, a.seed),
-              csec_at(129 + 16 * k, a.seed), c0, c1);
+            if (s < ns) acc2(gld2(q + 64 * s), sw0[s + 2 * k], sw0[s + 2 * k + 1], c0, c1);
+        acc2(gld2(data + hj + len - 64 + 16 * k), csec_at(121 + 16 * k, seed),
+             csec_at(129 + 16 * k, seed), c0, c1);
         a0 += c0;
         a1 += c1;
     }
-    uint64_t tA = fold64(a0 ^ csec_at(11 + 16 * k, a.seed), a1 ^ csec_at(19 + 16 * k, a.seed));
-    uint64_t tB = (a.csum_type == kXxh3_128)
-                      ? fold64(a0 ^ csec_at(117 + 16 * k, a.seed), a1 ^ csec_at(125 + 16 * k, a.seed))
+    uint64_t tA = fold64(a0 ^ csec_at(11 + 16 * k, seed), a1 ^ csec_at(19 + 16 * k, seed));
+    uint64_t tB = (csum_type == kXxh3_128)
+                      ? fold64(a0 ^ csec_at(117 + 16 * k, seed), a1 ^ csec_at(125 + 16 * k, seed))
                       : 0;
     tA = quad_sum(tA);
     tB = quad_sum(tB);
     RowWin r;
     r.weak = 0;
     r.lo = xxh3_aval(len * P64_1 + tA);
-    r.hi = (a.csum_type == kXxh3_128) ? xxh3_aval(~(len * P64_2) + tB) : 0;
+    r.hi = (csum_type == kXxh3_128) ? xxh3_aval(~(len * P64_2) + tB) : 0;
     return r;
 }
 
@@ -940,7 +965,8 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 uint64_t tf = wclock(wp);
                 RowWin w;
                 if (wide) {
-                    w = wide_windows(a, rs, lane, qh, nq, L);
+                    w = wide_windows((g_u8 *)(uintptr_t)a.data, (l_u64 *)rs.w, a.seed, a.csum_type,
+                                     lane, qh, nq, L);
                 } else {
                     const int64_t orow = by_row(qh, lane, nq);
                     // (two blocks in flight here: the next batch's stage 1 is live)
