@@ -394,27 +394,37 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
 // ---- wide flushes: up to 16 windows, address-lockstep ----------------------
 // At real C4 density a resync after an edit visits ~64 false-alarm windows of
 // one block length within ~2 block lengths of source; hashed four at a time
-// (rows_window) every flush re-streams the whole span, and with every wave of
-// the chip doing the same the spans do not stay in L2.  Here window j (lanes
-// 4j .. 4j+3, lane k owning accumulators 2k, 2k+1 and reading bytes
-// [16k, 16k + 16) of every stripe -- the signature pass's layout) hashes its
-// block b = t - tau_j in iteration t, tau_j = (h_j - h_0) >> 10, so every
-// window of the wave reads inside [h_0 + 1024 t, h_0 + 1024 t + 2048): the
-// wave's loads walk the span once, as one sliding 2 KiB, and the 16 windows
-// share each line.  Windows not yet started or already finished compute on a
-// clamped block and keep their accumulators.  Same XXH3 as rows_window; the
-// results of window j sit in lanes 4j .. 4j+3.
+// (rows_window) every flush re-streams the whole span, latency-bound on the
+// 8 KiB a wave keeps in flight.  Here window j (lanes 4j .. 4j+3, lane k owning
+// accumulators 2k, 2k+1 and reading bytes [16k, 16k + 16) of every stripe --
+// the signature pass's layout) hashes its block b = t - tau_j in iteration t,
+// tau_j = (h_j - h_0) >> 10, so every window of the wave reads inside the same
+// 2 KiB, [h_0 + 1024 t, h_0 + 1024 t + 2048).  The wave loads each KiB of
+// that span once, 16 bytes per lane, kWideD iterations ahead (4 registers per
+// KiB in flight), and writes it into a per-wave LDS ring of two 1 KiB slots
+// plus a mirror of slot 0 (so a window's 2 KiB are always contiguous); the
+// windows read their stripes from there (unaligned ds_read_b128).  Windows
+// not yet started or already finished compute on stale bytes and keep their
+// accumulators.  Same XXH3 as rows_window; window j's results sit in lanes
+// 4j .. 4j+3.
 constexpr uint32_t kWideQ = 16;
+constexpr uint32_t kWideD = 8;                            // KiB in flight per wave
+constexpr uint32_t kWideRingBytes = 3 * 1024;             // per wave: slots 0, 1, mirror of 0
 
-// Not inlined: inlined, its registers and the STEP state live across a flush
-// spill 75 VGPRs of the walk (26 without it); called, 33.
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
 typedef __attribute__((address_space(3))) const uint64_t l_u64;
+typedef __attribute__((address_space(3))) uint8_t l_u8;
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) const u64x2 g_u64x2;
 // 16 bytes at any byte address (one global_load_dwordx4: gfx950 unaligned mode)
 __device__ __forceinline__ u64x2 gld2(g_u8 *p) {
     return *(g_u64x2 *)p;
+}
+// 16 bytes of LDS at any byte address (one ds_read_b128: gfx950 unaligned DS access)
+__device__ __forceinline__ u64x2 lld2(const l_u8 *p) {
+    u64x2 v;
+    __builtin_memcpy(&v, (const uint8_t *)p, 16);
+    return v;
 }
 __device__ __forceinline__ void acc2(const u64x2 d, uint64_t k0s, uint64_t k1s, uint64_t &c0,
                                      uint64_t &c1) {
@@ -423,14 +433,18 @@ __device__ __forceinline__ void acc2(const u64x2 d, uint64_t k0s, uint64_t k1s, 
     c1 += (uint64_t)(uint32_t)k1 * (k1 >> 32) + d.x;
 }
 
-// (typed pointers and uniform scalars: a call boundary would otherwise turn
-// every load into a flat one and the block loop into a divergent one)
-__device__ __noinline__ RowWin wide_windows(g_u8 *data, l_u64 *sw0, uint64_t seed, int csum_type,
-                                            uint32_t lane, int64_t qh, uint32_t nq, uint64_t len) {
+// Not inlined: inlined, its registers and the STEP state live across a flush
+// spill 75 VGPRs of the walk (26 without it).  Typed pointers and uniform
+// scalars: a call boundary would otherwise turn every load into a flat one
+// and the block loop into a divergent one.
+__device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw0, l_u8 *ring,
+                                            uint64_t seed, int csum_type, uint32_t lane, int64_t qh,
+                                            uint32_t nq, uint64_t len) {
     using namespace vsstrong;
     nq = uni(nq);
     len = uni64(len);
     seed = uni64(seed);
+    dlen = uni64(dlen);
     csum_type = unis(csum_type);
     const uint32_t j = lane >> 2, k = lane & 3;
     const int64_t h0 = (int64_t)rdl64((uint64_t)qh, 0);
@@ -439,48 +453,73 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, l_u64 *sw0, uint64_t see
                                                              (int)(j < nq ? j : 0), 64) << 32) |
                                  (uint32_t)__shfl((int)(uint32_t)qh, (int)(j < nq ? j : 0), 64));
     const uint32_t tau = (uint32_t)((hj - h0) >> 10);
+    const uint32_t rj = (uint32_t)(hj - h0) - 1024 * tau;   // window j's offset in iteration t's 2 KiB
     const uint32_t nb = (uint32_t)((len - 1) / 1024);
     const uint32_t T = uni((uint32_t)((hl - h0) >> 10)) + nb;
-    g_u8 *p = data + hj + 16 * k;
     uint64_t a0 = (k == 0) ? P32_3 : (k == 1) ? P64_2 : (k == 2) ? P64_4 : P64_5;
     uint64_t a1 = (k == 0) ? P64_1 : (k == 1) ? P64_3 : (k == 2) ? P32_2 : P32_1;
     const uint64_t scr0 = sw0[16 + 2 * k], scr1 = sw0[17 + 2 * k];
-    // block of iteration t: clamp(t - tau, 0, nb - 1)
-    auto addr = [&](uint32_t t) -> g_u8 * {
-        const uint32_t b = t < tau ? 0u : min(t - tau, nb - 1);
-        return p + (uint64_t)b * 1024;
+    // this lane's secret words for stripe s: sk[s], sk[s + 1] (17 registers pairs)
+    uint64_t sk[17];
+#pragma unroll
+    for (uint32_t i = 0; i < 17; ++i) sk[i] = sw0[2 * k + i];
+    // KiB n of the span: [h0 + 1024 n, + 1024), lane l's 16 bytes (clamped at
+    // the data end: no active window reads past it).  The loads are issued in
+    // asm and waited for by hand (vmcnt counts in issue order): the compiler's
+    // own accounting of a register ring carried across the loop's back edge
+    // waits for every load at the loop head, which exposes a full memory
+    // latency per group of kWideD iterations.
+    const uint64_t src = (uint64_t)(uintptr_t)(data + h0 + 16 * lane);
+    const uint64_t room = dlen - 16 - ((uint64_t)h0 + 16 * lane);
+    auto fetch = [&](uint32_t n) -> u32x4 {
+        const uint64_t o = 1024ull * n;
+        const uint64_t at = src + (o < room ? o : room);
+        u32x4 v;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(at) : "memory");
+        return v;
     };
-    // stripes 0..7 (lo) and 8..15 (hi) of an iteration; each half is loaded
-    // while the other is hashed
-    u64x2 lo[8], hi[8];
+    // KiB n into slot n & 1 (and slot 0's mirror); the ring is this wave's
+    auto put = [&](uint32_t n, const u32x4 v) {
+        *(__attribute__((address_space(3))) u32x4 *)(ring + 1024 * (n & 1) + 16 * lane) = v;
+        if ((n & 1) == 0) *(__attribute__((address_space(3))) u32x4 *)(ring + 2048 + 16 * lane) = v;
+    };
+    u32x4 inflight[kWideD];   // KiB t + 1 + i for i < kWideD, at the top of iteration t
     {
-        g_u8 *q = addr(0);
-#pragma unroll
-        for (uint32_t s = 0; s < 8; ++s) lo[s] = gld2(q + 64 * s);
+        u32x4 v0 = fetch(0);
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(v0) :: "memory");
+        put(0, v0);
     }
-    for (uint32_t t = 0; t < T; ++t) {
-        g_u8 *q = addr(t), *qn = addr(t + 1);
-        // the secret words are re-read from LDS every iteration (ds_read2_b64
-        // per stripe) rather than held in 64 registers
-        l_u64 *sw = sw0;
-        asm volatile("" : "+v"(sw));
-        uint64_t c0 = 0, c1 = 0;
 #pragma unroll
-        for (uint32_t s = 0; s < 8; ++s) hi[s] = gld2(q + 512 + 64 * s);
-        __builtin_amdgcn_sched_barrier(6);   // (ALU may cross; the loads stay ahead of the other half's hashing)
+    for (uint32_t i = 0; i < kWideD; ++i) inflight[i] = fetch(1 + i);
+    for (uint32_t t0 = 0; t0 < T; t0 += kWideD) {
 #pragma unroll
-        for (uint32_t s = 0; s < 8; ++s) acc2(lo[s], sw[s + 2 * k], sw[s + 2 * k + 1], c0, c1);
+        for (uint32_t u = 0; u < kWideD; ++u) {
+            const uint32_t t = t0 + u;
+            if (t >= T) break;
+            // KiB t + 1 (the oldest of the kWideD loads in flight) joins the
+            // ring (slot t + 1 & 1; KiB t stays in the other slot); the
+            // register goes on to KiB t + 1 + kWideD
+            asm volatile("s_waitcnt vmcnt(%1)" : "+v"(inflight[u]) : "n"(kWideD - 1) : "memory");
+            put(t + 1, inflight[u]);
+            inflight[u] = fetch(t + 1 + kWideD);
+            const l_u8 *w = ring + 1024 * (t & 1) + rj + 16 * k;
+            // all 16 stripe reads in flight before any is hashed
+            u64x2 d[16];
 #pragma unroll
-        for (uint32_t s = 0; s < 8; ++s) lo[s] = gld2(qn + 64 * s);
-        __builtin_amdgcn_sched_barrier(6);
+            for (uint32_t s = 0; s < 16; ++s) d[s] = lld2(w + 64 * s);
+            __builtin_amdgcn_sched_barrier(0);
+            uint64_t c0 = 0, c1 = 0;
 #pragma unroll
-        for (uint32_t s = 0; s < 8; ++s)
-            acc2(hi[s], sw[8 + s + 2 * k], sw[8 + s + 2 * k + 1], c0, c1);
-        const bool on = t >= tau && t - tau < nb;
-        const uint64_t n0 = scramble(a0 + c0, scr0), n1 = scramble(a1 + c1, scr1);
-        a0 = on ? n0 : a0;
-        a1 = on ? n1 : a1;
+            for (uint32_t s = 0; s < 16; ++s) acc2(d[s], sk[s], sk[s + 1], c0, c1);
+            const bool on = t >= tau && t - tau < nb;
+            const uint64_t n0 = scramble(a0 + c0, scr0), n1 = scramble(a1 + c1, scr1);
+            a0 = on ? n0 : a0;
+            a1 = on ? n1 : a1;
+        }
     }
+    // the loads still in flight write registers the caller will reuse
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    g_u8 *p = data + hj + 16 * k;
     // the partial block (ns stripes, no scramble) and the last stripe
     const uint32_t ns = (uint32_t)(((len - 1) - (uint64_t)nb * 1024) / 64);
     {
@@ -696,6 +735,7 @@ __device__ __forceinline__ int64_t by_row(int64_t v, uint32_t lane, uint32_t nv)
 // is dropped, so matches and false alarms are hash_search's.
 template <uint32_t RING>
 __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const uint32_t *lfilt,
+                                  uint8_t *wring,
                                   uint32_t lane, int64_t o, int32_t want, int64_t stop,
                                   int64_t *out_off, int32_t *out_idx, int64_t *out_fab,
                                   uint32_t cap, const SpecView *spec, WProf &wp,
@@ -965,8 +1005,9 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 uint64_t tf = wclock(wp);
                 RowWin w;
                 if (wide) {
-                    w = wide_windows((g_u8 *)(uintptr_t)a.data, (l_u64 *)rs.w, a.seed, a.csum_type,
-                                     lane, qh, nq, L);
+                    w = wide_windows((g_u8 *)(uintptr_t)a.data, a.dlen, (l_u64 *)rs.w,
+                                     (l_u8 *)wring + (threadIdx.x >> 6) * kWideRingBytes,
+                                     a.seed, a.csum_type, lane, qh, nq, L);
                 } else {
                     const int64_t orow = by_row(qh, lane, nq);
                     // (two blocks in flight here: the next batch's stage 1 is live)
@@ -1056,6 +1097,7 @@ template <uint32_t T, uint32_t RING>
 __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
     __shared__ uint32_t lfilt[kLdsFiltWordsW];
     __shared__ uint64_t lsec[24];
+    __shared__ __attribute__((aligned(16))) uint8_t wring[kWideRingBytes * (kWalkThreads / 64)];
     load_secret(lsec, a.seed);
     load_prefilter(a, lfilt);
     const uint32_t lane = threadIdx.x & 63;
@@ -1069,7 +1111,7 @@ __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
         const uint64_t base = (uint64_t)k * a.cap;
         FaRec rec{a.spec_fao + (uint64_t)k * a.facap, a.spec_fac + (uint64_t)k * a.facap,
                   a.facap, 0};
-        const SegResult r = walk_segment<RING>(a, rs, lfilt, lane, e, w, seg_hi(a, k),
+        const SegResult r = walk_segment<RING>(a, rs, lfilt, wring, lane, e, w, seg_hi(a, k),
                                                a.spec_off + base, a.spec_idx + base,
                                                a.spec_fab + base, a.cap, nullptr, wp, &rec);
         wadd(wp, kPrSeg, ts);
@@ -1156,6 +1198,7 @@ __device__ __forceinline__ bool stitch_visited(const RsWalkArgs &a, uint32_t k, 
 __global__ __launch_bounds__(kWalkThreads) void rs_walk_stitch_kernel(RsWalkArgs a) {
     __shared__ uint32_t lfilt[kLdsFiltWordsW];
     __shared__ uint64_t lsec[24];
+    __shared__ __attribute__((aligned(16))) uint8_t wring[kWideRingBytes * (kWalkThreads / 64)];
     load_secret(lsec, a.seed);
     load_prefilter(a, lfilt);
     const uint32_t lane = threadIdx.x & 63;
@@ -1192,7 +1235,7 @@ __global__ __launch_bounds__(kWalkThreads) void rs_walk_stitch_kernel(RsWalkArgs
             }
         }
         if (walk) {
-            r = walk_segment<kWalkRing>(a, rs, lfilt, lane, ws, w, seg_hi(a, k), a.fin_off + base,
+            r = walk_segment<kWalkRing>(a, rs, lfilt, wring, lane, ws, w, seg_hi(a, k), a.fin_off + base,
                                     a.fin_idx + base, a.fin_fab + base, a.cap, &sv, wp);
             r.fa += fadj;
         }
