@@ -9,5 +9,8 @@ bash tools/gpu.sh bench ab2_share_wide $S &&
 bash tools/gpu.sh bench ab2_share_q4 $S --walk-opt walk_flush_windows=4 &&
 bash tools/gpu.sh bench ab2_c4_wide $C &&
 bash tools/gpu.sh bench ab2_c4_q4 $C --walk-opt walk_flush_windows=4 &&
+bash tools/gpu.sh bench ab2_share_wide_nopred $S --walk-opt walk_flush_predict=0 &&
+bash tools/gpu.sh bench ab2_c4_q4_nopred $C --walk-opt walk_flush_windows=4,walk_flush_predict=0 &&
+bash tools/gpu.sh bench ab2_share_q4_nopred $S --walk-opt walk_flush_windows=4,walk_flush_predict=0 &&
 bash tools/gpu.sh bench ab2_share_wide_r2 $S || exit $?
 python3 tools/ab_table.py gpurun_out/bench_ab2_*.log | tee gpurun_out/ab2_walk_table.txt

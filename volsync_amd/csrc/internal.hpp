@@ -442,6 +442,7 @@ struct RsWalkArgs {
     int32_t *exitw_new;
     uint32_t flushq;                 // STEP hits queued per flush: 4 (rows) or 16 (wide)
     uint32_t flushspan;              // flush once the scan ran this far past the first hit (0: no bound)
+    uint32_t flushpredict;           // flush at a hit whose weak sum is block want .. want + 2's
     uint64_t *dbg;                   // debug builds: per-wave progress records (host-mapped)
     uint64_t *prof;                  // VS_WALK_PROF builds: per-wave phase cycles/counts [waves][16]
 };

@@ -222,6 +222,7 @@ struct vs_rsync {
     bool opt_prefilter = true;      // the walk's LDS prefilter
     uint32_t opt_flushq = 16;       // STEP hits per flush (4: rows only; 16: wide passes)
     uint32_t opt_flushspan = 0;     // flush once the scan is this far past the first hit (0: none)
+    bool opt_flushpredict = true;   // flush at a likely resync hit (weak sum of block want .. want + 2)
     uint64_t fs_piece = 0;          // file-sum piece in 1 KiB blocks (0: 2^18)
     // streamed forms (host-fed files): see the MatchStream / SigStream section
     MatchStream *mst = nullptr;
@@ -980,6 +981,7 @@ int walk_scan(vs_rsync *h) {
     if (!h->opt_prefilter) a.lbits = 0;   // VS_OPT_WALK_PREFILTER 0: no LDS prefilter
     a.flushq = h->opt_flushq;
     a.flushspan = h->opt_flushspan;
+    a.flushpredict = h->opt_flushpredict ? 1u : 0u;
     const size_t ns = std::max<uint32_t>(a.nseg, 1), nc = ns * a.cap;
     VS_TRY(h->w_spec_off.ensure(nc * 8));
     VS_TRY(h->w_spec_idx.ensure(nc * 4));
@@ -2298,6 +2300,9 @@ VS_API int vs_rsync_set_option(vs_rsync *h, int option, int64_t value) {
         case VS_OPT_WALK_FLUSH_SPAN:
             if (value < 0 || value > (1ll << 30)) return fail(VS_ERR_ARG, "flush span out of range");
             h->opt_flushspan = (uint32_t)value;
+            return 0;
+        case VS_OPT_WALK_FLUSH_PREDICT:
+            h->opt_flushpredict = value != 0;
             return 0;
         case VS_OPT_WALK_PREFILTER:
             h->opt_prefilter = value != 0;

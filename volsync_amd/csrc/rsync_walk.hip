@@ -408,6 +408,7 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
 // accumulators.  Same XXH3 as rows_window; window j's results sit in lanes
 // 4j .. 4j+3.
 constexpr uint32_t kWideQ = 16;
+constexpr uint32_t kPredict = 3;   // blocks want .. want + 2 flag a likely resync hit
 constexpr uint32_t kWideD = 8;                            // KiB in flight per wave
 constexpr uint32_t kWideRingBytes = 3 * 1024;             // per wave: slots 0, 1, mirror of 0
 
@@ -837,6 +838,16 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
         int64_t qh = 0;
         uint32_t qsum = 0;
         bool matched = false;
+        // The likely resync: after an edit inside block want, the walk usually
+        // matches block want + 1 (or a few later), so a hit whose weak sum is
+        // one of theirs is flushed at once instead of after more hits past it
+        // (a.flushpredict; only when a flush runs, never what it finds)
+        uint32_t pw[kPredict];
+#pragma unroll
+        for (uint32_t m = 0; m < kPredict; ++m) {
+            const uint32_t b = (uint32_t)want + m;
+            pw[m] = (a.flushpredict && want >= 0 && b < a.count) ? uni(a.sum1[b]) : 0xffffffffu;
+        }
         uint4 cwo, cwi;         // the batch's leaving / entering bytes (16 per lane)
         batch_load(a, A, lane, cwo, cwi);
         // Stage 1 of a batch: its window sums, the LDS prefilter and the
@@ -970,6 +981,7 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
             // queue the hits in offset order (lane order, then bit order);
             // a full queue is flushed and queueing goes on with the batch's
             // remaining hits (all past the last visited one)
+            bool predicted = false;
             for (;;) {
                 tsub = wclock(wp);
                 uint64_t lanes = __ballot(hit != 0);
@@ -990,6 +1002,13 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                     ++nq;
                     if (lane == hl) hit &= hit - 1;
                     lanes = __ballot(hit != 0);
+                    bool likely = false;
+#pragma unroll
+                    for (uint32_t m = 0; m < kPredict; ++m) likely |= sv == pw[m];
+                    if (likely) {
+                        predicted = true;
+                        break;
+                    }
                 }
                 wadd(wp, kPrStepQueue, tsub);
                 const bool more = lanes != 0;              // hits of this batch not yet queued
@@ -998,7 +1017,8 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 const bool span = a.flushspan && nq &&
                                   (int64_t)(A + kBatch) - (int64_t)rdl64((uint64_t)qh, 0) >=
                                       (int64_t)a.flushspan;
-                if (!(nq == fq || (!more && last && nq) || span)) break;
+                if (!(nq == fq || (!more && last && nq) || span || predicted)) break;
+                predicted = false;
                 // hash the queued windows together, visit them in order: more
                 // than kRows in one address-lockstep pass, else one per row
                 const bool wide = nq > kRows;
