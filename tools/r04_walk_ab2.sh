@@ -7,7 +7,7 @@ C="--mode rsync --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline"
 bash tools/gpu.sh tests tests/test_gpu_rsync.py -x -k "walk or c4 or stitch or shard or golden" &&
 bash tools/gpu.sh bench ab2_share_wide $S &&
 bash tools/gpu.sh bench ab2_share_q4 $S --walk-opt walk_flush_windows=4 &&
-bash tools/gpu.sh bench ab2_c4_wide $C &&
+bash tools/gpu.sh bench ab2_c4_wide $C --walk-opt walk_flush_windows=16 &&
 bash tools/gpu.sh bench ab2_c4_q4 $C --walk-opt walk_flush_windows=4 &&
 bash tools/gpu.sh bench ab2_share_wide_nopred $S --walk-opt walk_flush_predict=0 &&
 bash tools/gpu.sh bench ab2_c4_q4_nopred $C --walk-opt walk_flush_windows=4,walk_flush_predict=0 &&
