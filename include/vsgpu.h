@@ -567,8 +567,8 @@ int vs_restic_pack_header(const uint8_t *types, const uint32_t *lengths, const u
                                       * prefilter (default 1) */
 #define VS_OPT_WALK_FLUSH_WINDOWS 7  /* rsync: STEP weak hits hashed per flush: 16 =
                                       * address-lockstep passes over the resync span
-                                      * (blocks > 1 KiB), 4 = four windows per pass,
-                                      * 0 = 16 from 2^20 table blocks, else 4 (default) */
+                                      * (blocks > 1 KiB; 0 = default), 4 = four
+                                      * windows per pass */
 #define VS_OPT_WALK_FLUSH_SPAN 8     /* rsync: flush once the scan is this many bytes
                                       * past the first queued hit (0 = no bound; default) */
 #define VS_OPT_WALK_FLUSH_PREDICT 9  /* rsync: 1 = flush the STEP queue at once at a hit

@@ -220,7 +220,7 @@ struct vs_rsync {
     int32_t opt_facap = -1;         // false-alarm windows recorded per segment (-1: automatic)
     bool opt_host_walk = false;     // the host walk for every checksum type
     bool opt_prefilter = true;      // the walk's LDS prefilter
-    uint32_t opt_flushq = 0;        // STEP hits per flush (4: rows only; 16: wide passes; 0: by table size)
+    uint32_t opt_flushq = 0;        // STEP hits per flush (4: rows only; 16 or 0: wide passes)
     uint32_t opt_flushspan = 0;     // flush once the scan is this far past the first hit (0: none)
     bool opt_flushpredict = true;   // flush at a likely resync hit (weak sum of block want .. want + 2)
     uint64_t fs_piece = 0;          // file-sum piece in 1 KiB blocks (0: 2^18)
@@ -979,10 +979,7 @@ int walk_scan(vs_rsync *h) {
     a.filt_l = h->d_filt.as<uint32_t>() + ((1ull << h->fbits) / 32);
     a.filt_b = (const uint64_t *)(a.filt_l + ((1ull << a.lbits) / 32));
     if (!h->opt_prefilter) a.lbits = 0;   // VS_OPT_WALK_PREFILTER 0: no LDS prefilter
-    // wide flushes pay off where false alarms are dense (≈ 64 per edit at the
-    // real C4's 2 M blocks); at 512 K blocks (≈ 16 per edit) a 16-deep queue
-    // steps too far past the resync
-    a.flushq = h->opt_flushq ? h->opt_flushq : ((int64_t)h->count >= (1 << 20) ? 16u : 4u);
+    a.flushq = h->opt_flushq ? h->opt_flushq : 16u;   // wide flushes
     a.flushspan = h->opt_flushspan;
     a.flushpredict = h->opt_flushpredict ? 1u : 0u;
     const size_t ns = std::max<uint32_t>(a.nseg, 1), nc = ns * a.cap;

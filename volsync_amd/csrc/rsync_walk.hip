@@ -409,7 +409,10 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
 // 4j .. 4j+3.
 constexpr uint32_t kWideQ = 16;
 constexpr uint32_t kPredict = 3;   // blocks want .. want + 2 flag a likely resync hit
-constexpr uint32_t kWideD = 8;                            // KiB in flight per wave
+#ifndef VS_WIDE_D
+#define VS_WIDE_D 8
+#endif
+constexpr uint32_t kWideD = VS_WIDE_D;                    // KiB in flight per wave
 constexpr uint32_t kWideRingBytes = 3 * 1024;             // per wave: slots 0, 1, mirror of 0
 
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
@@ -460,10 +463,14 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
     uint64_t a0 = (k == 0) ? P32_3 : (k == 1) ? P64_2 : (k == 2) ? P64_4 : P64_5;
     uint64_t a1 = (k == 0) ? P64_1 : (k == 1) ? P64_3 : (k == 2) ? P32_2 : P32_1;
     const uint64_t scr0 = sw0[16 + 2 * k], scr1 = sw0[17 + 2 * k];
-    // this lane's secret words for stripe s: sk[s], sk[s + 1] (17 registers pairs)
+    // this lane's secret words for stripe s: sk[s], sk[s + 1] (17 register pairs)
+#if VS_WIDE_SK_LDS
+    l_u64 *sk = sw0 + 2 * k;
+#else
     uint64_t sk[17];
 #pragma unroll
     for (uint32_t i = 0; i < 17; ++i) sk[i] = sw0[2 * k + i];
+#endif
     // KiB n of the span: [h0 + 1024 n, + 1024), lane l's 16 bytes (clamped at
     // the data end: no active window reads past it).  The loads are issued in
     // asm and waited for by hand (vmcnt counts in issue order): the compiler's
