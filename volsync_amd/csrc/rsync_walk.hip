@@ -463,14 +463,10 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
     uint64_t a0 = (k == 0) ? P32_3 : (k == 1) ? P64_2 : (k == 2) ? P64_4 : P64_5;
     uint64_t a1 = (k == 0) ? P64_1 : (k == 1) ? P64_3 : (k == 2) ? P32_2 : P32_1;
     const uint64_t scr0 = sw0[16 + 2 * k], scr1 = sw0[17 + 2 * k];
-    // this lane's secret words for stripe s: sk[s], sk[s + 1] (17 register pairs)
-#if VS_WIDE_SK_LDS
+    // this lane's secret words for stripe s: sk[s], sk[s + 1], read from LDS
+    // (held in 34 registers instead, the walk around the call spilled 23 more
+    // VGPRs and ran 5-7 % slower: profiles/r04_walk_lds/ab3_*)
     l_u64 *sk = sw0 + 2 * k;
-#else
-    uint64_t sk[17];
-#pragma unroll
-    for (uint32_t i = 0; i < 17; ++i) sk[i] = sw0[2 * k + i];
-#endif
     // KiB n of the span: [h0 + 1024 n, + 1024), lane l's 16 bytes (clamped at
     // the data end: no active window reads past it).  The loads are issued in
     // asm and waited for by hand (vmcnt counts in issue order): the compiler's
