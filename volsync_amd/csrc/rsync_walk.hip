@@ -409,6 +409,9 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
 // 4j .. 4j+3.
 constexpr uint32_t kWideQ = 16;
 constexpr uint32_t kPredict = 3;   // blocks want .. want + 2 flag a likely resync hit
+#ifndef VS_WIDE_MIN
+#define VS_WIDE_MIN (kRows + 1)   // fewer queued windows take the four-row pass
+#endif
 #ifndef VS_WIDE_D
 #define VS_WIDE_D 8
 #endif
@@ -1024,7 +1027,7 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 predicted = false;
                 // hash the queued windows together, visit them in order: more
                 // than kRows in one address-lockstep pass, else one per row
-                const bool wide = nq > kRows;
+                const bool wide = fq == kWideQ && nq >= VS_WIDE_MIN;
                 uint64_t tf = wclock(wp);
                 RowWin w;
                 if (wide) {
