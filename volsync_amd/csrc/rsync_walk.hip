@@ -461,6 +461,9 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
                                  (uint32_t)__shfl((int)(uint32_t)qh, (int)(j < nq ? j : 0), 64));
     const uint32_t tau = (uint32_t)((hj - h0) >> 10);
     const uint32_t rj = (uint32_t)(hj - h0) - 1024 * tau;   // window j's offset in iteration t's 2 KiB
+#if VS_WIDE_ALIGNED
+    const uint32_t sh = rj & 3;                              // its bytes' offset in LDS dwords
+#endif
     const uint32_t nb = (uint32_t)((len - 1) / 1024);
     const uint32_t T = uni((uint32_t)((hl - h0) >> 10)) + nb;
     uint64_t a0 = (k == 0) ? P32_3 : (k == 1) ? P64_2 : (k == 2) ? P64_4 : P64_5;
@@ -513,7 +516,22 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
             // all 16 stripe reads in flight before any is hashed
             u64x2 d[16];
 #pragma unroll
-            for (uint32_t s = 0; s < 16; ++s) d[s] = lld2(w + 64 * s);
+            for (uint32_t s = 0; s < 16; ++s) {
+#if VS_WIDE_ALIGNED
+                // five 4-byte-aligned dwords, realigned by the window's byte
+                // offset (unaligned ds_read_b128s cost the LDS several passes)
+                typedef __attribute__((address_space(3))) const uint32_t l_u32;
+                l_u32 *q = (l_u32 *)(w + 64 * s - sh);
+                const uint32_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3], x4 = q[4];
+                const uint32_t y0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
+                const uint32_t y1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+                const uint32_t y2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
+                const uint32_t y3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
+                d[s] = u64x2{((uint64_t)y1 << 32) | y0, ((uint64_t)y3 << 32) | y2};
+#else
+                d[s] = lld2(w + 64 * s);
+#endif
+            }
             __builtin_amdgcn_sched_barrier(0);
             uint64_t c0 = 0, c1 = 0;
 #pragma unroll
