@@ -403,15 +403,13 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
 // that span once, 16 bytes per lane, kWideD iterations ahead (4 registers per
 // KiB in flight), and writes it into a per-wave LDS ring of two 1 KiB slots
 // plus a mirror of slot 0 (so a window's 2 KiB are always contiguous); the
-// windows read their stripes from there (unaligned ds_read_b128).  Windows
+// windows read their stripes from there (five aligned dwords per 16 bytes,
+// realigned with v_alignbyte by the window's byte offset).  Windows
 // not yet started or already finished compute on stale bytes and keep their
 // accumulators.  Same XXH3 as rows_window; window j's results sit in lanes
 // 4j .. 4j+3.
 constexpr uint32_t kWideQ = 16;
 constexpr uint32_t kPredict = 3;   // blocks want .. want + 2 flag a likely resync hit
-#ifndef VS_WIDE_MIN
-#define VS_WIDE_MIN (kRows + 1)   // fewer queued windows take the four-row pass
-#endif
 #ifndef VS_WIDE_D
 #define VS_WIDE_D 8
 #endif
@@ -426,12 +424,6 @@ typedef __attribute__((address_space(1))) const u64x2 g_u64x2;
 // 16 bytes at any byte address (one global_load_dwordx4: gfx950 unaligned mode)
 __device__ __forceinline__ u64x2 gld2(g_u8 *p) {
     return *(g_u64x2 *)p;
-}
-// 16 bytes of LDS at any byte address (one ds_read_b128: gfx950 unaligned DS access)
-__device__ __forceinline__ u64x2 lld2(const l_u8 *p) {
-    u64x2 v;
-    __builtin_memcpy(&v, (const uint8_t *)p, 16);
-    return v;
 }
 __device__ __forceinline__ void acc2(const u64x2 d, uint64_t k0s, uint64_t k1s, uint64_t &c0,
                                      uint64_t &c1) {
@@ -461,9 +453,7 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
                                  (uint32_t)__shfl((int)(uint32_t)qh, (int)(j < nq ? j : 0), 64));
     const uint32_t tau = (uint32_t)((hj - h0) >> 10);
     const uint32_t rj = (uint32_t)(hj - h0) - 1024 * tau;   // window j's offset in iteration t's 2 KiB
-#if VS_WIDE_ALIGNED
     const uint32_t sh = rj & 3;                              // its bytes' offset in LDS dwords
-#endif
     const uint32_t nb = (uint32_t)((len - 1) / 1024);
     const uint32_t T = uni((uint32_t)((hl - h0) >> 10)) + nb;
     uint64_t a0 = (k == 0) ? P32_3 : (k == 1) ? P64_2 : (k == 2) ? P64_4 : P64_5;
@@ -517,9 +507,9 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
             u64x2 d[16];
 #pragma unroll
             for (uint32_t s = 0; s < 16; ++s) {
-#if VS_WIDE_ALIGNED
                 // five 4-byte-aligned dwords, realigned by the window's byte
-                // offset (unaligned ds_read_b128s cost the LDS several passes)
+                // offset: unaligned ds_read_b128s took the LDS several passes
+                // each (share walk 54.9 -> 45.8 ms, profiles/r04_walk_lds/ab5_*)
                 typedef __attribute__((address_space(3))) const uint32_t l_u32;
                 l_u32 *q = (l_u32 *)(w + 64 * s - sh);
                 const uint32_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3], x4 = q[4];
@@ -528,9 +518,6 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
                 const uint32_t y2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
                 const uint32_t y3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
                 d[s] = u64x2{((uint64_t)y1 << 32) | y0, ((uint64_t)y3 << 32) | y2};
-#else
-                d[s] = lld2(w + 64 * s);
-#endif
             }
             __builtin_amdgcn_sched_barrier(0);
             uint64_t c0 = 0, c1 = 0;
@@ -1045,7 +1032,7 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 predicted = false;
                 // hash the queued windows together, visit them in order: more
                 // than kRows in one address-lockstep pass, else one per row
-                const bool wide = fq == kWideQ && nq >= VS_WIDE_MIN;
+                const bool wide = fq == kWideQ && nq > kRows;   // (wide for every flush: no faster)
                 uint64_t tf = wclock(wp);
                 RowWin w;
                 if (wide) {
