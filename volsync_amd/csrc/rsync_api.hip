@@ -340,7 +340,10 @@ int build_table(vs_rsync *h) {
     // blocks 32 and 16 bits per key are within 1 % and 8 bits per key loses
     // 5 % (profiles/r02_walk_ab).
     const uint32_t lc = ceil_log2(std::max<uint32_t>(count, 1));
-    h->fbits = std::min<uint32_t>(std::max<uint32_t>(std::min(lc + 5, 25u), 10), 28);
+#ifndef VS_FBITS_CAP
+#define VS_FBITS_CAP 25u   // 4 MiB: one XCD's L2
+#endif
+    h->fbits = std::min<uint32_t>(std::max<uint32_t>(std::min(lc + 5, VS_FBITS_CAP), 10), 28);
     const size_t n = std::max<uint32_t>(count, 1);
     VS_TRY(h->d_keys.ensure(n * 8));
     VS_TRY(h->d_tkey.ensure(n * 8));
