@@ -398,7 +398,9 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
         // on the other
         producer = wave == (t & 1);
 #endif
-        __builtin_amdgcn_s_setprio(producer ? 0 : 2);  // the rounds are the critical path
+        // the rounds are the critical path
+        if (producer) __builtin_amdgcn_s_setprio(0);
+        else __builtin_amdgcn_s_setprio(2);
         const bool quad = t < qt;  // wave-uniform
         const uint32_t my = quad ? (producer ? lane : lane >> 2) : lane;
         const uint32_t idx = quad ? t * 16 + my : nq + (t - qt) * 64 + my;
