@@ -376,8 +376,7 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
     // runs every quad tile it gets before its first split tile
     uint4 *const zero_kw = &wk[0][512];
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;   // wave-uniform
-    bool producer = wave == 0;
+    const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;  // wave-uniform
     const uint32_t n = *a.n_cur;
     const uint32_t nq = min(a.quad_chains, n);
     const uint32_t qt = (nq + 15) / 16;
@@ -386,21 +385,13 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
         for (uint32_t i = threadIdx.x; i < 16 * 16; i += blockDim.x) zero_kw[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
     }
+    if (!producer) __builtin_amdgcn_s_setprio(2);  // the rounds are the critical path
     for (;;) {
         if (threadIdx.x == 0) tile_sh = atomicAdd(a.tile_ctr, 1u);
         __syncthreads();
         const uint32_t t = tile_sh;
         __syncthreads();
         if (t >= ntiles) break;
-#if VS_SHA_ALTERNATE
-        // the roles alternate tile by tile: a workgroup's two waves sit on two
-        // SIMDs, and fixed roles put every producer on one and every consumer
-        // on the other
-        producer = wave == (t & 1);
-#endif
-        // the rounds are the critical path
-        if (producer) __builtin_amdgcn_s_setprio(0);
-        else __builtin_amdgcn_s_setprio(2);
         const bool quad = t < qt;  // wave-uniform
         const uint32_t my = quad ? (producer ? lane : lane >> 2) : lane;
         const uint32_t idx = quad ? t * 16 + my : nq + (t - qt) * 64 + my;
