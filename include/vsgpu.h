@@ -553,7 +553,7 @@ int vs_restic_pack_header(const uint8_t *types, const uint32_t *lengths, const u
  * product settings; results are identical under every option (they change
  * which kernels run or how work is split, never what is computed). */
 #define VS_OPT_WALK_SEGMENT_BLOCKS 1 /* rsync: device walk segment length in blocks
-                                      * (0 = automatic: 32, shorter for ranges too
+                                      * (0 = automatic: 48, shorter for ranges too
                                       * small to give every wave two segments) */
 #define VS_OPT_FILE_SUM_PIECE 2      /* rsync: file-sum read-back piece in 1 KiB blocks
                                       * (0 = 2^18: 16 MiB of contribution rows) */

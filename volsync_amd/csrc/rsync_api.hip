@@ -947,14 +947,15 @@ int walk_scan(vs_rsync *h) {
     a.lo = r.own_lo - r.origin;
     a.hi = r.own_hi - r.origin;
     {
-        // segment length: 32 blocks (4 MiB at C4; 16 measured slower, 64
-        // within noise), shorter -- down to 1 MiB -- when the
-        // range is too small to give every wave of the grid two segments (a
-        // streamed piece of 256 MiB: 256 segments instead of 64 idle-heavy
-        // ones).  vs_rsync_set_walk_segment overrides it.
+        // segment length: 48 blocks (6 MiB at C4; with the wide flushes 16,
+        // 24, 32, 64 and 96 measured slower), shorter -- down
+        // to 1 MiB -- when the range is too small to give every wave of the
+        // grid two segments (a streamed piece of 256 MiB: 256 segments
+        // instead of 43 idle-heavy ones).  VS_OPT_WALK_SEGMENT_BLOCKS
+        // overrides it.
         const int64_t range = std::max<int64_t>(a.hi - a.lo, 1);
         const int64_t waves = (int64_t)std::max(h->cus, 1) * 8;
-        int64_t sl = (int64_t)h->blength * (h->seg_blocks ? h->seg_blocks : 32);
+        int64_t sl = (int64_t)h->blength * (h->seg_blocks ? h->seg_blocks : 48);
         if (!h->seg_blocks && range / sl < 2 * waves)
             sl = std::max<int64_t>(range / (2 * waves), h->blength);
         a.seg_len = std::max<int64_t>(sl, 1 << 20);
