@@ -732,7 +732,7 @@ def test_file_sum_jobs_fifo(gpu):
     (0, 1, 16, 40000, 0), (0, 1, 4, 3000, 0)])
 def test_walk_segment_lengths_exact(gpu, seg, prefilter, flushq, span, predict):
     """The device walk with other segment lengths (VS_OPT_WALK_SEGMENT_BLOCKS;
-    the default 0 is 32 blocks, shorter for small ranges), without the LDS
+    the default 0 is 48 blocks, shorter for small ranges), without the LDS
     prefilter (VS_OPT_WALK_PREFILTER 0), with four-window flushes in place of
     the wide address-lockstep ones (VS_OPT_WALK_FLUSH_WINDOWS) and with flushes
     bounded by a span (VS_OPT_WALK_FLUSH_SPAN), with and without the early
