@@ -341,7 +341,10 @@ int build_table(vs_rsync *h) {
     // 5 % (profiles/r02_walk_ab).
     const uint32_t lc = ceil_log2(std::max<uint32_t>(count, 1));
 #ifndef VS_FBITS_CAP
-#define VS_FBITS_CAP 25u   // 4 MiB: one XCD's L2
+// 2 MiB: half of one XCD's L2, so the walk's filter gathers stay in it beside
+// the window bytes (at the real C4's 2 M blocks the 4 MiB filter's misses were
+// half the walk's fetch: 5.5 -> 2.8 B per source byte)
+#define VS_FBITS_CAP 24u
 #endif
     h->fbits = std::min<uint32_t>(std::max<uint32_t>(std::min(lc + 5, VS_FBITS_CAP), 10), 28);
     const size_t n = std::max<uint32_t>(count, 1);
