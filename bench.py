@@ -67,6 +67,7 @@ def cpu_baseline(sample_bytes: int, threads: int):
                   f"{bool(O.lib().ref_have_openssl())}); chunker alone 1 core "
                   f"{sample_bytes / dt_chunk / 1e9:.3f} GB/s",
         "cpu": _cpu_model(),
+        "nproc": os.cpu_count(),   # the host's logical CPUs (the baseline used `cores` of them)
     }
 
 
@@ -101,7 +102,7 @@ def rsync_cpu_baseline(sample_bytes: int):
             "sample": f"{sample_bytes >> 20} MiB destination (seed 4) + C4-mutated source (seed 5), "
                       f"blength {bl}, xxh128; signatures {t1 - t0:.2f} s, match {t2 - t1:.2f} s, "
                       f"{len(m)} matches",
-            "cpu": _cpu_model()}
+            "cpu": _cpu_model(), "nproc": os.cpu_count()}
 
 
 
@@ -567,7 +568,7 @@ def smallfiles_cpu_baseline(sizes, sample_files: int, threads: int):
     return {"value": round(float(sz.sum()) / dt / 1e9, 3), "unit": "GB/s", "cores": threads,
             "kind": "port", "sample": f"{len(sz)} files ({float(sz.sum()) / 2**30:.2f} GiB) of the "
             f"C5 size distribution, hashlib/OpenSSL SHA-256 on {threads} threads",
-            "cpu": _cpu_model()}
+            "cpu": _cpu_model(), "nproc": os.cpu_count()}
 
 
 def smallfiles_main(args):
@@ -709,7 +710,7 @@ def seal_cpu_baseline(sizes, keys, sample_bytes: int, threads: int):
     return {"value": round(float(sz.sum()) / dt / 1e9, 3), "unit": "GB/s", "cores": threads,
             "kind": "port", "sample": f"{nb} blobs ({float(sz.sum()) / 2**30:.2f} GiB) of the same "
             f"size distribution, libcrypto AES-256-CTR + Poly1305 on {threads} threads",
-            "cpu": _cpu_model()}
+            "cpu": _cpu_model(), "nproc": os.cpu_count()}
 
 
 def seal_main(args):
