@@ -411,9 +411,12 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
 constexpr uint32_t kWideQ = 16;
 constexpr uint32_t kPredict = 3;   // blocks want .. want + 2 flag a likely resync hit
 #ifndef VS_WIDE_D
-#define VS_WIDE_D 8
+#define VS_WIDE_D 4
 #endif
-constexpr uint32_t kWideD = VS_WIDE_D;                    // KiB in flight per wave
+// KiB in flight per wave: 4 (2, 4, 6, 8 measured 44.6, 45.2, 46.5, 46.3 ms of
+// share walk: fewer registers held across the call beat a deeper prefetch,
+// profiles/r04_walk_step/ab_wd*)
+constexpr uint32_t kWideD = VS_WIDE_D;
 constexpr uint32_t kWideRingBytes = 3 * 1024;             // per wave: slots 0, 1, mirror of 0
 
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
