@@ -727,23 +727,24 @@ def test_file_sum_jobs_fifo(gpu):
     m.close()
 
 
-@pytest.mark.parametrize("seg,prefilter,flushq,span,predict", [
-    (8, 1, 16, 0, 1), (16, 1, 4, 0, 1), (64, 1, 16, 8192, 1), (0, 0, 16, 0, 1),
-    (0, 1, 16, 40000, 0), (0, 1, 4, 3000, 0)])
-def test_walk_segment_lengths_exact(gpu, seg, prefilter, flushq, span, predict):
+@pytest.mark.parametrize("seg,prefilter,flushq,span,predict,tail", [
+    (8, 1, 16, 0, 1, 0), (16, 1, 4, 0, 1, 0), (64, 1, 16, 8192, 1, 0), (0, 0, 16, 0, 1, 0),
+    (0, 1, 16, 40000, 0, 0), (0, 1, 4, 3000, 0, 0), (0, 1, 16, 0, 1, 30), (32, 1, 16, 0, 1, 90)])
+def test_walk_segment_lengths_exact(gpu, seg, prefilter, flushq, span, predict, tail):
     """The device walk with other segment lengths (VS_OPT_WALK_SEGMENT_BLOCKS;
     the default 0 is 48 blocks, shorter for small ranges), without the LDS
     prefilter (VS_OPT_WALK_PREFILTER 0), with four-window flushes in place of
     the wide address-lockstep ones (VS_OPT_WALK_FLUSH_WINDOWS) and with flushes
     bounded by a span (VS_OPT_WALK_FLUSH_SPAN), with and without the early
-    flush at a likely resync (VS_OPT_WALK_FLUSH_PREDICT): more or fewer speculative
+    flush at a likely resync (VS_OPT_WALK_FLUSH_PREDICT), with quarter-length
+    tail segments (VS_OPT_WALK_TAIL_PCT): more or fewer speculative
     segments, stitches and flushes, the same hash_search -- seeded shifted /
     overwritten sources (false alarms, runs, short last blocks), the C4
     parameters on a 1 GiB basis, and the 4-way sharded walk."""
     from volsync_amd import Matcher, SumStruct
     from volsync_amd._lib import (VS_OPT_WALK_FLUSH_PREDICT, VS_OPT_WALK_FLUSH_SPAN,
                                   VS_OPT_WALK_FLUSH_WINDOWS, VS_OPT_WALK_PREFILTER,
-                                  VS_OPT_WALK_SEGMENT_BLOCKS)
+                                  VS_OPT_WALK_SEGMENT_BLOCKS, VS_OPT_WALK_TAIL_PCT)
 
     def opts(m):
         m.set_option(VS_OPT_WALK_SEGMENT_BLOCKS, seg)
@@ -751,6 +752,7 @@ def test_walk_segment_lengths_exact(gpu, seg, prefilter, flushq, span, predict):
         m.set_option(VS_OPT_WALK_FLUSH_WINDOWS, flushq)
         m.set_option(VS_OPT_WALK_FLUSH_SPAN, span)
         m.set_option(VS_OPT_WALK_FLUSH_PREDICT, predict)
+        m.set_option(VS_OPT_WALK_TAIL_PCT, tail)
     for csum_type, seed, n, frac, bs in [(R.CSUM_XXH3_128, 0x5EED5EED, 40 << 20, 0.10, 0),
                                          (R.CSUM_XXH3_64, 7, 12 << 20, 0.30, 0),
                                          (R.CSUM_XXH3_128, 1, 6 << 20, 0.20, 1000),

@@ -392,6 +392,8 @@ struct RsWalkArgs {
     int64_t full_end;      // offsets below it have a full window (F - blength + 1)
     int64_t lo, hi;        // the owned range
     int64_t seg_len;
+    int64_t seg_len2;      // segments nseg1.. (the tail): this long
+    uint32_t nseg1;
     uint32_t nseg, cap;    // segments, match capacity per segment
     uint32_t blength, count, remainder;
     int csum_type;

@@ -223,6 +223,7 @@ struct vs_rsync {
     uint32_t opt_flushq = 0;        // STEP hits per flush (4: rows only; 16 or 0: wide passes)
     uint32_t opt_flushspan = 0;     // flush once the scan is this far past the first hit (0: none)
     bool opt_flushpredict = true;   // flush at a likely resync hit (weak sum of block want .. want + 2)
+    int32_t opt_tailpct = 0;        // % of the walk range in quarter-length tail segments
     uint64_t fs_piece = 0;          // file-sum piece in 1 KiB blocks (0: 2^18)
     // streamed forms (host-fed files): see the MatchStream / SigStream section
     MatchStream *mst = nullptr;
@@ -964,6 +965,20 @@ int walk_scan(vs_rsync *h) {
         a.seg_len = std::max<int64_t>(sl, 1 << 20);
     }
     a.nseg = (uint32_t)((a.hi - a.lo + a.seg_len - 1) / a.seg_len);
+    a.nseg1 = a.nseg;
+    a.seg_len2 = a.seg_len;
+    if (h->opt_tailpct > 0) {
+        // the last tailpct % of the range in segments a quarter as long,
+        // handed out last (waves take segments in index order), so the
+        // grid's last waves finish closer together
+        const int64_t range = a.hi - a.lo, L2 = std::max<int64_t>(a.seg_len / 4, 1 << 20);
+        if (L2 < a.seg_len) {
+            const int64_t big = range * (100 - h->opt_tailpct) / 100 / a.seg_len;
+            a.nseg1 = (uint32_t)big;
+            a.seg_len2 = L2;
+            a.nseg = (uint32_t)(big + (range - big * a.seg_len + L2 - 1) / L2);
+        }
+    }
     a.cap = (uint32_t)(a.seg_len / h->blength + 2);
     a.blength = (uint32_t)h->blength;
     a.count = (uint32_t)h->count;
@@ -998,7 +1013,7 @@ int walk_scan(vs_rsync *h) {
     VS_TRY(h->w_fin_fab.ensure(nc * 8));
     VS_TRY(h->w_spec_n.ensure(ns * 4));
     // false-alarm windows of the speculative walks: up to 1024 per segment (a
-    // 4 MiB segment of the real C4 averages ~200; more falls back to a
+    // 6 MiB segment of the real C4 averages ~300; more falls back to a
     // re-walk), at most 256 MiB of records per walk (small blocks, many
     // segments)
     a.facap = (uint32_t)std::max<uint64_t>(
@@ -2308,6 +2323,10 @@ VS_API int vs_rsync_set_option(vs_rsync *h, int option, int64_t value) {
         case VS_OPT_WALK_FLUSH_SPAN:
             if (value < 0 || value > (1ll << 30)) return fail(VS_ERR_ARG, "flush span out of range");
             h->opt_flushspan = (uint32_t)value;
+            return 0;
+        case VS_OPT_WALK_TAIL_PCT:
+            if (value < 0 || value > 90) return fail(VS_ERR_ARG, "tail share out of range");
+            h->opt_tailpct = (int32_t)value;
             return 0;
         case VS_OPT_WALK_FLUSH_PREDICT:
             h->opt_flushpredict = value != 0;
