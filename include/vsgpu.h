@@ -575,7 +575,8 @@ int vs_restic_pack_header(const uint8_t *types, const uint32_t *lengths, const u
                                       * whose weak sum is that of block want_i .. want_i + 2,
                                       * the usual resync after an edit (default 1) */
 #define VS_OPT_WALK_TAIL_PCT 10      /* rsync: % of the walk range cut into quarter-length
-                                      * segments handed out last (default 0) */
+                                      * segments handed out last (-1 = automatic, the
+                                      * default: 20 below four segments per wave, else 10) */
 #define VS_OPT_SHA_QUAD_PCT 16       /* cdc / sha: chains within this % of the longest
                                       * run in latency (quad) mode in the final drain
                                       * (default 80; 0 = split mode only) */

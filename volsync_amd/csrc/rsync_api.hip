@@ -223,7 +223,7 @@ struct vs_rsync {
     uint32_t opt_flushq = 0;        // STEP hits per flush (4: rows only; 16 or 0: wide passes)
     uint32_t opt_flushspan = 0;     // flush once the scan is this far past the first hit (0: none)
     bool opt_flushpredict = true;   // flush at a likely resync hit (weak sum of block want .. want + 2)
-    int32_t opt_tailpct = 0;        // % of the walk range in quarter-length tail segments
+    int32_t opt_tailpct = -1;       // % of the walk range in quarter-length tail segments (-1: automatic)
     uint64_t fs_piece = 0;          // file-sum piece in 1 KiB blocks (0: 2^18)
     // streamed forms (host-fed files): see the MatchStream / SigStream section
     MatchStream *mst = nullptr;
@@ -967,13 +967,17 @@ int walk_scan(vs_rsync *h) {
     a.nseg = (uint32_t)((a.hi - a.lo + a.seg_len - 1) / a.seg_len);
     a.nseg1 = a.nseg;
     a.seg_len2 = a.seg_len;
-    if (h->opt_tailpct > 0) {
-        // the last tailpct % of the range in segments a quarter as long,
-        // handed out last (waves take segments in index order), so the
-        // grid's last waves finish closer together
+    // the last tail % of the range in segments a quarter as long, handed out
+    // last (waves take segments in index order), so the grid's last waves
+    // finish closer together: 20 % when the grid gets fewer than four
+    // segments per wave, else 10 % (the real C4's rank: walk 44.6 -> 41.2 ms;
+    // the 64 GiB shape: 42.0 -> 41.1)
+    const int64_t waves = (int64_t)std::max(h->cus, 1) * 8;
+    const int32_t tailpct = h->opt_tailpct >= 0 ? h->opt_tailpct : ((int64_t)a.nseg < 4 * waves ? 20 : 10);
+    if (tailpct > 0) {
         const int64_t range = a.hi - a.lo, L2 = std::max<int64_t>(a.seg_len / 4, 1 << 20);
         if (L2 < a.seg_len) {
-            const int64_t big = range * (100 - h->opt_tailpct) / 100 / a.seg_len;
+            const int64_t big = range * (100 - tailpct) / 100 / a.seg_len;
             a.nseg1 = (uint32_t)big;
             a.seg_len2 = L2;
             a.nseg = (uint32_t)(big + (range - big * a.seg_len + L2 - 1) / L2);
@@ -2325,7 +2329,7 @@ VS_API int vs_rsync_set_option(vs_rsync *h, int option, int64_t value) {
             h->opt_flushspan = (uint32_t)value;
             return 0;
         case VS_OPT_WALK_TAIL_PCT:
-            if (value < 0 || value > 90) return fail(VS_ERR_ARG, "tail share out of range");
+            if (value < -1 || value > 90) return fail(VS_ERR_ARG, "tail share out of range");
             h->opt_tailpct = (int32_t)value;
             return 0;
         case VS_OPT_WALK_FLUSH_PREDICT:
