@@ -436,7 +436,7 @@ __device__ __forceinline__ void acc2(const u64x2 d, uint64_t k0s, uint64_t k1s, 
 }
 
 // Not inlined: inlined, its registers and the STEP state live across a flush
-// spill 75 VGPRs of the walk (26 without it).  Typed pointers and uniform
+// spilled 75 VGPRs of the walk (26 without it; called, 64).  Typed pointers and uniform
 // scalars: a call boundary would otherwise turn every load into a flat one
 // and the block loop into a divergent one.
 __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw0, l_u8 *ring,
