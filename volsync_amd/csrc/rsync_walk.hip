@@ -409,7 +409,10 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
 // accumulators.  Same XXH3 as rows_window; window j's results sit in lanes
 // 4j .. 4j+3.
 constexpr uint32_t kWideQ = 16;
-constexpr uint32_t kPredict = 3;   // blocks want .. want + 2 flag a likely resync hit
+#ifndef VS_PREDICT
+#define VS_PREDICT 3
+#endif
+constexpr uint32_t kPredict = VS_PREDICT;   // blocks want .. want + 2 flag a likely resync hit
 #ifndef VS_WIDE_D
 #define VS_WIDE_D 4
 #endif
