@@ -111,20 +111,6 @@ __device__ __forceinline__ void window_words(uint32_t (&d)[17], const uint4 &s0,
     for (int k = 0; k < 17; ++k) d[k] = ch(m2, t[k + 2], t[k]);
 }
 
-#if VS_SHA_LDS_WINDOW
-// The same words read from the staging area at dword granularity: the lane's
-// carried segment at uint4 5 lane, the block's four at 5 lane + 1 .. 4, so
-// d[k] = dword 20 lane + q + k and no realignment selects are needed; the
-// next carried segment is the window's last uint4.
-__device__ __forceinline__ void window_lds(uint32_t (&d)[17], uint4 &c, const uint4 *stage,
-                                           uint32_t lane, uint32_t q) {
-    const uint32_t *w = (const uint32_t *)(stage + 5 * lane) + q;
-#pragma unroll
-    for (int k = 0; k < 17; ++k) d[k] = w[k];
-    c = stage[5 * lane + 4];
-}
-#endif
-
 // Big-endian message words W[0..15] of the block at ptr from its raw words.
 __device__ __forceinline__ void message(uint32_t (&w)[16], const uint32_t (&d)[17], uint64_t ptr,
                                         uint64_t end, uint64_t len) {
@@ -334,11 +320,7 @@ __device__ __forceinline__ void produce_tile(uint4 (&wk)[2][16 * 64], const ShaC
     const uint64_t so = 16 + 16 * (lane & 3);
     // staged segments: chain c, segment t at uint4 index 5 c + t (80-byte
     // stride: conflict-free ds_write_b128 / ds_read_b128)
-#if VS_SHA_LDS_WINDOW
-    const uint32_t wr = 5 * (lane >> 2) + (lane & 3) + 1;
-#else
     const uint32_t wr = 5 * (lane >> 2) + (lane & 3);
-#endif
     uint4 R[4], c = load_seg(A, e, safe), S[4];
     uint32_t d[17], w[16];
 #pragma unroll
@@ -346,19 +328,12 @@ __device__ __forceinline__ void produce_tile(uint4 (&wk)[2][16 * 64], const ShaC
     // block 0 -> slot 0
 #pragma unroll
     for (int i = 0; i < 4; ++i) wk[0][80 * i + wr] = R[i];
-#if VS_SHA_LDS_WINDOW
-    wk[0][5 * lane] = c;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + 64 + so, LE[i], LS[i]);
-    window_lds(d, c, wk[0], lane, q);
-#else
 #pragma unroll
     for (int t = 0; t < 4; ++t) S[t] = wk[0][5 * lane + t];
 #pragma unroll
     for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + 64 + so, LE[i], LS[i]);
     window_words(d, c, S, q);
     c = S[3];
-#endif
     if (mine > 0) {
         message(w, d, p, e, L);
         schedule_to_lds(w, wk[0], lane, QUAD);
@@ -371,19 +346,12 @@ __device__ __forceinline__ void produce_tile(uint4 (&wk)[2][16 * 64], const ShaC
         const uint64_t nb = 64ull * (j + 2) + so;
 #pragma unroll
         for (int i = 0; i < 4; ++i) slot[80 * i + wr] = R[i];
-#if VS_SHA_LDS_WINDOW
-        slot[5 * lane] = c;
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + nb, LE[i], LS[i]);
-#if VS_SHA_LDS_WINDOW
-        window_lds(d, c, slot, lane, q);
-#else
 #pragma unroll
         for (int t = 0; t < 4; ++t) S[t] = slot[5 * lane + t];
         window_words(d, c, S, q);
         c = S[3];
-#endif
         if (j + 1 < mine) {
             message(w, d, p + 64ull * (j + 1), e, L);
             schedule_to_lds(w, slot, lane, QUAD);
@@ -574,11 +542,7 @@ __global__ __launch_bounds__(64 * kWideWaves, 3) void sha_slice_wide_kernel(ShaS
             LS[i] = (uint64_t)__shfl((long long)safe, src, 64);
         }
         const uint64_t so = 16 + 16 * (lane & 3);
-#if VS_SHA_LDS_WINDOW
-        const uint32_t wr = 5 * (lane >> 2) + (lane & 3) + 1;
-#else
         const uint32_t wr = 5 * (lane >> 2) + (lane & 3);
-#endif
         uint32_t st[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) st[i] = ch0.st[i];
@@ -589,24 +553,16 @@ __global__ __launch_bounds__(64 * kWideWaves, 3) void sha_slice_wide_kernel(ShaS
             // block j's segments arrived during block j-1; fetch block j+1's now
 #pragma unroll
             for (int i = 0; i < 4; ++i) stage[80 * i + wr] = R[i];
-#if VS_SHA_LDS_WINDOW
-            stage[5 * lane] = c;
-#endif
             const uint64_t nb = 64ull * (j + 1) + so;
 #pragma unroll
             for (int i = 0; i < 4; ++i) R[i] = load_seg(LA[i] + nb, LE[i], LS[i]);
             wave_lds_sync();
-            uint32_t d[17], w[16];
-#if VS_SHA_LDS_WINDOW
-            window_lds(d, c, stage, lane, q);
-            wave_lds_sync();
-#else
 #pragma unroll
             for (int k = 0; k < 4; ++k) S[k] = stage[5 * lane + k];
             wave_lds_sync();
+            uint32_t d[17], w[16];
             window_words(d, c, S, q);
             c = S[3];
-#endif
             if (j < mine) {
                 message(w, d, p + 64ull * j, e, L);
                 compress_regs(st, w);
