@@ -2,7 +2,8 @@
 # Round 4's GPU runs, one subcommand each (run on the box through gpurun; each
 # step has its own time limit in tools/gpu.sh and the steps stop at the first
 # failure).  The A/B variants were built with tools/build_variant.sh as noted;
-# where the winner became the code, its macro is gone (regs, aligned, sha),
+# where the winner became the code or the variant lost, its macro is gone
+# (regs, aligned, sha, shalds),
 # and the lines stay as the record of how the committed logs were made.
 #
 #   closing     the whole -m gpu suite, smoke(), the bench lines, all of C3
