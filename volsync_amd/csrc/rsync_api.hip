@@ -975,7 +975,10 @@ int walk_scan(vs_rsync *h) {
     const int64_t waves = (int64_t)std::max(h->cus, 1) * 8;
     const int32_t tailpct = h->opt_tailpct >= 0 ? h->opt_tailpct : ((int64_t)a.nseg < 4 * waves ? 20 : 10);
     if (tailpct > 0) {
-        const int64_t range = a.hi - a.lo, L2 = std::max<int64_t>(a.seg_len / 4, 1 << 20);
+#ifndef VS_TAIL_DIV
+#define VS_TAIL_DIV 4
+#endif
+        const int64_t range = a.hi - a.lo, L2 = std::max<int64_t>(a.seg_len / VS_TAIL_DIV, 1 << 20);
         if (L2 < a.seg_len) {
             const int64_t big = range * (100 - tailpct) / 100 / a.seg_len;
             a.nseg1 = (uint32_t)big;
