@@ -23,6 +23,7 @@
 #   predict     build p1, p6 (-DVS_PREDICT=N), wd2 (-DVS_WIDE_D=2) -> profiles/r04_walk_step/ab_pred*
 #   shalds      build shalds (-DVS_SHA_LDS_WINDOW=1)        -> profiles/r04_sha_ab
 #   taildiv     build td3, td6 (-DVS_TAIL_DIV=N: tail segments a third / sixth long)
+#   runring     build rr2, rr6 (-DVS_WALK_RRING=N: RUN-window blocks in flight)
 #   walkprof    build walkprof (-DVS_WALK_PROF=1): walk phase profiles
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 S="--mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum"
@@ -99,9 +100,12 @@ case $1 in
   taildiv)
     L="base=,td3=$(var td3),td6=$(var td6)"
     ab ab_td_share 2 "$L" $S && ab ab_td_c4 2 "$L" $C ;;
+  runring)
+    L="base=,rr2=$(var rr2),rr6=$(var rr6)"
+    ab ab_rr_share 2 "$L" $S && ab ab_rr_c4 2 "$L" $C ;;
   walkprof)
     bash tools/c4_walkprof.sh --share 3/8 --per-gpu-gib 32 > gpurun_out/walkprof2_share.txt 2>&1 &&
     bash tools/c4_walkprof.sh > gpurun_out/walkprof2_c4.txt 2>&1 ;;
-  *) echo "usage: tools/r04_runs.sh closing|benches|rsync|profiles|multirank|flush|regs|aligned|step|seg|lookahead|tail|sha|predict|shalds|taildiv|walkprof" >&2
+  *) echo "usage: tools/r04_runs.sh closing|benches|rsync|profiles|multirank|flush|regs|aligned|step|seg|lookahead|tail|sha|predict|shalds|taildiv|runring|walkprof" >&2
      exit 2 ;;
 esac
