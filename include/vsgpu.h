@@ -580,6 +580,9 @@ int vs_restic_pack_header(const uint8_t *types, const uint32_t *lengths, const u
 #define VS_OPT_SHA_QUAD_PCT 16       /* cdc / sha: chains within this % of the longest
                                       * run in latency (quad) mode in the final drain
                                       * (default 80; 0 = split mode only) */
+#define VS_OPT_SHA_GRID_PER_CU 18   /* cdc / sha: persistent hash grid per CU: split-mode
+                                      * workgroups (default 5) / throughput-mode waves
+                                      * per SIMD (default 3); 0 = default */
 #define VS_OPT_FP_GENERIC 17         /* cdc: 1 = the generic fingerprint address code
                                       * even where the FAST variant applies */
 #define VS_OPT_SEAL_FUSED 32         /* seal: 0 = separate CTR and MAC kernels (default 1) */

@@ -1,0 +1,43 @@
+#!/bin/bash
+# Round 5's GPU runs, one subcommand each (through gpurun; every GPU step has
+# its own time limit in tools/gpu.sh or here, and the chain stops at the first
+# failure).
+#   first     VALU probe 3, the CDC + C3 GPU tests, fingerprint A/B (fpb0 =
+#             -DVS_FP_BITOP3=0), C2 bench at the driver's 20/5, its trace-only
+#             rocprofv3 run, one C3 rank at 20/5          -> profiles/r05_*
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+mkdir -p gpurun_out
+var() { echo "volsync_amd/lib/var/$1/libvsgpu.so"; }
+ab() {  # ab <log> <rounds> <libs> <script args...>
+  local log=$1 rounds=$2 libs=$3
+  shift 3
+  timeout -k 10 900 python3 -u tools/ab.py --rounds "$rounds" --libs "$libs" -- "$@" \
+    > "gpurun_out/$log.log" 2>&1
+  local rc=$?
+  echo "=== $log rc=$rc"; tail -n 8 "gpurun_out/$log.log"
+  return $rc
+}
+trace() {  # trace <tag> <bench args...>: kernel trace + stats only (no counters)
+  local tag=$1 out=$PWD/gpurun_out/trace_$1 repo=$PWD
+  shift
+  mkdir -p "$out"
+  (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/raw" \
+     -o run --output-format csv -- python3 "$repo/bench.py" "$@") > "$out/bench.log" 2>&1
+  local rc=$?
+  echo "=== trace_$tag rc=$rc"; tail -n 2 "$out/bench.log" | cut -c1-300
+  [ $rc -eq 0 ] || return $rc
+  find "$out/raw" -name '*kernel_stats.csv' -exec cp {} "$out/kernel_stats.csv" \;
+  find "$out/raw" -name '*kernel_trace.csv' -exec cp {} "$out/kernel_trace.csv" \;
+  rm -rf "$out/raw"
+}
+case $1 in
+  first)
+    timeout -k 10 120 tools/valu/valu_ops3 > gpurun_out/valu_ops3.json 2> gpurun_out/valu_ops3.err &&
+    echo "=== valu_ops3 ok" &&
+    bash tools/gpu.sh tests tests/test_gpu_c3.py tests/test_gpu_cdc.py -x &&
+    ab fp_ab 3 "fpb0=$(var fpb0),new=" tools/fp_only.py --gib 64 --reps 5 &&
+    bash tools/gpu.sh bench c2 --gpus 1 --steps 20 --warmup 5 &&
+    trace c2 --gpus 1 --steps 20 --warmup 5 &&
+    bash tools/gpu.sh bench c3r3 --share 3/8 --steps 20 --warmup 5 --no-cpu-baseline ;;
+  *) echo "usage: tools/r05_runs.sh first" >&2; exit 2 ;;
+esac

@@ -22,7 +22,7 @@ rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestam
 
 def durs(name, min_ms=0.0):
     return [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows
-            if r["Kernel_Name"].split("(")[0].endswith(name)
+            if name in r["Kernel_Name"].split("(")[0]
             and (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 >= min_ms]
 
 
@@ -31,7 +31,7 @@ timed = sha[a.warmup + 1: a.warmup + 1 + a.steps + 1]
 print("sha_slice_kernel dispatches (ms):", [round(x, 2) for x in sha])
 print(f"  timed region: {len(timed)} launches, total {sum(timed):.1f} ms, "
       f"avg {sum(timed) / len(timed):.2f} ms, per volume {sum(timed) / a.steps:.2f} ms")
-fp = durs("fp_kernel<2>", 1.0)
+fp = durs("fp_kernel", 1.0)
 ft = fp[a.warmup: a.warmup + a.steps]
-print("fp_kernel<2> volume passes (ms):", [round(x, 2) for x in fp])
+print("fp_kernel volume passes (ms):", [round(x, 2) for x in fp])
 print(f"  timed region: {len(ft)} launches, avg {sum(ft) / len(ft):.2f} ms")

@@ -35,6 +35,7 @@ VS_OPT_WALK_FLUSH_PREDICT = 9
 VS_OPT_WALK_TAIL_PCT = 10
 VS_OPT_SHA_QUAD_PCT = 16
 VS_OPT_FP_GENERIC = 17
+VS_OPT_SHA_GRID_PER_CU = 18
 VS_OPT_SEAL_FUSED = 32
 
 u8p = ctypes.POINTER(ctypes.c_uint8)

@@ -1357,6 +1357,11 @@ VS_API int vs_blob_dedup(vs_sha *h, const uint8_t *dev_ids, size_t n, uint32_t *
 // the options a vs_cdc / vs_sha handle takes (vsgpu.h); the engine's quad
 // (latency-mode) share of the final drain: 0 = split mode only
 static int sha_option(ShaEngine &e, int option, int64_t value) {
+    if (option == VS_OPT_SHA_GRID_PER_CU) {
+        if (value < 0 || value > 5) return fail(VS_ERR_ARG, "grid per CU out of range [0, 5]");
+        e.grid_per_cu = (uint32_t)value;
+        return 0;
+    }
     if (option != VS_OPT_SHA_QUAD_PCT) return fail(VS_ERR_ARG, "unknown option " + std::to_string(option));
     if (value < 0 || value > 1000) return fail(VS_ERR_ARG, "quad share out of range");
     e.quad_pct = (uint32_t)value;

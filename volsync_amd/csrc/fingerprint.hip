@@ -78,20 +78,36 @@ __device__ __forceinline__ uint64_t lds_u64(const char *lds, uint32_t byte_addr)
     return *(const uint64_t *)(lds + byte_addr);
 }
 
+// Issue costs on gfx950 (profiles/r05_valu, tools/valu/valu_ops3.hip): v_perm,
+// v_alignbit, v_and_or and v_bfe take ~4.2 cycles per wave-instruction, while
+// v_bitop3 whose three sources are VGPRs, v_lshrrev with an inline shift and
+// the two-operand logic ops take ~2.3.  kFF00 is 0xff00 held in a VGPR (an
+// SGPR or literal operand would make the v_bitop3 a 4.2-cycle one).
+#ifndef VS_FP_BITOP3
+#define VS_FP_BITOP3 1
+#endif
+
 // One byte of the rolling window.  oldw/neww hold the evicted / incoming byte
-// in byte lane J.
-template <int J, bool FAST = false>
+// in byte lane J.  FAST: deg >= 48 (sh >= 8); SH8 >= 0: sh - 8 known at
+// compile time (restic's polynomials have degree 53: SH8 = 5).
+template <int J, bool FAST = false, int SH8 = -1>
 __device__ __forceinline__ void roll(uint32_t &hi, uint32_t &lo, uint32_t oldw, uint32_t neww,
-                                     uint32_t lane8, uint32_t sh, const char *lds) {
+                                     uint32_t lane8, uint32_t sh, const char *lds,
+                                     uint32_t kFF00 = 0xff00u) {
     const uint32_t lane8o = lane8 | kOut8Byte;
     // lane8o = lane*8 | 0x10000 (OUT8 base): one v_perm builds
-    // [lane*8, b_old, 0x01, 0x00] = 0x10000 + b_old*256 + lane*8
-    const uint32_t oaddr = __builtin_amdgcn_perm(lane8o, oldw, 0x0c060004u | (J << 8));
-    // MOD address idx*256 + lane*8.  FAST (deg >= 48, sh >= 8): a two-operand
-    // shift (half the issue cost of a three-operand VOP3) and one v_and_or
-    // instead of v_bfe + v_lshl_or
-    const uint32_t maddr = FAST ? (((hi >> (sh - 8)) & 0xff00u) | lane8)
-                                : ((__builtin_amdgcn_ubfe(hi, sh, 8) << 8) | lane8);
+    // [lane*8, b_old, 0x01, 0x00] = 0x10000 + b_old*256 + lane*8; byte 1
+    // needs no move: (oldw & 0xff00) | lane8o, one all-VGPR v_bitop3
+    const uint32_t oaddr = (VS_FP_BITOP3 && SH8 >= 0 && J == 1)
+                               ? __builtin_amdgcn_bitop3_b32(oldw, kFF00, lane8o, 0xEA)
+                               : __builtin_amdgcn_perm(lane8o, oldw, 0x0c060004u | (J << 8));
+    // MOD address idx*256 + lane*8.  FAST: a two-operand shift and one v_and_or
+    // instead of v_bfe + v_lshl_or; with SH8 the shift is an inline constant
+    // and the and-or an all-VGPR v_bitop3 ((a & b) | c = 0xEA)
+    const uint32_t maddr =
+        (VS_FP_BITOP3 && SH8 >= 0) ? __builtin_amdgcn_bitop3_b32(hi >> SH8, kFF00, lane8, 0xEA)
+        : FAST                     ? (((hi >> (sh - 8)) & 0xff00u) | lane8)
+                                   : ((__builtin_amdgcn_ubfe(hi, sh, 8) << 8) | lane8);
     const uint64_t ov = lds_u64(lds, oaddr);
     const uint64_t mv = lds_u64(lds, maddr);
     const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 24);            // hi<<8 | lo>>24
@@ -113,8 +129,9 @@ __device__ __forceinline__ void roll_warm(uint32_t &hi, uint32_t &lo, uint32_t n
 }
 
 // kernel variants: mask within the low digest word / wider than 32 bits /
-// FAST = low word and deg >= 48 (the restic default): cheaper MOD address
-constexpr int kFpNarrow = 0, kFpWide = 1, kFpFast = 2;
+// FAST = low word and deg >= 48: cheaper MOD address / FAST53 = FAST with
+// deg == 53 (every restic repository polynomial): the shift an inline constant
+constexpr int kFpNarrow = 0, kFpWide = 1, kFpFast = 2, kFpFast53 = 3;
 
 template <bool WIDE>
 __device__ __forceinline__ uint32_t cut_bits(uint32_t hi, uint32_t lo, uint32_t mlo,
@@ -160,7 +177,8 @@ __device__ __forceinline__ void process_group_pf(uint32_t (&hi)[CH], uint32_t (&
                                                  GBuf (&old)[CH], const GBuf (&nw)[CH],
                                                  uint32_t (&m)[CH], uint32_t lane8, uint32_t sh,
                                                  const char *lds, const FpArgs &a,
-                                                 const int64_t (&nxt)[CH]) {
+                                                 const int64_t (&nxt)[CH], uint32_t kFF00,
+                                                 uint32_t mlo) {
 #pragma unroll
     for (int c = 0; c < CH; ++c) m[c] = 0xffffffffu;
 #pragma unroll
@@ -171,17 +189,18 @@ __device__ __forceinline__ void process_group_pf(uint32_t (&hi)[CH], uint32_t (&
             for (int j = 0; j < 4; ++j) {
 #pragma unroll
                 for (int c = 0; c < CH; ++c) {
-                    constexpr bool F = MODE == kFpFast;
+                    constexpr bool F = MODE == kFpFast || MODE == kFpFast53;
+                    constexpr int S8 = MODE == kFpFast53 ? 5 : -1;
                     switch (j) {
-                        case 0: roll<0, F>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
-                        case 1: roll<1, F>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
-                        case 2: roll<2, F>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
-                        default: roll<3, F>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds); break;
+                        case 0: roll<0, F, S8>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds, kFF00); break;
+                        case 1: roll<1, F, S8>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds, kFF00); break;
+                        case 2: roll<2, F, S8>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds, kFF00); break;
+                        default: roll<3, F, S8>(hi[c], lo[c], old[c][w], nw[c][w], lane8, sh, lds, kFF00); break;
                     }
                     // (a v_min_u16 prefilter on the low 16 digest bits measured
                     // slower: 27.8 vs 22.8 ms per 64 GiB)
                     m[c] = __builtin_elementwise_min(
-                        m[c], cut_bits<MODE == kFpWide>(hi[c], lo[c], a.mask_lo, a.mask_hi));
+                        m[c], cut_bits<MODE == kFpWide>(hi[c], lo[c], mlo, a.mask_hi));
                 }
             }
         }
@@ -300,7 +319,8 @@ __device__ __forceinline__ uint32_t note_group(uint32_t notes, uint32_t g) {
 // for a padding chain (it computes but records nothing).
 template <int CH, bool GUARD, int MODE>
 __device__ __forceinline__ void run_strips(const FpArgs &a, const char *lds, uint32_t lane8,
-                                           const uint64_t (&kk)[CH], const bool (&valid)[CH]) {
+                                           const uint64_t (&kk)[CH], const bool (&valid)[CH],
+                                           uint32_t kFF00, uint32_t mlo) {
     const uint32_t sh = a.idx_shift;
     const uint32_t G = a.strip / kGB;  // groups per strip, even (and < 256)
     int64_t sb[CH];  // strip base (data offset)
@@ -336,7 +356,8 @@ __device__ __forceinline__ void run_strips(const FpArgs &a, const char *lds, uin
         int64_t nx_[CH];                                                                  \
         _Pragma("unroll") for (int c = 0; c < CH; ++c)                                    \
             nx_[c] = sb[c] + kGB * (int64_t)min((GI) + 1, G - 1);                          \
-        process_group_pf<CH, GUARD, MODE>(hi, lo, OLD, NEW, m, lane8, sh, lds, a, nx_);     \
+        process_group_pf<CH, GUARD, MODE>(hi, lo, OLD, NEW, m, lane8, sh, lds, a, nx_,      \
+                                          kFF00, mlo);                                    \
         _Pragma("unroll") for (int c = 0; c < CH; ++c) {                                  \
             if (m[c] == 0) notes[c] = note_group(notes[c], (GI));                         \
         }                                                                                 \
@@ -379,6 +400,13 @@ __global__ __launch_bounds__(THREADS) void fp_kernel(FpArgs a) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t lane8 = (threadIdx.x & 31) * 8;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // 0xff00 and the cut mask as VGPR operands (opaque to the compiler, which
+    // would otherwise fold them into SGPR / literal operands: see roll())
+    uint32_t kFF00 = 0xff00u, mlo = a.mask_lo;
+    if (VS_FP_BITOP3 && MODE == kFpFast53) {
+        asm volatile("v_mov_b32 %0, 0xff00" : "=v"(kFF00));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(mlo) : "s"(a.mask_lo));
+    }
     // bounds-checked strips: one per lane on wave 0 of workgroup 0
     if (blockIdx.x == 0 && wave == 0) {
         for (uint64_t e0 = 0; e0 < a.n_edge; e0 += 64) {
@@ -387,7 +415,7 @@ __global__ __launch_bounds__(THREADS) void fp_kernel(FpArgs a) {
             const uint64_t ee = v ? e : 0;
             const uint64_t kk[1] = {ee < a.k_lo ? ee : a.k_hi + (ee - a.k_lo)};
             const bool vv[1] = {v};
-            run_strips<1, true, MODE>(a, lds, lane8, kk, vv);
+            run_strips<1, true, MODE>(a, lds, lane8, kk, vv, kFF00, mlo);
         }
     }
     // interior strips: units of 64 * kChains strips, kChains per lane
@@ -405,17 +433,20 @@ __global__ __launch_bounds__(THREADS) void fp_kernel(FpArgs a) {
             vv[c] = k < a.k_hi;
             kk[c] = vv[c] ? k : k0;
         }
-        run_strips<kChains, false, MODE>(a, lds, lane8, kk, vv);
+        run_strips<kChains, false, MODE>(a, lds, lane8, kk, vv, kFF00, mlo);
     }
 }
 
 hipError_t launch_fingerprint(const FpArgs &a, bool wide, bool fast, int cus, hipStream_t s) {
+    const bool deg53 = fast && a.idx_shift == 13;
     const uint64_t units = (a.k_hi - a.k_lo + kUnit - 1) / kUnit;
     if (units == 0 && a.n_edge == 0) return hipSuccess;
     const uint64_t grid =
         std::max<uint64_t>(1, std::min<uint64_t>(units, (uint64_t)std::max(cus, 1)));
     if (wide)
         fp_kernel<kFpWide, kFpThreads><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
+    else if (deg53)
+        fp_kernel<kFpFast53, kFpThreads><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
     else if (fast)
         fp_kernel<kFpFast, kFpThreads><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
     else

@@ -263,6 +263,9 @@ struct ShaEngine {
     // with at least quad_frac_pct % of the longest chain's remaining blocks
     // (VSGPU_SHA_QUAD_PCT overrides; 0 disables, 100+ only the longest bucket)
     uint32_t quad_pct = 80;
+    // persistent-grid cap (VS_OPT_SHA_GRID_PER_CU): split mode workgroups per
+    // CU (default 5, the LDS limit), throughput mode waves per SIMD (default 3)
+    uint32_t grid_per_cu = 0;
     uint32_t *hist_h = nullptr;  // pinned: the drain's bucket histogram
     int launch(uint32_t budget, int mode, hipStream_t s);
     void release();

@@ -823,12 +823,14 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
     if (kb) VS_HIP(hipEventRecord(ka, s));
     if (mode == kShaWide) {
         // persistent grid: 3 waves per SIMD (launch bounds: <= 168 VGPRs)
-        const uint64_t slots = (uint64_t)std::max(cus, 1) * 4 * 3 / kWideWaves;
+        const uint64_t slots =
+            std::max<uint64_t>((uint64_t)std::max(cus, 1) * 4 * (grid_per_cu ? grid_per_cu : 3) / kWideWaves, 1);
         const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWideWaves - 1) / kWideWaves, slots);
         sha_slice_wide_kernel<<<grid, 64 * kWideWaves, 0, s>>>(a);
     } else {
         // persistent grid: LDS (32 KiB per workgroup) admits 5 workgroups per CU
-        const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)std::max(cus, 1) * 5);
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(
+            tiles, (uint64_t)std::max(cus, 1) * (grid_per_cu ? grid_per_cu : 5));
         sha_slice_kernel<<<grid, 128, 0, s>>>(a);
     }
     if (kb) {
