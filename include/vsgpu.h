@@ -304,8 +304,9 @@ int vs_rsync_timing(vs_rsync *h, double ms_out[5]);
  * block contributions on the device plus one serial scramble chain on a host
  * thread; MD5 and XXH64 -- serial chains with no parallel
  * form -- are hashed on a library host thread from the file's bytes read back
- * through the same pinned ring.  Any length.  Blocks until done; jobs other
- * calls left in flight stay in flight (their _wait order is unchanged). */
+ * through the same pinned ring.  Any length.  Blocks until done.  It runs on
+ * a job of its own: jobs other calls left in flight stay in flight, keep their
+ * _wait order and do not limit it (nor does it count toward their 4). */
 int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_type,
                       uint8_t out[16]);
 /* The same, asynchronous: _start queues the device part (after work queued on
@@ -313,7 +314,8 @@ int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_ty
  * runs on a library thread while the caller goes on (e.g. with the match walk
  * over the same file).  dev_src must stay valid and unchanged until its _wait.
  * Up to 4 jobs (whole files or block ranges) may be in flight per handle,
- * each with its own host thread and 3 pieces of device memory: _wait returns
+ * each with its own host thread and (XXH3 only) 3 pieces of device memory
+ * for its contribution rows: _wait returns
  * the OLDEST job's digest (jobs complete in start order; the _blocks_ form
  * shares the queue). */
 int vs_rsync_file_sum_start(vs_rsync *h, const void *dev_src, int64_t len, int csum_type);

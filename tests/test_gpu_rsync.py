@@ -587,8 +587,11 @@ def test_c4_real_density_window_exact(gpu):
     assert (ds[:4096].cpu().numpy() == host[data_lo - win_lo:data_lo - win_lo + 4096]).all()
     m.load_sums_device(cnt, bl, s2l, rem, s1.data_ptr(), s2.data_ptr(), csum, seed)
     assert len(want) > 14000 and fa > 50000   # the density this test is for
-    # the rank's speculative walk + the stitch from the true entry, then the
-    # streamed form's walk from the true entry directly (has_entry)
+    # the rank's speculative walk + the stitch from the true entry.  (The
+    # streamed form's walk from a piece's true entry -- match_scan's has_entry
+    # path -- is covered at the 64 GiB table density by
+    # tests/test_gpu_rsync_stream.py's 3 GiB C4-plan files; no public entry
+    # point starts a streamed walk in mid-file, as this window would need.)
     m.match_scan(ds.data_ptr(), n, data_lo, plan.total, lo, hi)
     gexit = m.match_stitch(e, w)
     nm = m.match_finish()
@@ -724,6 +727,17 @@ def test_file_sum_jobs_fifo(gpu):
         assert m.file_sum_wait() == _file_sum_want(files[k].tobytes(), 8), k
     with pytest.raises(VsError):
         m.file_sum_wait()
+    # the blocking form has a job of its own, so with three jobs
+    # in flight it can be called again and again (it used to take the 4th
+    # FIFO slot until the older jobs were waited for)
+    for k in range(3):
+        m.file_sum_start(devs[k].data_ptr(), len(files[k]), 8)
+    for csum in (6, 5, 8, 7):
+        assert m.file_sum(devs[3].data_ptr(), len(files[3]), csum) == \
+            _file_sum_want(files[3].tobytes(), csum)
+    m.file_sum_start(devs[3].data_ptr(), len(files[3]), 8)   # the 4th slot is still free
+    for k in range(4):
+        assert m.file_sum_wait() == _file_sum_want(files[k].tobytes(), 8), k
     m.close()
 
 

@@ -191,3 +191,61 @@ def test_file_sum_relay_gloo(world, args):
     want = xxhash.xxh3_128_intdigest(data.tobytes()).to_bytes(16, "little").hex()
     assert res[-1]["r"] == [want] * files
     assert sum(r["nb"] for r in res) == (n - 1) // 1024
+
+
+def test_file_sum_relay_refuses_short_blocks():
+    """with blength < 1024 a rank's last whole 1 KiB block can end
+    past the bytes it holds (own_hi + blength - 1); the relay refuses such a
+    split instead of reading past the rank's buffer."""
+    from volsync_amd.rsync_shard import FileSumRelay, SourceShard
+    n = 3 * (1024 * 100 + 1)          # own_hi of rank 0 = 1024 * 100 + 1: rounds up by 1023
+    bl, _, _, _ = O.rsync_sizes(n)
+    assert bl == 700
+    spec = SourceShard.for_rank(n, bl, 3, 0)
+    with pytest.raises(ValueError, match="beyond its data"):
+        FileSumRelay(None, spec, 0, spec.data_lo, None, None, None,
+                     init=R.xxh3_acc_init, finish=lambda *a: b"")
+    # C4's blength (131072) and any blength >= 1024 always fit
+    for world in (2, 3, 8):
+        for r in range(world):
+            sp = SourceShard.for_rank(n * 7, 1024, world, r)
+            fs = FileSumRelay(OracleChain(np.zeros(1, np.uint8), 0), sp, 0, sp.data_lo,
+                              None, None, None, init=R.xxh3_acc_init, finish=lambda *a: b"")
+            fs.close()
+
+
+@pytest.mark.timeout(60)
+def test_file_sum_relay_poison_propagates():
+    """a rank whose chain fails hands a poison state on, so every
+    later rank's relay reports RelayAborted instead of waiting forever in
+    recv(); the ranks before it are unaffected."""
+    import queue
+    from volsync_amd.rsync_shard import FileSumRelay, RelayAborted, SourceShard
+
+    class Broken(OracleChain):
+        def file_sum_blocks_start(self, addr, nblocks, acc):
+            raise IOError("device lost")
+
+    n, bl, world = 3 << 20, 65536, 3
+    data = O.synth(59, 0, n)
+    qs = [queue.Queue() for _ in range(world)]
+    relays = []
+    for r in range(world):
+        sp = SourceShard.for_rank(n, bl, world, r)
+        win = data[sp.data_lo:sp.data_hi].copy()
+        fsm = (Broken if r == 1 else OracleChain)(win, sp.data_lo)
+        relays.append(FileSumRelay(
+            fsm, sp, sp.data_lo, sp.data_lo,
+            send=(lambda acc, r=r: qs[r].put(acc)),
+            recv=(lambda r=r: qs[r - 1].get(timeout=30)),
+            last=lambda win=win: win[len(win) - 1088:].tobytes(),
+            init=R.xxh3_acc_init, finish=lambda acc, last, ln, cs: b"x"))
+    for fs in relays:
+        fs.submit()
+    assert len(relays[0].results()) == 1
+    with pytest.raises(IOError, match="device lost"):
+        relays[1].results()
+    with pytest.raises(RelayAborted):
+        relays[2].results()
+    for fs in relays:
+        fs.close()

@@ -77,7 +77,7 @@ struct FsJob {
     DevBuf dC;                            // device ring of contribution rows
     const uint8_t *src = nullptr;
     std::thread th;
-    bool active = false, whole = false, serial = false, consumed = false;
+    bool active = false, whole = false, serial = false;
     int device = 0, csum = 0, rc = 0;
     std::string err;
     uint64_t len = 0, nb = 0;
@@ -192,6 +192,7 @@ struct vs_rsync {
     static constexpr uint32_t kFsJobs = 4;
     FsJob fs[kFsJobs];
     uint32_t fs_head = 0, fs_tail = 0;   // jobs [head, tail) are in flight
+    FsJob fs_sync;                       // the blocking vs_rsync_file_sum's own job
     double fs_dev_ms = 0, fs_host_ms = 0; // the last job waited for
     DevBuf rc_pieces;               // receiver reconstruction
     // scan
@@ -1412,7 +1413,7 @@ int fs_setup(FsJob &j, int device) {
 }
 
 // the job's rings, sized for its piece length (kept across jobs)
-int fs_rings(FsJob &j, uint64_t piece) {
+int fs_rings(FsJob &j, uint64_t piece, bool serial) {
     if (piece != j.piece || !j.hC[0]) {
         for (auto &p : j.hC) pinned_free(p), p = nullptr;
         j.piece = piece;
@@ -1420,6 +1421,9 @@ int fs_rings(FsJob &j, uint64_t piece) {
             if (!(p = (uint8_t *)pinned_alloc(j.piece * 64)))
                 return fail(VS_ERR_NOMEM, "pinned file-sum ring");
     }
+    // MD5 / XXH64 (and XXH3 of <= 240 bytes) read the source bytes back
+    // through the pinned ring only: no device contribution rows
+    if (serial) return 0;
     return j.dC.ensure((size_t)FsJob::kRing * j.piece * 64);
 }
 
@@ -1466,24 +1470,19 @@ void fs_account(vs_rsync *h, const FsJob &j) {
     h->fs_host_ms = j.host_ms;
 }
 
-// jobs whose result a blocking vs_rsync_file_sum already took leave the FIFO
-// once everything older has been waited for
-void fs_pop_consumed(vs_rsync *h) {
-    while (h->fs_head != h->fs_tail && h->fs[h->fs_head % vs_rsync::kFsJobs].consumed) {
-        h->fs[h->fs_head % vs_rsync::kFsJobs].consumed = false;
-        h->fs_head++;
-    }
-}
-
 // whole: the digest of the file p[0, len); else the accumulators after the
-// whole blocks p[0, len) (len a multiple of 1024) chained from acc_in
+// whole blocks p[0, len) (len a multiple of 1024) chained from acc_in.  The
+// job is the FIFO's next slot, or sync (the blocking form's own job, outside
+// the FIFO, so it neither waits for nor counts against the jobs in flight).
 int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
-             const uint64_t *acc_in) {
-    if (h->fs_tail - h->fs_head == vs_rsync::kFsJobs)
+             const uint64_t *acc_in, FsJob *sync = nullptr) {
+    if (!sync && h->fs_tail - h->fs_head == vs_rsync::kFsJobs)
         return fail(VS_ERR_STATE, "4 whole-file checksums in flight: wait for one first");
-    FsJob &j = h->fs[h->fs_tail % vs_rsync::kFsJobs];
+    FsJob &j = sync ? *sync : h->fs[h->fs_tail % vs_rsync::kFsJobs];
+    const bool xxh3 = csum == VS_CSUM_XXH3_64 || csum == VS_CSUM_XXH3_128;
+    const bool serial = whole && (!xxh3 || len <= 240);
     VS_TRY(fs_setup(j, h->device));
-    VS_TRY(fs_rings(j, h->fs_piece ? h->fs_piece : (1ull << 18)));
+    VS_TRY(fs_rings(j, h->fs_piece ? h->fs_piece : (1ull << 18), serial));
     j.whole = whole;
     j.csum = csum;
     j.len = len;
@@ -1491,9 +1490,7 @@ int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
     j.rc = 0;
     j.err.clear();
     j.host_ms = j.dev_ms = 0;
-    j.consumed = false;
-    const bool xxh3 = csum == VS_CSUM_XXH3_64 || csum == VS_CSUM_XXH3_128;
-    j.serial = whole && (!xxh3 || len <= 240);
+    j.serial = serial;
     // after the caller's null-stream work and this handle's queued work
     VS_HIP(hipEventRecord(j.ev_in, h->stream));
     VS_HIP(hipStreamWaitEvent(j.s, j.ev_in, 0));
@@ -1517,7 +1514,7 @@ int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
         serial_sum_final(ss, j.digest);
     }
     j.active = true;
-    h->fs_tail++;
+    if (!sync) h->fs_tail++;
     return 0;
 }
 
@@ -1654,6 +1651,8 @@ int ms_error(MatchStream *m) {
     return 0;
 }
 
+int ms_build(vs_rsync *h, MatchStream *m, int64_t flen, int fcsum, uint64_t piece, uint32_t ring);
+
 int ms_begin(vs_rsync *h, int64_t flen, int fcsum, uint64_t piece, uint32_t ring) {
     if (!h->loaded) return fail(VS_ERR_STATE, "vs_rsync_match_begin before vs_rsync_load_sums");
     if (flen < 0) return fail(VS_ERR_ARG, "negative file length");
@@ -1664,8 +1663,15 @@ int ms_begin(vs_rsync *h, int64_t flen, int fcsum, uint64_t piece, uint32_t ring
         return fail(VS_ERR_ARG, "piece must be >= 1 MiB and a multiple of 1024, ring 2..8");
     VS_TRY(rs_dev(h));
     ms_release(h);
-    MatchStream *m = new MatchStream();
-    h->mst = m;
+    h->mst = new MatchStream();
+    // a stream that fails to come up is released whole: no
+    // half-built ring without its walk thread is left behind for _feed/_next
+    const int rc = ms_build(h, h->mst, flen, fcsum, piece, ring);
+    if (rc < 0) ms_release(h);
+    return rc;
+}
+
+int ms_build(vs_rsync *h, MatchStream *m, int64_t flen, int fcsum, uint64_t piece, uint32_t ring) {
     m->flen = flen;
     m->halo = h->blength - 1;
     // a piece never shorter than the walk's halo; small files get one slot's worth
@@ -1691,7 +1697,13 @@ int ms_begin(vs_rsync *h, int64_t flen, int fcsum, uint64_t piece, uint32_t ring
     h->matches.clear();
     h->st_cand = h->st_fa = h->st_hashed = 0;
     h->st_rounds = 0;
-    if (m->np) m->th = std::thread(ms_worker, h, m);
+    if (m->np) {
+        try {
+            m->th = std::thread(ms_worker, h, m);
+        } catch (const std::exception &e) {
+            return fail(VS_ERR_NOMEM, std::string("streamed match walk thread: ") + e.what());
+        }
+    }
     return 0;
 }
 
@@ -1827,6 +1839,9 @@ void ss_release(vs_rsync *h) {
     h->sst = nullptr;
 }
 
+int ss_build(SigStream *s, int64_t len, int32_t blength, int32_t s2length, int csum, uint32_t seed,
+             uint64_t piece, uint32_t ring, int64_t count);
+
 int ss_begin(vs_rsync *h, int64_t len, int32_t blength, int32_t s2length, int csum, uint32_t seed,
              uint64_t piece, uint32_t ring) {
     VS_TRY(check_csum(csum));
@@ -1839,8 +1854,14 @@ int ss_begin(vs_rsync *h, int64_t len, int32_t blength, int32_t s2length, int cs
     if (count > INT32_MAX) return fail(VS_ERR_ARG, "block count overflows int32");
     VS_TRY(rs_dev(h));
     ss_release(h);
-    SigStream *s = new SigStream();
-    h->sst = s;
+    h->sst = new SigStream();
+    const int rc = ss_build(h->sst, len, blength, s2length, csum, seed, piece, ring, count);
+    if (rc < 0) ss_release(h);   // as ms_begin: nothing half-built stays on the handle
+    return rc;
+}
+
+int ss_build(SigStream *s, int64_t len, int32_t blength, int32_t s2length, int csum, uint32_t seed,
+             uint64_t piece, uint32_t ring, int64_t count) {
     s->len = len;
     s->blength = blength;
     s->s2length = s2length;
@@ -2000,6 +2021,7 @@ VS_API void vs_rsync_close(vs_rsync *h) {
     ms_release(h);
     ss_release(h);
     for (FsJob &j : h->fs) fs_release(j);
+    fs_release(h->fs_sync);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (DevBuf *b : {&h->d_sum1, &h->d_keys, &h->d_tkey, &h->d_dir, &h->d_filt, &h->d_tmp, &h->d_bkt, &h->px,
                       &h->pt, &h->pxs, &h->pts, &h->partials, &h->c_off, &h->c_sum, &h->c_off2,
@@ -2169,24 +2191,27 @@ VS_API int vs_rsync_file_sum_wait(vs_rsync *h, uint8_t out[16]) {
     h->fs_head++;
     const int rc = fs_finish(j);   // joins the job's thread, syncs its stream
     j.active = false;
-    fs_pop_consumed(h);
     VS_TRY(rc);
     fs_account(h, j);
     fs_digest(j, out);
     return 0;
 }
 
-// the blocking form waits for its own job only: jobs the caller already has in
-// flight keep their FIFO order (the slot is skipped when they are waited for)
+// the blocking form runs on its own job and waits for it only: jobs the
+// caller already has in flight keep their FIFO order and their count
 VS_API int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_type,
                              uint8_t out[16]) {
     if (!out) return fail(VS_ERR_ARG, "bad arguments");
-    VS_TRY(vs_rsync_file_sum_start(h, dev_src, len, csum_type));
-    FsJob &j = h->fs[(h->fs_tail - 1) % vs_rsync::kFsJobs];
+    if (!h || len < 0 || (len && !dev_src)) return fail(VS_ERR_ARG, "bad arguments");
+    if (csum_type != VS_CSUM_MD5 && csum_type != VS_CSUM_XXH64 && csum_type != VS_CSUM_XXH3_64 &&
+        csum_type != VS_CSUM_XXH3_128)
+        return fail(VS_ERR_ARG, "unsupported checksum type");
+    VS_TRY(rs_dev(h));
+    VS_TRY(order_after_null(h));
+    FsJob &j = h->fs_sync;
+    VS_TRY(fs_start(h, (const uint8_t *)dev_src, (uint64_t)len, csum_type, true, nullptr, &j));
     const int rc = fs_finish(j);
     j.active = false;
-    j.consumed = true;
-    fs_pop_consumed(h);
     VS_TRY(rc);
     fs_account(h, j);
     fs_digest(j, out);
@@ -2211,7 +2236,6 @@ VS_API int vs_rsync_file_sum_blocks_wait(vs_rsync *h, uint64_t acc_out[8]) {
     h->fs_head++;
     const int rc = fs_finish(j);   // joins the job's thread, syncs its stream
     j.active = false;
-    fs_pop_consumed(h);
     VS_TRY(rc);
     fs_account(h, j);
     memcpy(acc_out, j.acc, 64);

@@ -240,7 +240,7 @@ __device__ __forceinline__ void acc16(const uint4 v, uint64_t k0s, uint64_t k1s,
     } while (0)
 #endif
 
-// Optional per-wave phase timing (a.prof != nullptr; VSGPU_WALK_PROF=1):
+// Optional per-wave phase timing (a.prof != nullptr, set in profiling builds):
 // s_memtime cycles and counts per phase, summed into a.prof[wave * 16 + ...]
 enum : int {
     kPrRun = 0, kPrStep = 1, kPrFlush = 2, kPrChain = 3, kPrSeg = 4,
@@ -250,10 +250,11 @@ enum : int {
     kPrStepSums = 8, kPrStepLds = 9, kPrStepGather = 10, kPrStepProbe = 11, kPrStepQueue = 12,
     kPrN = 16
 };
-// The counters live in scalar registers; compiled in only with VS_WALK_PROF
-// (tools/build_variant.sh walkprof -DVS_WALK_PROF=1, run with VSGPU_LIB=...
-// and VSGPU_WALK_PROF=1): 16 phases x two u64 otherwise spill SGPRs into VGPR
-// lanes all over the production kernel.
+// The counters live in scalar registers; compiled in only with the build
+// flag VS_WALK_PROF (tools/build_variant.sh walkprof -DVS_WALK_PROF=1; that
+// library, selected by VSGPU_LIB=..., profiles every walk -- the library reads
+// no environment variable): 16 phases x two u64 otherwise spill SGPRs into
+// VGPR lanes all over the production kernel.
 #ifdef VS_WALK_PROF
 struct WProf {
     bool on;

@@ -204,6 +204,10 @@ def run_walk_shards_local(handles: Sequence, specs: Sequence[SourceShard], ptrs:
 # independent, so a relay thread per rank runs file k's chain while its
 # successor runs file k-1's: a systolic pipeline whose rate is one rank's
 # chain per file, with a fill latency of world - 1 chains.
+class RelayAborted(RuntimeError):
+    """An earlier rank of the file-sum relay failed (it sent the poison state)."""
+
+
 class FileSumRelay:
     """One rank's relay thread.  fsm: a Matcher (or a test double with
     file_sum_blocks_start / _wait); ptr: address of file offset data_lo in
@@ -212,7 +216,11 @@ class FileSumRelay:
     from the initial state); last(): the file's last min(len, 1088) bytes
     (the last rank only).  submit() queues one file, results() waits for all
     queued files and returns the last rank's digests (others: the states
-    they handed on)."""
+    they handed on).
+
+    Failure: a rank whose chain raises hands send(None) on -- a poison state
+    -- so every later rank's recv() returns None and its relay raises
+    RelayAborted instead of blocking for a state that never comes."""
 
     def __init__(self, fsm, spec: SourceShard, ptr: int, data_lo: int, send, recv, last,
                  csum: int = 8, init=None, finish=None):
@@ -223,6 +231,15 @@ class FileSumRelay:
         self.b_hi = min(-(-spec.own_hi // 1024), nb_file)
         if spec.rank == spec.world - 1:
             self.b_hi = nb_file
+        # the rank chains bytes [b_lo * 1024, b_hi * 1024), which must lie in
+        # the bytes it holds: own_hi rounds up to a 1 KiB block by at most
+        # 1023 bytes, and the halo is blength - 1 (so blength >= 1024 always
+        # suffices; sum_sizes_sqroot gives 700 only for files <= 490000 bytes)
+        if self.b_lo < self.b_hi and (self.b_lo * 1024 < spec.data_lo
+                                      or self.b_hi * 1024 > spec.data_hi):
+            raise ValueError(f"FileSumRelay: rank {spec.rank} would chain bytes "
+                             f"[{self.b_lo * 1024}, {self.b_hi * 1024}) beyond its data "
+                             f"[{spec.data_lo}, {spec.data_hi}) (blength {spec.blength} < 1024)")
         self.spec, self.fsm, self.csum = spec, fsm, csum
         self.addr = ptr + self.b_lo * 1024 - data_lo
         self.send, self.recv, self.last = send, recv, last
@@ -244,9 +261,11 @@ class FileSumRelay:
             job = self._q.get()
             if job is None:
                 return
+            spec = self.spec
             try:
-                spec = self.spec
                 acc = self._init() if spec.rank == 0 else self.recv()
+                if acc is None:
+                    raise RelayAborted(f"rank {spec.rank - 1} aborted the relay")
                 self.fsm.file_sum_blocks_start(self.addr, self.nblocks, acc)
                 acc = self.fsm.file_sum_blocks_wait()
                 if spec.rank < spec.world - 1:
@@ -256,6 +275,11 @@ class FileSumRelay:
                     self._out.append(self._finish(acc, self.last(), spec.length, self.csum).hex())
             except Exception as e:  # reported by results()
                 self._err.append(e)
+                if spec.rank < spec.world - 1:
+                    try:
+                        self.send(None)   # poison: the later ranks fail, not hang
+                    except Exception as e2:  # the transport itself is gone
+                        self._err.append(e2)
             finally:
                 self._q.task_done()
 
@@ -277,18 +301,26 @@ class FileSumRelay:
 def torch_relay_p2p(rank: int, world: int, group=None):
     """(send, recv) of the 8 accumulators to the next / from the previous rank
     over torch.distributed point-to-point on CPU tensors (a gloo group of its
-    own: the relay thread runs beside the main thread's collectives)."""
+    own: the relay thread runs beside the main thread's collectives).  A
+    message is 9 int64: a flag (0 = state, 1 = poison) and the accumulators;
+    send(None) sends the poison and recv() returns None for it."""
     import numpy as np
     import torch
     import torch.distributed as dist
 
     def send(acc):
-        t = torch.from_numpy(np.ascontiguousarray(acc, np.uint64).view(np.int64).copy())
+        t = torch.zeros(9, dtype=torch.int64)
+        if acc is None:
+            t[0] = 1
+        else:
+            t[1:] = torch.from_numpy(np.ascontiguousarray(acc, np.uint64).view(np.int64).copy())
         dist.send(t, dst=rank + 1, group=group)
 
     def recv():
-        t = torch.zeros(8, dtype=torch.int64)
+        t = torch.zeros(9, dtype=torch.int64)
         dist.recv(t, src=rank - 1, group=group)
-        return t.numpy().view(np.uint64).copy()
+        if int(t[0]):
+            return None
+        return t[1:].numpy().view(np.uint64).copy()
 
     return send, recv
