@@ -571,6 +571,20 @@ def smallfiles_cpu_baseline(sizes, sample_files: int, threads: int):
             "cpu": _cpu_model(), "nproc": os.cpu_count()}
 
 
+def c5_layout(files: int, rank: int = 0):
+    """C5's file population: `files` files of 4-64 KiB drawn
+    from files // 2 distinct payloads (seed 6 + rank).  Payload j is bytes
+    [j * 64 KiB, j * 64 KiB + psize[j]) of the synthetic stream seed 6, and
+    file i is payload pick[i] whole, so a file's content -- and blob ID --
+    depends on pick[i] alone.  -> (sizes, pick, psize, npay)"""
+    import numpy as np
+    npay = max(1, files // 2)
+    rng = np.random.default_rng(6 + rank)
+    psize = rng.integers(4096, 65537, npay)
+    pick = rng.integers(0, npay, files)
+    return psize[pick], pick, psize, npay
+
+
 def smallfiles_main(args):
     """C5: 1 M files of 4-64 KiB (seed 6) drawn from 500 K distinct payloads
     (dedup-heavy), packed contiguously in HBM with an offsets array.  Every file
@@ -585,11 +599,8 @@ def smallfiles_main(args):
     from volsync_amd import DeviceSha256, synth_fill_device
 
     world, rank, local, dev = dist_setup()
-    nf, npay = args.files, max(1, args.files // 2)
-    rng = np.random.default_rng(6 + rank)
-    psize = rng.integers(4096, 65537, npay)
-    pick = rng.integers(0, npay, nf)
-    sizes = psize[pick]
+    nf = args.files
+    sizes, pick, psize, npay = c5_layout(nf, rank)
     offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
     total = int(sizes.sum())
     # payload j = synthetic stream (seed 6) at j * 64 KiB; files gathered into
@@ -620,10 +631,30 @@ def smallfiles_main(args):
     sh.set_wide(args.hash_wide, args.wide_drain)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
+    # the repository's index (restic SaveBlob: a blob the master index holds
+    # is not stored again; a scheduled backup re-runs `restic backup` into an
+    # initialised repository, /root/reference/mover-restic/entry.sh:43-65):
+    # the previous backup held payloads [0, npay / 2) -- their IDs, found in
+    # this batch -- and other blobs, 432 K IDs in all, sorted once per backup
+    # (untimed), as LoadIndex builds the master index once
+    sh.run(packed.data_ptr(), ofd.data_ptr(), lens.data_ptr(), nf, ids.data_ptr(), stream)
+    torch.cuda.synchronize(dev)
+    _, rep = np.unique(pick, return_index=True)
+    old_ids = ids[torch.from_numpy(rep[pick[rep] < npay // 2]).to(dev)]
+    n_known = max(args.known_ids, len(old_ids))
+    other = torch.from_numpy(np.random.default_rng(99).integers(
+        0, 256, (n_known - len(old_ids), 32), dtype=np.uint8)).to(dev)
+    known = torch.cat([old_ids, other]).contiguous()
+    sh.index_sort(known.data_ptr(), n_known, stream)
+    torch.cuda.synchronize(dev)
+
     def step():
         sh.run(packed.data_ptr(), ofd.data_ptr(), lens.data_ptr(), nf, ids.data_ptr(), stream)
-        # SaveBlob's dedup on the device (vs_blob_dedup): first occurrence per ID
-        return sh.dedup(ids.data_ptr(), nf, first.data_ptr(), stream)
+        # SaveBlob's dedup on the device (vs_blob_dedup_known): per blob, known
+        # to the index or its first occurrence in the batch; the count of the
+        # new distinct IDs (the blobs this backup stores)
+        return sh.dedup_known(ids.data_ptr(), nf, known.data_ptr(), n_known, first.data_ptr(),
+                              stream)
 
     for _ in range(args.warmup):
         step()
@@ -656,6 +687,25 @@ def smallfiles_main(args):
     # (the dedup included: an upper bound on the hash time)
     k_ms = ev0.elapsed_time(ev1) / args.steps
     gbs = total / k_ms / 1e6
+    # the dedup alone (after the timed region): against the index, and the
+    # batch-only form (vs_blob_dedup) with its distinct-ID count
+    dd = {}
+    for name, fn in (("known", lambda: sh.dedup_known(ids.data_ptr(), nf, known.data_ptr(),
+                                                      n_known, first.data_ptr(), stream, False)),
+                     ("batch", lambda: sh.dedup(ids.data_ptr(), nf, first.data_ptr(), stream,
+                                                False))):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            fn()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        dd[name] = e0.elapsed_time(e1) / 5
+    distinct = sh.dedup(ids.data_ptr(), nf, first.data_ptr(), stream)
+    # exactness: SHA-256 over all blob IDs in file order (tests/golden/
+    # make_golden_full.py c5), and the distinct count
+    import hashlib
+    id_digest = hashlib.sha256(ids.cpu().numpy().tobytes()).hexdigest()
     if rank == 0:
         out = {
             "metric": "GB/s SHA-256 blob IDs (restic, C5 small files)",
@@ -666,8 +716,14 @@ def smallfiles_main(args):
             "data": "synthetic (splitmix64 payloads, device-resident, packed)",
             "config": {"workload": f"C5: {nf} files of 4-64 KiB from {npay} payloads"
                                    f"{' per rank' if world > 1 else ''}",
-                       "bytes": total, "unique_ids": uniq,
+                       "bytes": total, "unique_ids": distinct,
                        "parallelism": f"replicas x{world}"},
+            "dedup": {"form": "vs_blob_dedup_known inside the step (SaveBlob against the index)",
+                      "known_index_ids": n_known, "known_from_batch": len(old_ids),
+                      "new_unique_ids": uniq, "batch_unique_ids": distinct,
+                      "dedup_known_ms": round(dd["known"], 3),
+                      "dedup_batch_only_ms": round(dd["batch"], 3)},
+            "exact": {"files": nf, "unique_ids": distinct, "id_digest": id_digest},
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                          "valu_frac": round(gbs * SHA_OPS_PER_BYTE / 1e3 / VALU_PEAK_TOPS, 4),
@@ -675,6 +731,10 @@ def smallfiles_main(args):
                          "kernel": "sha256 (hash engine, unbounded slice)"},
             "hash_wide": args.hash_wide,
         }
+        g = _goldens().get("c5", {}).get(str(nf))
+        if g and world == 1:
+            out["exact"]["golden_match"] = (g["unique_ids"], g["id_digest"], g["bytes"]) == \
+                (distinct, id_digest, total)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = smallfiles_cpu_baseline(sizes, 200000, args.cpu_threads)
         print(json.dumps(out), flush=True)
@@ -1242,6 +1302,8 @@ def main():
     ap.add_argument("--read-mib", type=int, default=64,
                     help="rsync-host: bytes per feed (the reader's read size)")
     ap.add_argument("--files", type=int, default=1_000_000, help="smallfiles: files per GPU")
+    ap.add_argument("--known-ids", type=int, default=432_000,
+                    help="smallfiles: IDs in the repository's index the dedup checks against")
     ap.add_argument("--share", default=None, metavar="R/N",
                     help="run rank R's share of the N-rank problem on this one GPU; rsync: "
                          "the full table, its D blocks and S range (3/8 with --per-gpu-gib 32 "

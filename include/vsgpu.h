@@ -192,6 +192,22 @@ void vs_sha256_close(vs_sha *h);
  * default stream); scratch lives in the vs_sha handle. */
 int vs_blob_dedup(vs_sha *h, const uint8_t *dev_ids, size_t n, uint32_t *dev_first,
                   uint64_t *n_unique, void *hip_stream);
+/* The same against the repository's index as well (restic v0.13.1
+ * Repository.SaveBlob: known = !idx.AddPending(BlobHandle{id, t}) -- a blob
+ * the master index already holds is not stored again; a scheduled backup
+ * re-runs `restic backup` into an initialised repository,
+ * /root/reference/mover-restic/entry.sh:43-65, so most IDs are known):
+ * dev_known holds n_known 32-byte IDs of one blob type, prepared once per
+ * backup by vs_blob_index_sort.  dev_first[i] = VS_DEDUP_KNOWN when ID i is
+ * in the index, else as vs_blob_dedup; *n_new (optional; waits) = the
+ * distinct IDs the index does not hold, i.e. the blobs SaveBlob stores. */
+#define VS_DEDUP_KNOWN 0xffffffffu
+int vs_blob_dedup_known(vs_sha *h, const uint8_t *dev_ids, size_t n, const uint8_t *dev_known,
+                        size_t n_known, uint32_t *dev_first, uint64_t *n_new, void *hip_stream);
+/* Sorts n device-resident 32-byte IDs in place into the order
+ * vs_blob_dedup_known searches (by the first 8 bytes, big-endian).  Queued on
+ * hip_stream; scratch lives in the handle. */
+int vs_blob_index_sort(vs_sha *h, uint8_t *dev_known, size_t n, void *hip_stream);
 /* syncthing's scanner (lib/scanner; SURVEY.md 8(f)4, mover-syncthing/entry.sh:
  * 130-135): SHA-256 of every block_size block of a device buffer of len bytes
  * (the last block short), n = ceil(len / block_size) digests into dev_out.

@@ -121,7 +121,7 @@ static void chunker_reset_state(ref_chunker *c) {
 static uint64_t read_full(ref_chunker *c, uint8_t *dst, uint64_t cap) {
     uint64_t n = c->src_len - c->src_off;
     if (n > cap) n = cap;
-    memcpy(dst, c->src + c->src_off, n);
+    if (n) memcpy(dst, c->src + c->src_off, n);   /* an empty source may be NULL */
     c->src_off += n;
     return n;
 }
@@ -284,7 +284,7 @@ void ref_sha256(const uint8_t *data, uint64_t len, uint8_t out[32]) {
     uint8_t tail[128];
     uint64_t rem = len - 64 * full;
     memset(tail, 0, sizeof tail);
-    memcpy(tail, data + 64 * full, rem);
+    if (rem) memcpy(tail, data + 64 * full, rem);   /* len 0: data may be NULL */
     tail[rem] = 0x80;
     uint64_t tl = (rem < 56) ? 64 : 128;
     uint64_t bits = len * 8;

@@ -26,7 +26,10 @@ the false alarms before the merge are the speculative record's `fab`), else
 the range is re-walked whole.  256 GiB also gets the 8-rank split of the real
 C4 (SourceShard), per rank: its own matches, false alarms and true entry.
 
-usage: python tests/golden/make_golden_full.py [cdc|c3|rsync|filesum|all] [--threads T]
+C5 (bench.py --mode smallfiles): the digest of all 1 M blob IDs in file order,
+the distinct-ID count and the bytes.
+
+usage: python tests/golden/make_golden_full.py [cdc|c3|rsync|filesum|c5|all] [--threads T]
        [--rsync-gib G ...] [--skip-c3]
 writes tests/golden/full_configs.json (merged with what is there).
 """
@@ -267,9 +270,31 @@ def file_sum_golden(dlen: int, threads: int) -> str:
     return h.intdigest().to_bytes(16, "little").hex()
 
 
+def c5_golden(files: int, threads: int) -> dict:
+    """C5 (bench.py --mode smallfiles, c5_layout): SHA-256 over the 32-byte
+    blob IDs of all files in file order, the number of distinct IDs and the
+    file bytes.  A file's content is its payload, so each distinct payload is
+    hashed once (hashlib / OpenSSL, `threads` threads) from the C oracle's
+    synthetic stream."""
+    import bench
+    sizes, pick, psize, npay = bench.c5_layout(files, 0)
+    used = np.unique(pick)
+    ids = np.zeros((npay, 32), np.uint8)
+
+    def one(j):
+        ids[j] = np.frombuffer(hashlib.sha256(O.synth(6, int(j) << 16, int(psize[j])).tobytes())
+                               .digest(), np.uint8)
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(one, used.tolist()))
+    d = digest(ids[pick])
+    return {"files": files, "bytes": int(sizes.sum()), "unique_ids": int(len(used)),
+            "id_digest": d, "payloads": npay}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="?", default="all", choices=["cdc", "c3", "rsync", "filesum", "all"])
+    ap.add_argument("what", nargs="?", default="all",
+                    choices=["cdc", "c3", "rsync", "filesum", "c5", "all"])
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     ap.add_argument("--rsync-gib", type=int, nargs="*", default=[8, 16, 64, 128, 256])
     ap.add_argument("--skip-c3", action="store_true", help="cdc: keep the 1 TiB entries")
@@ -306,6 +331,10 @@ def main():
             ent["file_sum"] = file_sum_golden(g * GiB, a.threads)
             print(f"file sum of the {g} GiB C4 source in {time.time() - t0:.0f} s", flush=True)
             json.dump(data, open(OUT, "w"), indent=1)
+    if a.what in ("c5", "all"):
+        t0 = time.time()
+        data.setdefault("c5", {})["1000000"] = c5_golden(1_000_000, a.threads)
+        print(f"C5 IDs in {time.time() - t0:.0f} s", flush=True)
     json.dump(data, open(OUT, "w"), indent=1)
 
 

@@ -9,7 +9,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-ORACLE_SO = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+# VSGPU_ORACLE_LIB: the sanitizer build of the oracle (tools/asan_build.sh)
+ORACLE_SO = os.environ.get("VSGPU_ORACLE_LIB") or os.path.join(ORACLE_DIR, "build", "liboracle.so")
 
 _lib = None
 

@@ -81,3 +81,16 @@ def test_rsync_entries_consistent(gold):
     for g in (8, 16, 64, 128, 256):
         e = rs[str(g * GiB)]
         assert e["dlen"] == g * GiB and len(e["digest"]) == 64 and len(e["file_sum"]) == 32
+
+
+def test_c5_entry_matches_layout(gold):
+    """The C5 golden (bench.py --mode smallfiles checks its line against it):
+    its byte count and distinct-ID count follow from bench.c5_layout -- one
+    distinct blob per distinct payload -- so the layout the digest was made
+    from is the one the bench runs."""
+    import bench
+    g = gold["c5"]["1000000"]
+    sizes, pick, psize, npay = bench.c5_layout(1_000_000, 0)
+    assert g["bytes"] == int(sizes.sum()) and g["payloads"] == npay
+    assert g["unique_ids"] == len(np.unique(pick))
+    assert len(g["id_digest"]) == 64

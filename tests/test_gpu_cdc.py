@@ -596,6 +596,56 @@ def test_blob_dedup_c5_size(gpu, n):
     sh.close()
 
 
+@pytest.mark.parametrize("n,known_frac", [(1_000_000, 0.5), (77_777, 0.0), (50_000, 1.0)])
+def test_blob_dedup_known_index(gpu, n, known_frac):
+    """SaveBlob against the repository's index (vs_blob_index_sort +
+    vs_blob_dedup_known; restic v0.13.1 Repository.SaveBlob skips a blob the
+    master index holds, /root/reference/mover-restic/entry.sh:43-65 re-runs
+    backups into an initialised repository): 1 M blob IDs from 500 K distinct
+    ones, half of the distinct IDs in a 'known' index padded with IDs the
+    batch never uses (some sharing a batch ID's first 8 bytes, the sort key);
+    every blob's mark (known, or its first occurrence) and the count of new
+    distinct IDs against a host set."""
+    import torch
+    from volsync_amd import DeviceSha256
+    from volsync_amd._lib import VS_DEDUP_KNOWN
+    rng = np.random.default_rng(13 + n)
+    distinct = rng.integers(0, 256, (n // 2, 32), dtype=np.uint8)
+    ids_h = distinct[rng.integers(0, len(distinct), n)]
+    nk = int(len(distinct) * known_frac)
+    extra = rng.integers(0, 256, (max(nk // 4, 1), 32), dtype=np.uint8)
+    extra[::3, :8] = distinct[: len(extra[::3]), :8]          # same prefix, other ID
+    known_h = np.concatenate([distinct[rng.permutation(len(distinct))[:nk]], extra])
+    known_h = known_h[rng.permutation(len(known_h))]
+    kset = {bytes(r) for r in known_h}
+    first_seen, want, new = {}, np.empty(n, np.int64), 0
+    for i, r in enumerate(ids_h):
+        b = bytes(r)
+        if b in kset:
+            want[i] = VS_DEDUP_KNOWN
+        else:
+            f = first_seen.setdefault(b, i)
+            want[i] = f
+            new += f == i
+    ids = torch.from_numpy(ids_h).cuda()
+    known = torch.from_numpy(known_h).cuda()
+    first = torch.zeros(n, dtype=torch.int32, device="cuda")
+    sh = DeviceSha256()
+    sh.index_sort(known.data_ptr(), len(known_h))
+    ks = known.cpu().numpy()
+    keys = ks[:, :8].copy().view(">u8").ravel()
+    assert (np.diff(keys.astype(np.uint64)) >= 0).all()            # sorted by prefix
+    assert {bytes(r) for r in ks} == kset and len(ks) == len(known_h)   # a permutation
+    for _ in range(2):
+        assert sh.dedup_known(ids.data_ptr(), n, known.data_ptr(), len(known_h),
+                              first.data_ptr()) == new
+        assert np.array_equal(first.cpu().numpy().view(np.uint32).astype(np.int64), want)
+    # an empty index is vs_blob_dedup
+    assert sh.dedup_known(ids.data_ptr(), n, 0, 0, first.data_ptr()) == len(first_seen) + \
+        len({bytes(r) for r in ids_h} & kset)
+    sh.close()
+
+
 def test_sha256_blocks_syncthing(gpu):
     """syncthing's scanner blocks: SHA-256 of every block of a
     device buffer, for the block size lib/protocol picks and a larger one,

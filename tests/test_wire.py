@@ -293,3 +293,152 @@ def test_zstd_tokens_runs_and_long_tokens():
     assert got[1] == lit[:150_000]
     assert PyZstdReceiver().file(s, bl, basis_len) == got
     assert len(s) < len(src) // 4   # zero runs and 2-bit literals compress
+
+
+# ---- malformed input from a peer --------------------------
+# Every parser below reads bytes a network peer sent.  Each malformed form must
+# come back as VS_ERR_ARG with a message, never as a read past the input or an
+# output array; tools/asan_build.sh runs these under ASan + UBSan.
+def c_read_sums(wire: bytes, cap: int = 64):
+    c, b, s, r = (ctypes.c_int32() for _ in range(4))
+    # arrays of at most 64 blocks: a larger `cap` claims more than they hold,
+    # which is safe only when the parser refuses before writing (tests below)
+    r1 = (ctypes.c_uint32 * max(min(cap, 64), 1))()
+    r2 = (ctypes.c_uint8 * max(min(cap, 64) * 16, 1))()
+    check(lib.vs_rsync_read_sums(wire, len(wire), ctypes.byref(c), ctypes.byref(b),
+                                 ctypes.byref(s), ctypes.byref(r), r1, r2, cap))
+    return c.value, b.value, s.value, r.value
+
+
+def test_read_sums_malformed():
+    good = py_sums(3, 700, 5, 12, [1, 2, 3], list(range(15)))
+    assert c_read_sums(good) == (3, 700, 5, 12)
+    for k in range(16):          # every truncation of the 16-byte head
+        with pytest.raises(VsError, match="truncated sum head"):
+            c_read_sums(good[:k])
+    for k in range(16, len(good)):   # head whole, sums cut anywhere
+        with pytest.raises(VsError, match="truncated sums"):
+            c_read_sums(good[:k])
+    bad_heads = [(-1, 700, 5, 12), (3, -700, 5, 12), (3, (1 << 17) + 8, 5, 12), (3, 700, 17, 12),
+                 (3, 700, -1, 12), (3, 700, 5, -1), (3, 700, 5, 701), (3, 0, 5, 0),
+                 (-(1 << 31), 700, 2, 0)]
+    for h in bad_heads:
+        with pytest.raises(VsError, match="invalid sum head"):
+            c_read_sums(struct.pack("<iiii", *h) + bytes(64))
+    # a head that claims 2^31 - 1 blocks: refused by size, nothing read past the input
+    huge = struct.pack("<iiii", (1 << 31) - 1, 700, 2, 0) + bytes(64)
+    with pytest.raises(VsError, match="too small"):
+        c_read_sums(huge, cap=64)
+    with pytest.raises(VsError, match="truncated sums"):
+        # a caller that sized its arrays by the claim: the body is checked
+        # against n before anything is written (the arrays here are small)
+        c_read_sums(huge, cap=(1 << 31))
+    # the last-block rule: remainder == blength and count 0 are legal heads
+    assert c_read_sums(struct.pack("<iiii", 0, 0, 2, 0)) == (0, 0, 2, 0)
+    assert c_read_sums(struct.pack("<iiii", 1, 700, 2, 700) + bytes(6)) == (1, 700, 2, 700)
+
+
+def test_read_tokens_malformed():
+    blen, basis_len = 700, 700 * 3 + 5   # 4 blocks, the last 5 bytes long
+    src = bytes(range(256)) * 40
+    m = [(0, 3), (5, 0), (2000, 1)]
+    good = c_tokens(m, src, blen, basis_len)
+    assert c_read_tokens(good, blen, basis_len)[0] == m
+    for k in range(len(good)):                  # every truncation
+        with pytest.raises(VsError, match="truncated"):
+            c_read_tokens(good[:k], blen, basis_len)
+    end = struct.pack("<i", 0)
+    with pytest.raises(VsError, match="past the basis"):
+        c_read_tokens(struct.pack("<i", -5) + end, blen, basis_len)          # block 4 of 4
+    with pytest.raises(VsError, match="past the basis"):
+        c_read_tokens(struct.pack("<i", -(1 << 31)) + end, blen, basis_len)  # INT32_MIN
+    with pytest.raises(VsError, match="past the basis"):
+        c_read_tokens(struct.pack("<i", -1) + end, blen, 0)                  # empty basis
+    with pytest.raises(VsError, match="truncated literal"):
+        c_read_tokens(struct.pack("<i", (1 << 31) - 1) + b"x" * 64 + end, blen, basis_len)
+    # output arrays too small for what the stream holds
+    nm, nl, fl = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_int64()
+    one = (VsMatch * 1)()
+    with pytest.raises(VsError, match="match buffer too small"):
+        check(lib.vs_rsync_read_tokens(good, len(good), blen, basis_len, one, 1, ctypes.byref(nm),
+                                       None, 0, ctypes.byref(nl), ctypes.byref(fl)))
+    lit = (ctypes.c_uint8 * 3)()
+    with pytest.raises(VsError, match="literal buffer too small"):
+        check(lib.vs_rsync_read_tokens(good, len(good), blen, basis_len, None, 0, ctypes.byref(nm),
+                                       lit, 3, ctypes.byref(nl), ctypes.byref(fl)))
+
+
+def test_read_tokens_zstd_malformed():
+    from volsync_amd import ZstdTokens
+    blen, nblk = 64, 100
+    basis_len = blen * nblk
+    rng = np.random.default_rng(5)
+    lit = rng.integers(0, 256, 3000, dtype=np.uint8).tobytes()
+    m, pos = [], 0
+    for i in list(range(20)) + [50, 7]:
+        m.append((pos, i))
+        pos += blen
+    src = bytes(pos) + lit
+    good = ZstdTokens().write(m, src, blen, basis_len, blen)
+    assert ZstdTokens().read(good, blen, basis_len, 64, len(src))[0] == m
+
+    def rd(stream, basis=basis_len):
+        return ZstdTokens().read(stream, blen, basis, 64, len(src) + 64)
+
+    # every truncation of a real stream (cut inside a flag, a TOKEN_LONG, a run
+    # count, a DEFLATED_DATA header or its compressed bytes -- a zstd frame cut
+    # mid-block): an error or, where the cut falls between whole tokens, a
+    # shorter file; never a read past the input
+    for k in range(len(good)):
+        try:
+            got = rd(good[:k])
+        except VsError as e:
+            assert "truncated" in str(e) or "ZSTD" in str(e), e
+        else:
+            assert got[3] <= k
+    with pytest.raises(VsError, match="truncated"):
+        rd(b"")
+    with pytest.raises(VsError, match="past the basis"):
+        rd(bytes([0x80 | 63, 0x80 | 63, 0]), basis=blen * 100)     # relative tokens 63, 126
+    with pytest.raises(VsError, match="past the basis"):
+        rd(bytes([0x20]) + struct.pack("<i", -7) + b"\x00")          # TOKEN_LONG, negative
+    with pytest.raises(VsError, match="past the basis"):
+        rd(bytes([0x20]) + struct.pack("<i", nblk) + b"\x00")        # TOKEN_LONG, one past
+    with pytest.raises(VsError, match="past the basis"):
+        rd(bytes([0x21]) + struct.pack("<i", 95) + bytes([10, 0, 0]))  # TOKENRUN_LONG 95..105
+    # a DEFLATED_DATA piece of garbage: zstd refuses it
+    with pytest.raises(VsError, match="ZSTD"):
+        rd(bytes([0x40, 16]) + rng.integers(0, 256, 16, dtype=np.uint8).tobytes() + b"\x00")
+
+
+def test_wire_parsers_random_bytes():
+    """Seeded random byte strings (and random mutations of real streams) into
+    all three peer-facing parsers: each returns OK or VS_ERR_ARG, nothing else
+    (under tools/asan_build.sh: no memory error either)."""
+    from volsync_amd import ZstdTokens
+    rng = np.random.default_rng(2026)
+    blen, basis_len = 512, 512 * 40
+    src = rng.integers(0, 4, 30_000, dtype=np.uint8).tobytes()
+    m = [(0, 1), (512, 2), (4000, 39), (9000, 0)]
+    plain = c_tokens(m, src, blen, basis_len)
+    zst = ZstdTokens().write(m, src, blen, basis_len, blen)
+    sums = py_sums(40, blen, 4, 0, list(range(40)), list(range(160)))
+    for it in range(1500):
+        kind = it % 3
+        base = (plain, zst, sums)[kind]
+        if it % 2:
+            s = rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8).tobytes()
+        else:
+            b = bytearray(base)
+            for _ in range(int(rng.integers(1, 6))):
+                b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+            s = bytes(b[:int(rng.integers(0, len(b) + 1))])
+        try:
+            if kind == 0:
+                c_read_tokens(s, blen, basis_len)
+            elif kind == 1:
+                ZstdTokens().read(s, blen, basis_len, 4096, 1 << 20)
+            else:
+                c_read_sums(s, cap=64)
+        except VsError as e:
+            assert e.code == -1, e

@@ -36,6 +36,7 @@ VS_OPT_WALK_TAIL_PCT = 10
 VS_OPT_SHA_QUAD_PCT = 16
 VS_OPT_FP_GENERIC = 17
 VS_OPT_SHA_GRID_PER_CU = 18
+VS_DEDUP_KNOWN = 0xFFFFFFFF
 VS_OPT_SEAL_FUSED = 32
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -113,6 +114,8 @@ def _load() -> ctypes.CDLL:
         "vs_cdc_set_batch_bytes": (c_int, [vp, c_u64]),
         "vs_cdc_stream_stats": (c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
         "vs_blob_dedup": (c_int, [vp, vp, c_size, vp, ctypes.POINTER(c_u64), vp]),
+        "vs_blob_dedup_known": (c_int, [vp, vp, c_size, vp, c_size, vp, ctypes.POINTER(c_u64), vp]),
+        "vs_blob_index_sort": (c_int, [vp, vp, c_size, vp]),
         "vs_rsync_file_sum": (c_int, [vp, vp, ctypes.c_int64, c_int, ctypes.c_char_p]),
         "vs_rsync_file_sum_start": (c_int, [vp, vp, ctypes.c_int64, c_int]),
         "vs_rsync_file_sum_wait": (c_int, [vp, ctypes.c_char_p]),

@@ -373,6 +373,23 @@ class DeviceSha256:
                                 ctypes.c_void_p(stream or None)))
         return int(u.value) if count else None
 
+    def dedup_known(self, dev_ids: int, n: int, dev_known: int, n_known: int, dev_first: int,
+                    stream: Optional[int] = None, count: bool = True) -> Optional[int]:
+        """SaveBlob's dedup against the repository's index too
+        (vs_blob_dedup_known): dev_first[i] = VS_DEDUP_KNOWN for a known ID;
+        returns the number of distinct new IDs (waits) when count is set."""
+        u = ctypes.c_uint64(0)
+        check(lib.vs_blob_dedup_known(self._h, ctypes.c_void_p(dev_ids), n,
+                                      ctypes.c_void_p(dev_known), n_known,
+                                      ctypes.c_void_p(dev_first), ctypes.byref(u) if count else None,
+                                      ctypes.c_void_p(stream or None)))
+        return int(u.value) if count else None
+
+    def index_sort(self, dev_known: int, n: int, stream: Optional[int] = None) -> None:
+        """vs_blob_index_sort: the known IDs into dedup_known's search order."""
+        check(lib.vs_blob_index_sort(self._h, ctypes.c_void_p(dev_known), n,
+                                     ctypes.c_void_p(stream or None)))
+
     def close(self) -> None:
         if self._h:
             lib.vs_sha256_close(self._h)

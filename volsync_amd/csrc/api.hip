@@ -1213,6 +1213,8 @@ struct vs_sha {
     int device = 0;
     ShaEngine eng;
     DevBuf dd_tmp;                  // vs_blob_dedup scratch
+    DevBuf dd_flag;                 // vs_blob_dedup_known: per-blob "in the index" flags
+    DevBuf ix_tmp;                  // vs_blob_index_sort scratch
     uint64_t *dd_pinned = nullptr;
     DevBuf blk_off, blk_len;        // vs_sha256_blocks descriptors
     DevBuf vf_ids, vf_cnt;          // vs_blob_verify scratch
@@ -1351,6 +1353,45 @@ VS_API int vs_blob_dedup(vs_sha *h, const uint8_t *dev_ids, size_t n, uint32_t *
         VS_HIP(hipStreamSynchronize(s));
         *n_unique = h->dd_pinned[0];
     }
+    return 0;
+}
+
+VS_API int vs_blob_dedup_known(vs_sha *h, const uint8_t *dev_ids, size_t n,
+                               const uint8_t *dev_known, size_t n_known, uint32_t *dev_first,
+                               uint64_t *n_new, void *hip_stream) {
+    if (!h || (n_known && !dev_known)) return fail(VS_ERR_ARG, "bad arguments");
+    if (((uintptr_t)dev_known & 15) != 0) return fail(VS_ERR_ARG, "known IDs must be 16-byte aligned");
+    // the batch's own first occurrences (vs_blob_dedup), without its count
+    VS_TRY(vs_blob_dedup(h, dev_ids, n, dev_first, nullptr, hip_stream));
+    const hipStream_t s = (hipStream_t)hip_stream;
+    VS_TRY(h->dd_flag.ensure(dedup_known_tmp_bytes(std::max<size_t>(n, 1))));
+    unsigned long long *cnt = (unsigned long long *)h->dd_tmp.p + 8;   // its own 8-byte slot
+    VS_HIP(launch_dedup_known(dev_ids, n, dev_known, n_known, dev_first, h->dd_flag.p, cnt, s));
+    VS_HIP(hipEventRecord(h->done, s));
+    if (n_new) {
+        if (!h->dd_pinned &&
+            hipHostMalloc((void **)&h->dd_pinned, 64, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(VS_ERR_NOMEM, "pinned read-back buffer");
+        }
+        VS_HIP(hipMemcpyAsync(h->dd_pinned, cnt, 8, hipMemcpyDeviceToHost, s));
+        VS_HIP(hipStreamSynchronize(s));
+        *n_new = h->dd_pinned[0];
+    }
+    return 0;
+}
+
+VS_API int vs_blob_index_sort(vs_sha *h, uint8_t *dev_known, size_t n, void *hip_stream) {
+    if (!h || (n && !dev_known)) return fail(VS_ERR_ARG, "bad arguments");
+    if (n > 0x7fffffffull) return fail(VS_ERR_ARG, "more than 2^31 - 1 known IDs (radix sort count)");
+    if (((uintptr_t)dev_known & 15) != 0) return fail(VS_ERR_ARG, "known IDs must be 16-byte aligned");
+    VS_TRY(enter_device(h->device));
+    const hipStream_t s = (hipStream_t)hip_stream;
+    if (h->ran) VS_HIP(hipStreamWaitEvent(s, h->done, 0));
+    VS_TRY(h->ix_tmp.ensure(index_sort_tmp_bytes(std::max<size_t>(n, 1)) + 256));
+    VS_HIP(launch_index_sort(dev_known, n, h->ix_tmp.p, h->ix_tmp.cap, s));
+    VS_HIP(hipEventRecord(h->done, s));
+    h->ran = true;
     return 0;
 }
 

@@ -67,7 +67,119 @@ __global__ void dd_first_kernel(const uint8_t *ids, uint64_t n, const uint64_t *
     if ((threadIdx.x & 63) == 0 && b) atomicAdd(n_unique, (unsigned long long)__popcll(b));
 }
 
+// ---- the repository's index (restic Repository.SaveBlob: idx.AddPending
+// fails for a blob the master index already holds) ----------------------------
+// The known IDs come as a device array sorted by their first 8 bytes read
+// big-endian (vs_blob_index_sort; the order of IDs sharing a prefix is
+// irrelevant): membership is a lower_bound on the prefix, then a full 32-byte
+// compare over the run of equal prefixes.
+__device__ __forceinline__ uint64_t id_key(const uint8_t *p) {
+    const uint2 w = *(const uint2 *)p;
+    return ((uint64_t)__builtin_bswap32(w.x) << 32) | __builtin_bswap32(w.y);
+}
+
+__device__ bool id_known(const uint8_t *id, const uint8_t *known, uint64_t n_known) {
+    const uint64_t k = id_key(id);
+    uint64_t lo = 0, hi = n_known;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (id_key(known + 32 * mid) < k) lo = mid + 1;
+        else hi = mid;
+    }
+    const uint4 *x = (const uint4 *)id;
+    const uint4 x0 = x[0], x1 = x[1];
+    for (uint64_t q = lo; q < n_known && id_key(known + 32 * q) == k; ++q) {
+        const uint4 *y = (const uint4 *)(known + 32 * q);
+        const uint4 y0 = y[0], y1 = y[1];
+        if (x0.x == y0.x && x0.y == y0.y && x0.z == y0.z && x0.w == y0.w && x1.x == y1.x &&
+            x1.y == y1.y && x1.z == y1.z && x1.w == y1.w)
+            return true;
+    }
+    return false;
+}
+
+// first occurrences only: flag[i] = 1 when blob i's ID is in the index
+__global__ void dd_known_kernel(const uint8_t *ids, uint64_t n, const uint8_t *known,
+                                uint64_t n_known, const uint32_t *first, uint8_t *flag) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    flag[i] = (first[i] == (uint32_t)i && id_known(ids + 32 * i, known, n_known)) ? 1 : 0;
+}
+
+// every blob whose first occurrence is known: first = kDedupKnown; the count
+// becomes the distinct IDs the index does not hold (the blobs SaveBlob stores)
+__global__ void dd_mark_known_kernel(uint64_t n, const uint8_t *flag, uint32_t *first,
+                                     unsigned long long *n_new) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool is_new = false;
+    if (i < n) {
+        const uint32_t f = first[i];
+        if (flag[f]) first[i] = kDedupKnown;
+        else is_new = f == (uint32_t)i;
+    }
+    const uint64_t b = __ballot(is_new);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(n_new, (unsigned long long)__popcll(b));
+}
+
+__global__ void idx_keys_kernel(const uint8_t *ids, uint64_t n, uint64_t *keys, uint32_t *idx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = id_key(ids + 32 * i);
+    idx[i] = (uint32_t)i;
+}
+
+__global__ void idx_gather_kernel(const uint8_t *src, uint64_t n, const uint32_t *sidx,
+                                  uint8_t *dst) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 2 * n) return;   // two 16-byte halves per ID
+    const uint64_t r = i >> 1, h = i & 1;
+    ((uint4 *)dst)[2 * r + h] = ((const uint4 *)src)[2 * (uint64_t)sidx[r] + h];
+}
+
 }  // namespace
+
+size_t dedup_known_tmp_bytes(uint64_t n) { return n + 256; }
+
+hipError_t launch_dedup_known(const uint8_t *ids, uint64_t n, const uint8_t *known,
+                              uint64_t n_known, uint32_t *first, void *flag_tmp,
+                              unsigned long long *n_new_dev, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(n_new_dev, 0, 8, s);
+    if (e != hipSuccess || !n) return e;
+    const uint32_t blocks = (uint32_t)((n + 255) / 256);
+    dd_known_kernel<<<blocks, 256, 0, s>>>(ids, n, known, n_known, first, (uint8_t *)flag_tmp);
+    dd_mark_known_kernel<<<blocks, 256, 0, s>>>(n, (const uint8_t *)flag_tmp, first, n_new_dev);
+    return hipGetLastError();
+}
+
+size_t index_sort_tmp_bytes(uint64_t n) {
+    size_t b = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint64_t *)nullptr,
+                                             (uint64_t *)nullptr, (const uint32_t *)nullptr,
+                                             (uint32_t *)nullptr, (int)n, 0, 64);
+    // keys, sorted keys, idx, sorted idx, a copy of the IDs, then the scratch
+    return n * (8 + 8 + 4 + 4 + 32) + 512 + b;
+}
+
+hipError_t launch_index_sort(uint8_t *ids, uint64_t n, void *tmp, size_t tmp_bytes,
+                             hipStream_t s) {
+    if (n < 2) return hipSuccess;
+    uint8_t *t = (uint8_t *)tmp;
+    uint8_t *copy = (uint8_t *)(((uintptr_t)t + 15) & ~(uintptr_t)15);
+    uint64_t *keys = (uint64_t *)(copy + 32 * n);
+    uint64_t *skeys = keys + n;
+    uint32_t *idx = (uint32_t *)(skeys + n);
+    uint32_t *sidx = idx + n;
+    uint8_t *scratch = (uint8_t *)(((uintptr_t)(sidx + n) + 255) & ~(uintptr_t)255);
+    size_t sb = tmp_bytes - (size_t)(scratch - t);
+    const uint32_t blocks = (uint32_t)((n + 255) / 256);
+    idx_keys_kernel<<<blocks, 256, 0, s>>>(ids, n, keys, idx);
+    hipError_t e = hipMemcpyAsync(copy, ids, 32 * n, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return e;
+    e = hipcub::DeviceRadixSort::SortPairs(scratch, sb, keys, skeys, idx, sidx, (int)n, 0, 64, s);
+    if (e != hipSuccess) return e;
+    idx_gather_kernel<<<(uint32_t)((2 * n + 255) / 256), 256, 0, s>>>(copy, n, sidx, ids);
+    return hipGetLastError();
+}
 
 size_t dedup_tmp_bytes(uint64_t n) {
     size_t b = 0;

@@ -522,6 +522,15 @@ hipError_t launch_recon(uint8_t *dst, const uint8_t *basis, const uint8_t *lit,
                         const ReconPiece *pieces, uint64_t n, int cus, hipStream_t s);
 // SaveBlob dedup (dedup.hip): first[i] = smallest index with ids[i]'s ID
 size_t dedup_tmp_bytes(uint64_t n);
+// vs_blob_dedup with the repository's index: first[i] = kDedupKnown for a
+// blob whose ID the (vs_blob_index_sort-ed) known array holds
+constexpr uint32_t kDedupKnown = 0xffffffffu;
+size_t dedup_known_tmp_bytes(uint64_t n);
+hipError_t launch_dedup_known(const uint8_t *ids, uint64_t n, const uint8_t *known,
+                              uint64_t n_known, uint32_t *first, void *flag_tmp,
+                              unsigned long long *n_new_dev, hipStream_t s);
+size_t index_sort_tmp_bytes(uint64_t n);
+hipError_t launch_index_sort(uint8_t *ids, uint64_t n, void *tmp, size_t tmp_bytes, hipStream_t s);
 hipError_t launch_dedup(const uint8_t *ids, uint64_t n, uint32_t *first, void *tmp,
                         size_t tmp_bytes, unsigned long long *n_unique_dev, hipStream_t s);
 hipError_t launch_rs_sort_cands(void *tmp, size_t tmp_bytes, const uint64_t *off_in,

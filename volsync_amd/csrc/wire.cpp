@@ -83,7 +83,11 @@ VS_API int vs_rsync_read_sums(const uint8_t *in, size_t n, int32_t *count, int32
     if (!in || n < 16 || !count || !blength || !s2length || !remainder)
         return fail(VS_ERR_ARG, "truncated sum head");
     const int32_t c = get_i32(in), b = get_i32(in + 4), s2 = get_i32(in + 8), r = get_i32(in + 12);
-    if (c < 0 || b < 0 || s2 < 0 || s2 > 16 || r < 0 || (c && r > b))
+    // io.c read_sum_head's checks (protocol >= 30: blength <= MAX_BLOCK_SIZE
+    // = 2^17, s2length <= MAX_DIGEST_LEN = 16, 0 <= remainder <= blength),
+    // plus a positive blength whenever there are blocks (every later use
+    // divides by it)
+    if (c < 0 || b < 0 || b > (1 << 17) || s2 < 0 || s2 > 16 || r < 0 || r > b || (c && !b))
         return fail(VS_ERR_ARG, "invalid sum head");
     *count = c;
     *blength = b;
