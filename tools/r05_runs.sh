@@ -5,6 +5,8 @@
 #   first     VALU probe 3, the CDC + C3 GPU tests, fingerprint A/B (fpb0 =
 #             -DVS_FP_BITOP3=0), C2 bench at the driver's 20/5, its trace-only
 #             rocprofv3 run, one C3 rank at 20/5          -> profiles/r05_*
+#   second    the whole -m gpu suite, C5 (known-index dedup, golden), the C4
+#             shape with R7, one real-C4 rank, a C4 kernel+copy+API trace
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
 var() { echo "volsync_amd/lib/var/$1/libvsgpu.so"; }
@@ -30,6 +32,19 @@ trace() {  # trace <tag> <bench args...>: kernel trace + stats only (no counters
   find "$out/raw" -name '*kernel_trace.csv' -exec cp {} "$out/kernel_trace.csv" \;
   rm -rf "$out/raw"
 }
+c4trace() {  # c4trace <tag> <bench args...>: kernels + copies + HIP API (no counters)
+  local tag=$1 out=$PWD/gpurun_out/c4trace_$1 repo=$PWD
+  shift
+  mkdir -p "$out"
+  (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --hip-runtime-trace \
+     --memory-copy-trace -d "$out/raw" -o run --output-format csv -- python3 "$repo/bench.py" "$@") \
+     > "$out/bench.log" 2>&1
+  local rc=$?
+  echo "=== c4trace_$tag rc=$rc"; tail -n 1 "$out/bench.log" | cut -c1-300
+  [ $rc -eq 0 ] || return $rc
+  python3 tools/c4_timeline.py "$out/raw" > "$out/timeline.txt" 2>&1
+  rm -rf "$out/raw"
+}
 case $1 in
   first)
     timeout -k 10 120 tools/valu/valu_ops3 > gpurun_out/valu_ops3.json 2> gpurun_out/valu_ops3.err &&
@@ -39,5 +54,12 @@ case $1 in
     bash tools/gpu.sh bench c2 --gpus 1 --steps 20 --warmup 5 &&
     trace c2 --gpus 1 --steps 20 --warmup 5 &&
     bash tools/gpu.sh bench c3r3 --share 3/8 --steps 20 --warmup 5 --no-cpu-baseline ;;
-  *) echo "usage: tools/r05_runs.sh first" >&2; exit 2 ;;
+  second)
+    bash tools/gpu.sh tests &&
+    bash tools/gpu.sh bench c5 --mode smallfiles --steps 5 --warmup 1 &&
+    bash tools/gpu.sh bench c4 --mode rsync --steps 5 --warmup 1 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c4share_nofs --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 \
+      --warmup 1 --no-file-sum &&
+    c4trace c4 --mode rsync --steps 3 --warmup 1 --no-cpu-baseline ;;
+  *) echo "usage: tools/r05_runs.sh first|second" >&2; exit 2 ;;
 esac
