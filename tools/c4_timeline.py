@@ -19,8 +19,9 @@ def main():
     d = sys.argv[1]
     ev = []
     for r in rows(d, "*kernel_trace.csv"):
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "K",
-                   r["Kernel_Name"].split("(")[0].replace("void ", "")[-48:]))
+                   name.split("(")[0].replace("void ", "")[-48:]))
     for r in rows(d, "*memory_copy_trace.csv"):
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C",
                    f"{r.get('Direction', 'copy')} {r.get('Bytes', '')}B"))

@@ -45,6 +45,19 @@ c4trace() {  # c4trace <tag> <bench args...>: kernels + copies + HIP API (no cou
   python3 tools/c4_timeline.py "$out/raw" > "$out/timeline.txt" 2>&1
   rm -rf "$out/raw"
 }
+c4copy() {  # c4copy <tag> <bench args...>: kernels + memory copies (no API trace, no counters)
+  local tag=$1 out=$PWD/gpurun_out/c4copy_$1 repo=$PWD
+  shift
+  mkdir -p "$out"
+  (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace \
+     -d "$out/raw" -o run --output-format csv -- python3 "$repo/bench.py" "$@") > "$out/bench.log" 2>&1
+  local rc=$?
+  echo "=== c4copy_$tag rc=$rc"; tail -n 1 "$out/bench.log" | cut -c1-300
+  [ $rc -eq 0 ] || return $rc
+  python3 tools/c4_timeline.py "$out/raw" > "$out/timeline.txt" 2>&1
+  find "$out/raw" -name '*memory_copy_trace.csv' -exec cp {} "$out/memory_copy_trace.csv" \;
+  rm -rf "$out/raw"
+}
 case $1 in
   first)
     timeout -k 10 120 tools/valu/valu_ops3 > gpurun_out/valu_ops3.json 2> gpurun_out/valu_ops3.err &&
@@ -61,5 +74,25 @@ case $1 in
     bash tools/gpu.sh bench c4share_nofs --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 \
       --warmup 1 --no-file-sum &&
     c4trace c4 --mode rsync --steps 3 --warmup 1 --no-cpu-baseline ;;
-  *) echo "usage: tools/r05_runs.sh first|second" >&2; exit 2 ;;
+  d2h)
+    timeout -k 10 300 tools/probe/bin/d2h_overlap > gpurun_out/d2h_overlap.json 2> gpurun_out/d2h_overlap.err &&
+    echo "=== d2h ok" && cat gpurun_out/d2h_overlap.json &&
+    c4copy c4 --mode rsync --steps 3 --warmup 1 --no-cpu-baseline ;;
+  d2hprof)
+    out=$PWD/gpurun_out/d2hprof; mkdir -p "$out"; repo=$PWD
+    (cd /tmp && TMPDIR=/tmp timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --stats \
+       -d "$out/cpp" -o run --output-format csv -- "$repo/tools/probe/bin/d2h_overlap") \
+       > "$out/cpp.log" 2>&1 && echo "=== cpp ok" &&
+    (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats \
+       -d "$out/torch" -o run --output-format csv -- python3 "$repo/tools/probe/d2h_torch.py") \
+       > "$out/torch.log" 2>&1 && echo "=== torch ok" && tail -n 1 "$out/torch.log" &&
+    find "$out" -name '*stats.csv' | sort ;;
+  d2hapi)
+    out=$PWD/gpurun_out/d2hapi; mkdir -p "$out"; repo=$PWD
+    timeout -k 10 200 python3 tools/probe/d2h_apis.py > "$out/plain.log" 2>&1 && echo "=== plain ok" &&
+    tail -n 1 "$out/plain.log" &&
+    (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats \
+       -d "$out/prof" -o run --output-format csv -- python3 "$repo/tools/probe/d2h_apis.py") \
+       > "$out/prof.log" 2>&1 && echo "=== prof ok" && rm -f "$out"/prof/*trace.csv ;;
+  *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi" >&2; exit 2 ;;
 esac

@@ -33,6 +33,23 @@ int enter_device(int device);
         if (r_ < 0) return r_;       \
     } while (0)
 
+// ---- device-to-host copies on an SDMA engine (xfer.cpp) --------------------------
+// hsa_amd_memory_async_copy: runs beside kernels that hold every CU, where the
+// HIP runtime's blit-kernel copies would queue behind them.  The caller orders
+// it after the kernel that wrote the source (an event synchronisation).
+struct DmaD2H {
+    static constexpr int kSignals = 4;
+    bool init(int device);                     // false: no DMA path (use hipMemcpyAsync)
+    void release();
+    bool start(int slot, void *dst, const void *src, size_t n);  // async; signal `slot`
+    void wait(int slot);                       // until copy `slot` has landed
+    bool ready = false;
+
+  private:
+    uint64_t gpu_ = 0, cpu_ = 0;               // hsa_agent_t handles
+    uint64_t sig_[kSignals] = {};              // hsa_signal_t handles
+};
+
 // ---- host memory the DMA engines touch (xfer.cpp) -------------------------------
 // The library page-locks only memory it allocated itself (hipHostMalloc):
 // registering heap storage pins pages it shares with the caller's buffers.

@@ -61,13 +61,21 @@ struct RsRun {
 };
 
 // One whole-file checksum in flight (R7).  XXH3 of a long
-// file: the block contributions are computed on the device one piece at a
-// time into a 3-deep device ring, read back into a pinned ring on the job's
-// own stream -- the copy engine runs beside the walk's kernels -- and chained
-// on a host thread as each piece lands.  MD5, XXH64 and XXH3 of <= 240 bytes
-// are serial chains: the file's bytes come back through the same ring and
-// are hashed on the host thread.  Device memory per job: 3 pieces.
+// file, rows first (round 5): one kernel computes every 1 KiB block's
+// contribution row (64 B) into a device buffer of len / 16 bytes as soon as
+// the job starts -- before the caller's walk takes the CUs -- and the rows
+// come back on an SDMA engine (DmaD2H; a HIP copy in a PyTorch process is a
+// blit kernel, which waits for CUs the persistent walk holds) into a pinned
+// ring, chained on a host thread as each piece lands.  Without the DMA path,
+// or for files whose rows exceed kRowsCap, contributions are computed one
+// piece at a time into a 3-deep device ring instead.  MD5, XXH64 and XXH3 of
+// <= 240 bytes are serial chains: the file's bytes come back through the same
+// pinned ring and are hashed on the host thread.
 struct FsJob {
+    static constexpr uint64_t kRowsCap = 8ull << 30;   // rows of a 128 GiB file
+    DmaD2H dma;
+    DevBuf rows;                          // rows-first: every block's row
+    bool rows_first = false;
     static constexpr int kRing = 3;
     uint64_t piece = 1ull << 18;          // blocks per piece (16 MiB of rows; serial: of bytes)
     hipStream_t s = nullptr;
@@ -1349,6 +1357,40 @@ void fs_thread(FsJob *j) {
         (void)hipGetLastError();
     };
     if (hipSetDevice(j->device) != hipSuccess) return fail_here(hipGetLastError(), "hipSetDevice");
+    if (j->rows_first) {
+        // every row is on the device once the kernel's event fires; pieces come
+        // back on the DMA engine, copy i overlapping the chain of piece i - 1
+        const hipError_t e = hipEventSynchronize(j->kev[0][1]);
+        if (e != hipSuccess) return fail_here(e, "file-sum rows kernel");
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, j->kev[0][0], j->kev[0][1]) == hipSuccess) kms = ms;
+        (void)hipGetLastError();
+        const uint8_t *rows = j->rows.as<uint8_t>();
+        auto start = [&](uint64_t i) -> bool {
+            const uint64_t i0 = i * per, n = std::min(per, items - i0);
+            return j->dma.start((int)(i % FsJob::kRing), j->hC[i % FsJob::kRing], rows + i0 * 64, n * 64);
+        };
+        if (j->whole) {   // the file's last <= 1088 bytes, for the finish
+            const uint64_t keep = std::min<uint64_t>(j->len, 1088);
+            if (!j->dma.start(FsJob::kRing, j->hlast, j->src + j->len - keep, keep))
+                return fail_here(hipErrorUnknown, "file-sum tail read-back (DMA)");
+        }
+        if (!start(0)) return fail_here(hipErrorUnknown, "file-sum rows read-back (DMA)");
+        for (uint64_t i = 0; i < np; ++i) {
+            const int r = (int)(i % FsJob::kRing);
+            j->dma.wait(r);
+            if (i + 1 < np && !start(i + 1))   // slot (i+1) % R: its chain finished last round
+                return fail_here(hipErrorUnknown, "file-sum rows read-back (DMA)");
+            const uint64_t i0 = i * per, n = std::min(per, items - i0);
+            const double c0 = now_ms();
+            xxh3_chain_rows((const uint64_t *)j->hC[r], n, j->acc);
+            chain += now_ms() - c0;
+        }
+        if (j->whole) j->dma.wait(FsJob::kRing);
+        j->host_ms = chain;
+        j->dev_ms = kms;
+        return;
+    }
     SerialSum ss;
     if (serial) serial_sum_init(ss, j->csum);
     auto issue = [&](uint64_t i) -> bool {
@@ -1424,7 +1466,7 @@ int fs_rings(FsJob &j, uint64_t piece, bool serial) {
     // MD5 / XXH64 (and XXH3 of <= 240 bytes) read the source bytes back
     // through the pinned ring only: no device contribution rows
     if (serial) return 0;
-    return j.dC.ensure((size_t)FsJob::kRing * j.piece * 64);
+    return 0;   // the device ring (piece mode only) is sized in fs_start
 }
 
 // waits for the job (if any); the job's status becomes the return value
@@ -1449,6 +1491,8 @@ int fs_finish(FsJob &j) {
 void fs_release(FsJob &j) {
     if (j.th.joinable()) j.th.join();
     if (j.s) (void)hipStreamSynchronize(j.s);
+    j.dma.release();
+    j.rows.release();
     for (auto &p : j.hC) pinned_free(p), p = nullptr;
     pinned_free(j.hlast);
     j.hlast = nullptr;
@@ -1494,15 +1538,27 @@ int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
     // after the caller's null-stream work and this handle's queued work
     VS_HIP(hipEventRecord(j.ev_in, h->stream));
     VS_HIP(hipStreamWaitEvent(j.s, j.ev_in, 0));
+    j.rows_first = false;
     if (j.serial) {
         j.nb = 0;
     } else {
         j.nb = whole ? (len - 1) / 1024 : len / 1024;
         if (whole || !acc_in) xxh3_init_acc(j.acc);
         else memcpy(j.acc, acc_in, 64);
-        if (whole) {   // the last partial block, last stripe: read back for the finish
-            const uint64_t keep = std::min<uint64_t>(len, 1088);
-            VS_HIP(hipMemcpyAsync(j.hlast, p + len - keep, keep, hipMemcpyDeviceToHost, j.s));
+        j.rows_first = j.nb > 0 && j.nb * 64 <= FsJob::kRowsCap && j.dma.init(j.device);
+        if (j.rows_first) {
+            // all rows now, in stream order after the caller's queued work and
+            // ahead of whatever the caller queues next (the walk)
+            VS_TRY(j.rows.ensure((size_t)j.nb * 64));
+            VS_HIP(hipEventRecord(j.kev[0][0], j.s));
+            VS_HIP(launch_fs_contrib(p, j.nb, j.rows.as<uint64_t>(), j.s));
+            VS_HIP(hipEventRecord(j.kev[0][1], j.s));
+        } else {
+            VS_TRY(j.dC.ensure((size_t)FsJob::kRing * j.piece * 64));
+            if (whole) {   // the last partial block, last stripe: read back for the finish
+                const uint64_t keep = std::min<uint64_t>(len, 1088);
+                VS_HIP(hipMemcpyAsync(j.hlast, p + len - keep, keep, hipMemcpyDeviceToHost, j.s));
+            }
         }
     }
     if (j.th.joinable()) j.th.join();   // (fs_finish joined it; never terminate())

@@ -16,9 +16,122 @@
 #include <thread>
 #include <vector>
 
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <mutex>
+
 #include "internal.hpp"
 
 namespace vsgpu {
+
+// ---- device-to-host copies on a DMA engine (round 5) ---------------------------
+// Inside a PyTorch process the library shares torch's bundled HIP runtime, and
+// that runtime performs hipMemcpyAsync device-to-host copies as blit kernels
+// (__amd_rocclr_copyBuffer), which need a free CU: behind a persistent kernel
+// that holds every CU (the rsync walk) they wait until it ends
+// (tools/probe/d2h_apis.py: every hipMemcpy* form but one runs as a blit; the
+// HSA runtime's own async copy runs on an SDMA engine, beside anything).  The
+// whole-file checksum reads its contribution rows back this way.  HSA is the
+// runtime under HIP (already initialised by it; hsa_init only counts a user).
+namespace {
+struct DmaAgents {
+    bool tried = false, ok = false;
+    hsa_agent_t gpu{}, cpu{};
+};
+std::mutex g_dma_mu;
+DmaAgents g_dma[64];
+
+struct AgentFind {
+    uint32_t bdf = 0, domain = 0;
+    hsa_agent_t gpu{}, cpu{};
+    bool found = false;
+};
+
+hsa_status_t agent_cb(hsa_agent_t a, void *p) {
+    AgentFind *f = (AgentFind *)p;
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+    if (t == HSA_DEVICE_TYPE_CPU && !f->cpu.handle) f->cpu = a;
+    if (t == HSA_DEVICE_TYPE_GPU && !f->found) {
+        uint32_t bdf = 0, dom = 0;
+        if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) == HSA_STATUS_SUCCESS &&
+            hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) == HSA_STATUS_SUCCESS &&
+            bdf == f->bdf && dom == f->domain) {
+            f->gpu = a;
+            f->found = true;
+        }
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+// the HSA agents of HIP device `device` (matched by PCI domain / bus / device
+// / function) and a CPU agent; false when they cannot be found
+bool dma_agents(int device, hsa_agent_t *gpu, hsa_agent_t *cpu) {
+    if (device < 0 || device >= 64) return false;
+    std::lock_guard<std::mutex> lk(g_dma_mu);
+    DmaAgents &d = g_dma[device];
+    if (!d.tried) {
+        d.tried = true;
+        int bus = 0, dev = 0, dom = 0;
+        if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+            hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
+            hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device) != hipSuccess) {
+            (void)hipGetLastError();
+        } else if (hsa_init() == HSA_STATUS_SUCCESS) {
+            AgentFind f;
+            f.bdf = ((uint32_t)bus << 8) | ((uint32_t)dev << 3);
+            f.domain = (uint32_t)dom;
+            if (hsa_iterate_agents(agent_cb, &f) == HSA_STATUS_SUCCESS && f.found && f.cpu.handle) {
+                d.gpu = f.gpu;
+                d.cpu = f.cpu;
+                d.ok = true;
+            }
+        }
+    }
+    *gpu = d.gpu;
+    *cpu = d.cpu;
+    return d.ok;
+}
+}  // namespace
+
+bool DmaD2H::init(int device) {
+    if (!ready) {
+        hsa_agent_t g{}, c{};
+        ready = dma_agents(device, &g, &c);
+        gpu_ = g.handle;
+        cpu_ = c.handle;
+        for (int i = 0; ready && i < kSignals; ++i) {
+            hsa_signal_t t{};
+            if (hsa_signal_create(0, 0, nullptr, &t) != HSA_STATUS_SUCCESS) {
+                for (int k = 0; k < i; ++k) hsa_signal_destroy(hsa_signal_t{sig_[k]});
+                ready = false;
+            }
+            sig_[i] = t.handle;
+        }
+    }
+    return ready;
+}
+
+void DmaD2H::release() {
+    if (!ready) return;
+    for (int i = 0; i < kSignals; ++i) hsa_signal_destroy(hsa_signal_t{sig_[i]});
+    ready = false;
+}
+
+bool DmaD2H::start(int slot, void *dst, const void *src, size_t n) {
+    const hsa_signal_t s{sig_[slot]};
+    hsa_signal_store_screlease(s, 1);
+    return hsa_amd_memory_async_copy(dst, hsa_agent_t{cpu_}, src, hsa_agent_t{gpu_}, n, 0, nullptr,
+                                     s) == HSA_STATUS_SUCCESS;
+}
+
+void DmaD2H::wait(int slot) {
+    const hsa_signal_t s{sig_[slot]};
+    while (hsa_signal_wait_scacquire(s, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                     HSA_WAIT_STATE_BLOCKED) != 0) {
+    }
+}
 
 // The staging copies are the host side of every pageable feed (the Go
 // Chunker's read buffer is pageable): one thread copies ~20 GB/s, a third of
