@@ -49,13 +49,13 @@ c4copy() {  # c4copy <tag> <bench args...>: kernels + memory copies (no API trac
   local tag=$1 out=$PWD/gpurun_out/c4copy_$1 repo=$PWD
   shift
   mkdir -p "$out"
-  (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace \
+  (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --stats \
      -d "$out/raw" -o run --output-format csv -- python3 "$repo/bench.py" "$@") > "$out/bench.log" 2>&1
   local rc=$?
   echo "=== c4copy_$tag rc=$rc"; tail -n 1 "$out/bench.log" | cut -c1-300
   [ $rc -eq 0 ] || return $rc
   python3 tools/c4_timeline.py "$out/raw" > "$out/timeline.txt" 2>&1
-  find "$out/raw" -name '*memory_copy_trace.csv' -exec cp {} "$out/memory_copy_trace.csv" \;
+  find "$out/raw" -name '*_stats.csv' -exec cp {} "$out/" \;
   rm -rf "$out/raw"
 }
 case $1 in
@@ -94,5 +94,17 @@ case $1 in
     (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats \
        -d "$out/prof" -o run --output-format csv -- python3 "$repo/tools/probe/d2h_apis.py") \
        > "$out/prof.log" 2>&1 && echo "=== prof ok" && rm -f "$out"/prof/*trace.csv ;;
-  *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi" >&2; exit 2 ;;
+  r7)
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py tests/test_gpu_rsync_stream.py -x &&
+    bash tools/gpu.sh bench c4r7 --mode rsync --steps 5 --warmup 1 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c4r7_10 --mode rsync --steps 10 --warmup 2 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c4share_r7 --mode rsync --share 3/8 --per-gpu-gib 32 --steps 6 --warmup 1 &&
+    c4copy c4r7 --mode rsync --steps 3 --warmup 1 --no-cpu-baseline ;;
+  r7b)
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py -x &&
+    bash tools/gpu.sh bench c4r7_10 --mode rsync --steps 10 --warmup 2 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c4r7_20 --mode rsync --steps 20 --warmup 2 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c4share_r7 --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 &&
+    c4copy c4r7b --mode rsync --steps 3 --warmup 1 --no-cpu-baseline ;;
+  *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b" >&2; exit 2 ;;
 esac

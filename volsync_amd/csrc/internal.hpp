@@ -481,7 +481,8 @@ hipError_t launch_rs_buckets(const uint64_t *tkey, uint32_t count, uint32_t rema
 hipError_t launch_rs_collect(const RsWalkArgs &a, uint32_t *cnt, uint32_t *pos, uint32_t *partials,
                              uint4 *out, unsigned long long *fa_total, hipStream_t s);
 hipError_t launch_rs_pad_sum2(const uint8_t *sum2, uint32_t count, uint32_t s2length,
-                              uint64_t *out, hipStream_t s);
+                              uint64_t *out, hipStream_t s, const uint32_t *sum1_in = nullptr,
+                              uint32_t *sum1_out = nullptr);
 // whole-file checksum (filesum.hip + filesum_host.cpp):
 // contributions of nb whole 1 KiB blocks -> C[nb][8] (block-major)
 hipError_t launch_fs_contrib(const uint8_t *p, uint64_t nb, uint64_t *C, hipStream_t s);

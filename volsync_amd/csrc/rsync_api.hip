@@ -1547,12 +1547,15 @@ int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
         else memcpy(j.acc, acc_in, 64);
         j.rows_first = j.nb > 0 && j.nb * 64 <= FsJob::kRowsCap && j.dma.init(j.device);
         if (j.rows_first) {
-            // all rows now, in stream order after the caller's queued work and
-            // ahead of whatever the caller queues next (the walk)
+            // all rows now, on the handle's stream: after the caller's queued
+            // work and ahead of whatever it queues next (the signatures, the
+            // walk).  On the job's low-priority stream the kernel ran beside
+            // the caller's next kernels and held CUs their small follow-up
+            // launches then waited for (the sum-table copy: 1 -> 10 ms).
             VS_TRY(j.rows.ensure((size_t)j.nb * 64));
-            VS_HIP(hipEventRecord(j.kev[0][0], j.s));
-            VS_HIP(launch_fs_contrib(p, j.nb, j.rows.as<uint64_t>(), j.s));
-            VS_HIP(hipEventRecord(j.kev[0][1], j.s));
+            VS_HIP(hipEventRecord(j.kev[0][0], h->stream));
+            VS_HIP(launch_fs_contrib(p, j.nb, j.rows.as<uint64_t>(), h->stream));
+            VS_HIP(hipEventRecord(j.kev[0][1], h->stream));
         } else {
             VS_TRY(j.dC.ensure((size_t)FsJob::kRing * j.piece * 64));
             if (whole) {   // the last partial block, last stripe: read back for the finish
@@ -2167,13 +2170,11 @@ VS_API int vs_rsync_load_sums_device(vs_rsync *h, int32_t count, int32_t blength
     const double t0 = now_ms();
     VS_TRY(h->d_sum1.ensure((size_t)std::max(count, 1) * 4));
     VS_TRY(order_after_null(h));
-    if (count)
-        VS_HIP(hipMemcpyAsync(h->d_sum1.p, dev_sum1, (size_t)count * 4, hipMemcpyDeviceToDevice,
-                              h->stream));
     VS_TRY(h->d_sum2p.ensure((size_t)std::max(count, 1) * 16));
-    if (count)
+    if (count)   // sum1 copied and sum2 padded in one kernel
         VS_HIP(launch_rs_pad_sum2(dev_sum2, (uint32_t)count, (uint32_t)s2length,
-                                  h->d_sum2p.as<uint64_t>(), h->stream));
+                                  h->d_sum2p.as<uint64_t>(), h->stream, dev_sum1,
+                                  h->d_sum1.as<uint32_t>()));
     VS_TRY(build_table(h));
     h->ms[1] = now_ms() - t0;
     return 0;

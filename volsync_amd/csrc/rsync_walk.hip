@@ -1296,11 +1296,15 @@ __global__ __launch_bounds__(kWalkThreads) void rs_walk_stitch_kernel(RsWalkArgs
     WPROG(a, lane, 22, 0, 0);
 }
 
-// sum2 (count x s2length bytes) -> 16 zero-padded bytes per block
+// sum2 (count x s2length bytes) -> 16 zero-padded bytes per block; with
+// sum1_in, also the handle's copy of sum1 (a kernel, not a runtime copy: in a
+// PyTorch process hipMemcpyAsync is a blit kernel, and that one measured 12 ms
+// for 2 MiB beside the whole-file checksum's SDMA read-back)
 __global__ void rs_pad_sum2_kernel(const uint8_t *sum2, uint32_t count, uint32_t s2length,
-                                   uint64_t *out) {
+                                   uint64_t *out, const uint32_t *sum1_in, uint32_t *sum1_out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
+    if (sum1_in) sum1_out[i] = sum1_in[i];
     uint64_t v[2] = {0, 0};
     for (uint32_t j = 0; j < s2length; ++j)
         v[j >> 3] |= (uint64_t)sum2[(uint64_t)i * s2length + j] << (8 * (j & 7));
@@ -1387,9 +1391,11 @@ hipError_t launch_rs_collect(const RsWalkArgs &a, uint32_t *cnt, uint32_t *pos, 
 }
 
 hipError_t launch_rs_pad_sum2(const uint8_t *sum2, uint32_t count, uint32_t s2length,
-                              uint64_t *out, hipStream_t s) {
+                              uint64_t *out, hipStream_t s, const uint32_t *sum1_in,
+                              uint32_t *sum1_out) {
     if (!count) return hipSuccess;
-    rs_pad_sum2_kernel<<<(count + 255) / 256, 256, 0, s>>>(sum2, count, s2length, out);
+    rs_pad_sum2_kernel<<<(count + 255) / 256, 256, 0, s>>>(sum2, count, s2length, out, sum1_in,
+                                                            sum1_out);
     return hipGetLastError();
 }
 
