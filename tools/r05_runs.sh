@@ -106,5 +106,8 @@ case $1 in
     bash tools/gpu.sh bench c4r7_20 --mode rsync --steps 20 --warmup 2 --no-cpu-baseline &&
     bash tools/gpu.sh bench c4share_r7 --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 &&
     c4copy c4r7b --mode rsync --steps 3 --warmup 1 --no-cpu-baseline ;;
-  *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b" >&2; exit 2 ;;
+  fpchains)
+    ab fp_chains 3 "base=,t512c4=$(var fpt512c4),t512c3=$(var fpt512c3),c3=$(var fpc3),t1024=$(var fpt1024)" \
+      tools/fp_only.py --gib 64 --reps 5 ;;
+  *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains" >&2; exit 2 ;;
 esac

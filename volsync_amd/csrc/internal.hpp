@@ -149,8 +149,14 @@ void pol_tables(uint64_t pol, uint64_t out_tab[256], uint64_t mod_tab[256]);
 void pol_out8(uint64_t pol, const uint64_t out_tab[256], uint64_t out8[256]);
 
 // ---- fingerprint pass ------------------------------------------------------
+// 16 waves per CU (128 VGPRs; the hot loop spill-free, 78 spilled VGPRs in
+// the rare re-roll / bounds-checked paths) against 12 (168 VGPRs): 21.4 vs
+// 21.8 ms per 64 GiB in three interleaved rounds, C2 1033.7 vs 1023.3 GB/s
+// (profiles/r05_fp); more chains per wave instead (3 or 4 strips per lane at
+// 8 or 12 waves) measured 25.8-26.7 ms: the pass wants independent waves
+// issuing, not deeper per-wave interleaving
 #ifndef VS_FP_THREADS
-#define VS_FP_THREADS 768
+#define VS_FP_THREADS 1024
 #endif
 constexpr int kFpThreads = VS_FP_THREADS;  // one workgroup per CU (LDS: 128 KiB tables)
 constexpr int kFpCopies = 32;      // lane-private table copies: conflict-free ds_read_b64
