@@ -26,6 +26,8 @@
 // offset and want_i) until it makes a match the speculative walk also made,
 // from where the two are identical.  The result is
 // bit-identical to hash_search: same matches, same false-alarm count.
+#include <utility>
+
 #include "internal.hpp"
 #include "strong.hpp"
 
@@ -183,11 +185,19 @@ __device__ __forceinline__ uint4 ldu16(const uint8_t *p) {
 // The seeded custom secret (XXH3_initCustomSecret: even words + seed, odd
 // words - seed), 24 words, staged in LDS once per workgroup: a lane reads its
 // stripe's two words with one ds_read2_b64 instead of holding 20 registers.
+// Words 24 .. 69 hold the pairs (w[i], w[i + 1]), i < 23, 16-byte aligned:
+// the wide flushes read a stripe's two words with one ds_read_b128 at a
+// lane-dependent stripe (wide_windows).
 struct RowSec {
-    const uint64_t *w;   // LDS, [24]
+    const uint64_t *w;   // LDS, [kSecWords]
 };
+constexpr uint32_t kSecWords = 24 + 2 * 23;
 __device__ __forceinline__ void load_secret(uint64_t *lsec, uint64_t seed) {
     if (threadIdx.x < 24) lsec[threadIdx.x] = vsstrong::sec64(threadIdx.x, seed);
+    if (threadIdx.x < 46) {
+        const uint32_t i = threadIdx.x >> 1;
+        lsec[24 + threadIdx.x] = vsstrong::sec64(i + (threadIdx.x & 1), seed);
+    }
 }
 
 __device__ __forceinline__ uint64_t scramble(uint64_t a, uint64_t sec) {
@@ -422,11 +432,51 @@ constexpr uint32_t kPredict = VS_PREDICT;   // blocks want .. want + 2 flag a li
 // profiles/r04_walk_step/ab_wd*)
 constexpr uint32_t kWideD = VS_WIDE_D;
 constexpr uint32_t kWideRingBytes = 3 * 1024;             // per wave: slots 0, 1, mirror of 0
+#ifndef VS_WIDE_RD
+#define VS_WIDE_RD 1
+#endif
+
+// f(integral_constant<uint32_t, I>) for I < N, unrolled at compile time (asm
+// immediates need constants)
+template <class F, uint32_t... I>
+__device__ __forceinline__ void sfor_(F &&f, std::integer_sequence<uint32_t, I...>) {
+    (f(std::integral_constant<uint32_t, I>{}), ...);
+}
+template <uint32_t N, class F>
+__device__ __forceinline__ void sfor(F &&f) {
+    sfor_(f, std::make_integer_sequence<uint32_t, N>{});
+}
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+// stripe S of a wide flush: 24 ring bytes (three ds_read_b64 from the
+// lane's rotated stripe base rb) and its secret pair (ds_read_b128); the
+// registers are written when wide_wait says so
+template <uint32_t S>
+__device__ __forceinline__ void wide_issue(uint32_t rb, uint32_t sb, uint64_t &r01, uint64_t &r23,
+                                           uint64_t &r45, u64x2 &kk) {
+    asm volatile(
+        "ds_read_b64 %0, %4 offset:%6\n\t"
+        "ds_read_b64 %1, %4 offset:%7\n\t"
+        "ds_read_b64 %2, %4 offset:%8\n\t"
+        "ds_read_b128 %3, %5 offset:%9"
+        : "=v"(r01), "=v"(r23), "=v"(r45), "=v"(kk)
+        : "v"(rb), "v"(sb), "n"(256 * (S >> 2)), "n"(256 * (S >> 2) + 8), "n"(256 * (S >> 2) + 16),
+          "n"(64 * (S >> 2))
+        : "memory");
+}
+// the Vth of eight stripes issued back to back has landed once at most the
+// later stripes' reads are outstanding (four each; the counter holds 15)
+template <uint32_t V>
+__device__ __forceinline__ void wide_wait(uint64_t &r01, uint64_t &r23, uint64_t &r45, u64x2 &kk) {
+    asm volatile("s_waitcnt lgkmcnt(%4)"
+                 : "+v"(r01), "+v"(r23), "+v"(r45), "+v"(kk)
+                 : "n"(4 * (7 - V) < 15 ? 4 * (7 - V) : 15)
+                 : "memory");
+}
 
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
 typedef __attribute__((address_space(3))) const uint64_t l_u64;
 typedef __attribute__((address_space(3))) uint8_t l_u8;
-typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) const u64x2 g_u64x2;
 // 16 bytes at any byte address (one global_load_dwordx4: gfx950 unaligned mode)
 __device__ __forceinline__ u64x2 gld2(g_u8 *p) {
@@ -455,9 +505,16 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
     const uint32_t j = lane >> 2, k = lane & 3;
     const int64_t h0 = (int64_t)rdl64((uint64_t)qh, 0);
     const int64_t hl = (int64_t)rdl64((uint64_t)qh, (int)(nq - 1));
+#if VS_WIDE_RD
+    // windows past nq copy window 0 (lower half) or 8 (upper half, if live)
+    // and read its addresses: an LDS broadcast, no bank of their own
+    const uint32_t jd = j < nq ? j : (j >= 8 && nq > 8 ? 8u : 0u);
+#else
+    const uint32_t jd = j < nq ? j : 0u;
+#endif
     const int64_t hj = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)qh >> 32),
-                                                             (int)(j < nq ? j : 0), 64) << 32) |
-                                 (uint32_t)__shfl((int)(uint32_t)qh, (int)(j < nq ? j : 0), 64));
+                                                             (int)jd, 64) << 32) |
+                                 (uint32_t)__shfl((int)(uint32_t)qh, (int)jd, 64));
     const uint32_t tau = (uint32_t)((hj - h0) >> 10);
     const uint32_t rj = (uint32_t)(hj - h0) - 1024 * tau;   // window j's offset in iteration t's 2 KiB
     const uint32_t sh = rj & 3;                              // its bytes' offset in LDS dwords
@@ -466,10 +523,54 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
     uint64_t a0 = (k == 0) ? P32_3 : (k == 1) ? P64_2 : (k == 2) ? P64_4 : P64_5;
     uint64_t a1 = (k == 0) ? P64_1 : (k == 1) ? P64_3 : (k == 2) ? P32_2 : P32_1;
     const uint64_t scr0 = sw0[16 + 2 * k], scr1 = sw0[17 + 2 * k];
+#if VS_WIDE_RD
+    // Bank-balanced stripe order.  A lane reads its 16 bytes of a stripe as
+    // three aligned ds_read_b64 (24 bytes from (rj & ~7) + 16 k + 64 sigma,
+    // realigned below), whose bank pair -- (address / 8) mod 32 within a
+    // 256-byte bank row -- is b + 8 sigma, b = (rj >> 3) + 2 k, plus the
+    // wave's ring base, common to all its lanes.  A half-wave (8 windows x 4 lanes)
+    // meets the 32 pairs in 8 classes (b mod 8), four pairs each (sigma
+    // mod 4 picks one); each lane walks its stripes in the order
+    // sigma = 4 g + ((u + q) & 3) for s = 4 g + u, q chosen so that the
+    // lanes of one class take distinct pairs at every s (their rank in the
+    // class, mod 4).  Random window offsets otherwise put several lanes of a
+    // half on one bank (the dword reads: 54 % of LDS cycles conflicted,
+    // profiles/r04_end).  XXH3 sums the stripes' contributions, so the order
+    // is free; the secret pair follows sigma.
+    uint32_t q;
+    {
+        const uint32_t b = (rj >> 3) + 2 * k;
+        const uint32_t cls = b & 7;
+        const bool part = j < nq || j == 8;
+        const uint64_t below = ((1ull << lane) - 1) & (lane < 32 ? 0xffffffffull : 0xffffffff00000000ull);
+        uint64_t mine = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < 8; ++c) {
+            const uint64_t m = __ballot(part && cls == c);
+            mine = cls == c ? m : mine;
+        }
+        const uint32_t rank = (uint32_t)__builtin_popcountll(mine & below);
+        const uint32_t qs = (uint32_t)(rank - (b >> 3)) & 3;
+        const uint32_t src = j < nq ? lane : (j >= 8 ? 32 + k : k);
+        q = (uint32_t)__shfl((int)qs, (int)src, 64);
+    }
+    const uint32_t e4 = (rj >> 2) & 1;   // the 16 bytes start in the qword's upper dword
+    const bool up = e4 != 0;
+    // LDS byte addresses: the ring, and the secret pairs (2 k + sigma)
+    const uint32_t ringa = (uint32_t)(uintptr_t)ring;
+    const uint32_t seca = (uint32_t)(uintptr_t)(sw0 + 24) + 32 * k;
+    uint32_t roff[4], sb[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+        roff[u] = (rj & ~7u) + 16 * k + 64 * ((u + q) & 3);
+        sb[u] = seca + 16 * ((u + q) & 3);
+    }
+#else
     // this lane's secret words for stripe s: sk[s], sk[s + 1], read from LDS
     // (held in 34 registers instead, the walk around the call spilled 23 more
     // VGPRs and ran 5-7 % slower: profiles/r04_walk_lds/ab3_*)
     l_u64 *sk = sw0 + 2 * k;
+#endif
     // KiB n of the span: [h0 + 1024 n, + 1024), lane l's 16 bytes (clamped at
     // the data end: no active window reads past it).  The loads are issued in
     // asm and waited for by hand (vmcnt counts in issue order): the compiler's
@@ -498,6 +599,7 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
     }
 #pragma unroll
     for (uint32_t i = 0; i < kWideD; ++i) inflight[i] = fetch(1 + i);
+    static_assert(kWideD % 2 == 0, "t & 1 == u & 1 below");
     for (uint32_t t0 = 0; t0 < T; t0 += kWideD) {
 #pragma unroll
         for (uint32_t u = 0; u < kWideD; ++u) {
@@ -509,6 +611,42 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
             asm volatile("s_waitcnt vmcnt(%1)" : "+v"(inflight[u]) : "n"(kWideD - 1) : "memory");
             put(t + 1, inflight[u]);
             inflight[u] = fetch(t + 1 + kWideD);
+            uint64_t c0 = 0, c1 = 0;
+#if VS_WIDE_RD
+            // the reads are issued in asm and waited for by hand: plain
+            // loads the compiler merges into ds_read2_b64 (8 LDS cycles
+            // against 2 for a ds_read_b64), volatile ones it waits for one
+            // stripe at a time
+            const uint32_t tb = (t & 1) << 10;
+            uint32_t rb[4];
+#pragma unroll
+            for (uint32_t w = 0; w < 4; ++w) rb[w] = ringa + roff[w] + tb;
+            sfor<2>([&](auto H) {
+                constexpr uint32_t h = decltype(H)::value;
+                uint64_t r01[8], r23[8], r45[8];
+                u64x2 kk[8];
+                sfor<8>([&](auto V) {
+                    constexpr uint32_t v = decltype(V)::value, s = 8 * h + v, w = s & 3;
+                    wide_issue<s>(rb[w], sb[w], r01[v], r23[v], r45[v], kk[v]);
+                });
+                sfor<8>([&](auto V) {
+                    constexpr uint32_t v = decltype(V)::value;
+                    wide_wait<v>(r01[v], r23[v], r45[v], kk[v]);
+                    const uint32_t r0 = (uint32_t)r01[v], r1 = (uint32_t)(r01[v] >> 32),
+                                   r2 = (uint32_t)r23[v], r3 = (uint32_t)(r23[v] >> 32),
+                                   r4 = (uint32_t)r45[v], r5 = (uint32_t)(r45[v] >> 32);
+                    const uint32_t z0 = up ? r1 : r0, z1 = up ? r2 : r1, z2 = up ? r3 : r2,
+                                   z3 = up ? r4 : r3, z4 = up ? r5 : r4;
+                    const uint32_t y0 = __builtin_amdgcn_alignbyte(z1, z0, sh);
+                    const uint32_t y1 = __builtin_amdgcn_alignbyte(z2, z1, sh);
+                    const uint32_t y2 = __builtin_amdgcn_alignbyte(z3, z2, sh);
+                    const uint32_t y3 = __builtin_amdgcn_alignbyte(z4, z3, sh);
+                    acc2(u64x2{((uint64_t)y1 << 32) | y0, ((uint64_t)y3 << 32) | y2}, kk[v].x,
+                         kk[v].y, c0, c1);
+                    __builtin_amdgcn_sched_barrier(0);   // hash stripe v before waiting for v + 1
+                });
+            });
+#else
             const l_u8 *w = ring + 1024 * (t & 1) + rj + 16 * k;
             // all 16 stripe reads in flight before any is hashed
             u64x2 d[16];
@@ -527,9 +665,9 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
                 d[s] = u64x2{((uint64_t)y1 << 32) | y0, ((uint64_t)y3 << 32) | y2};
             }
             __builtin_amdgcn_sched_barrier(0);
-            uint64_t c0 = 0, c1 = 0;
 #pragma unroll
             for (uint32_t s = 0; s < 16; ++s) acc2(d[s], sk[s], sk[s + 1], c0, c1);
+#endif
             const bool on = t >= tau && t - tau < nb;
             const uint64_t n0 = scramble(a0 + c0, scr0), n1 = scramble(a1 + c1, scr1);
             a0 = on ? n0 : a0;
@@ -1136,8 +1274,8 @@ __device__ __forceinline__ int64_t seg_hi(const RsWalkArgs &a, uint32_t k) {
 template <uint32_t T, uint32_t RING>
 __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
     __shared__ uint32_t lfilt[kLdsFiltWordsW];
-    __shared__ uint64_t lsec[24];
-    __shared__ __attribute__((aligned(16))) uint8_t wring[kWideRingBytes * (kWalkThreads / 64)];
+    __shared__ __attribute__((aligned(16))) uint64_t lsec[kSecWords];
+    __shared__ __attribute__((aligned(16))) uint8_t wring[kWideRingBytes * (kWalkThreads / 64) + 16];
     load_secret(lsec, a.seed);
     load_prefilter(a, lfilt);
     const uint32_t lane = threadIdx.x & 63;
@@ -1237,8 +1375,8 @@ __device__ __forceinline__ bool stitch_visited(const RsWalkArgs &a, uint32_t k, 
 // re-walks from it, merging into its speculative walk
 __global__ __launch_bounds__(kWalkThreads) void rs_walk_stitch_kernel(RsWalkArgs a) {
     __shared__ uint32_t lfilt[kLdsFiltWordsW];
-    __shared__ uint64_t lsec[24];
-    __shared__ __attribute__((aligned(16))) uint8_t wring[kWideRingBytes * (kWalkThreads / 64)];
+    __shared__ __attribute__((aligned(16))) uint64_t lsec[kSecWords];
+    __shared__ __attribute__((aligned(16))) uint8_t wring[kWideRingBytes * (kWalkThreads / 64) + 16];
     load_secret(lsec, a.seed);
     load_prefilter(a, lfilt);
     const uint32_t lane = threadIdx.x & 63;
