@@ -13,7 +13,8 @@ per SIMD.  Two classes dominate:
   ~4.2 cycles: v_alignbit/v_alignbyte/v_perm/v_add3/v_and_or/v_lshl_or/
                v_lshlrev_b32/v_bfe/v_min_u32, DPP/SDWA forms, v_bitop3_b32
                reading an SGPR, 64-bit shifts/adds;
-  v_cndmask_b32 reading VCC measured 22.7 cycles.
+  v_cndmask_b32: 4.25 as _e64 with an SGPR-pair mask, ~2.3 as _e32 reading the
+  VCC a v_cmp just wrote (the pair averages 3.3; profiles/r05_start/valu_ops3.json).
 The output is the issue-cycle floor of one trip of the loop, per wave:
 python tools/isa_mix.py volsync_amd/lib/obj/sha256-hip-amdgcn-amd-amdhsa-gfx950.s sha_slice_kernel
 """
@@ -39,7 +40,7 @@ COST = {
     "v_mul_lo_u32": SLOW, "v_mul_hi_u32": SLOW, "v_dot4_u32_u8": SLOW, "v_bfrev_b32": SLOW,
     "v_lshrrev_b64": SLOW, "v_lshlrev_b64": SLOW, "v_lshl_add_u64": SLOW,
     "v_add_co_u32": SLOW, "v_addc_co_u32": SLOW, "v_pk_mov_b32": SLOW, "v_pk_add_u16": SLOW,
-    "v_min3_u16": 8.2, "v_cndmask_b32": 22.7,
+    "v_min3_u16": 8.2, "v_cndmask_b32": FAST,
 }
 
 LABEL_RE = re.compile(r"^(\.LBB\d+_\d+):")
@@ -71,6 +72,8 @@ def classify(mn: str, ops: str):
             return "valu", SLOW if any(re.match(r"^(s\d|s\[|vcc|exec)", s) for s in srcs) else FAST
         if base in ("v_readfirstlane_b32", "v_readlane_b32", "v_writelane_b32"):
             return "valu", SLOW
+        if base == "v_cndmask_b32":
+            return "valu", SLOW if mn.endswith("_e64") else FAST
         if base.startswith("v_cmp") or base.startswith("v_cmpx"):
             return "valu", SLOW
         return "valu", COST.get(base, SLOW)
