@@ -36,13 +36,26 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 # reach ~2.35.  Priced at 2.4 GHz (above the measured 2.17-2.39 GHz, so the
 # fraction is not flattered): 256 CU x 4 SIMD x 64 lanes x 2.4 GHz / 4.2.
 VALU_PEAK_TOPS = 256 * 4 * 64 * 2.4e9 / 4.2 / 1e12   # 37.4 T lane-ops/s
-# the datasheet-style 2-cycle issue rate, reported beside it (valu_frac_2cyc)
-VALU_2CYC_TOPS = 256 * 4 * 64 * 2.4e9 / 2.0 / 1e12   # 78.6 T lane-ops/s
 # VALU lane-instructions per input byte, from SQ_INSTS_VALU (wave-instructions)
 # x 64 / bytes in profiles/r01_final: SHA-256 ~1490 per 64-byte block, the
 # fingerprint ~8.8 per byte
 SHA_OPS_PER_BYTE = 1490 / 64
 FP_OPS_PER_BYTE = 8.8
+# Mix-weighted issue cost: the hot loops' VALU
+# instructions priced by issue class (tools/isa_mix.py over the gfx950 ISA,
+# profiles/r05_isa): SHA-256's split engine, consumer rounds (905 VALU,
+# 3181.6 cycles per 64-chain block) + producer schedule (781, 2560.1) -> 3.41
+# cycles per instruction; the fingerprint's Fast53 strip loop (2228, 6773.6
+# per 256 chain-bytes) -> 3.04.  valu_frac = lane-ops/s x that cost over
+# 256 CU x 4 SIMD x 64 lanes x 2.4 GHz: the fraction of the issue floor.
+SHA_MIX_CYC = (3181.6 + 2560.1) / (905 + 781)
+FP_MIX_CYC = 6773.6 / 2228
+ISSUE_LANE_CYC = 256 * 4 * 64 * 2.4e9 / 1e12   # T lane-cycles/s
+
+
+def valu_frac(gbs: float, ops_per_byte: float, cyc: float) -> float:
+    """Fraction of the VALU issue floor used at gbs GB/s (mix-weighted)."""
+    return round(gbs * ops_per_byte / 1e3 * cyc / ISSUE_LANE_CYC, 4)
 
 
 def cpu_baseline(sample_bytes: int, threads: int):
@@ -726,8 +739,8 @@ def smallfiles_main(args):
             "exact": {"files": nf, "unique_ids": distinct, "id_digest": id_digest},
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                         "valu_frac": round(gbs * SHA_OPS_PER_BYTE / 1e3 / VALU_PEAK_TOPS, 4),
-                         "valu_frac_2cyc": round(gbs * SHA_OPS_PER_BYTE / 1e3 / VALU_2CYC_TOPS, 4),
+                         "valu_frac": valu_frac(gbs, SHA_OPS_PER_BYTE, SHA_MIX_CYC),
+                         "valu_frac_flat42": round(gbs * SHA_OPS_PER_BYTE / 1e3 / VALU_PEAK_TOPS, 4),
                          "kernel": "sha256 (hash engine, unbounded slice)"},
             "hash_wide": args.hash_wide,
         }
@@ -1462,12 +1475,12 @@ def main():
         "fingerprint": {"bound": "hbm", "achieved": round(fp_gbs, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(fp_gbs / HBM_PEAK_GBS, 4),
                         "traffic": None,
-                        "valu_frac": round(fp_gbs * FP_OPS_PER_BYTE / 1e3 / VALU_PEAK_TOPS, 4),
-                        "valu_frac_2cyc": round(fp_gbs * FP_OPS_PER_BYTE / 1e3 / VALU_2CYC_TOPS, 4)},
+                        "valu_frac": valu_frac(fp_gbs, FP_OPS_PER_BYTE, FP_MIX_CYC),
+                        "valu_frac_flat42": round(fp_gbs * FP_OPS_PER_BYTE / 1e3 / VALU_PEAK_TOPS, 4)},
         "sha256": {"bound": "hbm", "achieved": round(sha_gbs, 1), "peak": HBM_PEAK_GBS,
                    "unit": "GB/s", "frac": round(sha_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                   "valu_frac": round(sha_gbs * SHA_OPS_PER_BYTE / 1e3 / VALU_PEAK_TOPS, 4),
-                   "valu_frac_2cyc": round(sha_gbs * SHA_OPS_PER_BYTE / 1e3 / VALU_2CYC_TOPS, 4)},
+                   "valu_frac": valu_frac(sha_gbs, SHA_OPS_PER_BYTE, SHA_MIX_CYC),
+                   "valu_frac_flat42": round(sha_gbs * SHA_OPS_PER_BYTE / 1e3 / VALU_PEAK_TOPS, 4)},
     }
     # roofline.traffic: HBM bytes per step from the committed rocprofv3
     # FETCH_SIZE/WRITE_SIZE passes (profiles/traffic.json, tools/traffic.py),
@@ -1521,9 +1534,10 @@ def main():
             "stages_ms_per_step": {k: round(v, 3) for k, v in per_step.items()},
             "kernels": roof,
             # the whole step shares one resource: VALU issue (fingerprint +
-            # SHA-256 lane-ops over the step time, against the measured peak)
-            "pipeline_valu_frac": round(total * args.steps / dt * (SHA_OPS_PER_BYTE + FP_OPS_PER_BYTE)
-                                        / world / 1e12 / VALU_PEAK_TOPS, 4),
+            # SHA-256 lane-ops over the step time, each priced by its mix)
+            "pipeline_valu_frac": round(total * args.steps / dt / world / 1e12
+                                        * (SHA_OPS_PER_BYTE * SHA_MIX_CYC + FP_OPS_PER_BYTE * FP_MIX_CYC)
+                                        / ISSUE_LANE_CYC, 4),
             "hash_slice_blocks": args.hash_slice,
             "hash_stream": args.hash_stream,
             "hash_wide": args.hash_wide, "wide_drain": args.wide_drain,

@@ -112,9 +112,10 @@ case $1 in
   walk)  # bank-balanced wide-flush reads (VS_WIDE_RD=1) against the dword reads (rd0)
     S="--mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum"
     C="--mode rsync --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline"
-    bash tools/gpu.sh tests tests/test_gpu_rsync.py tests/test_gpu_cdc.py -x &&
-    ab walk_share 2 "rd0=$(var rd0),new=" bench.py $S &&
-    ab walk_c4 2 "rd0=$(var rd0),new=" bench.py $C &&
-    bash tools/gpu.sh prof r05_walk_share rs_walk $S ;;
+    L="rd0=$(var rd0),p2=$(var p2),new=,p4=$(var p4)"
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py -x &&
+    ab walk2_share 2 "$L" bench.py $S &&
+    ab walk2_c4 2 "$L" bench.py $C &&
+    bash tools/gpu.sh prof r05_walk2_share rs_walk $S ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac

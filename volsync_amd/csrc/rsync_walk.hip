@@ -464,13 +464,18 @@ __device__ __forceinline__ void wide_issue(uint32_t rb, uint32_t sb, uint64_t &r
           "n"(64 * (S >> 2))
         : "memory");
 }
-// the Vth of eight stripes issued back to back has landed once at most the
-// later stripes' reads are outstanding (four each; the counter holds 15)
-template <uint32_t V>
+// a stripe's four reads have landed once at most N later LDS operations
+// are outstanding (the counter holds 15)
+#ifndef VS_WIDE_PIPE
+#define VS_WIDE_PIPE 3
+#endif
+constexpr uint32_t kWidePipe = VS_WIDE_PIPE;   // stripes in flight per lane
+template <uint32_t N>
 __device__ __forceinline__ void wide_wait(uint64_t &r01, uint64_t &r23, uint64_t &r45, u64x2 &kk) {
+    static_assert(N <= 15, "lgkmcnt");
     asm volatile("s_waitcnt lgkmcnt(%4)"
                  : "+v"(r01), "+v"(r23), "+v"(r45), "+v"(kk)
-                 : "n"(4 * (7 - V) < 15 ? 4 * (7 - V) : 15)
+                 : "n"(N)
                  : "memory");
 }
 
@@ -555,7 +560,7 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
         q = (uint32_t)__shfl((int)qs, (int)src, 64);
     }
     const uint32_t e4 = (rj >> 2) & 1;   // the 16 bytes start in the qword's upper dword
-    const bool up = e4 != 0;
+    const uint32_t upm = e4 ? 0xffffffffu : 0u;   // select mask (a VGPR: v_bitop3 stays 2.3 cycles)
     // LDS byte addresses: the ring, and the secret pairs (2 k + sigma)
     const uint32_t ringa = (uint32_t)(uintptr_t)ring;
     const uint32_t seca = (uint32_t)(uintptr_t)(sw0 + 24) + 32 * k;
@@ -621,30 +626,42 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
             uint32_t rb[4];
 #pragma unroll
             for (uint32_t w = 0; w < 4; ++w) rb[w] = ringa + roff[w] + tb;
-            sfor<2>([&](auto H) {
-                constexpr uint32_t h = decltype(H)::value;
-                uint64_t r01[8], r23[8], r45[8];
-                u64x2 kk[8];
-                sfor<8>([&](auto V) {
-                    constexpr uint32_t v = decltype(V)::value, s = 8 * h + v, w = s & 3;
-                    wide_issue<s>(rb[w], sb[w], r01[v], r23[v], r45[v], kk[v]);
-                });
-                sfor<8>([&](auto V) {
-                    constexpr uint32_t v = decltype(V)::value;
-                    wide_wait<v>(r01[v], r23[v], r45[v], kk[v]);
-                    const uint32_t r0 = (uint32_t)r01[v], r1 = (uint32_t)(r01[v] >> 32),
-                                   r2 = (uint32_t)r23[v], r3 = (uint32_t)(r23[v] >> 32),
-                                   r4 = (uint32_t)r45[v], r5 = (uint32_t)(r45[v] >> 32);
-                    const uint32_t z0 = up ? r1 : r0, z1 = up ? r2 : r1, z2 = up ? r3 : r2,
-                                   z3 = up ? r4 : r3, z4 = up ? r5 : r4;
-                    const uint32_t y0 = __builtin_amdgcn_alignbyte(z1, z0, sh);
-                    const uint32_t y1 = __builtin_amdgcn_alignbyte(z2, z1, sh);
-                    const uint32_t y2 = __builtin_amdgcn_alignbyte(z3, z2, sh);
-                    const uint32_t y3 = __builtin_amdgcn_alignbyte(z4, z3, sh);
-                    acc2(u64x2{((uint64_t)y1 << 32) | y0, ((uint64_t)y3 << 32) | y2}, kk[v].x,
-                         kk[v].y, c0, c1);
-                    __builtin_amdgcn_sched_barrier(0);   // hash stripe v before waiting for v + 1
-                });
+            // three stripes in flight: stripe v + 3 is issued once v is hashed
+            uint64_t r01[16], r23[16], r45[16];
+            u64x2 kk[16];
+            sfor<kWidePipe>([&](auto V) {
+                constexpr uint32_t v = decltype(V)::value;
+                wide_issue<v>(rb[v & 3], sb[v & 3], r01[v], r23[v], r45[v], kk[v]);
+            });
+            sfor<16>([&](auto V) {
+                constexpr uint32_t v = decltype(V)::value;
+                constexpr uint32_t later = 15 - v < kWidePipe - 1 ? 15 - v : kWidePipe - 1;
+                wide_wait<4 * later>(r01[v], r23[v], r45[v], kk[v]);
+                const uint32_t r0 = (uint32_t)r01[v], r1 = (uint32_t)(r01[v] >> 32),
+                               r2 = (uint32_t)r23[v], r3 = (uint32_t)(r23[v] >> 32),
+                               r4 = (uint32_t)r45[v], r5 = (uint32_t)(r45[v] >> 32);
+                // all-VGPR v_bitop3 selects (2.3 cycles; a v_cndmask on an
+                // SGPR mask issues at 4.25)
+                const uint32_t z0 = __builtin_amdgcn_bitop3_b32(upm, r1, r0, 0xCA),
+                               z1 = __builtin_amdgcn_bitop3_b32(upm, r2, r1, 0xCA),
+                               z2 = __builtin_amdgcn_bitop3_b32(upm, r3, r2, 0xCA),
+                               z3 = __builtin_amdgcn_bitop3_b32(upm, r4, r3, 0xCA),
+                               z4 = __builtin_amdgcn_bitop3_b32(upm, r5, r4, 0xCA);
+                const uint32_t y0 = __builtin_amdgcn_alignbyte(z1, z0, sh);
+                const uint32_t y1 = __builtin_amdgcn_alignbyte(z2, z1, sh);
+                const uint32_t y2 = __builtin_amdgcn_alignbyte(z3, z2, sh);
+                const uint32_t y3 = __builtin_amdgcn_alignbyte(z4, z3, sh);
+                acc2(u64x2{((uint64_t)y1 << 32) | y0, ((uint64_t)y3 << 32) | y2}, kk[v].x,
+                     kk[v].y, c0, c1);
+                // the sums here, in stripe order: left to itself the compiler
+                // defers all 32 multiplies to the end and holds every
+                // stripe's words live (248 VGPRs, 46 of them saved per call)
+                asm volatile("" : "+v"(c0), "+v"(c1));
+                if constexpr (v + kWidePipe < 16)
+                    wide_issue<v + kWidePipe>(rb[(v + kWidePipe) & 3], sb[(v + kWidePipe) & 3],
+                                              r01[v + kWidePipe], r23[v + kWidePipe],
+                                              r45[v + kWidePipe], kk[v + kWidePipe]);
+                __builtin_amdgcn_sched_barrier(0);
             });
 #else
             const l_u8 *w = ring + 1024 * (t & 1) + rj + 16 * k;
