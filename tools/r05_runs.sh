@@ -117,5 +117,8 @@ case $1 in
     ab walk2_share 2 "$L" bench.py $S &&
     ab walk2_c4 2 "$L" bench.py $C &&
     bash tools/gpu.sh prof r05_walk2_share rs_walk $S ;;
+  sdma)  # does an SDMA device-to-host copy slow a latency-bound kernel? (THP / d2d controls)
+    timeout -k 10 300 tools/probe/bin/sdma_interf > gpurun_out/sdma_interf.json 2> gpurun_out/sdma_interf.err &&
+    echo "=== sdma ok" && cat gpurun_out/sdma_interf.json ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac
