@@ -71,6 +71,9 @@ static void dma(void *dst, hsa_agent_t dagent, const void *src, size_t total, si
 }
 
 int main() {
+    CK(hipSetDevice(0));
+    CK(hipFree(nullptr));   // the HIP runtime initialises HSA
+    if (hsa_init() != HSA_STATUS_SUCCESS) return 5;
     if (hsa_iterate_agents(find_agent, nullptr) != HSA_STATUS_SUCCESS) return 4;
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));

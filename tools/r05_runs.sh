@@ -118,7 +118,14 @@ case $1 in
     ab walk2_c4 2 "$L" bench.py $C &&
     bash tools/gpu.sh prof r05_walk2_share rs_walk $S ;;
   sdma)  # does an SDMA device-to-host copy slow a latency-bound kernel? (THP / d2d controls)
+    cat /sys/kernel/mm/transparent_hugepage/enabled > gpurun_out/thp.txt 2>&1
     timeout -k 10 300 tools/probe/bin/sdma_interf > gpurun_out/sdma_interf.json 2> gpurun_out/sdma_interf.err &&
     echo "=== sdma ok" && cat gpurun_out/sdma_interf.json ;;
+  diag)  # sdma probe, R7 with 3 / 2 file-sum jobs and none, C2 counters
+    bash tools/r05_runs.sh sdma &&
+    bash tools/gpu.sh bench c4r7_j3 --mode rsync --steps 10 --warmup 2 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c4r7_j2 --mode rsync --steps 10 --warmup 2 --no-cpu-baseline --file-sum-jobs 2 &&
+    bash tools/gpu.sh bench c4_nofs --mode rsync --steps 10 --warmup 2 --no-cpu-baseline --no-file-sum &&
+    bash tools/gpu.sh prof r05_c2 "fp_kernel|sha_slice" --gpus 1 --steps 5 --warmup 2 ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac
