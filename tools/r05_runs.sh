@@ -127,5 +127,8 @@ case $1 in
     bash tools/gpu.sh bench c4r7_j2 --mode rsync --steps 10 --warmup 2 --no-cpu-baseline --file-sum-jobs 2 &&
     bash tools/gpu.sh bench c4_nofs --mode rsync --steps 10 --warmup 2 --no-cpu-baseline --no-file-sum &&
     bash tools/gpu.sh prof r05_c2 "fp_kernel|sha_slice" --gpus 1 --steps 5 --warmup 2 ;;
+  r7iso)  # which part of R7 slows the walk: the host chain (fsnochain), the read-back (fsnodma)
+    L="base=,nochain=$(var fsnochain),nodma=$(var fsnodma)"
+    ab r7iso_c4 2 "$L" bench.py --mode rsync --steps 8 --warmup 2 --no-cpu-baseline ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac
