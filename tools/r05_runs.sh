@@ -130,5 +130,18 @@ case $1 in
   r7iso)  # which part of R7 slows the walk: the host chain (fsnochain), the read-back (fsnodma)
     L="base=,nochain=$(var fsnochain),nodma=$(var fsnodma)"
     ab r7iso_c4 2 "$L" bench.py --mode rsync --steps 8 --warmup 2 --no-cpu-baseline ;;
+  r7clock)  # the walk's effective clock with and without R7 (one counter pass each)
+    for cfg in r7 nofs; do
+      extra=""; [ $cfg = nofs ] && extra="--no-file-sum"
+      out=$PWD/gpurun_out/r7clock_$cfg; mkdir -p "$out/trace"; repo=$PWD
+      (cd /tmp && TMPDIR=/tmp timeout -k 10 400 rocprofv3 --kernel-trace --stats --pmc SQ_WAVES SQ_BUSY_CYCLES \
+         SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-include-regex "rs_walk_spec|rs_sig|fs_contrib" \
+         -d "$out/pmc_sq" -o run --output-format csv -- python3 "$repo/bench.py" --mode rsync --steps 4 --warmup 1 \
+         --no-cpu-baseline $extra) > "$out/bench.log" 2>&1 || exit $?
+      echo "=== r7clock $cfg ok"
+      find "$out/pmc_sq" -name '*kernel_stats.csv' -exec cp {} "$out/trace/" \;
+      python3 tools/summarize_prof.py "$out" --out "gpurun_out/r7clock_${cfg}_sum" > "$out/sum.log" 2>&1
+      rm -rf "$out/pmc_sq"
+    done ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac
