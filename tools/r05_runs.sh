@@ -143,5 +143,18 @@ case $1 in
       python3 tools/summarize_prof.py "$out" --out "gpurun_out/r7clock_${cfg}_sum" > "$out/sum.log" 2>&1
       rm -rf "$out/pmc_sq"
     done ;;
+  r7cyc)  # walk cycles per wave (s_memtime) with and without R7: clock or contention?
+    for cfg in r7 nofs r7b; do
+      extra=""; [ $cfg = nofs ] && extra="--no-file-sum"
+      VSGPU_LIB=$PWD/$(var walkprof) timeout -k 10 400 python bench.py --mode rsync --steps 4 --warmup 1 \
+        --no-cpu-baseline $extra > gpurun_out/r7cyc_$cfg.log 2>&1 || exit $?
+      echo "=== r7cyc $cfg"; grep "walk prof" gpurun_out/r7cyc_$cfg.log | tail -1 | cut -c1-400
+    done ;;
+  r7trace)  # per-job file-sum timelines (VS_FS_TRACE build) over four processes, to catch both modes
+    for i in 1 2 3 4; do
+      VSGPU_LIB=$PWD/$(var fstrace) timeout -k 10 400 python bench.py --mode rsync --steps 8 --warmup 2 \
+        --no-cpu-baseline > gpurun_out/r7trace_$i.log 2>&1 || exit $?
+      echo "=== r7trace $i: $(tail -1 gpurun_out/r7trace_$i.log | cut -c1-160)"
+    done ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac

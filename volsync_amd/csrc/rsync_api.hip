@@ -92,6 +92,7 @@ struct FsJob {
     uint64_t acc[8] = {};
     uint8_t digest[16] = {};
     double host_ms = 0, dev_ms = 0;
+    double t_call = 0;   // fs_start (VS_FS_TRACE builds report the job's timeline)
 };
 
 // ---- streamed forms: a file fed from host memory in order -------------------
@@ -1347,6 +1348,9 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
 #ifndef VS_FS_DIAG
 #define VS_FS_DIAG 0
 #endif
+#ifndef VS_FS_TRACE
+#define VS_FS_TRACE 0
+#endif
 void fs_thread(FsJob *j) {
     const bool serial = j->serial;
     const uint64_t unit = serial ? 1 : 1024;             // source bytes per item
@@ -1363,7 +1367,12 @@ void fs_thread(FsJob *j) {
     if (j->rows_first) {
         // every row is on the device once the kernel's event fires; pieces come
         // back on the DMA engine, copy i overlapping the chain of piece i - 1
+        const double t_thread = now_ms();
+        double dwait = 0;
+        (void)t_thread;
         const hipError_t e = hipEventSynchronize(j->kev[0][1]);
+        const double t_rows = now_ms();
+        (void)t_rows;
         if (e != hipSuccess) return fail_here(e, "file-sum rows kernel");
         float ms = 0;
         if (hipEventElapsedTime(&ms, j->kev[0][0], j->kev[0][1]) == hipSuccess) kms = ms;
@@ -1384,7 +1393,9 @@ void fs_thread(FsJob *j) {
         if (!start(0)) return fail_here(hipErrorUnknown, "file-sum rows read-back (DMA)");
         for (uint64_t i = 0; i < np; ++i) {
             const int r = (int)(i % FsJob::kRing);
+            const double w0 = now_ms();
             j->dma.wait(r);
+            dwait += now_ms() - w0;
             if (i + 1 < np && !start(i + 1))   // slot (i+1) % R: its chain finished last round
                 return fail_here(hipErrorUnknown, "file-sum rows read-back (DMA)");
             const uint64_t i0 = i * per, n = std::min(per, items - i0);
@@ -1400,6 +1411,16 @@ void fs_thread(FsJob *j) {
         if (j->whole) j->dma.wait(FsJob::kRing);
         j->host_ms = chain;
         j->dev_ms = kms;
+#if VS_FS_TRACE
+        {
+            static const double epoch = now_ms();
+            fprintf(stderr, "fs trace: job %p call %.1f thread %.1f rows %.1f dmawait %.1f chain %.1f end %.1f ms\n",
+                    (void *)j, j->t_call - epoch, t_thread - epoch, t_rows - epoch, dwait, chain,
+                    now_ms() - epoch);
+        }
+#else
+        (void)dwait;
+#endif
         return;
     }
     SerialSum ss;
@@ -1545,6 +1566,7 @@ int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
     j.rc = 0;
     j.err.clear();
     j.host_ms = j.dev_ms = 0;
+    j.t_call = now_ms();
     j.serial = serial;
     // after the caller's null-stream work and this handle's queued work
     VS_HIP(hipEventRecord(j.ev_in, h->stream));
