@@ -156,5 +156,8 @@ case $1 in
         --no-cpu-baseline > gpurun_out/r7trace_$i.log 2>&1 || exit $?
       echo "=== r7trace $i: $(tail -1 gpurun_out/r7trace_$i.log | cut -c1-160)"
     done ;;
+  numa)  # D2H DMA rate by NUMA node of the destination, by thread count, by SDMA engine
+    timeout -k 10 300 tools/probe/bin/d2h_numa > gpurun_out/d2h_numa.json 2> gpurun_out/d2h_numa.err;
+    rc=$?; cat gpurun_out/d2h_numa.json; head -5 gpurun_out/d2h_numa.err; exit $rc ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac
