@@ -125,15 +125,17 @@ int main() {
         std::ifstream f("/sys/devices/system/node/node" + std::to_string(n) + "/cpulist");
         if (f) nodes.push_back(n);
     }
-    uint32_t engines = 0;
+    uint32_t engines = 0, preferred = 0;
     hsa_amd_memory_copy_engine_status(g_cpu, g_gpu, &engines);
+    const int pst = (int)hsa_amd_memory_get_preferred_copy_engine(g_cpu, g_gpu, &preferred);
     const size_t n = 1ull << 30;
     void *dsrc;
     CK(hipMalloc(&dsrc, 3 * n));
     CK(hipMemset(dsrc, 1, 3 * n));
     printf("{\"gpu_bdf\": \"%s\", \"gpu_numa_node\": \"%s\", \"nodes_online\": \"%s\", "
-           "\"sdma_engine_mask_free\": %u, \"cpu_of_main\": %d, \"results\": [\n",
-           bdf, gnode.c_str(), online.c_str(), engines, sched_getcpu());
+           "\"sdma_engine_mask_free\": %u, \"preferred_mask\": %u, \"preferred_status\": %d, "
+           "\"cpu_of_main\": %d, \"results\": [\n",
+           bdf, gnode.c_str(), online.c_str(), engines, preferred, pst, sched_getcpu());
     bool first = true;
     auto line = [&](const std::string &what, double gbps) {
         printf("%s {\"what\": \"%s\", \"GBps\": %.1f}\n", first ? "" : ",", what.c_str(), gbps);
@@ -180,6 +182,22 @@ int main() {
         const bool ok = dma(hm, dsrc, n, e);
         line("hipHostMalloc, SDMA engine " + std::to_string(e) + (ok ? "" : " (refused)"),
              ok ? n / (now_ms() - t0) / 1e6 : 0);
+    }
+    // three threads at once on the preferred engine (else engine 1)
+    {
+        const int e = preferred ? __builtin_ctz(preferred) : 1;
+        void *b[3];
+        for (auto &x : b) CK(hipHostMalloc(&x, n, hipHostMallocDefault));
+        const double t0 = now_ms();
+        std::vector<std::thread> th;
+        for (int k = 0; k < 3; ++k) th.emplace_back(dma, b[k], (const char *)dsrc + k * n, n, e);
+        for (auto &t : th) t.join();
+        line("three threads (aggregate), all on SDMA engine " + std::to_string(e), 3 * n / (now_ms() - t0) / 1e6);
+        const double t1 = now_ms();
+        std::vector<std::thread> th2;
+        for (int k = 0; k < 3; ++k) th2.emplace_back(dma, b[k], (const char *)dsrc + k * n, n, -1);
+        for (auto &t : th2) t.join();
+        line("three threads (aggregate), runtime's choice", 3 * n / (now_ms() - t1) / 1e6);
     }
     printf("]}\n");
     return 0;

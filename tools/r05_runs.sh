@@ -159,5 +159,17 @@ case $1 in
   numa)  # D2H DMA rate by NUMA node of the destination, by thread count, by SDMA engine
     timeout -k 10 300 tools/probe/bin/d2h_numa > gpurun_out/d2h_numa.json 2> gpurun_out/d2h_numa.err;
     rc=$?; cat gpurun_out/d2h_numa.json; head -5 gpurun_out/d2h_numa.err; exit $rc ;;
+  r7eng)  # R7 with the read-back pinned to the preferred SDMA engine: four processes + the share
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py -x -k "file_sum" &&
+    for i in 1 2 3 4; do
+      VSGPU_LIB=$PWD/$(var fstrace) timeout -k 10 400 python bench.py --mode rsync --steps 10 --warmup 2 \
+        --no-cpu-baseline > gpurun_out/r7eng_$i.log 2>&1 || exit $?
+      echo "=== r7eng $i: $(tail -1 gpurun_out/r7eng_$i.log | cut -c1-160)"
+    done &&
+    for i in 1 2; do
+      timeout -k 10 400 python bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 \
+        > gpurun_out/r7eng_share_$i.log 2>&1 || exit $?
+      echo "=== r7eng share $i: $(tail -1 gpurun_out/r7eng_share_$i.log | cut -c1-160)"
+    done ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac

@@ -45,6 +45,8 @@ struct DmaD2H {
     void wait(int slot);                       // until copy `slot` has landed
     bool ready = false;
 
+    int engine = -1;                           // the SDMA engine copies go to (-1: the runtime's pick)
+
   private:
     uint64_t gpu_ = 0, cpu_ = 0;               // hsa_agent_t handles
     uint64_t sig_[kSignals] = {};              // hsa_signal_t handles
