@@ -171,5 +171,17 @@ case $1 in
         > gpurun_out/r7eng_share_$i.log 2>&1 || exit $?
       echo "=== r7eng share $i: $(tail -1 gpurun_out/r7eng_share_$i.log | cut -c1-160)"
     done ;;
+  final)  # the round's closing evidence -> gpurun_out (copied to profiles/r05_end)
+    bash tools/gpu.sh tests && bash tools/gpu.sh smoke && bash "$0" benches ;;
+  benches)
+    bash tools/gpu.sh bench c2 --gpus 1 --steps 20 --warmup 5 &&
+    bash tools/gpu.sh bench c3r3 --share 3/8 --steps 20 --warmup 5 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c4 --mode rsync --steps 10 --warmup 2 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c4_nofs --mode rsync --steps 5 --warmup 1 --no-file-sum &&
+    bash tools/gpu.sh bench c4share --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 &&
+    bash tools/gpu.sh bench c4share_nofs --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum &&
+    bash tools/gpu.sh bench c5 --mode smallfiles --steps 5 --warmup 1 &&
+    bash tools/gpu.sh bench seal --mode seal --steps 3 --warmup 1 &&
+    trace c2_end --gpus 1 --steps 20 --warmup 5 ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac
