@@ -38,7 +38,7 @@ int enter_device(int device);
 // HIP runtime's blit-kernel copies would queue behind them.  The caller orders
 // it after the kernel that wrote the source (an event synchronisation).
 struct DmaD2H {
-    static constexpr int kSignals = 4;
+    static constexpr int kSignals = 20;
     bool init(int device);                     // false: no DMA path (use hipMemcpyAsync)
     void release();
     bool start(int slot, void *dst, const void *src, size_t n);  // async; signal `slot`

@@ -66,7 +66,9 @@ struct RsRun {
 // the job starts -- before the caller's walk takes the CUs -- and the rows
 // come back on an SDMA engine (DmaD2H; a HIP copy in a PyTorch process is a
 // blit kernel, which waits for CUs the persistent walk holds) into a pinned
-// ring, chained on a host thread as each piece lands.  Without the DMA path,
+// buffer of the same size, all of its chunks queued at once so that the
+// engine serves jobs in order at its full rate, chained on a host thread as
+// each chunk lands.  Without the DMA path,
 // or for files whose rows exceed kRowsCap, contributions are computed one
 // piece at a time into a 3-deep device ring instead.  MD5, XXH64 and XXH3 of
 // <= 240 bytes are serial chains: the file's bytes come back through the same
@@ -75,6 +77,9 @@ struct FsJob {
     static constexpr uint64_t kRowsCap = 8ull << 30;   // rows of a 128 GiB file
     DmaD2H dma;
     DevBuf rows;                          // rows-first: every block's row
+    uint8_t *hrows = nullptr;             // rows-first: their pinned copy
+    uint64_t hrows_cap = 0;
+    static constexpr int kChunks = 16;    // rows-first read-back: copies queued per job
     bool rows_first = false;
     static constexpr int kRing = 3;
     uint64_t piece = 1ull << 18;          // blocks per piece (16 MiB of rows; serial: of bytes)
@@ -1378,37 +1383,43 @@ void fs_thread(FsJob *j) {
         if (hipEventElapsedTime(&ms, j->kev[0][0], j->kev[0][1]) == hipSuccess) kms = ms;
         (void)hipGetLastError();
         const uint8_t *rows = j->rows.as<uint8_t>();
-        auto start = [&](uint64_t i) -> bool {
-            const uint64_t i0 = i * per, n = std::min(per, items - i0);
-            return j->dma.start((int)(i % FsJob::kRing), j->hC[i % FsJob::kRing], rows + i0 * 64, n * 64);
-        };
+        // The whole read-back is queued at once, in kChunks copies (one
+        // signal each): the engine then serves this job's chunks back to back
+        // at its full rate, and the next job's after them.  With one copy in
+        // flight per job (a 3-deep ring of 16 MiB pieces, round 5's first
+        // form) three concurrent jobs shared the engine piece by piece; each
+        // chain then waited on its own copies and the jobs stayed
+        // overlapped: 240-266 ms of copy waits per job against 3-64 in the
+        // runs where they happened to stagger (profiles/r05_r7/trace).
+        const uint64_t total = items * 64;
+        const uint64_t cb = ((total + FsJob::kChunks - 1) / FsJob::kChunks + 63) & ~63ull;
+        const uint64_t nc = (total + cb - 1) / cb;
         if (j->whole) {   // the file's last <= 1088 bytes, for the finish
             const uint64_t keep = std::min<uint64_t>(j->len, 1088);
-            if (!j->dma.start(FsJob::kRing, j->hlast, j->src + j->len - keep, keep))
+            if (!j->dma.start(FsJob::kChunks, j->hlast, j->src + j->len - keep, keep))
                 return fail_here(hipErrorUnknown, "file-sum tail read-back (DMA)");
         }
-#if VS_FS_DIAG == 2   // diagnostic builds only (tools/r05_runs.sh r7iso): no read-back at all
-        (void)start;
-#else
-        if (!start(0)) return fail_here(hipErrorUnknown, "file-sum rows read-back (DMA)");
-        for (uint64_t i = 0; i < np; ++i) {
-            const int r = (int)(i % FsJob::kRing);
-            const double w0 = now_ms();
-            j->dma.wait(r);
-            dwait += now_ms() - w0;
-            if (i + 1 < np && !start(i + 1))   // slot (i+1) % R: its chain finished last round
+#if VS_FS_DIAG != 2   // (diagnostic builds, tools/r05_runs.sh r7iso: 2 = no read-back at all)
+        for (uint64_t c = 0; c < nc; ++c)
+            if (!j->dma.start((int)c, j->hrows + c * cb, rows + c * cb, std::min(cb, total - c * cb)))
                 return fail_here(hipErrorUnknown, "file-sum rows read-back (DMA)");
-            const uint64_t i0 = i * per, n = std::min(per, items - i0);
+        for (uint64_t c = 0; c < nc; ++c) {
+            const double w0 = now_ms();
+            j->dma.wait((int)c);
+            dwait += now_ms() - w0;
+            const uint64_t n = std::min(cb, total - c * cb) / 64;
             const double c0 = now_ms();
 #if VS_FS_DIAG != 1   // (1: the read-back without the host chain)
-            xxh3_chain_rows((const uint64_t *)j->hC[r], n, j->acc);
+            xxh3_chain_rows((const uint64_t *)(j->hrows + c * cb), n, j->acc);
 #else
             (void)n;
 #endif
             chain += now_ms() - c0;
         }
+#else
+        (void)nc;
 #endif
-        if (j->whole) j->dma.wait(FsJob::kRing);
+        if (j->whole) j->dma.wait(FsJob::kChunks);
         j->host_ms = chain;
         j->dev_ms = kms;
 #if VS_FS_TRACE
@@ -1525,6 +1536,9 @@ void fs_release(FsJob &j) {
     if (j.s) (void)hipStreamSynchronize(j.s);
     j.dma.release();
     j.rows.release();
+    pinned_free(j.hrows);
+    j.hrows = nullptr;
+    j.hrows_cap = 0;
     for (auto &p : j.hC) pinned_free(p), p = nullptr;
     pinned_free(j.hlast);
     j.hlast = nullptr;
@@ -1579,6 +1593,12 @@ int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
         if (whole || !acc_in) xxh3_init_acc(j.acc);
         else memcpy(j.acc, acc_in, 64);
         j.rows_first = j.nb > 0 && j.nb * 64 <= FsJob::kRowsCap && j.dma.init(j.device);
+        if (j.rows_first && j.hrows_cap < j.nb * 64) {   // the pinned copy (kept across jobs)
+            pinned_free(j.hrows);
+            j.hrows = (uint8_t *)pinned_alloc((size_t)j.nb * 64);
+            j.hrows_cap = j.hrows ? j.nb * 64 : 0;
+            j.rows_first = j.hrows != nullptr;   // else the bounded piece ring
+        }
         if (j.rows_first) {
             // all rows now, on the handle's stream: after the caller's queued
             // work and ahead of whatever it queues next (the signatures, the
