@@ -1593,10 +1593,27 @@ int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
         if (whole || !acc_in) xxh3_init_acc(j.acc);
         else memcpy(j.acc, acc_in, 64);
         j.rows_first = j.nb > 0 && j.nb * 64 <= FsJob::kRowsCap && j.dma.init(j.device);
-        if (j.rows_first && j.hrows_cap < j.nb * 64) {   // the pinned copy (kept across jobs)
-            pinned_free(j.hrows);
-            j.hrows = (uint8_t *)pinned_alloc((size_t)j.nb * 64);
-            j.hrows_cap = j.hrows ? j.nb * 64 : 0;
+        if (j.rows_first && j.hrows_cap < j.nb * 64) {
+            // The pinned copy, kept across jobs.  Page-locking 4 GiB takes
+            // ~175 ms on the caller's thread, so every idle slot of the FIFO
+            // is sized at once (the first file pays for all, not the first
+            // file of each slot: profiles/r05_r7/queued)
+            auto grow = [&](FsJob &o) {
+                pinned_free(o.hrows);
+                o.hrows = (uint8_t *)pinned_alloc((size_t)j.nb * 64);
+                o.hrows_cap = o.hrows ? j.nb * 64 : 0;
+            };
+            grow(j);
+            if (!sync)
+                for (uint32_t k = 0; k < vs_rsync::kFsJobs; ++k) {
+                    FsJob &o = h->fs[k];
+                    const uint32_t pos = (k - h->fs_head) % vs_rsync::kFsJobs;
+                    const bool busy = pos < h->fs_tail - h->fs_head;   // in flight
+                    if (&o != &j && !busy && o.hrows_cap < j.nb * 64) {
+                        if (o.th.joinable()) o.th.join();
+                        grow(o);
+                    }
+                }
             j.rows_first = j.hrows != nullptr;   // else the bounded piece ring
         }
         if (j.rows_first) {
