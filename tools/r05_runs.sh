@@ -176,7 +176,7 @@ case $1 in
   benches)
     bash tools/gpu.sh bench c2 --gpus 1 --steps 20 --warmup 5 &&
     bash tools/gpu.sh bench c3r3 --share 3/8 --steps 20 --warmup 5 --no-cpu-baseline &&
-    bash tools/gpu.sh bench c4 --mode rsync --steps 10 --warmup 2 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c4 --mode rsync --steps 20 --warmup 2 --no-cpu-baseline &&
     bash tools/gpu.sh bench c4_nofs --mode rsync --steps 5 --warmup 1 --no-file-sum &&
     bash tools/gpu.sh bench c4share --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 &&
     bash tools/gpu.sh bench c4share_nofs --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum &&
