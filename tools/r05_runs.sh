@@ -183,5 +183,10 @@ case $1 in
     bash tools/gpu.sh bench c5 --mode smallfiles --steps 5 --warmup 1 &&
     bash tools/gpu.sh bench seal --mode seal --steps 3 --warmup 1 &&
     trace c2_end --gpus 1 --steps 20 --warmup 5 ;;
+  walkwd)  # deeper flush prefetch now that wide_windows holds 136 VGPRs (no callee saves)
+    S="--mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum"
+    C="--mode rsync --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline"
+    L="base=,wd6=$(var wd6),wd8=$(var wd8)"
+    ab walkwd_share 2 "$L" bench.py $S && ab walkwd_c4 2 "$L" bench.py $C ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac
