@@ -425,11 +425,15 @@ constexpr uint32_t kWideQ = 16;
 #endif
 constexpr uint32_t kPredict = VS_PREDICT;   // blocks want .. want + 2 flag a likely resync hit
 #ifndef VS_WIDE_D
-#define VS_WIDE_D 4
+#define VS_WIDE_D 8
 #endif
-// KiB in flight per wave: 4 (2, 4, 6, 8 measured 44.6, 45.2, 46.5, 46.3 ms of
-// share walk: fewer registers held across the call beat a deeper prefetch,
-// profiles/r04_walk_step/ab_wd*)
+// KiB in flight per wave: 8.  Round 4 measured 2, 4, 6, 8 at 44.6, 45.2, 46.5,
+// 46.3 ms of share walk (fewer registers held across the call beat a deeper
+// prefetch, profiles/r04_walk_step/ab_wd*); with round 5's 136-VGPR flush (no
+// callee saves) 4, 6, 8 measure 41.67-41.76, 41.56-41.58, 41.08-41.13 ms at
+// the share and 41.0-41.3, 41.05-41.16, 40.64-40.75 at the 64 GiB shape
+// (profiles/r05_walk/prefetch); 12 and 16 no longer unroll (the ring goes to
+// scratch)
 constexpr uint32_t kWideD = VS_WIDE_D;
 constexpr uint32_t kWideRingBytes = 3 * 1024;             // per wave: slots 0, 1, mirror of 0
 #ifndef VS_WIDE_RD
