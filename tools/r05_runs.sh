@@ -188,5 +188,11 @@ case $1 in
     C="--mode rsync --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline"
     L="base=,wd6=$(var wd6),wd8=$(var wd8)"
     ab walkwd_share 2 "$L" bench.py $S && ab walkwd_c4 2 "$L" bench.py $C ;;
+  post)  # after the 8 KiB flush prefetch: the rsync GPU tests and the walk lines
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py tests/test_gpu_rsync_stream.py -x &&
+    bash tools/gpu.sh bench c4share_nofs_wd8 --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum &&
+    bash tools/gpu.sh bench c4_nofs_wd8 --mode rsync --steps 5 --warmup 1 --no-file-sum &&
+    bash tools/gpu.sh bench c4_wd8 --mode rsync --steps 20 --warmup 2 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c4share_wd8 --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac
