@@ -194,5 +194,7 @@ case $1 in
     bash tools/gpu.sh bench c4_nofs_wd8 --mode rsync --steps 5 --warmup 1 --no-file-sum &&
     bash tools/gpu.sh bench c4_wd8 --mode rsync --steps 20 --warmup 2 --no-cpu-baseline &&
     bash tools/gpu.sh bench c4share_wd8 --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 ;;
+  fpocc)  # fingerprint occupancy against the SHA slices sharing the CUs: 512 / 768 / 1024 threads
+    ab fpocc_c2 2 "base=,t512=$(var fpt512),t768=$(var fpt768)" bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac
