@@ -196,5 +196,9 @@ case $1 in
     bash tools/gpu.sh bench c4share_wd8 --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 ;;
   fpocc)  # fingerprint occupancy against the SHA slices sharing the CUs: 512 / 768 / 1024 threads
     ab fpocc_c2 2 "base=,t512=$(var fpt512),t768=$(var fpt768)" bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
+  fsab)  # contribution rows kernel: 8 lanes per block (128-byte lines per instruction) against 4
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py tests/test_gpu_rsync_stream.py -x -k "file_sum or relay or stream" &&
+    ab fsab_c4 2 "fs4=$(var fs4),new=" bench.py --mode rsync --steps 10 --warmup 2 --no-cpu-baseline &&
+    ab fsab_share 2 "fs4=$(var fs4),new=" bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac

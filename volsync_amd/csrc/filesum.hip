@@ -34,6 +34,47 @@ __device__ __forceinline__ uint4 ldu16(const uint8_t *p) {
 // reads one 64-byte row per block.  Lane (g, m) of a wave owns block
 // 16 w + g, accumulators 2m and 2m + 1: the four lanes of a block read its
 // 64-byte stripes as one contiguous 64-byte access and write its row as one.
+#ifndef VS_FS_LANES
+#define VS_FS_LANES 8
+#endif
+#if VS_FS_LANES == 8
+// Eight lanes per block: lane (g, m8) of a wave owns block 8 w + g and reads
+// 16 bytes at 16 m8 of every 128-byte pair of stripes, so one load
+// instruction covers eight blocks' whole 128-byte lines (four lanes per
+// block touched 64-byte halves: the other half came in the next
+// instruction); lanes m8 and m8 + 4 then add their two stripes' sums.
+__global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint64_t nb,
+                                                         uint64_t *C) {
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, g = lane >> 3, m8 = lane & 7, m = m8 & 3, h = m8 >> 2;
+    const uint64_t b0 = (gid >> 6) * 8 + g;
+    const bool live = b0 < nb;
+    const uint64_t b = live ? b0 : nb - 1;   // (dead lanes still take part in the sum)
+    const uint8_t *q = p + b * 1024 + 16 * m8;
+    uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+        const uint32_t s = 2 * i + h;
+        const uint4 v = ldu16(q + 128 * i);
+        const uint64_t d0 = ((uint64_t)v.y << 32) | v.x, d1 = ((uint64_t)v.w << 32) | v.z;
+        const uint64_t k0 = d0 ^ kSecret64[s + 2 * m], k1 = d1 ^ kSecret64[s + 2 * m + 1];
+        c0 += (uint64_t)(uint32_t)k0 * (k0 >> 32) + d1;
+        c1 += (uint64_t)(uint32_t)k1 * (k1 >> 32) + d0;
+    }
+    // + the partner lane's stripes (lane ^ 4)
+    c0 += ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(c0 >> 32), 4, 64) << 32) |
+          (uint32_t)__shfl_xor((int)(uint32_t)c0, 4, 64);
+    c1 += ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(c1 >> 32), 4, 64) << 32) |
+          (uint32_t)__shfl_xor((int)(uint32_t)c1, 4, 64);
+    if (!live || h) return;
+    uint4 o;
+    o.x = (uint32_t)c0;
+    o.y = (uint32_t)(c0 >> 32);
+    o.z = (uint32_t)c1;
+    o.w = (uint32_t)(c1 >> 32);
+    *(uint4 *)(C + b * 8 + 2 * m) = o;
+}
+#else
 __global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint64_t nb,
                                                          uint64_t *C) {
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -57,12 +98,13 @@ __global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint6
     o.w = (uint32_t)(c1 >> 32);
     *(uint4 *)(C + b * 8 + 2 * m) = o;
 }
+#endif
 
 }  // namespace
 
 hipError_t launch_fs_contrib(const uint8_t *p, uint64_t nb, uint64_t *C, hipStream_t s) {
     if (!nb) return hipSuccess;
-    const uint64_t waves = (nb + 15) / 16;
+    const uint64_t waves = (nb + 64 / VS_FS_LANES - 1) / (64 / VS_FS_LANES);
     fs_contrib_kernel<<<(uint32_t)((waves + 3) / 4), 256, 0, s>>>(p, nb, C);
     return hipGetLastError();
 }
