@@ -200,5 +200,7 @@ case $1 in
     bash tools/gpu.sh tests tests/test_gpu_rsync.py tests/test_gpu_rsync_stream.py -x -k "file_sum or relay or stream" &&
     ab fsab_c4 2 "fs4=$(var fs4),new=" bench.py --mode rsync --steps 10 --warmup 2 --no-cpu-baseline &&
     ab fsab_share 2 "fs4=$(var fs4),new=" bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 ;;
+  fsab2)  # contribution rows kernel: 16 lanes per block against 8
+    ab fsab2_c4 2 "new=,fs16=$(var fs16)" bench.py --mode rsync --steps 10 --warmup 2 --no-cpu-baseline ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac

@@ -37,37 +37,43 @@ __device__ __forceinline__ uint4 ldu16(const uint8_t *p) {
 #ifndef VS_FS_LANES
 #define VS_FS_LANES 8
 #endif
-#if VS_FS_LANES == 8
+#if VS_FS_LANES >= 8
 // Eight lanes per block: lane (g, m8) of a wave owns block 8 w + g and reads
 // 16 bytes at 16 m8 of every 128-byte pair of stripes, so one load
 // instruction covers eight blocks' whole 128-byte lines (four lanes per
 // block touched 64-byte halves: the other half came in the next
 // instruction); lanes m8 and m8 + 4 then add their two stripes' sums.
 // 64 GiB: 13.8 -> 12.4 ms, and the walk after it 52.2 -> 50.3 ms (the clock
-// the pass costs it; profiles/r05_r7/contrib8)
+// the pass costs it; profiles/r05_r7/contrib8).  (VS_FS_LANES = 16: four
+// blocks of 256-byte runs per instruction, two rounds of sums.)
 __global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint64_t nb,
                                                          uint64_t *C) {
+    constexpr uint32_t LN = VS_FS_LANES, SP = LN / 4;   // lanes per block, stripes per load
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63, g = lane >> 3, m8 = lane & 7, m = m8 & 3, h = m8 >> 2;
-    const uint64_t b0 = (gid >> 6) * 8 + g;
+    const uint32_t lane = threadIdx.x & 63, g = lane / LN, ml = lane & (LN - 1), m = ml & 3,
+                   h = ml >> 2;
+    const uint64_t b0 = (gid >> 6) * (64 / LN) + g;
     const bool live = b0 < nb;
-    const uint64_t b = live ? b0 : nb - 1;   // (dead lanes still take part in the sum)
-    const uint8_t *q = p + b * 1024 + 16 * m8;
+    const uint64_t b = live ? b0 : nb - 1;   // (dead lanes still take part in the sums)
+    const uint8_t *q = p + b * 1024 + 16 * ml;
     uint64_t c0 = 0, c1 = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) {
-        const uint32_t s = 2 * i + h;
-        const uint4 v = ldu16(q + 128 * i);
+    for (uint32_t i = 0; i < 16 / SP; ++i) {
+        const uint32_t s = SP * i + h;
+        const uint4 v = ldu16(q + 64 * SP * i);
         const uint64_t d0 = ((uint64_t)v.y << 32) | v.x, d1 = ((uint64_t)v.w << 32) | v.z;
         const uint64_t k0 = d0 ^ kSecret64[s + 2 * m], k1 = d1 ^ kSecret64[s + 2 * m + 1];
         c0 += (uint64_t)(uint32_t)k0 * (k0 >> 32) + d1;
         c1 += (uint64_t)(uint32_t)k1 * (k1 >> 32) + d0;
     }
-    // + the partner lane's stripes (lane ^ 4)
-    c0 += ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(c0 >> 32), 4, 64) << 32) |
-          (uint32_t)__shfl_xor((int)(uint32_t)c0, 4, 64);
-    c1 += ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(c1 >> 32), 4, 64) << 32) |
-          (uint32_t)__shfl_xor((int)(uint32_t)c1, 4, 64);
+    // + the other lanes' stripes of the block (lane ^ 4, ^ 8, ...)
+#pragma unroll
+    for (uint32_t o = 4; o < LN; o <<= 1) {
+        c0 += ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(c0 >> 32), (int)o, 64) << 32) |
+              (uint32_t)__shfl_xor((int)(uint32_t)c0, (int)o, 64);
+        c1 += ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(c1 >> 32), (int)o, 64) << 32) |
+              (uint32_t)__shfl_xor((int)(uint32_t)c1, (int)o, 64);
+    }
     if (!live || h) return;
     uint4 o;
     o.x = (uint32_t)c0;
