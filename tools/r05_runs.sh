@@ -202,5 +202,10 @@ case $1 in
     ab fsab_share 2 "fs4=$(var fs4),new=" bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 ;;
   fsab2)  # contribution rows kernel: 16 lanes per block against 8
     ab fsab2_c4 2 "new=,fs16=$(var fs16)" bench.py --mode rsync --steps 10 --warmup 2 --no-cpu-baseline ;;
+  steprange)  # STEP validity as one range per lane against a compare pair per offset (sr0)
+    S="--mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum"
+    C="--mode rsync --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline"
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py -x -k "walk or real_density or stitch or shard" &&
+    ab sr_share 2 "sr0=$(var sr0),new=" bench.py $S && ab sr_c4 2 "sr0=$(var sr0),new=" bench.py $C ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac

@@ -49,6 +49,9 @@ constexpr uint32_t kWalkThreads = VS_WALK_T;             // 8 waves (up to 256 V
 constexpr uint32_t kWalkRing = VS_WALK_RRING;                  // window blocks in flight per lane in the wave walk
 constexpr uint32_t kLdsFiltWordsW = 1u << 15;      // 2^20-bit LDS prefilter
 constexpr uint64_t kBatch = 1024;                  // STEP offsets per wave batch (16 per lane)
+#ifndef VS_STEP_RANGE
+#define VS_STEP_RANGE 1
+#endif
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -1068,7 +1071,6 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
             const uint32_t Y = excl_scan(E + 16u * P - (uint32_t)L * X, lane);
             uint32_t s1 = t1 + P;
             uint32_t s2 = t2 + 16u * lane * t1 + Y;
-            uint32_t valid = 0;
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
                 st.sums[t] = __builtin_amdgcn_perm(s2, s1, 0x05040100u);  // (s1 & 0xffff) | (s2 << 16)
@@ -1076,9 +1078,21 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 const int32_t xi = __builtin_amdgcn_sbfe((int)wi[t >> 2], 8 * (t & 3), 8);
                 s1 += (uint32_t)(xi - xo);
                 s2 = s2 - (uint32_t)L * (uint32_t)xo + s1;
+            }
+#if VS_STEP_RANGE
+            // offsets c + t in [fromb, fend): bits [lo, hi) (one range per
+            // lane, not a 64-bit compare pair per offset)
+            const int64_t lo = min<int64_t>(max<int64_t>(fromb - (int64_t)c, 0), 16);
+            const int64_t hi = min<int64_t>(max<int64_t>(fend - (int64_t)c, 0), 16);
+            const uint32_t valid = ((1u << (uint32_t)hi) - 1u) & ~((1u << (uint32_t)lo) - 1u);
+#else
+            uint32_t valid = 0;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
                 const int64_t qo = (int64_t)c + t;
                 valid |= (uint32_t)(qo >= fromb && qo < fend) << t;
             }
+#endif
             st.t1 = (uint32_t)__builtin_amdgcn_readlane((int)s1, 63);
             st.t2 = (uint32_t)__builtin_amdgcn_readlane((int)s2, 63);
             wadd(wp, kPrStepSums, tb);
