@@ -35,7 +35,7 @@ __device__ __forceinline__ uint4 ldu16(const uint8_t *p) {
 // 16 w + g, accumulators 2m and 2m + 1: the four lanes of a block read its
 // 64-byte stripes as one contiguous 64-byte access and write its row as one.
 #ifndef VS_FS_LANES
-#define VS_FS_LANES 8
+#define VS_FS_LANES 16
 #endif
 #if VS_FS_LANES >= 8
 // Eight lanes per block: lane (g, m8) of a wave owns block 8 w + g and reads
@@ -44,8 +44,9 @@ __device__ __forceinline__ uint4 ldu16(const uint8_t *p) {
 // block touched 64-byte halves: the other half came in the next
 // instruction); lanes m8 and m8 + 4 then add their two stripes' sums.
 // 64 GiB: 13.8 -> 12.4 ms, and the walk after it 52.2 -> 50.3 ms (the clock
-// the pass costs it; profiles/r05_r7/contrib8).  (VS_FS_LANES = 16: four
-// blocks of 256-byte runs per instruction, two rounds of sums.)
+// the pass costs it; profiles/r05_r7/contrib8).  Sixteen lanes (shipped):
+// four blocks' 256-byte runs per instruction, two rounds of sums; 12.3 ms,
+// and the walk after it 45.0-45.2 ms (profiles/r05_r7/contrib16).
 __global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint64_t nb,
                                                          uint64_t *C) {
     constexpr uint32_t LN = VS_FS_LANES, SP = LN / 4;   // lanes per block, stripes per load
