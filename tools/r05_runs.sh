@@ -207,5 +207,10 @@ case $1 in
     C="--mode rsync --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline"
     bash tools/gpu.sh tests tests/test_gpu_rsync.py -x -k "walk or real_density or stitch or shard" &&
     ab sr_share 2 "sr0=$(var sr0),new=" bench.py $S && ab sr_c4 2 "sr0=$(var sr0),new=" bench.py $C ;;
+  fsab3)  # contribution rows kernel: 32 / 64 lanes per block against 16
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py -x -k "file_sum" &&
+    VSGPU_LIB=$PWD/$(var fs64) bash tools/gpu.sh tests tests/test_gpu_rsync.py -x -k "file_sum" &&
+    ab fsab3_c4 2 "new=,fs32=$(var fs32),fs64=$(var fs64)" bench.py --mode rsync --steps 10 --warmup 2 --no-cpu-baseline &&
+    ab fsab3_share 1 "new=,fs32=$(var fs32),fs64=$(var fs64)" bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac
