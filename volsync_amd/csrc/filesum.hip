@@ -15,6 +15,8 @@
 // the contributions read back in pieces).  MD5, XXH64 and
 // XXH3 of <= 240 bytes are serial chains with no parallel form: the host
 // thread hashes the file's bytes as they are read back (filesum_host.cpp).
+#include <algorithm>
+
 #include "internal.hpp"
 #include "strong.hpp"
 
@@ -50,10 +52,14 @@ __device__ __forceinline__ uint4 ldu16(const uint8_t *p) {
 __global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint64_t nb,
                                                          uint64_t *C) {
     constexpr uint32_t LN = VS_FS_LANES, SP = LN / 4;   // lanes per block, stripes per load
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63, g = lane / LN, ml = lane & (LN - 1), m = ml & 3,
                    h = ml >> 2;
-    const uint64_t b0 = (gid >> 6) * (64 / LN) + g;
+    // a grid-stride loop over the waves' block groups (a 128 GiB file is
+    // 2^27 blocks: one wave per group would overrun the grid's size limit)
+    const uint64_t nw = (nb + 64 / LN - 1) / (64 / LN);
+    const uint64_t stride = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += stride) {
+    const uint64_t b0 = w * (64 / LN) + g;
     const bool live = b0 < nb;
     const uint64_t b = live ? b0 : nb - 1;   // (dead lanes still take part in the sums)
     const uint8_t *q = p + b * 1024 + 16 * ml;
@@ -75,13 +81,15 @@ __global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint6
         c1 += ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(c1 >> 32), (int)o, 64) << 32) |
               (uint32_t)__shfl_xor((int)(uint32_t)c1, (int)o, 64);
     }
-    if (!live || h) return;
-    uint4 o;
-    o.x = (uint32_t)c0;
-    o.y = (uint32_t)(c0 >> 32);
-    o.z = (uint32_t)c1;
-    o.w = (uint32_t)(c1 >> 32);
-    *(uint4 *)(C + b * 8 + 2 * m) = o;
+    if (live && !h) {
+        uint4 o;
+        o.x = (uint32_t)c0;
+        o.y = (uint32_t)(c0 >> 32);
+        o.z = (uint32_t)c1;
+        o.w = (uint32_t)(c1 >> 32);
+        *(uint4 *)(C + b * 8 + 2 * m) = o;
+    }
+    }
 }
 #else
 __global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint64_t nb,
@@ -114,7 +122,13 @@ __global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint6
 hipError_t launch_fs_contrib(const uint8_t *p, uint64_t nb, uint64_t *C, hipStream_t s) {
     if (!nb) return hipSuccess;
     const uint64_t waves = (nb + 64 / VS_FS_LANES - 1) / (64 / VS_FS_LANES);
-    fs_contrib_kernel<<<(uint32_t)((waves + 3) / 4), 256, 0, s>>>(p, nb, C);
+#if VS_FS_LANES >= 8
+    // up to 2^20 workgroups (4 M waves); the kernel strides over the rest
+    const uint64_t wgs = std::min<uint64_t>((waves + 3) / 4, 1ull << 20);
+#else
+    const uint64_t wgs = (waves + 3) / 4;
+#endif
+    fs_contrib_kernel<<<(uint32_t)wgs, 256, 0, s>>>(p, nb, C);
     return hipGetLastError();
 }
 
