@@ -123,8 +123,11 @@ hipError_t launch_fs_contrib(const uint8_t *p, uint64_t nb, uint64_t *C, hipStre
     if (!nb) return hipSuccess;
     const uint64_t waves = (nb + 64 / VS_FS_LANES - 1) / (64 / VS_FS_LANES);
 #if VS_FS_LANES >= 8
-    // up to 2^20 workgroups (4 M waves); the kernel strides over the rest
-    const uint64_t wgs = std::min<uint64_t>((waves + 3) / 4, 1ull << 20);
+    // one wave per block group up to 2^24 workgroups (the grid's 2^32-thread
+    // limit; at 16 lanes a 128 GiB file needs 2^23); the kernel strides over
+    // any rest.  (Capped at 2^20 workgroups, every wave striding, the 64 GiB
+    // pass took 12.7-12.9 ms against 12.3: profiles/r05_r7/contrib_lanes.)
+    const uint64_t wgs = std::min<uint64_t>((waves + 3) / 4, 1ull << 24);
 #else
     const uint64_t wgs = (waves + 3) / 4;
 #endif
