@@ -318,9 +318,10 @@ int vs_rsync_timing(vs_rsync *h, double ms_out[5]);
  * as sum_end writes it -- xxh128: LE low64 then LE high64; xxh3 / xxh64: LE
  * 64-bit value (out[8..15] zeroed); md5: the digest.  XXH3 runs as parallel
  * block contributions on the device plus one serial scramble chain on a host
- * thread; MD5 and XXH64 -- serial chains with no parallel
- * form -- are hashed on a library host thread from the file's bytes read back
- * through the same pinned ring.  Any length.  Blocks until done.  It runs on
+ * thread (for files up to 128 GiB the contribution rows,
+ * len / 16 bytes, are held on the device and in pinned host memory); MD5 and
+ * XXH64 -- serial chains with no parallel form -- are hashed on a library host
+ * thread from the file's bytes read back through a pinned ring.  Any length.  Blocks until done.  It runs on
  * a job of its own: jobs other calls left in flight stay in flight, keep their
  * _wait order and do not limit it (nor does it count toward their 4). */
 int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int csum_type,
