@@ -212,5 +212,8 @@ case $1 in
     VSGPU_LIB=$PWD/$(var fs64) bash tools/gpu.sh tests tests/test_gpu_rsync.py -x -k "file_sum" &&
     ab fsab3_c4 2 "new=,fs32=$(var fs32),fs64=$(var fs64)" bench.py --mode rsync --steps 10 --warmup 2 --no-cpu-baseline &&
     ab fsab3_share 1 "new=,fs32=$(var fs32),fs64=$(var fs64)" bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 ;;
+  endprof)  # counter passes of the final tree's walk (real-C4 rank) and C2 (perturbed: --pmc)
+    bash tools/gpu.sh prof r05_end_walkshare rs_walk --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum &&
+    bash tools/gpu.sh prof r05_end_c4 "rs_walk|fs_contrib|rs_sig" --mode rsync --steps 3 --warmup 1 ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac
