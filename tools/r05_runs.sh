@@ -128,6 +128,8 @@ case $1 in
     bash tools/gpu.sh bench c4_nofs --mode rsync --steps 10 --warmup 2 --no-cpu-baseline --no-file-sum &&
     bash tools/gpu.sh prof r05_c2 "fp_kernel|sha_slice" --gpus 1 --steps 5 --warmup 2 ;;
   r7iso)  # which part of R7 slows the walk: the host chain (fsnochain), the read-back (fsnodma)
+    # (historical: the VS_FS_DIAG build flag these variants used was removed
+    # after the run, profiles/r05_r7/iso)
     L="base=,nochain=$(var fsnochain),nodma=$(var fsnodma)"
     ab r7iso_c4 2 "$L" bench.py --mode rsync --steps 8 --warmup 2 --no-cpu-baseline ;;
   r7clock)  # the walk's effective clock with and without R7 (one counter pass each)
@@ -215,5 +217,10 @@ case $1 in
   endprof)  # counter passes of the final tree's walk (real-C4 rank) and C2 (perturbed: --pmc)
     bash tools/gpu.sh prof r05_end_walkshare rs_walk --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum &&
     bash tools/gpu.sh prof r05_end_c4 "rs_walk|fs_contrib|rs_sig" --mode rsync --steps 3 --warmup 1 ;;
+  clean)  # the tree after removing the losing / equal variant paths: walk + file-sum tests and lines
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py tests/test_gpu_rsync_stream.py -x &&
+    bash tools/gpu.sh bench c4share_nofs_clean --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum &&
+    bash tools/gpu.sh bench c4_clean --mode rsync --steps 20 --warmup 2 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c4share_clean --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac

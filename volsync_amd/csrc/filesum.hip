@@ -37,9 +37,10 @@ __device__ __forceinline__ uint4 ldu16(const uint8_t *p) {
 // 16 w + g, accumulators 2m and 2m + 1: the four lanes of a block read its
 // 64-byte stripes as one contiguous 64-byte access and write its row as one.
 #ifndef VS_FS_LANES
-#define VS_FS_LANES 16
+#define VS_FS_LANES 16   // 4 .. 64 (A/B builds: profiles/r05_r7/contrib*)
 #endif
-#if VS_FS_LANES >= 8
+static_assert(VS_FS_LANES >= 4 && VS_FS_LANES <= 64 && (VS_FS_LANES & (VS_FS_LANES - 1)) == 0,
+              "lanes per block");
 // Eight lanes per block: lane (g, m8) of a wave owns block 8 w + g and reads
 // 16 bytes at 16 m8 of every 128-byte pair of stripes, so one load
 // instruction covers eight blocks' whole 128-byte lines (four lanes per
@@ -91,46 +92,17 @@ __global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint6
     }
     }
 }
-#else
-__global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint64_t nb,
-                                                         uint64_t *C) {
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63, g = lane >> 2, m = lane & 3;
-    const uint64_t b = (gid >> 6) * 16 + g;
-    if (b >= nb) return;
-    const uint8_t *q = p + b * 1024 + 16 * m;
-    uint64_t c0 = 0, c1 = 0;
-#pragma unroll
-    for (uint32_t s = 0; s < 16; ++s) {
-        const uint4 v = ldu16(q + 64 * s);
-        const uint64_t d0 = ((uint64_t)v.y << 32) | v.x, d1 = ((uint64_t)v.w << 32) | v.z;
-        const uint64_t k0 = d0 ^ kSecret64[s + 2 * m], k1 = d1 ^ kSecret64[s + 2 * m + 1];
-        c0 += (uint64_t)(uint32_t)k0 * (k0 >> 32) + d1;
-        c1 += (uint64_t)(uint32_t)k1 * (k1 >> 32) + d0;
-    }
-    uint4 o;
-    o.x = (uint32_t)c0;
-    o.y = (uint32_t)(c0 >> 32);
-    o.z = (uint32_t)c1;
-    o.w = (uint32_t)(c1 >> 32);
-    *(uint4 *)(C + b * 8 + 2 * m) = o;
-}
-#endif
 
 }  // namespace
 
 hipError_t launch_fs_contrib(const uint8_t *p, uint64_t nb, uint64_t *C, hipStream_t s) {
     if (!nb) return hipSuccess;
     const uint64_t waves = (nb + 64 / VS_FS_LANES - 1) / (64 / VS_FS_LANES);
-#if VS_FS_LANES >= 8
     // one wave per block group up to 2^24 workgroups (the grid's 2^32-thread
     // limit; at 16 lanes a 128 GiB file needs 2^23); the kernel strides over
     // any rest.  (Capped at 2^20 workgroups, every wave striding, the 64 GiB
     // pass took 12.7-12.9 ms against 12.3: profiles/r05_r7/contrib_lanes.)
     const uint64_t wgs = std::min<uint64_t>((waves + 3) / 4, 1ull << 24);
-#else
-    const uint64_t wgs = (waves + 3) / 4;
-#endif
     fs_contrib_kernel<<<(uint32_t)wgs, 256, 0, s>>>(p, nb, C);
     return hipGetLastError();
 }

@@ -1350,9 +1350,6 @@ int match_device(vs_rsync *h, const void *dev_src, int64_t len, int64_t *n_match
 // bytes themselves, P * 64 at a time), then chained / hashed on the host.
 // Stream order on j->s keeps a device slot until its read-back is done; a
 // pinned slot is refilled only after the host consumed it.
-#ifndef VS_FS_DIAG
-#define VS_FS_DIAG 0
-#endif
 #ifndef VS_FS_TRACE
 #define VS_FS_TRACE 0
 #endif
@@ -1399,7 +1396,6 @@ void fs_thread(FsJob *j) {
             if (!j->dma.start(FsJob::kChunks, j->hlast, j->src + j->len - keep, keep))
                 return fail_here(hipErrorUnknown, "file-sum tail read-back (DMA)");
         }
-#if VS_FS_DIAG != 2   // (diagnostic builds, tools/r05_runs.sh r7iso: 2 = no read-back at all)
         for (uint64_t c = 0; c < nc; ++c)
             if (!j->dma.start((int)c, j->hrows + c * cb, rows + c * cb, std::min(cb, total - c * cb)))
                 return fail_here(hipErrorUnknown, "file-sum rows read-back (DMA)");
@@ -1409,16 +1405,9 @@ void fs_thread(FsJob *j) {
             dwait += now_ms() - w0;
             const uint64_t n = std::min(cb, total - c * cb) / 64;
             const double c0 = now_ms();
-#if VS_FS_DIAG != 1   // (1: the read-back without the host chain)
             xxh3_chain_rows((const uint64_t *)(j->hrows + c * cb), n, j->acc);
-#else
-            (void)n;
-#endif
             chain += now_ms() - c0;
         }
-#else
-        (void)nc;
-#endif
         if (j->whole) j->dma.wait(FsJob::kChunks);
         j->host_ms = chain;
         j->dev_ms = kms;

@@ -49,9 +49,6 @@ constexpr uint32_t kWalkThreads = VS_WALK_T;             // 8 waves (up to 256 V
 constexpr uint32_t kWalkRing = VS_WALK_RRING;                  // window blocks in flight per lane in the wave walk
 constexpr uint32_t kLdsFiltWordsW = 1u << 15;      // 2^20-bit LDS prefilter
 constexpr uint64_t kBatch = 1024;                  // STEP offsets per wave batch (16 per lane)
-#ifndef VS_STEP_RANGE
-#define VS_STEP_RANGE 1
-#endif
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -417,8 +414,9 @@ __device__ RowWin rows_window(const RsWalkArgs &a, const RowSec &rs, uint32_t la
 // that span once, 16 bytes per lane, kWideD iterations ahead (4 registers per
 // KiB in flight), and writes it into a per-wave LDS ring of two 1 KiB slots
 // plus a mirror of slot 0 (so a window's 2 KiB are always contiguous); the
-// windows read their stripes from there (five aligned dwords per 16 bytes,
-// realigned with v_alignbyte by the window's byte offset).  Windows
+// windows read their stripes from there (three aligned qwords per 16 bytes,
+// in a bank-balanced per-lane stripe order, realigned by the window's byte
+// offset; see wide_windows).  Windows
 // not yet started or already finished compute on stale bytes and keep their
 // accumulators.  Same XXH3 as rows_window; window j's results sit in lanes
 // 4j .. 4j+3.
@@ -439,9 +437,6 @@ constexpr uint32_t kPredict = VS_PREDICT;   // blocks want .. want + 2 flag a li
 // scratch)
 constexpr uint32_t kWideD = VS_WIDE_D;
 constexpr uint32_t kWideRingBytes = 3 * 1024;             // per wave: slots 0, 1, mirror of 0
-#ifndef VS_WIDE_RD
-#define VS_WIDE_RD 1
-#endif
 
 // f(integral_constant<uint32_t, I>) for I < N, unrolled at compile time (asm
 // immediates need constants)
@@ -517,13 +512,9 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
     const uint32_t j = lane >> 2, k = lane & 3;
     const int64_t h0 = (int64_t)rdl64((uint64_t)qh, 0);
     const int64_t hl = (int64_t)rdl64((uint64_t)qh, (int)(nq - 1));
-#if VS_WIDE_RD
     // windows past nq copy window 0 (lower half) or 8 (upper half, if live)
     // and read its addresses: an LDS broadcast, no bank of their own
     const uint32_t jd = j < nq ? j : (j >= 8 && nq > 8 ? 8u : 0u);
-#else
-    const uint32_t jd = j < nq ? j : 0u;
-#endif
     const int64_t hj = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)qh >> 32),
                                                              (int)jd, 64) << 32) |
                                  (uint32_t)__shfl((int)(uint32_t)qh, (int)jd, 64));
@@ -535,7 +526,6 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
     uint64_t a0 = (k == 0) ? P32_3 : (k == 1) ? P64_2 : (k == 2) ? P64_4 : P64_5;
     uint64_t a1 = (k == 0) ? P64_1 : (k == 1) ? P64_3 : (k == 2) ? P32_2 : P32_1;
     const uint64_t scr0 = sw0[16 + 2 * k], scr1 = sw0[17 + 2 * k];
-#if VS_WIDE_RD
     // Bank-balanced stripe order.  A lane reads its 16 bytes of a stripe as
     // three aligned ds_read_b64 (24 bytes from (rj & ~7) + 16 k + 64 sigma,
     // realigned below), whose bank pair -- (address / 8) mod 32 within a
@@ -577,12 +567,6 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
         roff[u] = (rj & ~7u) + 16 * k + 64 * ((u + q) & 3);
         sb[u] = seca + 16 * ((u + q) & 3);
     }
-#else
-    // this lane's secret words for stripe s: sk[s], sk[s + 1], read from LDS
-    // (held in 34 registers instead, the walk around the call spilled 23 more
-    // VGPRs and ran 5-7 % slower: profiles/r04_walk_lds/ab3_*)
-    l_u64 *sk = sw0 + 2 * k;
-#endif
     // KiB n of the span: [h0 + 1024 n, + 1024), lane l's 16 bytes (clamped at
     // the data end: no active window reads past it).  The loads are issued in
     // asm and waited for by hand (vmcnt counts in issue order): the compiler's
@@ -624,7 +608,6 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
             put(t + 1, inflight[u]);
             inflight[u] = fetch(t + 1 + kWideD);
             uint64_t c0 = 0, c1 = 0;
-#if VS_WIDE_RD
             // the reads are issued in asm and waited for by hand: plain
             // loads the compiler merges into ds_read2_b64 (8 LDS cycles
             // against 2 for a ds_read_b64), volatile ones it waits for one
@@ -670,28 +653,6 @@ __device__ __noinline__ RowWin wide_windows(g_u8 *data, uint64_t dlen, l_u64 *sw
                                               r45[v + kWidePipe], kk[v + kWidePipe]);
                 __builtin_amdgcn_sched_barrier(0);
             });
-#else
-            const l_u8 *w = ring + 1024 * (t & 1) + rj + 16 * k;
-            // all 16 stripe reads in flight before any is hashed
-            u64x2 d[16];
-#pragma unroll
-            for (uint32_t s = 0; s < 16; ++s) {
-                // five 4-byte-aligned dwords, realigned by the window's byte
-                // offset: unaligned ds_read_b128s took the LDS several passes
-                // each (share walk 54.9 -> 45.8 ms, profiles/r04_walk_lds/ab5_*)
-                typedef __attribute__((address_space(3))) const uint32_t l_u32;
-                l_u32 *q = (l_u32 *)(w + 64 * s - sh);
-                const uint32_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3], x4 = q[4];
-                const uint32_t y0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
-                const uint32_t y1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
-                const uint32_t y2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
-                const uint32_t y3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
-                d[s] = u64x2{((uint64_t)y1 << 32) | y0, ((uint64_t)y3 << 32) | y2};
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (uint32_t s = 0; s < 16; ++s) acc2(d[s], sk[s], sk[s + 1], c0, c1);
-#endif
             const bool on = t >= tau && t - tau < nb;
             const uint64_t n0 = scramble(a0 + c0, scr0), n1 = scramble(a1 + c1, scr1);
             a0 = on ? n0 : a0;
@@ -1079,20 +1040,12 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 s1 += (uint32_t)(xi - xo);
                 s2 = s2 - (uint32_t)L * (uint32_t)xo + s1;
             }
-#if VS_STEP_RANGE
             // offsets c + t in [fromb, fend): bits [lo, hi) (one range per
-            // lane, not a 64-bit compare pair per offset)
+            // lane, not a 64-bit compare pair per offset: share walk
+            // 41.4 -> 40.7 ms, profiles/r05_walk/steprange)
             const int64_t lo = min<int64_t>(max<int64_t>(fromb - (int64_t)c, 0), 16);
             const int64_t hi = min<int64_t>(max<int64_t>(fend - (int64_t)c, 0), 16);
             const uint32_t valid = ((1u << (uint32_t)hi) - 1u) & ~((1u << (uint32_t)lo) - 1u);
-#else
-            uint32_t valid = 0;
-#pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                const int64_t qo = (int64_t)c + t;
-                valid |= (uint32_t)(qo >= fromb && qo < fend) << t;
-            }
-#endif
             st.t1 = (uint32_t)__builtin_amdgcn_readlane((int)s1, 63);
             st.t2 = (uint32_t)__builtin_amdgcn_readlane((int)s2, 63);
             wadd(wp, kPrStepSums, tb);
