@@ -222,5 +222,9 @@ case $1 in
     bash tools/gpu.sh bench c4share_nofs_clean --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum &&
     bash tools/gpu.sh bench c4_clean --mode rsync --steps 20 --warmup 2 --no-cpu-baseline &&
     bash tools/gpu.sh bench c4share_clean --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 ;;
+  last)  # the final tree: the whole GPU suite, smoke, C2 at the driver's 20/5, C5
+    bash tools/gpu.sh tests && bash tools/gpu.sh smoke &&
+    bash tools/gpu.sh bench c2_last --gpus 1 --steps 20 --warmup 5 &&
+    bash tools/gpu.sh bench c5_last --mode smallfiles --steps 5 --warmup 1 ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac
