@@ -226,5 +226,32 @@ case $1 in
     bash tools/gpu.sh tests && bash tools/gpu.sh smoke &&
     bash tools/gpu.sh bench c2_last --gpus 1 --steps 20 --warmup 5 &&
     bash tools/gpu.sh bench c5_last --mode smallfiles --steps 5 --warmup 1 ;;
+  occ)  # walk occupancy: no LDS prefilter (8 waves / CU), and 12 waves / CU at 168 VGPRs
+    S="--mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum"
+    C="--mode rsync --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline"
+    VSGPU_LIB=$PWD/$(var occ3) bash tools/gpu.sh tests tests/test_gpu_rsync.py -x -k "walk or real_density or stitch or shard" &&
+    ab occ_share 2 "base=,nopf=$(var nopf),occ3=$(var occ3)" bench.py $S &&
+    ab occ_c4 2 "base=,nopf=$(var nopf),occ3=$(var occ3)" bench.py $C ;;
+  sig)  # signature pass: 8 / 16 lanes per block against 4
+    VSGPU_LIB=$PWD/$(var sig16) bash tools/gpu.sh tests tests/test_gpu_rsync.py -x -k "signature or golden or c4_params or sharded" &&
+    VSGPU_LIB=$PWD/$(var sig8) bash tools/gpu.sh tests tests/test_gpu_rsync.py -x -k "signatures_vs_golden" &&
+    ab sig_share 2 "base=,sig8=$(var sig8),sig16=$(var sig16)" bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum ;;
+  sig2)  # signature pass shipped at 8 lanes: the rsync GPU tests, then against 4 lanes at both shapes
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py tests/test_gpu_rsync_stream.py -x &&
+    ab sig2_share 3 "sig8=,sig4=$(var sig4)" bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum &&
+    ab sig2_c4 3 "sig8=,sig4=$(var sig4)" bench.py --mode rsync --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline ;;
+  wprof)  # walk phases per wave, with the wide flushes' iterations and windows per pass
+    for cfg in share c4; do
+      if [ $cfg = share ]; then args="--share 3/8 --per-gpu-gib 32"; else args="--no-cpu-baseline"; fi
+      VSGPU_LIB=$PWD/$(var walkprof) timeout -k 10 400 python bench.py --mode rsync --steps 3 --warmup 1 \
+        --no-file-sum $args > gpurun_out/wprof_$cfg.log 2>&1 || exit $?
+      echo "=== wprof $cfg"; grep "walk prof" gpurun_out/wprof_$cfg.log | tail -1 | cut -c1-900
+    done ;;
+  prio)  # wave priority: STEP batches (latency chains) above flushes and RUN windows (VALU)
+    S="--mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum"
+    C="--mode rsync --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline"
+    VSGPU_LIB=$PWD/$(var prio2) bash tools/gpu.sh tests tests/test_gpu_rsync.py -x -k "walk or real_density or stitch" &&
+    ab prio_share 2 "base=,prio1=$(var prio1),prio2=$(var prio2)" bench.py $S &&
+    ab prio_c4 2 "base=,prio1=$(var prio1),prio2=$(var prio2)" bench.py $C ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac

@@ -320,6 +320,131 @@ __global__ __launch_bounds__(256) void rs_sig_coop_kernel(RsSigArgs a) {
     }
 }
 
+// LN lanes per block (LN = 8 .. 64): lane (h, m) of a block's group reads
+// 16 bytes at 16 (4 h + m) of every run of LN / 4 stripes, so one load
+// instruction covers 64 / LN blocks' LN * 16-byte runs instead of sixteen
+// 64-byte pieces; lane m's accumulators 2m, 2m + 1 sum the group's stripes
+// (xor-shuffles over h) before each 1 KiB scramble, which every h repeats.
+#ifndef VS_SIG_LANES
+#define VS_SIG_LANES 8   // 4: rs_sig_coop_kernel; 8 .. 64: rs_sig_coopn_kernel
+#endif
+static_assert(VS_SIG_LANES >= 4 && VS_SIG_LANES <= 64 && (VS_SIG_LANES & (VS_SIG_LANES - 1)) == 0,
+              "lanes per block");
+template <uint32_t LN>
+__device__ __forceinline__ void coopn_long(const uint8_t *p, uint64_t len, uint64_t seed, uint32_t ml,
+                                           uint64_t &a0, uint64_t &a1, uint32_t &sx, uint32_t &sux) {
+    using namespace vsstrong;
+    constexpr uint32_t SP = LN / 4, NI = 16 / SP;
+    const uint32_t m = ml & 3, h = ml >> 2;
+    const uint64_t init[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+    a0 = init[0];
+    a1 = init[1];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+        a0 = (m == (uint32_t)j) ? init[2 * j] : a0;
+        a1 = (m == (uint32_t)j) ? init[2 * j + 1] : a1;
+    }
+    sx = 0;
+    sux = 0;
+    const uint64_t nb = (len - 1) / 1024;
+    const uint64_t scr0 = sec64(16 + 2 * m, seed), scr1 = sec64(17 + 2 * m, seed);
+    uint64_t ks0[NI], ks1[NI];
+#pragma unroll
+    for (uint32_t i = 0; i < NI; ++i) {
+        ks0[i] = sec64(SP * i + h + 2 * m, seed);
+        ks1[i] = sec64(SP * i + h + 2 * m + 1, seed);
+    }
+    auto fold = [&](uint64_t &c0, uint64_t &c1) {
+#pragma unroll
+        for (uint32_t o = 4; o < LN; o <<= 1) {
+            c0 += shfl_xor64(c0, (int)o);
+            c1 += shfl_xor64(c1, (int)o);
+        }
+    };
+    for (uint64_t b = 0; b < nb; ++b) {
+        const uint8_t *q = p + b * 1024 + 16 * ml;
+        uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < NI; ++i) {
+            uint64_t d0, d1;
+            ld16u(q + 64 * SP * i, d0, d1);
+            const uint32_t pos = (uint32_t)(b * 1024 + 64 * SP * i + 16 * ml);
+            weak8(d0, pos, sx, sux);
+            weak8(d1, pos + 8, sx, sux);
+            const uint64_t x0 = d0 ^ ks0[i], x1 = d1 ^ ks1[i];
+            c0 += (uint64_t)(uint32_t)x0 * (x0 >> 32) + d1;
+            c1 += (uint64_t)(uint32_t)x1 * (x1 >> 32) + d0;
+        }
+        fold(c0, c1);
+        a0 += c0;
+        a0 ^= a0 >> 47;
+        a0 ^= scr0;
+        a0 *= P32_1;
+        a1 += c1;
+        a1 ^= a1 >> 47;
+        a1 ^= scr1;
+        a1 *= P32_1;
+    }
+    // the partial block's ns stripes (no scramble)
+    const uint32_t ns = (uint32_t)(((len - 1) - nb * 1024) / 64);
+    {
+        uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < NI; ++i) {
+            const uint32_t s = SP * i + h;
+            if (s < ns) {
+                const uint64_t off = nb * 1024 + 64 * s + 16 * m;
+                uint64_t d0, d1;
+                ld16u(p + off, d0, d1);
+                weak8(d0, (uint32_t)off, sx, sux);
+                weak8(d1, (uint32_t)off + 8, sx, sux);
+                const uint64_t x0 = d0 ^ ks0[i], x1 = d1 ^ ks1[i];
+                c0 += (uint64_t)(uint32_t)x0 * (x0 >> 32) + d1;
+                c1 += (uint64_t)(uint32_t)x1 * (x1 >> 32) + d0;
+            }
+        }
+        fold(c0, c1);
+        a0 += c0;
+        a1 += c1;
+    }
+    // last stripe (overlaps): every h hashes it (the accumulators stay equal
+    // across h); h = 0 weak-sums it from the first byte no earlier stripe covered
+    const uint64_t covered = (nb * 16 + ns) * 64;
+    const uint64_t off = len - 64 + 16 * m;
+    uint64_t d0, d1;
+    ld16u(p + off, d0, d1);
+    coop4_stripe(a0, a1, d0, d1, 192 - 64 - 7, m, seed);
+    if (h == 0) {
+        const uint64_t sk0 = covered > off ? min<uint64_t>(covered - off, 8) : 0;
+        const uint64_t sk1 = covered > off + 8 ? min<uint64_t>(covered - off - 8, 8) : 0;
+        weak8(sk0 >= 8 ? 0 : d0 & (~0ull << (8 * sk0)), (uint32_t)off, sx, sux);
+        weak8(sk1 >= 8 ? 0 : d1 & (~0ull << (8 * sk1)), (uint32_t)off + 8, sx, sux);
+    }
+}
+
+template <uint32_t LN>
+__global__ __launch_bounds__(256) void rs_sig_coopn_kernel(RsSigArgs a) {
+    const uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / LN;
+    const uint32_t ml = threadIdx.x & (LN - 1), gbase = (threadIdx.x & 63) & ~(LN - 1);
+    const uint64_t b = g < a.count ? g : a.count - 1;  // whole groups stay active (shuffles)
+    const uint64_t pos = b * a.blength;
+    const uint64_t n = (b == a.count - 1 && a.remainder) ? a.remainder : a.blength;
+    uint32_t sx, sux, weak;
+    uint64_t lo, hi, a0, a1;
+    coopn_long<LN>(a.data + pos, n, a.seed, ml, a0, a1, sx, sux);
+    // the weak parts of lanes h > 0 join lanes h = 0; coop4_finish adds the four m
+#pragma unroll
+    for (uint32_t o = 4; o < LN; o <<= 1) {
+        sx += (uint32_t)__shfl_xor((int)sx, (int)o, 64);
+        sux += (uint32_t)__shfl_xor((int)sux, (int)o, 64);
+    }
+    coop4_finish(a0, a1, sx, sux, n, a.csum_type, a.seed, gbase, weak, lo, hi);
+    if (g < a.count && ml == 0) {
+        a.sum1[g] = weak;
+        put_strong(a.sum2 + g * a.s2length, a.s2length, lo, hi);
+    }
+}
+
 // candidate verification: 8 lanes per window (XXH3, every window > 240 bytes)
 __global__ __launch_bounds__(256) void rs_strong_coop_kernel(const uint8_t *data,
                                                              const uint64_t *offs,
@@ -343,9 +468,13 @@ static bool coop_ok(int csum_type) {
 
 hipError_t launch_rs_signatures(const RsSigArgs &a, hipStream_t s) {
     if (!a.count) return hipSuccess;
-    if (coop_ok(a.csum_type) && a.blength > 240 && (a.remainder == 0 || a.remainder > 240))
-        rs_sig_coop_kernel<<<(uint32_t)((a.count * 4 + 255) / 256), 256, 0, s>>>(a);
-    else
+    if (coop_ok(a.csum_type) && a.blength > 240 && (a.remainder == 0 || a.remainder > 240)) {
+        if (VS_SIG_LANES > 4)
+            rs_sig_coopn_kernel<VS_SIG_LANES>
+                <<<(uint32_t)((a.count * VS_SIG_LANES + 255) / 256), 256, 0, s>>>(a);
+        else
+            rs_sig_coop_kernel<<<(uint32_t)((a.count * 4 + 255) / 256), 256, 0, s>>>(a);
+    } else
         rs_sig_kernel<<<(uint32_t)((a.count + 127) / 128), 128, 0, s>>>(a);
     return hipGetLastError();
 }

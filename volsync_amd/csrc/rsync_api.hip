@@ -1121,7 +1121,8 @@ int walk_scan(vs_rsync *h) {
         VS_TRY(h->stage.d2h(pr.data(), a.prof, nprof * 8, h->stream));
         const char *names[kPh] = {"run", "step", "flush", "chain", "segment", "band-fill",
                                   "band-pairs", "band-chain", "step:sums", "step:lds",
-                                  "step:gather", "step:probe", "step:queue", "", "", ""};
+                                  "step:gather", "step:probe", "step:queue", "flush:iters",
+                                  "flush:windows", ""};
         double cyc[kPh] = {0}, cnt[kPh] = {0}, mx = 0;
         int waves = 0;
         for (size_t w = 0; w < nprof / (2 * kPh); ++w) {
