@@ -258,6 +258,8 @@ enum : int {
     // the wave walk's STEP batch, split: sums, LDS prefilter, blocked-filter
     // gathers, directory probes, queueing
     kPrStepSums = 8, kPrStepLds = 9, kPrStepGather = 10, kPrStepProbe = 11, kPrStepQueue = 12,
+    // wide flushes: iterations per pass, windows per pass (sums, not cycles)
+    kPrFlushIters = 13, kPrFlushWin = 14,
     kPrN = 16
 };
 // The counters live in scalar registers; compiled in only with the build
@@ -1167,6 +1169,15 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 // than kRows in one address-lockstep pass, else one per row
                 const bool wide = fq == kWideQ && nq > kRows;   // (wide for every flush: no faster)
                 uint64_t tf = wclock(wp);
+#ifdef VS_WALK_PROF
+                if (wp.on && wide) {   // the pass's iterations (KiB of span + blocks) and windows
+                    const int64_t s0 = (int64_t)rdl64((uint64_t)qh, 0), s1 = (int64_t)rdl64((uint64_t)qh, (int)(nq - 1));
+                    wp.cyc[kPrFlushIters] += (uint64_t)((s1 - s0) >> 10) + (L - 1) / 1024;
+                    wp.cnt[kPrFlushIters] += 1;
+                    wp.cyc[kPrFlushWin] += nq;
+                    wp.cnt[kPrFlushWin] += 1;
+                }
+#endif
                 RowWin w;
                 if (wide) {
                     w = wide_windows((g_u8 *)(uintptr_t)a.data, a.dlen, (l_u64 *)rs.w,
