@@ -741,24 +741,28 @@ def test_file_sum_jobs_fifo(gpu):
     m.close()
 
 
-@pytest.mark.parametrize("seg,prefilter,flushq,span,predict,tail", [
-    (8, 1, 16, 0, 1, 0), (16, 1, 4, 0, 1, 0), (64, 1, 16, 8192, 1, 0), (0, 0, 16, 0, 1, 0),
-    (0, 1, 16, 40000, 0, 0), (0, 1, 4, 3000, 0, 0), (0, 1, 16, 0, 1, 30), (32, 1, 16, 0, 1, 90)])
-def test_walk_segment_lengths_exact(gpu, seg, prefilter, flushq, span, predict, tail):
+@pytest.mark.parametrize("seg,prefilter,flushq,span,predict,tail,margin", [
+    (8, 1, 16, 0, 1, 0, -1), (16, 1, 4, 0, 1, 0, -1), (64, 1, 16, 8192, 1, 0, 777),
+    (0, 0, 16, 0, 1, 0, -1), (0, 1, 16, 40000, 0, 0, -1), (0, 1, 4, 3000, 0, 0, 0),
+    (0, 1, 16, 0, 1, 30, -1), (32, 1, 16, 0, 1, 90, -1), (0, 1, 16, 0, 1, -1, 0),
+    (8, 1, 16, 0, 1, -1, 131071), (0, 1, 16, 0, 1, -1, 1)])
+def test_walk_segment_lengths_exact(gpu, seg, prefilter, flushq, span, predict, tail, margin):
     """The device walk with other segment lengths (VS_OPT_WALK_SEGMENT_BLOCKS;
     the default 0 is 48 blocks, shorter for small ranges), without the LDS
     prefilter (VS_OPT_WALK_PREFILTER 0), with four-window flushes in place of
     the wide address-lockstep ones (VS_OPT_WALK_FLUSH_WINDOWS) and with flushes
     bounded by a span (VS_OPT_WALK_FLUSH_SPAN), with and without the early
     flush at a likely resync (VS_OPT_WALK_FLUSH_PREDICT), with quarter-length
-    tail segments (VS_OPT_WALK_TAIL_PCT): more or fewer speculative
+    tail segments (VS_OPT_WALK_TAIL_PCT), with segment starts at other margins
+    before a block boundary (VS_OPT_WALK_SEG_MARGIN): more or fewer speculative
     segments, stitches and flushes, the same hash_search -- seeded shifted /
     overwritten sources (false alarms, runs, short last blocks), the C4
     parameters on a 1 GiB basis, and the 4-way sharded walk."""
     from volsync_amd import Matcher, SumStruct
     from volsync_amd._lib import (VS_OPT_WALK_FLUSH_PREDICT, VS_OPT_WALK_FLUSH_SPAN,
                                   VS_OPT_WALK_FLUSH_WINDOWS, VS_OPT_WALK_PREFILTER,
-                                  VS_OPT_WALK_SEGMENT_BLOCKS, VS_OPT_WALK_TAIL_PCT)
+                                  VS_OPT_WALK_SEG_MARGIN, VS_OPT_WALK_SEGMENT_BLOCKS,
+                                  VS_OPT_WALK_TAIL_PCT)
 
     def opts(m):
         m.set_option(VS_OPT_WALK_SEGMENT_BLOCKS, seg)
@@ -767,6 +771,7 @@ def test_walk_segment_lengths_exact(gpu, seg, prefilter, flushq, span, predict, 
         m.set_option(VS_OPT_WALK_FLUSH_SPAN, span)
         m.set_option(VS_OPT_WALK_FLUSH_PREDICT, predict)
         m.set_option(VS_OPT_WALK_TAIL_PCT, tail)
+        m.set_option(VS_OPT_WALK_SEG_MARGIN, margin)
     for csum_type, seed, n, frac, bs in [(R.CSUM_XXH3_128, 0x5EED5EED, 40 << 20, 0.10, 0),
                                          (R.CSUM_XXH3_64, 7, 12 << 20, 0.30, 0),
                                          (R.CSUM_XXH3_128, 1, 6 << 20, 0.20, 1000),

@@ -253,5 +253,17 @@ case $1 in
     VSGPU_LIB=$PWD/$(var prio2) bash tools/gpu.sh tests tests/test_gpu_rsync.py -x -k "walk or real_density or stitch" &&
     ab prio_share 2 "base=,prio1=$(var prio1),prio2=$(var prio2)" bench.py $S &&
     ab prio_c4 2 "base=,prio1=$(var prio1),prio2=$(var prio2)" bench.py $C ;;
+  dw4)  # wide flush: dword-aligned ds_read_b64 (no selects) against qword-aligned + selects
+    S="--mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum"
+    C="--mode rsync --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline"
+    VSGPU_LIB=$PWD/$(var dw4) bash tools/gpu.sh tests tests/test_gpu_rsync.py -x -k "walk or real_density or stitch or shard" &&
+    ab dw4_share 3 "base=,dw4=$(var dw4)" bench.py $S &&
+    ab dw4_c4 2 "base=,dw4=$(var dw4)" bench.py $C ;;
+  margin)  # walk segments starting a margin before a block boundary (16 KiB shipped) against unaligned (m0)
+    S="--mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum"
+    C="--mode rsync --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline"
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py tests/test_gpu_rsync_stream.py -x &&
+    ab margin_share 2 "m16k=,m0=$(var m0),m4k=$(var m4096),m64k=$(var m65536)" bench.py $S &&
+    ab margin_c4 2 "m16k=,m0=$(var m0),m4k=$(var m4096),m64k=$(var m65536)" bench.py $C ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac

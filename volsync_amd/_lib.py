@@ -33,6 +33,7 @@ VS_OPT_WALK_FLUSH_WINDOWS = 7
 VS_OPT_WALK_FLUSH_SPAN = 8
 VS_OPT_WALK_FLUSH_PREDICT = 9
 VS_OPT_WALK_TAIL_PCT = 10
+VS_OPT_WALK_SEG_MARGIN = 11
 VS_OPT_SHA_QUAD_PCT = 16
 VS_OPT_FP_GENERIC = 17
 VS_OPT_SHA_GRID_PER_CU = 18

@@ -421,6 +421,7 @@ struct RsWalkArgs {
     int64_t lo, hi;        // the owned range
     int64_t seg_len;
     int64_t seg_len2;      // segments nseg1.. (the tail): this long
+    int64_t segb;          // segment k >= 1 starts at segb + k seg_len (k <= nseg1); segment 0 at lo
     uint32_t nseg1;
     uint32_t nseg, cap;    // segments, match capacity per segment
     uint32_t blength, count, remainder;

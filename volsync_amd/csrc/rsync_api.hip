@@ -239,6 +239,7 @@ struct vs_rsync {
     uint32_t opt_flushspan = 0;     // flush once the scan is this far past the first hit (0: none)
     bool opt_flushpredict = true;   // flush at a likely resync hit (weak sum of block want .. want + 2)
     int32_t opt_tailpct = -1;       // % of the walk range in quarter-length tail segments (-1: automatic)
+    int64_t opt_seg_margin = -1;    // walk segments start this far before a block boundary (-1: automatic)
     uint64_t fs_piece = 0;          // file-sum piece in 1 KiB blocks (0: 2^18)
     // streamed forms (host-fed files): see the MatchStream / SigStream section
     MatchStream *mst = nullptr;
@@ -979,7 +980,25 @@ int walk_scan(vs_rsync *h) {
             sl = std::max<int64_t>(range / (2 * waves), h->blength);
         a.seg_len = std::max<int64_t>(sl, 1 << 20);
     }
-    a.nseg = (uint32_t)((a.hi - a.lo + a.seg_len - 1) / a.seg_len);
+    // Segment starts a margin before a block boundary of the file: a
+    // speculative walk steps byte by byte from its segment's start to its
+    // first match, on average half a block when the start is arbitrary; where
+    // the source keeps the destination's block phase (in-place writes) or
+    // drifts from it by short inserts and deletes (C4), the first match lies
+    // about the margin past the start.  Segment 0 starts at lo.  Only when
+    // the segments are whole blocks and the range holds several.
+#ifndef VS_SEG_MARGIN
+#define VS_SEG_MARGIN 16384
+#endif
+    a.segb = a.lo;
+    {
+        const int64_t L = (int64_t)h->blength, M = h->opt_seg_margin >= 0 ? h->opt_seg_margin : VS_SEG_MARGIN;
+        if (M > 0 && a.seg_len % L == 0 && a.hi - a.lo >= 4 * a.seg_len) {
+            const int64_t rr = ((a.lo + a.seg_len + r.origin + M) % L + L) % L;
+            a.segb = a.lo - rr;   // segment 1 starts at lo + seg_len - rr, M before a boundary
+        }
+    }
+    a.nseg = (uint32_t)((a.hi - a.segb + a.seg_len - 1) / a.seg_len);
     a.nseg1 = a.nseg;
     a.seg_len2 = a.seg_len;
     // the last tail % of the range in segments a quarter as long, handed out
@@ -993,9 +1012,11 @@ int walk_scan(vs_rsync *h) {
 #ifndef VS_TAIL_DIV
 #define VS_TAIL_DIV 4
 #endif
-        const int64_t range = a.hi - a.lo, L2 = std::max<int64_t>(a.seg_len / VS_TAIL_DIV, 1 << 20);
+        const int64_t range = a.hi - a.segb, L2 = std::max<int64_t>(a.seg_len / VS_TAIL_DIV, 1 << 20);
         if (L2 < a.seg_len) {
-            const int64_t big = range * (100 - tailpct) / 100 / a.seg_len;
+            // (at least segment 0 when it ends at an aligned start)
+            const int64_t big = std::max<int64_t>(range * (100 - tailpct) / 100 / a.seg_len,
+                                                  a.segb < a.lo ? 1 : 0);
             a.nseg1 = (uint32_t)big;
             a.seg_len2 = L2;
             a.nseg = (uint32_t)(big + (range - big * a.seg_len + L2 - 1) / L2);
@@ -2475,6 +2496,10 @@ VS_API int vs_rsync_set_option(vs_rsync *h, int option, int64_t value) {
         case VS_OPT_WALK_TAIL_PCT:
             if (value < -1 || value > 90) return fail(VS_ERR_ARG, "tail share out of range");
             h->opt_tailpct = (int32_t)value;
+            return 0;
+        case VS_OPT_WALK_SEG_MARGIN:
+            if (value < -1 || value > (1ll << 32)) return fail(VS_ERR_ARG, "segment margin out of range");
+            h->opt_seg_margin = value;
             return 0;
         case VS_OPT_WALK_FLUSH_PREDICT:
             h->opt_flushpredict = value != 0;

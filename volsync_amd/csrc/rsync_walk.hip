@@ -1258,10 +1258,12 @@ __device__ __forceinline__ uint32_t next_segment(const RsWalkArgs &a, uint32_t l
     return uni(k);
 }
 
-// segments [0, nseg1) are seg_len long, the tail's seg_len2 (handed out last)
+// segments [1, nseg1) are seg_len long from segb (segment 0 runs from lo to
+// segment 1), the tail's seg_len2 (handed out last)
 __device__ __forceinline__ int64_t seg_lo(const RsWalkArgs &a, uint32_t k) {
-    return k <= a.nseg1 ? a.lo + (int64_t)k * a.seg_len
-                        : a.lo + (int64_t)a.nseg1 * a.seg_len + (int64_t)(k - a.nseg1) * a.seg_len2;
+    return k == 0        ? a.lo
+           : k <= a.nseg1 ? a.segb + (int64_t)k * a.seg_len
+                          : a.segb + (int64_t)a.nseg1 * a.seg_len + (int64_t)(k - a.nseg1) * a.seg_len2;
 }
 __device__ __forceinline__ int64_t seg_hi(const RsWalkArgs &a, uint32_t k) {
     return min(seg_lo(a, k + 1), a.hi);
