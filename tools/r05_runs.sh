@@ -265,5 +265,9 @@ case $1 in
     bash tools/gpu.sh tests tests/test_gpu_rsync.py tests/test_gpu_rsync_stream.py -x &&
     ab margin_share 2 "m16k=,m0=$(var m0),m4k=$(var m4096),m64k=$(var m65536)" bench.py $S &&
     ab margin_c4 2 "m16k=,m0=$(var m0),m4k=$(var m4096),m64k=$(var m65536)" bench.py $C ;;
+  margin2)  # segment margin 8 / 24 / 32 KiB against the shipped 16 KiB, then the share walk's counters
+    S="--mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum"
+    ab margin2_share 2 "m16k=,m8k=$(var m8192),m24k=$(var m24576),m32k=$(var m32768)" bench.py $S &&
+    bash tools/gpu.sh prof r05_end4_walkshare rs_walk --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac
