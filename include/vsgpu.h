@@ -598,7 +598,7 @@ int vs_restic_pack_header(const uint8_t *types, const uint32_t *lengths, const u
                                       * default: 20 below four segments per wave, else 10) */
 #define VS_OPT_WALK_SEG_MARGIN 11    /* rsync: device walk segments after the first start
                                       * this many bytes before a block boundary of the file
-                                      * (-1 = automatic, the default: 16384; 0 = segments
+                                      * (-1 = automatic, the default: 24576; 0 = segments
                                       * from the range start, unaligned) */
 #define VS_OPT_SHA_QUAD_PCT 16       /* cdc / sha: chains within this % of the longest
                                       * run in latency (quad) mode in the final drain

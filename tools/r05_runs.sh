@@ -269,5 +269,10 @@ case $1 in
     S="--mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum"
     ab margin2_share 2 "m16k=,m8k=$(var m8192),m24k=$(var m24576),m32k=$(var m32768)" bench.py $S &&
     bash tools/gpu.sh prof r05_end4_walkshare rs_walk --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum ;;
+  margin3)  # the shipped 24 KiB margin: the rsync GPU tests and the share / 64 GiB lines
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py tests/test_gpu_rsync_stream.py -x &&
+    bash tools/gpu.sh bench c4share_nofs_m24 --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum &&
+    bash tools/gpu.sh bench c4share_m24 --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 &&
+    bash tools/gpu.sh bench c4_m24 --mode rsync --steps 20 --warmup 2 --no-cpu-baseline ;;
   *) echo "usage: tools/r05_runs.sh first|second|d2h|d2hprof|d2hapi|r7|r7b|fpchains|walk" >&2; exit 2 ;;
 esac

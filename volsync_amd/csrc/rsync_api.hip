@@ -988,7 +988,7 @@ int walk_scan(vs_rsync *h) {
     // about the margin past the start.  Segment 0 starts at lo.  Only when
     // the segments are whole blocks and the range holds several.
 #ifndef VS_SEG_MARGIN
-#define VS_SEG_MARGIN 16384
+#define VS_SEG_MARGIN 24576
 #endif
     a.segb = a.lo;
     {
