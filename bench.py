@@ -58,29 +58,66 @@ def valu_frac(gbs: float, ops_per_byte: float, cyc: float) -> float:
     return round(gbs * ops_per_byte / 1e3 * cyc / ISSUE_LANE_CYC, 4)
 
 
+def host_threads() -> int:
+    """The logical CPUs this process may run on (its affinity mask: the GPU
+    box's whole host, nproc)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def _cpu_quota():
+    """The cgroup CPU quota in CPUs (cpu.max), or None when unlimited."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(sample_bytes: int, threads: int):
-    """Oracle port (oracle/cdc_ref.c) timed restic-style on the host: one chunker
-    thread + (threads-1) SHA-256 threads (OpenSSL, SHA-NI when present)."""
+    """Oracle port (oracle/cdc_ref.c) timed restic-style on the host (SURVEY.md
+    8(d) CPU baseline): (i) the chunker on 1 thread, (ii) SHA-256 of the chunk
+    list (OpenSSL, SHA-NI when present) on 1 thread and on `threads` threads,
+    (iii) restic's archiver shape -- 1 chunker thread + (threads - 1) SHA-256
+    threads -- which is `value`."""
+    import numpy as np
     from tests import oracle_lib as O
     data = O.synth(2, 0, sample_bytes)
     t0 = time.perf_counter()
     ch = O.cdc_hash(data, 0x3DA3358B4DC173, 512 << 10, 8 << 20, 20, n_hash=threads - 1)
     dt = time.perf_counter() - t0
-    # chunker alone on one core (what restic does per file)
+    # (i) the chunker alone on one core (what restic does per file)
     t1 = time.perf_counter()
     O.chunk_all(data, 0x3DA3358B4DC173, 512 << 10, 8 << 20, 20)
     dt_chunk = time.perf_counter() - t1
+    # (ii) SHA-256 over the chunk list: 1 thread, all threads
+    off = np.array([c[0] for c in ch], np.uint64)
+    ln = np.array([c[1] for c in ch], np.uint64)
+    t2 = time.perf_counter()
+    ids1, _ = O.sha256_list(data, off, ln, 1)
+    dt_sha1 = time.perf_counter() - t2
+    t3 = time.perf_counter()
+    idsn, ran = O.sha256_list(data, off, ln, threads)
+    dt_shan = time.perf_counter() - t3
+    ok = bytes(ids1.ravel()) == bytes(idsn.ravel()) == b"".join(bytes.fromhex(c[3]) for c in ch)
     return {
         "value": round(sample_bytes / dt / 1e9, 3),
         "unit": "GB/s",
         "cores": threads,
         "kind": "port",
         "sample": f"{sample_bytes >> 30} GiB of the C2 stream (seed 2), {len(ch)} chunks; "
-                  f"1 chunker thread + {threads - 1} SHA-256 threads (OpenSSL="
-                  f"{bool(O.lib().ref_have_openssl())}); chunker alone 1 core "
-                  f"{sample_bytes / dt_chunk / 1e9:.3f} GB/s",
+                  f"value = 1 chunker thread + {threads - 1} SHA-256 threads (OpenSSL="
+                  f"{bool(O.lib().ref_have_openssl())}), restic's archiver shape",
+        "legs_GBps": {"chunker_1_thread": round(sample_bytes / dt_chunk / 1e9, 3),
+                      "sha256_1_thread": round(sample_bytes / dt_sha1 / 1e9, 3),
+                      f"sha256_{ran}_threads": round(sample_bytes / dt_shan / 1e9, 3),
+                      "ids_agree": ok},
         "cpu": _cpu_model(),
-        "nproc": os.cpu_count(),   # the host's logical CPUs (the baseline used `cores` of them)
+        "nproc": os.cpu_count(),   # the host's logical CPUs
+        "affinity_cpus": host_threads(),
+        "cgroup_cpu_quota": _cpu_quota(),
     }
 
 
@@ -559,29 +596,34 @@ def rsync_main(args):
 
 
 def smallfiles_cpu_baseline(sizes, sample_files: int, threads: int):
-    """Go crypto/sha256 stand-in: OpenSSL SHA-256 via hashlib (which releases
-    the GIL), one blob per file over `threads` threads, on the first
-    `sample_files` files of the same size distribution (synthetic bytes)."""
-    import hashlib
-    from concurrent.futures import ThreadPoolExecutor
+    """Go crypto/sha256 stand-in on the host: OpenSSL SHA-256 (SHA-NI) per
+    file over `threads` threads (oracle ref_sha256_list, C pthreads: restic's
+    NumCPU BlobSaver goroutines), over the first `sample_files` files of the
+    C5 size distribution laid out back to back in a 4 GiB synthetic buffer
+    (wrapping), so the hashed bytes stream from DRAM as a packed batch would."""
     import numpy as np
-    sz = sizes[:sample_files]
-    raw = np.random.default_rng(7).integers(0, 256, int(sz.max()), dtype=np.uint8).tobytes()
-    mv = memoryview(raw)
-
-    def work(lo_hi):
-        lo, hi = lo_hi
-        for k in range(lo, hi):
-            hashlib.sha256(mv[: int(sz[k])]).digest()
-    parts = [(i * len(sz) // threads, (i + 1) * len(sz) // threads) for i in range(threads)]
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        list(ex.map(work, parts))
-    dt = time.perf_counter() - t0
-    return {"value": round(float(sz.sum()) / dt / 1e9, 3), "unit": "GB/s", "cores": threads,
+    from tests import oracle_lib as O
+    sz = np.asarray(sizes[:sample_files], np.uint64)
+    span = 4 << 30
+    buf = O.synth(6, 0, span)
+    off = (np.concatenate([[0], np.cumsum(sz)[:-1]]) % np.uint64(span - (1 << 17))).astype(np.uint64)
+    O.sha256_list(buf, off[:1000], sz[:1000], threads)   # warm the pages and threads
+    best, ran = None, threads
+    for _ in range(3):
+        t0 = time.perf_counter()
+        _, ran = O.sha256_list(buf, off, sz, threads)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    t1 = time.perf_counter()
+    O.sha256_list(buf, off[: len(sz) // 16], sz[: len(sz) // 16], 1)
+    dt1 = time.perf_counter() - t1
+    return {"value": round(float(sz.sum()) / best / 1e9, 3), "unit": "GB/s", "cores": ran,
             "kind": "port", "sample": f"{len(sz)} files ({float(sz.sum()) / 2**30:.2f} GiB) of the "
-            f"C5 size distribution, hashlib/OpenSSL SHA-256 on {threads} threads",
-            "cpu": _cpu_model(), "nproc": os.cpu_count()}
+            f"C5 size distribution packed in a 4 GiB buffer, OpenSSL SHA-256 on {ran} threads "
+            f"(best of 3)",
+            "legs_GBps": {"sha256_1_thread": round(float(sz[: len(sz) // 16].sum()) / dt1 / 1e9, 3)},
+            "cpu": _cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": host_threads(),
+            "cgroup_cpu_quota": _cpu_quota()}
 
 
 def c5_layout(files: int, rank: int = 0):
@@ -714,6 +756,15 @@ def smallfiles_main(args):
         e1.record()
         torch.cuda.synchronize(dev)
         dd[name] = e0.elapsed_time(e1) / 5
+    # one pass alone (every step hashes all its blobs to the end and carries
+    # nothing to the next, so the replayed step is this pass repeated): the
+    # IDs are cleared first, and the golden check below reads this pass's IDs
+    ids.zero_()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    step()
+    torch.cuda.synchronize(dev)
+    lat = time.perf_counter() - t1
     distinct = sh.dedup(ids.data_ptr(), nf, first.data_ptr(), stream)
     # exactness: SHA-256 over all blob IDs in file order (tests/golden/
     # make_golden_full.py c5), and the distinct count
@@ -736,6 +787,8 @@ def smallfiles_main(args):
                       "new_unique_ids": uniq, "batch_unique_ids": distinct,
                       "dedup_known_ms": round(dd["known"], 3),
                       "dedup_batch_only_ms": round(dd["batch"], 3)},
+            "single_pass": {"ms": round(lat * 1e3, 3), "GBps_per_gpu": round(total / lat / 1e9, 2),
+                            "note": "one step alone; the IDs checked below are its output"},
             "exact": {"files": nf, "unique_ids": distinct, "id_digest": id_digest},
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
@@ -749,7 +802,7 @@ def smallfiles_main(args):
             out["exact"]["golden_match"] = (g["unique_ids"], g["id_digest"], g["bytes"]) == \
                 (distinct, id_digest, total)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = smallfiles_cpu_baseline(sizes, 200000, args.cpu_threads)
+            out["cpu_baseline"] = smallfiles_cpu_baseline(sizes, len(sizes), args.cpu_threads)
         print(json.dumps(out), flush=True)
     sh.close()
     if world > 1:
@@ -1252,6 +1305,88 @@ def rsync_host_main(args):
     print(json.dumps(out), flush=True)
 
 
+def _chunk_records(dc, n: int, batch=None) -> bytes:
+    """The last finished batch's (or batch `batch`'s) chunk list as 56-byte
+    vs_chunk records (waits for their blob IDs)."""
+    import ctypes
+    from volsync_amd._lib import VsChunk, check, lib
+    if not n:
+        return b""
+    arr = (VsChunk * n)()
+    if batch is None:
+        check(lib.vs_cdc_get_chunks(dc._h, 0, n, arr))
+    else:
+        check(lib.vs_cdc_get_batch_chunks(dc._h, batch, 0, n, arr))
+    return ctypes.string_at(arr, 56 * n)
+
+
+# bench.py --distinct B: volume k of the run is the 64 GiB stream of seed
+# DISTINCT_SEEDS[k % B] (2 = C2's); goldens in full_configs.json
+# (make_golden_full.py distinct)
+DISTINCT_SEEDS = (2, 7, 8)
+
+
+def distinct_pass(args, dc, buf0, dlen: int, local: int, dev, stream) -> dict:
+    """The C2 step over B DISTINCT resident volumes in rotation, as a producer
+    refilling B buffers would run it: step k reuses volume k mod B's buffer
+    and therefore starts only once every blob ID of step k - B is final
+    (vs_cdc_fence; the engine drains when that batch's chunks are still
+    queued).  Nothing is replayed: every step chunks and hashes a volume
+    whose chains were never seen before."""
+    import hashlib
+    import torch
+    from volsync_amd import synth_fill_device
+    B = args.distinct
+    assert 1 <= B <= len(DISTINCT_SEEDS), B
+    seeds = DISTINCT_SEEDS[:B]
+    bufs = [buf0] + [torch.empty(dlen, dtype=torch.uint8, device=dev) for _ in range(B - 1)]
+    for b, sd in zip(bufs[1:], seeds[1:]):
+        synth_fill_device(b.data_ptr(), sd, 0, dlen, device=local, stream=stream)
+    torch.cuda.synchronize(dev)
+    dc.wait()
+    first, ring = dc.batches()
+    assert ring > B, (ring, B)
+    done = []
+
+    def dstep(j):
+        if j >= B:
+            dc.fence(first + j - B)
+        n, _ = dc.process(bufs[j % B].data_ptr(), dlen, 0, True)
+        done.append((first + j, seeds[j % B], n))
+
+    for j in range(args.warmup):
+        dstep(j)
+    dc.wait()
+    torch.cuda.synchronize(dev)
+    dc.timing(True)
+    t0 = time.perf_counter()
+    for j in range(args.warmup, args.warmup + args.steps):
+        dstep(j)
+    dc.wait()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    ms, launches = dc.timing(False)
+    det = dc.timing_detail()
+    gold = _goldens().get("cdc", {})
+    checks = []
+    for bi, sd, n in done[-B:]:
+        g = gold.get(str(sd), {}).get(str(dlen))
+        d = hashlib.sha256(_chunk_records(dc, n, batch=bi)).hexdigest()
+        checks.append({"seed": sd, "chunks": n, "digest": d,
+                       "golden_match": bool(g) and (g["chunks"], g["digest"]) == (n, d)})
+    del bufs[1:]
+    torch.cuda.empty_cache()
+    return {"volumes": B, "seeds": list(seeds),
+            "GBps": round(dlen * args.steps / dt / 1e9, 2),
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "stages_ms_per_step": {"fingerprint": round(ms[0] / args.steps, 3),
+                                   "sha256": round(det["sha_outside_fp_ms"] / args.steps, 3),
+                                   "sha256_inside_fp": round(det["sha_inside_fp_ms"] / args.steps, 3)},
+            "sha_launches": launches[2], "latency_mode_chains": det["quad_chains"],
+            "rule": "step k starts after every blob ID of step k - B is final (vs_cdc_fence)",
+            "exact": checks, "golden_match": all(c["golden_match"] for c in checks)}
+
+
 def _match_records(m, n: int) -> bytes:
     """The handle's last match list as 16-byte vs_match records."""
     import ctypes
@@ -1284,8 +1419,12 @@ def main():
     ap.add_argument("--per-gpu-gib", type=float, default=None,
                     help="bytes per GPU (default 64 GiB; the CDC mode at N > 1: C3's "
                          "128 GiB per GPU, i.e. 1 TiB over 8)")
+    ap.add_argument("--distinct", type=int, default=None,
+                    help="cdc, 1 GPU: also run the step over B distinct volumes in rotation "
+                         "(step k waits for step k-B's blob IDs; default 3 for C2, 0 = off)")
     ap.add_argument("--cpu-sample-gib", type=int, default=4)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baselines' threads (0 = every CPU of the host, nproc)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--file-sum-jobs", type=int, default=3,
                     help="rsync: whole-file checksums in flight (one host chain thread each)")
@@ -1325,9 +1464,14 @@ def main():
     ap.add_argument("--dry", action="store_true",
                     help="CPU/gloo rehearsal of the multi-rank protocol (no GPU; value null)")
     args = ap.parse_args()
+    if args.cpu_threads <= 0:
+        args.cpu_threads = host_threads()
     # C3: 1 TiB of the seed-3 stream over 8 GPUs, 128 GiB
     # resident per GPU; the CDC mode's N > 1 default is that per-GPU share
     args.c3_default = args.per_gpu_gib is None
+    if args.distinct is None:
+        args.distinct = 3 if (args.mode == "cdc" and args.gpus == 1 and not args.share
+                              and args.per_gpu_gib in (None, 64.0)) else 0
     if args.per_gpu_gib is None:
         args.per_gpu_gib = 64.0
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -1422,28 +1566,39 @@ def main():
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     ms, launches = dc.timing(False)
-    # one volume alone: single-volume latency and isolated stage times
-    dc.timing(True)
-    t1 = time.perf_counter()
-    step()
-    dc.wait()
-    lat = time.perf_counter() - t1
-    iso_ms, iso_launch = dc.timing(False)
+    detail = dc.timing_detail()
     # exactness evidence: the chunk list (this rank's chunks, gathered in rank
     # order) as vs_chunk records, SHA-256 -> golden (tests/golden/
     # make_golden_full.py); outside the timed region
-    import ctypes
     import hashlib
-    from volsync_amd._lib import VsChunk, check, lib
-    arr = (VsChunk * max(nch, 1))()
-    if nch:
-        check(lib.vs_cdc_get_chunks(dc._h, 0, nch, arr))
-    recs = ctypes.string_at(arr, 56 * nch) if nch else b""
+    recs = _chunk_records(dc, nch)
     if world > 1:
         parts = [None] * world if rank == 0 else None
         dist.gather_object(recs, parts, dst=0)
         recs = b"".join(parts) if rank == 0 else b""
     cdigest = hashlib.sha256(recs).hexdigest()
+    # one pass over one volume, nothing replayed or carried (the north star's
+    # workload: one restic backup of one volume, mover-restic/entry.sh:60-65):
+    # scan .. drain, every blob ID final at the end
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dc.timing(True)
+    t1 = time.perf_counter()
+    n_single = step()
+    dc.wait()
+    torch.cuda.synchronize(dev)
+    lat = time.perf_counter() - t1
+    iso_ms, iso_launch = dc.timing(False)
+    iso_detail = dc.timing_detail()
+    single_ok = _chunk_records(dc, n_single) == recs if world == 1 else None
+    if world > 1:
+        t = torch.tensor([lat], dtype=torch.float64, device=coll_device(dev))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        lat = float(t.item())
+    distinct = None
+    if args.distinct and world == 1 and not share:
+        distinct = distinct_pass(args, dc, buf, dlen, local, dev, stream)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=coll_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1455,6 +1610,12 @@ def main():
     own_bytes = spec.own_hi - spec.own_lo
     stages = ["fingerprint", "select", "sha256", "other"]
     per_step = {s: ms[i] / args.steps for i, s in enumerate(stages)}
+    # the SHA-256 stage is its kernels' time OUTSIDE every fingerprint window
+    # (HIP events on both streams against one anchor): a slice dispatched
+    # while the persistent fingerprint grid holds the CUs waits inside its
+    # span without hashing; the part inside the windows is reported beside it
+    sha_span_step = per_step["sha256"]
+    per_step["sha256"] = detail["sha_outside_fp_ms"] / args.steps
     # kernel roofline from the timed region (HIP events on each handle's stream,
     # so overlapped volumes share the chip): algorithmic bytes per launch = the
     # volume bytes -- the fingerprint pass reads each scanned byte once (plus a
@@ -1463,10 +1624,12 @@ def main():
     # fingerprint: one launch per volume; SHA-256: slices (one per step plus the
     # final drain) -- bytes hashed in the timed region / summed slice time
     fp_ms = ms[0] / args.steps
-    sha_ms = ms[2] / args.steps
+    sha_ms = per_step["sha256"]
     fp_gbs = own_bytes / fp_ms / 1e6 if fp_ms else 0.0
     sha_gbs = own_bytes / sha_ms / 1e6 if sha_ms else 0.0
     iso = {s: round(iso_ms[i], 3) for i, s in enumerate(stages)}
+    iso["sha256_span"] = iso["sha256"]
+    iso["sha256"] = round(iso_detail["sha_outside_fp_ms"], 3)
     # per-launch averages over the timed region, comparable with the
     # rocprofv3 kernel trace of the same command (profiles/r01_final)
     avg_launch = {s: round(ms[i] / launches[i], 3) if launches[i] else None
@@ -1495,8 +1658,11 @@ def main():
         pass
     roof["fingerprint"]["avg_launch_ms"] = avg_launch["fingerprint"]
     roof["fingerprint"]["launches"] = launches[0]
-    roof["sha256"]["avg_launch_ms"] = avg_launch["sha256"]
+    roof["sha256"]["avg_launch_ms"] = avg_launch["sha256"]   # span (rocprof-comparable)
     roof["sha256"]["launches"] = launches[2]
+    roof["sha256"]["busy_ms_per_step"] = round(per_step["sha256"], 3)
+    roof["sha256"]["span_ms_per_step"] = round(sha_span_step, 3)
+    roof["sha256"]["inside_fp_ms_per_step"] = round(detail["sha_inside_fp_ms"] / args.steps, 3)
     dom_name = "sha256" if per_step["sha256"] >= per_step["fingerprint"] else "fingerprint"
     roofline = dict(roof[dom_name])
     roofline["kernel"] = dom_name
@@ -1535,7 +1701,8 @@ def main():
             "kernels": roof,
             # the whole step shares one resource: VALU issue (fingerprint +
             # SHA-256 lane-ops over the step time, each priced by its mix)
-            "pipeline_valu_frac": round(total * args.steps / dt / world / 1e12
+            "pipeline_valu_frac": round((own_bytes if share else total) * args.steps / dt
+                                        / (1 if share else world) / 1e12
                                         * (SHA_OPS_PER_BYTE * SHA_MIX_CYC + FP_OPS_PER_BYTE * FP_MIX_CYC)
                                         / ISSUE_LANE_CYC, 4),
             "hash_slice_blocks": args.hash_slice,
@@ -1545,9 +1712,14 @@ def main():
             "rccl_world_size": dist.get_world_size() if world > 1 else 1,
             "dist_backend": dist.get_backend() if world > 1 else None,
             "exchange_rounds_last_step": xst.get("exchange_rounds", 0),
-            "single_volume": {"ms": round(lat * 1e3, 2),
-                              "GBps": round(total / lat / 1e9, 2),
-                              "stages_ms": iso},
+            # companion values, not the headline: one volume once (no replay,
+            # nothing carried across volumes), per GPU and whole job
+            "single_pass": {"ms": round(lat * 1e3, 2),
+                            "GBps_per_gpu": round(own_bytes / lat / 1e9, 2),
+                            "GBps": round((own_bytes if share else total) / lat / 1e9, 2),
+                            "stages_ms": iso,
+                            "latency_mode_chains": iso_detail["quad_chains"],
+                            "same_chunk_list": single_ok},
             "exact": {"chunks": nch, "digest": cdigest},
         }
         gold = gold_all
@@ -1559,6 +1731,8 @@ def main():
                                                 == (nch, cdigest))
         elif gold and gold.get("bytes") == total and gold.get("seed") == seed:
             out["exact"]["golden_match"] = (gold["chunks"], gold["digest"]) == (nch, cdigest)
+        if distinct is not None:
+            out["distinct"] = distinct
         if world == 1 and not args.no_cpu_baseline and not share:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_gib << 30, args.cpu_threads)
         print(json.dumps(out), flush=True)

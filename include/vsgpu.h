@@ -170,6 +170,20 @@ int vs_cdc_get_chunks(vs_cdc *h, uint64_t first, uint64_t n, vs_chunk *out);
  * stage: 0 fingerprint, 1 select, 2 sha256 (the hash kernels alone; their
  * histogram / scan / scatter bookkeeping launches are not timed), 3 other. */
 int vs_cdc_timing(vs_cdc *h, int enable, double ms_out[4], uint64_t launches_out[4]);
+/* Order the handle's next scan (on its stream) after the blob IDs of finished
+ * batch `batch` (0 = the first vs_cdc_finish of the handle) are final, as a
+ * producer about to overwrite that batch's bytes needs; when the batch's
+ * chunks are still queued beyond the slices already launched, the engine
+ * drains (every queued chunk is hashed to its end).  Does not block the host
+ * beyond that drain's set-up. */
+int vs_cdc_fence(vs_cdc *h, uint64_t batch);
+/* The SHA-256 kernel windows of the interval the last vs_cdc_timing call
+ * closed, against the fingerprint windows (HIP events on both streams, as ms
+ * after an anchor event recorded when timing was enabled): out[0] SHA-256
+ * kernel time, out[1] the part outside every fingerprint window, out[2] the
+ * part inside one, out[3] the fingerprint windows' union.  *quad_chains: the
+ * chains the final drains ran in latency (quad) mode since the last call. */
+int vs_cdc_timing_detail(vs_cdc *h, double out[4], uint64_t *quad_chains);
 
 /* ---- batched SHA-256 (restic.Hash over many blobs; C5 small files) ----
  * A vs_sha handle owns the scratch of the work-queue kernel.  run_device:
@@ -600,12 +614,20 @@ int vs_restic_pack_header(const uint8_t *types, const uint32_t *lengths, const u
                                       * this many bytes before a block boundary of the file
                                       * (-1 = automatic, the default: 24576; 0 = segments
                                       * from the range start, unaligned) */
-#define VS_OPT_SHA_QUAD_PCT 16       /* cdc / sha: chains within this % of the longest
-                                      * run in latency (quad) mode in the final drain
-                                      * (default 80; 0 = split mode only) */
+#define VS_OPT_SHA_QUAD_PCT 16       /* cdc / sha: which chains of a latency-bound final
+                                      * drain run in latency (quad) mode.  -1 (default):
+                                      * every chain that would finish after the drain's
+                                      * floor -- max(longest chain in quad mode, backlog
+                                      * at split throughput) -- in split mode beside the
+                                      * bulk; 1..1000: the chains within this % of the
+                                      * longest; 0 = split mode only */
 #define VS_OPT_SHA_GRID_PER_CU 18   /* cdc / sha: persistent hash grid per CU: split-mode
                                       * workgroups (default 5) / throughput-mode waves
                                       * per SIMD (default 3); 0 = default */
+#define VS_OPT_SHA_ISOLATE 19         /* cdc / sha: 1 (default) = a latency-bound final drain
+                                      * runs its quad tiles on CUs reserved for them (a
+                                      * CU-masked stream, one wave per SIMD) and the
+                                      * split tiles on the others; 0 = one launch */
 #define VS_OPT_FP_GENERIC 17         /* cdc: 1 = the generic fingerprint address code
                                       * even where the FAST variant applies */
 #define VS_OPT_SEAL_FUSED 32         /* seal: 0 = separate CTR and MAC kernels (default 1) */

@@ -357,32 +357,68 @@ typedef struct {
     const uint8_t *src;
     uint64_t *starts, *lens;
     uint8_t *ids;
-    volatile int64_t produced; /* chunks published by the chunker thread */
-    volatile int done;
+    int64_t produced;          /* chunks published by the chunker thread (guarded by mu) */
+    int done;                  /* the chunker has finished (guarded by mu) */
     int64_t next;              /* next chunk to claim (guarded by mu) */
     pthread_mutex_t mu;
+    pthread_cond_t cv;         /* a chunk was published, or the chunker finished */
 } hash_queue;
 
+/* A hasher blocks while no chunk is published, as restic's BlobSaver
+ * goroutines block on their channel: idle hashers take no CPU from the
+ * chunker thread however many there are. */
 static void *hash_worker(void *arg) {
     hash_queue *q = (hash_queue *)arg;
     for (;;) {
         int64_t i;
         pthread_mutex_lock(&q->mu);
-        for (;;) {
-            int64_t avail = __atomic_load_n(&q->produced, __ATOMIC_ACQUIRE);
-            if (q->next < avail) { i = q->next++; break; }
-            if (__atomic_load_n(&q->done, __ATOMIC_ACQUIRE) &&
-                q->next >= __atomic_load_n(&q->produced, __ATOMIC_ACQUIRE)) {
-                pthread_mutex_unlock(&q->mu);
-                return NULL;
-            }
+        while (q->next >= q->produced && !q->done) pthread_cond_wait(&q->cv, &q->mu);
+        if (q->next >= q->produced) {   /* done and drained */
             pthread_mutex_unlock(&q->mu);
-            sched_yield();
-            pthread_mutex_lock(&q->mu);
+            return NULL;
         }
+        i = q->next++;
         pthread_mutex_unlock(&q->mu);
         ref_sha256_fast(q->src + q->starts[i], q->lens[i], q->ids + 32 * i);
     }
+}
+
+/* SHA-256 of blobs src[off[i], off[i] + len[i]) on `threads` threads (an
+ * atomic work counter, 64 blobs per claim): restic's BlobSaver goroutines
+ * hashing a chunk list, the all-core CPU baseline (bench.py).  TEST / BASELINE
+ * INFRASTRUCTURE only.  Every blob is hashed; returns the threads that ran
+ * (fewer than asked when pthread_create fails), -1 without memory. */
+typedef struct {
+    const uint8_t *src;
+    const uint64_t *off, *len;
+    uint8_t *ids;
+    int64_t n, next;
+} list_queue;
+
+static void *list_worker(void *arg) {
+    list_queue *q = (list_queue *)arg;
+    for (;;) {
+        const int64_t i0 = __atomic_fetch_add(&q->next, 64, __ATOMIC_RELAXED);
+        if (i0 >= q->n) return NULL;
+        const int64_t i1 = i0 + 64 < q->n ? i0 + 64 : q->n;
+        for (int64_t i = i0; i < i1; ++i) ref_sha256_fast(q->src + q->off[i], q->len[i], q->ids + 32 * i);
+    }
+}
+
+int ref_sha256_list(const uint8_t *src, const uint64_t *off, const uint64_t *len, int64_t n,
+                    uint8_t *ids, int threads) {
+    list_queue q = {src, off, len, ids, n, 0};
+    if (threads < 1) threads = 1;
+    if (threads > 1024) threads = 1024;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
+    if (!th) return -1;
+    int started = 0;
+    for (; started < threads; ++started)
+        if (pthread_create(&th[started], NULL, list_worker, &q) != 0) break;
+    if (started == 0) list_worker(&q);
+    for (int t = 0; t < started; ++t) pthread_join(th[t], NULL);
+    free(th);
+    return started ? started : 1;
 }
 
 /* 1 chunker thread + n_hash hashing threads (n_hash 0: hash inline). */
@@ -395,6 +431,7 @@ int64_t ref_cdc_hash(const uint8_t *src, uint64_t len, uint64_t pol, uint64_t mi
     memset(&q, 0, sizeof q);
     q.src = src; q.starts = starts; q.lens = lens; q.ids = ids;
     pthread_mutex_init(&q.mu, NULL);
+    pthread_cond_init(&q.cv, NULL);
     pthread_t th[256];
     if (n_hash > 256) n_hash = 256;
     for (int t = 0; t < n_hash; ++t) pthread_create(&th[t], NULL, hash_worker, &q);
@@ -405,10 +442,19 @@ int64_t ref_cdc_hash(const uint8_t *src, uint64_t len, uint64_t pol, uint64_t mi
         starts[n] = s; lens[n] = l; cuts[n] = k;
         if (n_hash == 0) ref_sha256_fast(src + s, l, ids + 32 * n);
         n++;
-        __atomic_store_n(&q.produced, (int64_t)n, __ATOMIC_RELEASE);
+        if (n_hash) {
+            pthread_mutex_lock(&q.mu);
+            q.produced = (int64_t)n;
+            pthread_cond_signal(&q.cv);
+            pthread_mutex_unlock(&q.mu);
+        }
     }
-    __atomic_store_n(&q.done, 1, __ATOMIC_RELEASE);
+    pthread_mutex_lock(&q.mu);
+    q.done = 1;
+    pthread_cond_broadcast(&q.cv);
+    pthread_mutex_unlock(&q.mu);
     for (int t = 0; t < n_hash; ++t) pthread_join(th[t], NULL);
+    pthread_cond_destroy(&q.cv);
     pthread_mutex_destroy(&q.mu);
     ref_chunker_free(c);
     return rc ? rc : (int64_t)n;

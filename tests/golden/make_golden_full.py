@@ -29,7 +29,7 @@ C4 (SourceShard), per rank: its own matches, false alarms and true entry.
 C5 (bench.py --mode smallfiles): the digest of all 1 M blob IDs in file order,
 the distinct-ID count and the bytes.
 
-usage: python tests/golden/make_golden_full.py [cdc|c3|rsync|filesum|c5|all] [--threads T]
+usage: python tests/golden/make_golden_full.py [cdc|c3|distinct|rsync|filesum|c5|all] [--threads T]
        [--rsync-gib G ...] [--skip-c3]
 writes tests/golden/full_configs.json (merged with what is there).
 """
@@ -56,6 +56,7 @@ OUT = os.path.join(HERE, "full_configs.json")
 POL, MN, MX, AVG = 0x3DA3358B4DC173, 512 << 10, 8 << 20, 20
 GiB = 1 << 30
 CSUM_XXH3_128, SEED = 8, 0x5EED5EED
+DISTINCT_SEEDS = (2, 7, 8)   # bench.py --distinct: volume k of the run is seed [k % B]
 
 
 def chunk_records(starts, lens, cuts, ids) -> np.ndarray:
@@ -294,7 +295,7 @@ def c5_golden(files: int, threads: int) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("what", nargs="?", default="all",
-                    choices=["cdc", "c3", "rsync", "filesum", "c5", "all"])
+                    choices=["cdc", "c3", "distinct", "rsync", "filesum", "c5", "all"])
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     ap.add_argument("--rsync-gib", type=int, nargs="*", default=[8, 16, 64, 128, 256])
     ap.add_argument("--skip-c3", action="store_true", help="cdc: keep the 1 TiB entries")
@@ -318,6 +319,12 @@ def main():
                 cdc_golden(3, 1024 * GiB, [128 * GiB, 256 * GiB, 512 * GiB, 1024 * GiB], a.threads,
                            per_rank=128 * GiB))
         json.dump(data, open(OUT, "w"), indent=1)
+    if a.what in ("distinct", "all"):
+        # bench.py --distinct B: the C2 shape over distinct volumes, seeds 2, 7, 8
+        cdc = data.setdefault("cdc", {})
+        for sd in DISTINCT_SEEDS[1:]:
+            cdc.setdefault(str(sd), {}).update(cdc_golden(sd, 64 * GiB, [64 * GiB], a.threads))
+            json.dump(data, open(OUT, "w"), indent=1)
     if a.what in ("rsync", "all"):
         data.setdefault("rsync", {})
         for g in a.rsync_gib:

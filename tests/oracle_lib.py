@@ -29,6 +29,8 @@ def lib() -> ctypes.CDLL:
         L.ref_synth_fill.argtypes = [u64, u64, u64, vp]
         L.ref_sha256.argtypes = [vp, u64, vp]
         L.ref_sha256_fast.argtypes = [vp, u64, vp]
+        L.ref_sha256_list.restype = ci
+        L.ref_sha256_list.argtypes = [vp, vp, vp, ctypes.c_int64, vp, ci]
         L.ref_have_openssl.restype = ci
         L.ref_pol_deg.argtypes = [u64]
         L.ref_pol_mod.restype = u64
@@ -69,6 +71,20 @@ def cdc_hash(data: np.ndarray, pol: int, mn: int, mx: int, avg_bits: int, n_hash
     if n < 0:
         raise ValueError("oracle failed")
     return [(int(s[i]), int(ln[i]), int(c[i]), bytes(ids[i]).hex()) for i in range(n)]
+
+
+def sha256_list(src: np.ndarray, off: np.ndarray, ln: np.ndarray, threads: int):
+    """SHA-256 of src[off[i] : off[i] + ln[i]] on `threads` threads
+    (ref_sha256_list): ((n, 32) uint8 IDs, threads that ran)."""
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    ln = np.ascontiguousarray(ln, dtype=np.uint64)
+    ids = np.zeros((max(len(off), 1), 32), np.uint8)
+    ran = lib().ref_sha256_list(src.ctypes.data, off.ctypes.data, ln.ctypes.data, len(off),
+                                ids.ctypes.data, threads)
+    if ran < 0:
+        raise MemoryError("ref_sha256_list")
+    return ids[:len(off)], ran
 
 
 def synth(seed: int, off: int, n: int) -> np.ndarray:

@@ -475,10 +475,15 @@ def test_file_sum_multi_pass_and_other_types(gpu):
     m = Matcher()
     data = O.synth(62, 0, (9 << 20) + 321)
     t = to_dev(data)
+    # a nonzero piece forces the bounded device ring (XXH3's multi-piece
+    # contribution ring; the path files over 128 GiB and hosts without the
+    # DMA agents take); 0 = rows first (every row, then one SDMA read-back)
     m.set_option(VS_OPT_FILE_SUM_PIECE, 1000)
     for csum in (8, 7, 6, 5):
         assert m.file_sum(t.data_ptr(), len(data), csum) == _file_sum_want(data.tobytes(), csum)
     m.set_option(VS_OPT_FILE_SUM_PIECE, 0)
+    for csum in (8, 7):
+        assert m.file_sum(t.data_ptr(), len(data), csum) == _file_sum_want(data.tobytes(), csum)
     for path in FIX[:6]:
         _, _, src = load_fixture(path)
         ts = to_dev(src)

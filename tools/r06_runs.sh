@@ -1,0 +1,40 @@
+#!/bin/bash
+# Round 6's GPU runs, one subcommand each (through gpurun; every GPU step has
+# its own time limit in tools/gpu.sh or here, and the chain stops at the first
+# failure).
+#   first   host CPU facts, the CDC GPU tests, the single-pass drain A/B
+#           (latency-mode producer priority: qpp0 = -DVS_SHA_QUAD_PPRIO=0),
+#           C2 at the driver's 20/5 (single pass, --distinct 3, nproc
+#           baselines), C3 rank 3 at 20/5
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+mkdir -p gpurun_out
+var() { echo "volsync_amd/lib/var/$1/libvsgpu.so"; }
+ab() {  # ab <log> <rounds> <libs> <script args...>
+  local log=$1 rounds=$2 libs=$3
+  shift 3
+  timeout -k 10 900 python3 -u tools/ab.py --rounds "$rounds" --libs "$libs" -- "$@" \
+    > "gpurun_out/$log.log" 2>&1
+  local rc=$?
+  echo "=== $log rc=$rc"; tail -n 8 "gpurun_out/$log.log"
+  return $rc
+}
+hostinfo() {
+  { echo "nproc $(nproc)"; cat /sys/fs/cgroup/cpu.max 2>&1; grep -m1 "model name" /proc/cpuinfo
+    python3 -c "import os; print('affinity', len(os.sched_getaffinity(0)))"; } > gpurun_out/hostinfo.txt
+  cat gpurun_out/hostinfo.txt
+}
+case $1 in
+  first)
+    hostinfo &&
+    bash tools/gpu.sh tests tests/test_gpu_cdc.py -x &&
+    ab ab_single_c3r3 1 "new=,qpp0=$(var qpp0)" tools/single_pass.py --share 3/8 --quad auto,80 --rounds 2 &&
+    bash tools/gpu.sh bench c2 --gpus 1 --steps 20 --warmup 5 &&
+    bash tools/gpu.sh bench c3r3 --share 3/8 --steps 20 --warmup 5 --no-cpu-baseline ;;
+  iso)
+    bash tools/gpu.sh tests tests/test_gpu_cdc.py -x -k "sha256 or drain or blob" &&
+    bash tools/gpu.sh py tools/single_pass.py --share 3/8 --quad auto:1,auto:0,80:0 --rounds 3 &&
+    mv gpurun_out/py_single_pass.log gpurun_out/single_c3r3.log &&
+    bash tools/gpu.sh py tools/single_pass.py --gib 64 --quad auto:1,auto:0,80:0 --rounds 3 &&
+    mv gpurun_out/py_single_pass.log gpurun_out/single_c2.log ;;
+  *) echo "usage: tools/r06_runs.sh first|iso" >&2; exit 2 ;;
+esac

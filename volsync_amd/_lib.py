@@ -35,6 +35,7 @@ VS_OPT_WALK_FLUSH_PREDICT = 9
 VS_OPT_WALK_TAIL_PCT = 10
 VS_OPT_WALK_SEG_MARGIN = 11
 VS_OPT_SHA_QUAD_PCT = 16
+VS_OPT_SHA_ISOLATE = 19
 VS_OPT_FP_GENERIC = 17
 VS_OPT_SHA_GRID_PER_CU = 18
 VS_DEDUP_KNOWN = 0xFFFFFFFF
@@ -178,6 +179,8 @@ def _load() -> ctypes.CDLL:
         "vs_cdc_process": (c_int, [vp, vp, c_u64, c_u64, c_int, u64p, u64p]),
         "vs_cdc_get_chunks": (c_int, [vp, c_u64, c_u64, ctypes.POINTER(VsChunk)]),
         "vs_cdc_timing": (c_int, [vp, c_int, ctypes.POINTER(ctypes.c_double), u64p]),
+        "vs_cdc_timing_detail": (c_int, [vp, ctypes.POINTER(ctypes.c_double), u64p]),
+        "vs_cdc_fence": (c_int, [vp, ctypes.c_uint64]),
         "vs_sha256_open": (c_int, [c_int, ctypes.POINTER(vp)]),
         "vs_sha256_run_device": (c_int, [vp, vp, vp, vp, c_size, vp, vp]),
         "vs_sha256_close": (None, [vp]),

@@ -291,6 +291,21 @@ class DeviceChunker:
         check(lib.vs_cdc_timing(self._h, 1 if enable else 0, ms, cnt))
         return list(ms), list(cnt)
 
+    def fence(self, batch: int) -> None:
+        """Order the next scan after batch `batch`'s blob IDs are final
+        (vs_cdc_fence): what a producer overwriting that batch's bytes needs."""
+        check(lib.vs_cdc_fence(self._h, batch))
+
+    def timing_detail(self):
+        """The interval the last timing() call closed: SHA-256 kernel ms in
+        all, outside every fingerprint window, inside one, the fingerprint
+        windows' union; and the chunks the final drains hashed in latency mode."""
+        d = (ctypes.c_double * 4)()
+        q = ctypes.c_uint64(0)
+        check(lib.vs_cdc_timing_detail(self._h, d, ctypes.byref(q)))
+        return {"sha_ms": d[0], "sha_outside_fp_ms": d[1], "sha_inside_fp_ms": d[2],
+                "fp_union_ms": d[3], "quad_chains": q.value}
+
     def close(self) -> None:
         if self._h:
             lib.vs_cdc_close(self._h)

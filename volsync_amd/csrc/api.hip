@@ -137,6 +137,15 @@ struct vs_cdc {
     std::vector<hipEvent_t> ev_pool;
     double ms[4] = {0, 0, 0, 0};
     uint64_t launches[4] = {0, 0, 0, 0};
+    // the fingerprint and SHA-256 kernel windows of the timed region as
+    // [start, end) ms after `anchor` (recorded on the main stream when timing
+    // starts), so the SHA-256 time can be split into the part inside a
+    // fingerprint window and the part outside (vs_cdc_timing_detail)
+    hipEvent_t anchor = nullptr;
+    bool anchored = false;
+    std::vector<std::pair<double, double>> win_fp, win_sha;
+    double detail[4] = {0, 0, 0, 0};
+    uint64_t quad_chains = 0;  // chains the drains ran in latency mode (timed region)
 };
 
 namespace vsgpu {
@@ -185,6 +194,10 @@ static void drain_timers(vs_cdc *h) {
         if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
             h->ms[p.stage] += ms;
             h->launches[p.stage] += 1;
+            float t0 = 0;
+            if (h->anchored && (p.stage == kStFp || p.stage == kStSha) &&
+                hipEventElapsedTime(&t0, h->anchor, p.a) == hipSuccess)
+                (p.stage == kStFp ? h->win_fp : h->win_sha).push_back({t0, (double)t0 + ms});
         }
         h->ev_pool.push_back(p.a);
         h->ev_pool.push_back(p.b);
@@ -220,7 +233,9 @@ static int run_slice(vs_cdc *h, uint32_t budget) {
     // (comparable with a rocprofv3 kernel trace); its bookkeeping launches
     // (histogram, scan, scatter) are not timed
     if (h->timing) h->sha.ev_get = [h] { return get_event(h); };
+    h->sha.last_quad_chains = 0;
     const int rc = h->sha.slice(budget, h->hstream);
+    h->quad_chains += h->sha.last_quad_chains;
     h->sha.ev_get = nullptr;
     for (auto &p : h->sha.kernel_pairs) h->pend.push_back({kStSha, p.first, p.second});
     h->sha.kernel_pairs.clear();
@@ -1120,6 +1135,7 @@ VS_API void vs_cdc_close(vs_cdc *h) {
     PinnedVec<uint8_t>().swap(h->rb);
     if (h->ev_ready) (void)hipEventDestroy(h->ev_ready);
     if (h->ev_null) (void)hipEventDestroy(h->ev_null);
+    if (h->anchor) (void)hipEventDestroy(h->anchor);
     if (h->own_h) (void)hipStreamDestroy(h->own_h);
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
@@ -1190,6 +1206,17 @@ VS_API int vs_cdc_process(vs_cdc *h, const void *dev_data, uint64_t len, uint64_
 
 VS_API int vs_cdc_wait(vs_cdc *h) { return cdc_wait(h); }
 
+VS_API int vs_cdc_fence(vs_cdc *h, uint64_t batch) {
+    if (!h) return fail(VS_ERR_ARG, "null handle");
+    if (batch >= h->seq) return fail(VS_ERR_STATE, "no such finished batch");
+    VS_TRY(set_dev(h));
+    if (h->slots.empty()) return 0;
+    const size_t k = (size_t)(batch % h->slots.size());
+    // a recycled slot's batch was waited for when its slot was reused
+    if (h->slots[k].seq != batch) return 0;
+    return slot_free(h, k);
+}
+
 VS_API int vs_cdc_get_chunks(vs_cdc *h, uint64_t first, uint64_t n, vs_chunk *out) {
     return cdc_get_chunks(h, first, n, out);
 }
@@ -1201,11 +1228,47 @@ VS_API int vs_cdc_timing(vs_cdc *h, int enable, double ms_out[4], uint64_t launc
         for (int i = 0; i < 4; ++i) ms_out[i] = h->ms[i];
     if (launches_out)
         for (int i = 0; i < 4; ++i) launches_out[i] = h->launches[i];
+    // SHA-256 kernel time inside / outside the union of fingerprint windows
+    {
+        auto &f = h->win_fp;
+        std::sort(f.begin(), f.end());
+        std::vector<std::pair<double, double>> u;  // union of the fingerprint windows
+        for (auto &w : f) {
+            if (!u.empty() && w.first <= u.back().second) u.back().second = std::max(u.back().second, w.second);
+            else u.push_back(w);
+        }
+        double sha = 0, inside = 0, fp = 0;
+        for (auto &w : u) fp += w.second - w.first;
+        for (auto &w : h->win_sha) {
+            sha += w.second - w.first;
+            for (auto &v : u) inside += std::max(0.0, std::min(w.second, v.second) - std::max(w.first, v.first));
+        }
+        h->detail[0] = sha;
+        h->detail[1] = sha - inside;  // SHA-256 kernel time outside every fingerprint window
+        h->detail[2] = inside;
+        h->detail[3] = fp;            // the fingerprint windows' union
+        h->win_fp.clear();
+        h->win_sha.clear();
+    }
     for (int i = 0; i < 4; ++i) {
         h->ms[i] = 0;
         h->launches[i] = 0;
     }
     h->timing = enable != 0;
+    h->anchored = false;
+    if (h->timing) {
+        if (!h->anchor) VS_HIP(hipEventCreate(&h->anchor));
+        VS_HIP(hipEventRecord(h->anchor, h->stream));
+        h->anchored = true;
+    }
+    return 0;
+}
+
+VS_API int vs_cdc_timing_detail(vs_cdc *h, double out[4], uint64_t *quad_chains) {
+    if (!h || !out) return fail(VS_ERR_ARG, "bad arguments");
+    for (int i = 0; i < 4; ++i) out[i] = h->detail[i];
+    if (quad_chains) *quad_chains = h->quad_chains;
+    h->quad_chains = 0;
     return 0;
 }
 
@@ -1403,9 +1466,14 @@ static int sha_option(ShaEngine &e, int option, int64_t value) {
         e.grid_per_cu = (uint32_t)value;
         return 0;
     }
+    if (option == VS_OPT_SHA_ISOLATE) {
+        if (value < 0 || value > 1) return fail(VS_ERR_ARG, "isolate is 0 or 1");
+        e.isolate = value != 0;
+        return 0;
+    }
     if (option != VS_OPT_SHA_QUAD_PCT) return fail(VS_ERR_ARG, "unknown option " + std::to_string(option));
-    if (value < 0 || value > 1000) return fail(VS_ERR_ARG, "quad share out of range");
-    e.quad_pct = (uint32_t)value;
+    if (value < -1 || value > 1000) return fail(VS_ERR_ARG, "quad share out of range");
+    e.quad_pct = value < 0 ? ShaEngine::kQuadAuto : (uint32_t)value;
     return 0;
 }
 

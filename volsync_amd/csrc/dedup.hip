@@ -9,7 +9,7 @@
 // then, within each run of equal 8-byte prefixes, a full 32-byte compare
 // against the earlier members of the run (prefix collisions of distinct
 // SHA-256 IDs are vanishingly rare, but the result does not rely on it).
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "internal.hpp"
 
@@ -153,9 +153,8 @@ hipError_t launch_dedup_known(const uint8_t *ids, uint64_t n, const uint8_t *kno
 
 size_t index_sort_tmp_bytes(uint64_t n) {
     size_t b = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint64_t *)nullptr,
-                                             (uint64_t *)nullptr, (const uint32_t *)nullptr,
-                                             (uint32_t *)nullptr, (int)n, 0, 64);
+    (void)rocprim::radix_sort_pairs(nullptr, b, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                    (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)n, 0, 64);
     // keys, sorted keys, idx, sorted idx, a copy of the IDs, then the scratch
     return n * (8 + 8 + 4 + 4 + 32) + 512 + b;
 }
@@ -175,7 +174,7 @@ hipError_t launch_index_sort(uint8_t *ids, uint64_t n, void *tmp, size_t tmp_byt
     idx_keys_kernel<<<blocks, 256, 0, s>>>(ids, n, keys, idx);
     hipError_t e = hipMemcpyAsync(copy, ids, 32 * n, hipMemcpyDeviceToDevice, s);
     if (e != hipSuccess) return e;
-    e = hipcub::DeviceRadixSort::SortPairs(scratch, sb, keys, skeys, idx, sidx, (int)n, 0, 64, s);
+    e = rocprim::radix_sort_pairs(scratch, sb, keys, skeys, idx, sidx, (size_t)n, 0, 64, s);
     if (e != hipSuccess) return e;
     idx_gather_kernel<<<(uint32_t)((2 * n + 255) / 256), 256, 0, s>>>(copy, n, sidx, ids);
     return hipGetLastError();
@@ -183,9 +182,8 @@ hipError_t launch_index_sort(uint8_t *ids, uint64_t n, void *tmp, size_t tmp_byt
 
 size_t dedup_tmp_bytes(uint64_t n) {
     size_t b = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint64_t *)nullptr,
-                                             (uint64_t *)nullptr, (const uint32_t *)nullptr,
-                                             (uint32_t *)nullptr, (int)n, 0, 64);
+    (void)rocprim::radix_sort_pairs(nullptr, b, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                    (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)n, 0, 64);
     // keys, sorted keys, idx, sorted idx, counter, then the sort scratch
     return n * (8 + 8 + 4 + 4) + 512 + b;
 }
@@ -207,7 +205,7 @@ hipError_t launch_dedup(const uint8_t *ids, uint64_t n, uint32_t *first, void *t
     size_t sb = tmp_bytes - (size_t)(scratch - t);
     const uint32_t blocks = (uint32_t)((n + 255) / 256);
     dd_keys_kernel<<<blocks, 256, 0, s>>>(ids, n, keys, idx);
-    e = hipcub::DeviceRadixSort::SortPairs(scratch, sb, keys, skeys, idx, sidx, (int)n, 0, 64, s);
+    e = rocprim::radix_sort_pairs(scratch, sb, keys, skeys, idx, sidx, (size_t)n, 0, 64, s);
     if (e != hipSuccess) return e;
     dd_first_kernel<<<blocks, 256, 0, s>>>(ids, n, skeys, sidx, first, n_unique_dev);
     return hipGetLastError();

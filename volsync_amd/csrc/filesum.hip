@@ -98,11 +98,11 @@ __global__ __launch_bounds__(256) void fs_contrib_kernel(const uint8_t *p, uint6
 hipError_t launch_fs_contrib(const uint8_t *p, uint64_t nb, uint64_t *C, hipStream_t s) {
     if (!nb) return hipSuccess;
     const uint64_t waves = (nb + 64 / VS_FS_LANES - 1) / (64 / VS_FS_LANES);
-    // one wave per block group up to 2^24 workgroups (the grid's 2^32-thread
-    // limit; at 16 lanes a 128 GiB file needs 2^23); the kernel strides over
-    // any rest.  (Capped at 2^20 workgroups, every wave striding, the 64 GiB
+    // one wave per block group up to 2^24 - 1 workgroups (a grid's global
+    // size must stay below 2^32 threads; at 16 lanes a 128 GiB file needs
+    // 2^23); the kernel strides over any rest.  (Capped at 2^20 workgroups, every wave striding, the 64 GiB
     // pass took 12.7-12.9 ms against 12.3: profiles/r05_r7/contrib_lanes.)
-    const uint64_t wgs = std::min<uint64_t>((waves + 3) / 4, 1ull << 24);
+    const uint64_t wgs = std::min<uint64_t>((waves + 3) / 4, (1ull << 24) - 1);
     fs_contrib_kernel<<<(uint32_t)wgs, 256, 0, s>>>(p, nb, C);
     return hipGetLastError();
 }

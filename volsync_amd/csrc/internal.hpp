@@ -42,7 +42,7 @@ struct DmaD2H {
     bool init(int device);                     // false: no DMA path (use hipMemcpyAsync)
     void release();
     bool start(int slot, void *dst, const void *src, size_t n);  // async; signal `slot`
-    void wait(int slot);                       // until copy `slot` has landed
+    bool wait(int slot);                       // until copy `slot` has landed; false: it failed
     bool ready = false;
 
     int engine = -1;                           // the SDMA engine copies go to (-1: the runtime's pick)
@@ -255,7 +255,10 @@ struct ShaSliceArgs {
     uint32_t *tile_ctr;
     uint32_t budget;         // max blocks per chain in this slice (0xffffffff: all)
     uint32_t quad_chains;    // the first (longest) chains of the order run in latency mode
+    uint32_t tiles;          // kShaTilesAll / kShaTilesQuad / kShaTilesSplit: which tiles
+                             // this launch takes (an isolated drain launches both kinds apart)
 };
+enum { kShaTilesAll = 0, kShaTilesQuad = 1, kShaTilesSplit = 2 };
 
 // Host side of the engine: a double-buffered active list on the device, fed by
 // append_*() and advanced by slice(); every call queues on the given stream
@@ -284,10 +287,22 @@ struct ShaEngine {
     std::function<hipEvent_t()> ev_get;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> kernel_pairs;
     int init(int dev);
-    // the final drain runs its longest chains in latency (quad) mode: those
-    // with at least quad_frac_pct % of the longest chain's remaining blocks
-    // (VSGPU_SHA_QUAD_PCT overrides; 0 disables, 100+ only the longest bucket)
-    uint32_t quad_pct = 80;
+    // the final drain runs its longest chains in latency (quad) mode
+    // (VS_OPT_SHA_QUAD_PCT): kQuadAuto = every chain that would otherwise
+    // finish after the drain's floor; p = those with at least p % of the
+    // longest chain's remaining blocks; 0 disables
+    static constexpr uint32_t kQuadAuto = 0xffffffffu;
+    uint32_t quad_pct = kQuadAuto;
+    uint32_t last_quad_chains = 0;  // chains the last drain ran in quad mode (stats)
+    // Isolated latency drain (VS_OPT_SHA_ISOLATE, default on): the quad tiles
+    // run on a stream masked to a reserved set of CUs, two per CU (one wave
+    // per SIMD), and the split tiles on a stream masked to the rest, so the
+    // drain's critical chains never share a SIMD with the bulk
+    bool isolate = true;
+    uint32_t iso_cus = 0;                     // CUs reserved by iso_q's mask
+    hipStream_t iso_q = nullptr, iso_b = nullptr;
+    hipEvent_t iso_ev[3] = {nullptr, nullptr, nullptr};   // fork, quad done, bulk done
+    int iso_streams(uint32_t r);
     // persistent-grid cap (VS_OPT_SHA_GRID_PER_CU): split mode workgroups per
     // CU (default 5, the LDS limit), throughput mode waves per SIMD (default 3)
     uint32_t grid_per_cu = 0;

@@ -16,7 +16,7 @@
 //                 walk visits are computed in batches (rs_strong_kernel).
 // HBM layout: source/basis bytes as given (16-byte aligned base); candidates
 // (offset u64, sum u32) appended then radix-sorted by offset.  DESIGN.md 4.
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "internal.hpp"
 #include "strong.hpp"
@@ -538,8 +538,7 @@ hipError_t launch_rs_table(const uint32_t *sum1, uint32_t count, uint64_t *keys,
                            uint32_t fbits, uint32_t *filt, hipStream_t s) {
     if (!count) return hipSuccess;
     rs_keys_kernel<<<(count + 255) / 256, 256, 0, s>>>(sum1, count, keys);
-    hipError_t e = hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, keys, tkey, (int)count, 0, 64,
-                                                     s);
+    hipError_t e = rocprim::radix_sort_keys(tmp, tmp_bytes, keys, tkey, (size_t)count, 0, 64, s);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(filt, 0, rs_filter_bytes(fbits), s);
     if (e != hipSuccess) return e;
@@ -580,12 +579,12 @@ hipError_t launch_rs_buckets(const uint64_t *tkey, uint32_t count, uint32_t rema
 size_t rs_sort_tmp_bytes(uint64_t n_keys, bool pairs) {
     size_t b = 0;
     if (pairs)
-        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint64_t *)nullptr,
-                                                 (uint64_t *)nullptr, (const uint32_t *)nullptr,
-                                                 (uint32_t *)nullptr, (int)n_keys, 0, 64);
+        (void)rocprim::radix_sort_pairs(nullptr, b, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                        (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                        (size_t)n_keys, 0, 64);
     else
-        (void)hipcub::DeviceRadixSort::SortKeys(nullptr, b, (const uint64_t *)nullptr,
-                                                (uint64_t *)nullptr, (int)n_keys, 0, 64);
+        (void)rocprim::radix_sort_keys(nullptr, b, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                       (size_t)n_keys, 0, 64);
     return b;
 }
 
@@ -918,8 +917,8 @@ hipError_t launch_rs_sort_cands(void *tmp, size_t tmp_bytes, const uint64_t *off
                                 uint64_t *off_out, const uint32_t *sum_in, uint32_t *sum_out,
                                 uint64_t n, int end_bit, hipStream_t s) {
     if (!n) return hipSuccess;
-    return hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, off_in, off_out, sum_in, sum_out,
-                                              (int)n, 0, end_bit, s);
+    return rocprim::radix_sort_pairs(tmp, tmp_bytes, off_in, off_out, sum_in, sum_out, (size_t)n, 0,
+                                     (unsigned)end_bit, s);
 }
 
 }  // namespace vsgpu

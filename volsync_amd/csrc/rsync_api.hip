@@ -75,6 +75,10 @@ struct RsRun {
 // pinned ring and are hashed on the host thread.
 struct FsJob {
     static constexpr uint64_t kRowsCap = 8ull << 30;   // rows of a 128 GiB file
+    // pinned row copies per handle, over its jobs: three 64 GiB
+    // files in flight fit; beyond it idle slots give theirs up, then the job
+    // takes the piece ring
+    static constexpr uint64_t kPinnedRowsCap = 16ull << 30;
     DmaD2H dma;
     DevBuf rows;                          // rows-first: every block's row
     uint8_t *hrows = nullptr;             // rows-first: their pinned copy
@@ -1419,18 +1423,25 @@ void fs_thread(FsJob *j) {
                 return fail_here(hipErrorUnknown, "file-sum tail read-back (DMA)");
         }
         for (uint64_t c = 0; c < nc; ++c)
-            if (!j->dma.start((int)c, j->hrows + c * cb, rows + c * cb, std::min(cb, total - c * cb)))
+            if (!j->dma.start((int)c, j->hrows + c * cb, rows + c * cb, std::min(cb, total - c * cb))) {
+                // copies already queued still write into hrows / hlast: they
+                // must land before the job ends and its buffers can be freed
+                for (uint64_t k = 0; k < c; ++k) (void)j->dma.wait((int)k);
+                if (j->whole) (void)j->dma.wait(FsJob::kChunks);
                 return fail_here(hipErrorUnknown, "file-sum rows read-back (DMA)");
+            }
+        bool copies_ok = true;
         for (uint64_t c = 0; c < nc; ++c) {
             const double w0 = now_ms();
-            j->dma.wait((int)c);
+            copies_ok &= j->dma.wait((int)c);
             dwait += now_ms() - w0;
             const uint64_t n = std::min(cb, total - c * cb) / 64;
             const double c0 = now_ms();
             xxh3_chain_rows((const uint64_t *)(j->hrows + c * cb), n, j->acc);
             chain += now_ms() - c0;
         }
-        if (j->whole) j->dma.wait(FsJob::kChunks);
+        if (j->whole) copies_ok &= j->dma.wait(FsJob::kChunks);
+        if (!copies_ok) return fail_here(hipErrorUnknown, "file-sum rows read-back (DMA copy error)");
         j->host_ms = chain;
         j->dev_ms = kms;
 #if VS_FS_TRACE
@@ -1603,27 +1614,49 @@ int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
         j.nb = whole ? (len - 1) / 1024 : len / 1024;
         if (whole || !acc_in) xxh3_init_acc(j.acc);
         else memcpy(j.acc, acc_in, 64);
-        j.rows_first = j.nb > 0 && j.nb * 64 <= FsJob::kRowsCap && j.dma.init(j.device);
+        // rows first unless VS_OPT_FILE_SUM_PIECE asks for the piece ring (a
+        // nonzero piece forces it: tests reach the ring path that files over
+        // kRowsCap, a failed pin and hosts without the DMA path take)
+        j.rows_first = h->fs_piece == 0 && j.nb > 0 && j.nb * 64 <= FsJob::kRowsCap &&
+                       j.dma.init(j.device);
         if (j.rows_first && j.hrows_cap < j.nb * 64) {
-            // The pinned copy, kept across jobs.  Page-locking 4 GiB takes
-            // ~175 ms on the caller's thread, so every idle slot of the FIFO
-            // is sized at once (the first file pays for all, not the first
-            // file of each slot: profiles/r05_r7/queued)
-            auto grow = [&](FsJob &o) {
-                pinned_free(o.hrows);
-                o.hrows = (uint8_t *)pinned_alloc((size_t)j.nb * 64);
-                o.hrows_cap = o.hrows ? j.nb * 64 : 0;
+            // The pinned copy, kept across jobs and bounded per handle
+            // (kPinnedRowsCap over the FIFO's slots and the blocking job).
+            // Page-locking 4 GiB takes ~175 ms on the caller's thread, so idle
+            // slots are sized at once as far as the bound allows (the first
+            // file pays for all, not the first file of each slot:
+            // profiles/r05_r7/queued)
+            const uint64_t need = j.nb * 64;
+            auto busy = [&](uint32_t k) {   // slot k holds a job in flight
+                return ((k - h->fs_head) % vs_rsync::kFsJobs) < h->fs_tail - h->fs_head;
             };
-            grow(j);
+            auto total = [&] {
+                uint64_t t = h->fs_sync.hrows_cap;
+                for (auto &o : h->fs) t += o.hrows_cap;
+                return t;
+            };
+            auto drop = [&](FsJob &o) {
+                if (o.th.joinable()) o.th.join();
+                pinned_free(o.hrows);
+                o.hrows = nullptr;
+                o.hrows_cap = 0;
+            };
+            auto grow = [&](FsJob &o) {
+                drop(o);
+                o.hrows = (uint8_t *)pinned_alloc((size_t)need);
+                o.hrows_cap = o.hrows ? need : 0;
+            };
+            drop(j);
+            // over the bound: release idle slots' smaller copies first
+            for (uint32_t k = 0; k < vs_rsync::kFsJobs && total() + need > FsJob::kPinnedRowsCap; ++k)
+                if (&h->fs[k] != &j && !busy(k)) drop(h->fs[k]);
+            if (total() + need <= FsJob::kPinnedRowsCap) grow(j);
             if (!sync)
                 for (uint32_t k = 0; k < vs_rsync::kFsJobs; ++k) {
                     FsJob &o = h->fs[k];
-                    const uint32_t pos = (k - h->fs_head) % vs_rsync::kFsJobs;
-                    const bool busy = pos < h->fs_tail - h->fs_head;   // in flight
-                    if (&o != &j && !busy && o.hrows_cap < j.nb * 64) {
-                        if (o.th.joinable()) o.th.join();
+                    if (&o != &j && !busy(k) && o.hrows_cap < need &&
+                        total() - o.hrows_cap + need <= FsJob::kPinnedRowsCap)
                         grow(o);
-                    }
                 }
             j.rows_first = j.hrows != nullptr;   // else the bounded piece ring
         }

@@ -474,6 +474,15 @@ __device__ __forceinline__ void wide_issue(uint32_t rb, uint32_t sb, uint64_t &r
 #define VS_WIDE_PIPE 3
 #endif
 constexpr uint32_t kWidePipe = VS_WIDE_PIPE;   // stripes in flight per lane
+// wide_issue's loads are invisible to the compiler until wide_wait: a copy or
+// spill of r01 / r23 / r45 / kk between the two would read the registers
+// before the data lands.  tools/check_lds_asm.py checks the compiled walk for
+// that (every read of a pending destination VGPR before its s_waitcnt); the
+// shipped depths are the ones it has passed.
+#ifndef VS_WIDE_UNCHECKED
+static_assert(VS_WIDE_PIPE == 3 && VS_WIDE_D == 8,
+              "wide-flush depth not checked by tools/check_lds_asm.py (define VS_WIDE_UNCHECKED for A/B builds)");
+#endif
 template <uint32_t N>
 __device__ __forceinline__ void wide_wait(uint64_t &r01, uint64_t &r23, uint64_t &r45, u64x2 &kk) {
     static_assert(N <= 15, "lgkmcnt");

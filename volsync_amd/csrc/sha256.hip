@@ -360,6 +360,12 @@ __device__ __forceinline__ void produce_tile(uint4 (&wk)[2][16 * 64], const ShaC
     }
 }
 
+#ifndef VS_SHA_QUAD_PPRIO
+// latency tiles' producers at the consumers' priority: measured slower in a
+// mixed drain (C3 rank single pass 334-371 against 321-327 ms,
+// profiles/r06_first/ab_single_c3r3.log), so off
+#define VS_SHA_QUAD_PPRIO 0
+#endif
 // Tiles [0, qt) hold the first (longest) a.quad_chains chains of the order, 16
 // per tile, consumed in latency mode (compress_quad; the producer's lanes
 // 16..63 idle); the later tiles hold 64 chains each in split mode.
@@ -380,14 +386,17 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
     const uint32_t n = *a.n_cur;
     const uint32_t nq = min(a.quad_chains, n);
     const uint32_t qt = (nq + 15) / 16;
-    const uint32_t ntiles = qt + (n - nq + 63) / 64;
-    if (qt) {
+    // the launch's tile range: every tile, or (an isolated drain) the quad
+    // tiles alone / the split tiles alone
+    const uint32_t t_lo = a.tiles == kShaTilesSplit ? qt : 0u;
+    const uint32_t ntiles = a.tiles == kShaTilesQuad ? qt : qt + (n - nq + 63) / 64;
+    if (qt && a.tiles != kShaTilesSplit) {
         for (uint32_t i = threadIdx.x; i < 16 * 16; i += blockDim.x) zero_kw[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
     }
     if (!producer) __builtin_amdgcn_s_setprio(2);  // the rounds are the critical path
     for (;;) {
-        if (threadIdx.x == 0) tile_sh = atomicAdd(a.tile_ctr, 1u);
+        if (threadIdx.x == 0) tile_sh = t_lo + atomicAdd(a.tile_ctr, 1u);
         __syncthreads();
         const uint32_t t = tile_sh;
         __syncthreads();
@@ -407,8 +416,16 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
         steps = __builtin_amdgcn_readfirstlane(steps);
         if (steps == 0) continue;
         if (producer) {
-            if (quad) produce_tile<true>(wk, ch0, mine, steps, lane);
-            else produce_tile<false>(wk, ch0, mine, steps, lane);
+            if (quad) {
+                // a latency tile's producer feeds the drain's critical path:
+                // beside busy split tiles it would otherwise need ~6000
+                // cycles per block against the quad consumer's ~3800
+                if (VS_SHA_QUAD_PPRIO) __builtin_amdgcn_s_setprio(3);
+                produce_tile<true>(wk, ch0, mine, steps, lane);
+                if (VS_SHA_QUAD_PPRIO) __builtin_amdgcn_s_setprio(0);
+            } else {
+                produce_tile<false>(wk, ch0, mine, steps, lane);
+            }
         } else if (quad) {
             __builtin_amdgcn_s_setprio(3);  // the drain's critical path
             const uint32_t role = lane & 3, c = lane >> 2;
@@ -684,6 +701,15 @@ int ShaEngine::init(int dev) {
 }
 
 void ShaEngine::release() {
+    for (hipStream_t *q : {&iso_q, &iso_b})
+        if (*q) {
+            (void)hipStreamSynchronize(*q);
+            (void)hipStreamDestroy(*q);
+            *q = nullptr;
+        }
+    iso_cus = 0;
+    for (auto &e : iso_ev)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
     for (DevBuf *b : {&list[0], &list[1], &order, &hist, &ctl}) b->release();
     groups.clear();
     ub = 0;
@@ -784,8 +810,7 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
     VS_HIP(launch_scan_u32(hist.as<uint32_t>(), cursor, kShaBuckets, partials, 0xffffffffu, s));
     sha_scatter_kernel<<<sb, 256, 0, s>>>(list[cur].as<ShaChain>(), count(cur), budget, cursor,
                                           order.as<uint32_t>());
-    // quad drain: the chains within quad_pct % of the longest remaining one
-    // (bucket histogram read back: one synchronisation per drain)
+    // quad drain (bucket histogram read back: one synchronisation per drain)
     uint32_t quad_chains = 0;
     if (mode == kShaQuad) {
         VS_HIP(hipMemcpyAsync(hist_h, hist.p, kShaBuckets * 4, hipMemcpyDeviceToHost, s));
@@ -794,17 +819,34 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
         while (first < kShaBuckets && hist_h[first] == 0) ++first;
         double blocks = 0;
         for (uint32_t k = first; k < kShaBuckets; ++k) blocks += (double)hist_h[k] * bucket_blocks(k);
-        // latency-bound only: the backlog at split-mode throughput (~1.45 TB/s,
-        // 22.7 G blocks/s) clears well before the longest chain would at
-        // split-mode chain speed (~1.95 us per block); otherwise the quad
-        // tiles' idle producer lanes only cost throughput
-        if (first < kShaBuckets && blocks / 22.7e9 < 0.8 * 1.95e-6 * (double)bucket_blocks(first)) {
-            const uint64_t lmax = bucket_blocks(first);
-            for (uint32_t k = first; k < kShaBuckets; ++k) {
-                if (bucket_blocks(k) * 100 < lmax * quad_pct) break;
-                quad_chains += hist_h[k];
+        // Per-block costs of a chain: split mode beside a busy
+        // chip ~2.8 us (the producer crowded on its SIMD), quad mode ~1.6 us
+        // (11 issue slots per round); the backlog clears at split-mode
+        // throughput, ~1.45 TB/s = 22.7 G blocks/s.
+        constexpr double kSplitBlockS = 2.8e-6, kQuadBlockS = 1.6e-6, kBulkBlocksPerS = 22.7e9;
+        const double lmax = first < kShaBuckets ? (double)bucket_blocks(first) : 0.0;
+        const double t_bulk = blocks / kBulkBlocksPerS;
+        // latency-bound only: the longest chain in split mode would outlast the
+        // backlog; otherwise the quad tiles' idle producer lanes only cost
+        // throughput
+        if (first < kShaBuckets && lmax * kSplitBlockS > t_bulk) {
+            if (quad_pct == kQuadAuto) {
+                // the drain cannot end before max(longest chain in quad mode,
+                // backlog); every chain that would pass that floor in split
+                // mode runs in quad mode, started first (tile order)
+                const double floor_s = std::max(lmax * kQuadBlockS, t_bulk);
+                for (uint32_t k = first; k < kShaBuckets; ++k) {
+                    if ((double)bucket_blocks(k) * kSplitBlockS <= floor_s) break;
+                    quad_chains += hist_h[k];
+                }
+            } else {
+                for (uint32_t k = first; k < kShaBuckets; ++k) {
+                    if ((double)bucket_blocks(k) * 100 < lmax * quad_pct) break;
+                    quad_chains += hist_h[k];
+                }
             }
         }
+        last_quad_chains = quad_chains;
     }
     // zero the next list's count and the tile counter
     VS_HIP(hipMemsetAsync(count(nxt), 0, 4, s));
@@ -818,10 +860,39 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
     a.tile_ctr = count(2);
     a.budget = budget;
     a.quad_chains = quad_chains;
+    a.tiles = kShaTilesAll;
     const uint64_t tiles = (ub + 63) / 64 + (quad_chains + 15) / 16;
     hipEvent_t ka = ev_get ? ev_get() : nullptr, kb = ka ? ev_get() : nullptr;
     if (kb) VS_HIP(hipEventRecord(ka, s));
-    if (mode == kShaWide) {
+    const uint64_t qt = (quad_chains + 15) / 16;
+    // reserved CUs: two quad tiles per CU, in steps of 16 CUs, at most half
+    const uint32_t r_cus = (uint32_t)std::min<uint64_t>(((qt + 1) / 2 + 15) / 16 * 16,
+                                                         (uint64_t)std::max(cus, 2) / 2);
+    if (mode == kShaQuad && qt && isolate && iso_streams(r_cus) == 0) {
+        // the quad tiles on the reserved CUs, padded to 64 KiB of LDS per
+        // workgroup so that at most two share a CU (their four waves one per
+        // SIMD); the split tiles on the other CUs; s resumes after both
+        VS_HIP(hipMemsetAsync(count(3), 0, 4, s));
+        VS_HIP(hipEventRecord(iso_ev[0], s));
+        VS_HIP(hipStreamWaitEvent(iso_q, iso_ev[0], 0));
+        VS_HIP(hipStreamWaitEvent(iso_b, iso_ev[0], 0));
+        ShaSliceArgs aq = a, ab = a;
+        aq.tiles = kShaTilesQuad;
+        ab.tiles = kShaTilesSplit;
+        ab.tile_ctr = count(3);
+        sha_slice_kernel<<<(uint32_t)std::min<uint64_t>(qt, 2ull * iso_cus), 128, 32 * 1024, iso_q>>>(aq);
+        VS_HIP(hipGetLastError());
+        const uint64_t st = tiles - qt;
+        if (st) {
+            const uint64_t slots = (uint64_t)std::max<int>(cus - (int)iso_cus, 1) * (grid_per_cu ? grid_per_cu : 5);
+            sha_slice_kernel<<<(uint32_t)std::min<uint64_t>(st, slots), 128, 0, iso_b>>>(ab);
+            VS_HIP(hipGetLastError());
+        }
+        VS_HIP(hipEventRecord(iso_ev[1], iso_q));
+        VS_HIP(hipEventRecord(iso_ev[2], iso_b));
+        VS_HIP(hipStreamWaitEvent(s, iso_ev[1], 0));
+        VS_HIP(hipStreamWaitEvent(s, iso_ev[2], 0));
+    } else if (mode == kShaWide) {
         // persistent grid: 3 waves per SIMD (launch bounds: <= 168 VGPRs)
         const uint64_t slots =
             std::max<uint64_t>((uint64_t)std::max(cus, 1) * 4 * (grid_per_cu ? grid_per_cu : 3) / kWideWaves, 1);
@@ -850,6 +921,43 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
     }
     groups.swap(keep);
     ub = nub;
+    return 0;
+}
+
+// the isolated drain's two CU-masked streams: r reserved CUs spread evenly
+// over the mask (every XCD and shader engine gets its share), the rest for
+// the bulk.  A masked stream owns its hardware queue.  0 = ready.
+int ShaEngine::iso_streams(uint32_t r) {
+    if (r == 0 || r >= (uint32_t)cus) return -1;
+    if (iso_q && iso_cus == r) return 0;
+    for (hipStream_t *q : {&iso_q, &iso_b})
+        if (*q) {
+            (void)hipStreamSynchronize(*q);
+            (void)hipStreamDestroy(*q);
+            *q = nullptr;
+        }
+    iso_cus = 0;
+    for (auto &e : iso_ev)
+        if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            e = nullptr;
+            return -1;
+        }
+    const uint32_t words = ((uint32_t)cus + 31) / 32;
+    std::vector<uint32_t> mq(words, 0), mb(words, 0);
+    for (uint32_t i = 0; i < (uint32_t)cus; ++i) {
+        // CU i is reserved when floor(i r / cus) steps: r of them, evenly spaced
+        const bool res = (uint64_t)(i + 1) * r / (uint32_t)cus != (uint64_t)i * r / (uint32_t)cus;
+        (res ? mq : mb)[i / 32] |= 1u << (i % 32);
+    }
+    if (hipExtStreamCreateWithCUMask(&iso_q, words, mq.data()) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&iso_b, words, mb.data()) != hipSuccess) {
+        (void)hipGetLastError();
+        for (hipStream_t *q : {&iso_q, &iso_b})
+            if (*q) (void)hipStreamDestroy(*q), *q = nullptr;
+        return -1;
+    }
+    iso_cus = r;
     return 0;
 }
 

@@ -136,19 +136,25 @@ void DmaD2H::release() {
 bool DmaD2H::start(int slot, void *dst, const void *src, size_t n) {
     const hsa_signal_t s{sig_[slot]};
     hsa_signal_store_screlease(s, 1);
-    if (engine >= 0)
-        return hsa_amd_memory_async_copy_on_engine(dst, hsa_agent_t{cpu_}, src, hsa_agent_t{gpu_}, n, 0,
-                                                   nullptr, s, (hsa_amd_sdma_engine_id_t)(1u << engine),
-                                                   true) == HSA_STATUS_SUCCESS;
-    return hsa_amd_memory_async_copy(dst, hsa_agent_t{cpu_}, src, hsa_agent_t{gpu_}, n, 0, nullptr,
-                                     s) == HSA_STATUS_SUCCESS;
+    const hsa_status_t st =
+        engine >= 0
+            ? hsa_amd_memory_async_copy_on_engine(dst, hsa_agent_t{cpu_}, src, hsa_agent_t{gpu_}, n, 0,
+                                                  nullptr, s, (hsa_amd_sdma_engine_id_t)(1u << engine),
+                                                  true)
+            : hsa_amd_memory_async_copy(dst, hsa_agent_t{cpu_}, src, hsa_agent_t{gpu_}, n, 0, nullptr, s);
+    // not queued: nothing will ever lower the signal, so a later wait on
+    // this slot must not block
+    if (st != HSA_STATUS_SUCCESS) hsa_signal_store_screlease(s, 0);
+    return st == HSA_STATUS_SUCCESS;
 }
 
-void DmaD2H::wait(int slot) {
+bool DmaD2H::wait(int slot) {
     const hsa_signal_t s{sig_[slot]};
-    while (hsa_signal_wait_scacquire(s, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
-                                     HSA_WAIT_STATE_BLOCKED) != 0) {
-    }
+    hsa_signal_value_t v;
+    do {
+        v = hsa_signal_wait_scacquire(s, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+    } while (v >= 1);   // a spurious wake-up; a negative value is a copy error
+    return v == 0;
 }
 
 // The staging copies are the host side of every pageable feed (the Go
