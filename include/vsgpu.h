@@ -624,10 +624,10 @@ int vs_restic_pack_header(const uint8_t *types, const uint32_t *lengths, const u
 #define VS_OPT_SHA_GRID_PER_CU 18   /* cdc / sha: persistent hash grid per CU: split-mode
                                       * workgroups (default 5) / throughput-mode waves
                                       * per SIMD (default 3); 0 = default */
-#define VS_OPT_SHA_ISOLATE 19         /* cdc / sha: 1 (default) = a latency-bound final drain
-                                      * runs its quad tiles on CUs reserved for them (a
-                                      * CU-masked stream, one wave per SIMD) and the
-                                      * split tiles on the others; 0 = one launch */
+#define VS_OPT_SHA_ISOLATE 19         /* cdc / sha: 1 (default) = a latency-bound final
+                                      * drain gives each quad tile a CU of its own (its
+                                      * LDS padded to the whole CU), resident before the
+                                      * split tiles start beside it; 0 = one launch */
 #define VS_OPT_FP_GENERIC 17         /* cdc: 1 = the generic fingerprint address code
                                       * even where the FAST variant applies */
 #define VS_OPT_SEAL_FUSED 32         /* seal: 0 = separate CTR and MAC kernels (default 1) */

@@ -4,7 +4,7 @@
 VsError -6 "source upload failed": the one-shot vs_rsync_match's pageable
 hipMemcpy of the caller's source returned hipErrorInvalidValue.  The runtime
 refuses a pageable copy whose host range overlaps a *registered* range it does
-not fully lie in (probe: tools/probe/pin_overlap.py, profiles/r03_xfer), and
+not fully lie in (probe: tools/probe/pin_overlap.py at git 2fcace1, profiles/r03_xfer), and
 round 2's library registered heap storage (std::vector read-backs,
 hipHostRegister) that a later numpy array could come to occupy.
 

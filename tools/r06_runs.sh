@@ -32,9 +32,16 @@ case $1 in
     bash tools/gpu.sh bench c3r3 --share 3/8 --steps 20 --warmup 5 --no-cpu-baseline ;;
   iso)
     bash tools/gpu.sh tests tests/test_gpu_cdc.py -x -k "sha256 or drain or blob" &&
-    bash tools/gpu.sh py tools/single_pass.py --share 3/8 --quad auto:1,auto:0,80:0 --rounds 3 &&
+    bash tools/gpu.sh py tools/single_pass.py --share 3/8 --quad auto:1,auto:0 --rounds 3 &&
     mv gpurun_out/py_single_pass.log gpurun_out/single_c3r3.log &&
-    bash tools/gpu.sh py tools/single_pass.py --gib 64 --quad auto:1,auto:0,80:0 --rounds 3 &&
+    bash tools/gpu.sh py tools/single_pass.py --gib 64 --quad auto:1,auto:0 --rounds 3 &&
     mv gpurun_out/py_single_pass.log gpurun_out/single_c2.log ;;
-  *) echo "usage: tools/r06_runs.sh first|iso" >&2; exit 2 ;;
+  isotrace)
+    bash tools/r06_runs.sh iso && bash tools/r06_runs.sh trace ;;
+  trace)   # where the drain's tiles run (VS_SHA_TRACE build shatrace)
+    VSGPU_LIB=$PWD/$(var shatrace) bash tools/gpu.sh py tools/sha_trace.py --share 3/8 --quad auto:1,auto:0,auto:1 &&
+    mv gpurun_out/py_sha_trace.log gpurun_out/trace_c3r3.log &&
+    VSGPU_LIB=$PWD/$(var shatrace) bash tools/gpu.sh py tools/sha_trace.py --gib 64 --quad auto:1,auto:0 &&
+    mv gpurun_out/py_sha_trace.log gpurun_out/trace_c2.log ;;
+  *) echo "usage: tools/r06_runs.sh first|iso|trace" >&2; exit 2 ;;
 esac

@@ -2,8 +2,8 @@
 final, per drain rule.  One process, volume generated once.
   python tools/single_pass.py --gib 64                 # C2 (seed 2)
   python tools/single_pass.py --share 3/8              # C3 rank 3 (128 GiB of the seed-3 TiB)
-  --quad auto:1,auto:0,80:0   drain rules to compare, interleaved: VS_OPT_SHA_QUAD_PCT
-                              (auto = -1) : VS_OPT_SHA_ISOLATE
+  --quad auto:1,auto:2,auto:0   drain rules to compare, interleaved: VS_OPT_SHA_QUAD_PCT
+                              (auto = -1) : VS_OPT_SHA_ISOLATE (quad tiles per reserved CU)
 Prints one line per pass and a JSON summary (min / median per rule)."""
 import argparse
 import json

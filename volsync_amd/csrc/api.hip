@@ -1256,6 +1256,7 @@ VS_API int vs_cdc_timing(vs_cdc *h, int enable, double ms_out[4], uint64_t launc
     }
     h->timing = enable != 0;
     h->anchored = false;
+    if (h->timing) h->quad_chains = 0;
     if (h->timing) {
         if (!h->anchor) VS_HIP(hipEventCreate(&h->anchor));
         VS_HIP(hipEventRecord(h->anchor, h->stream));
@@ -1468,7 +1469,7 @@ static int sha_option(ShaEngine &e, int option, int64_t value) {
     }
     if (option == VS_OPT_SHA_ISOLATE) {
         if (value < 0 || value > 1) return fail(VS_ERR_ARG, "isolate is 0 or 1");
-        e.isolate = value != 0;
+        e.isolate = (uint32_t)value;
         return 0;
     }
     if (option != VS_OPT_SHA_QUAD_PCT) return fail(VS_ERR_ARG, "unknown option " + std::to_string(option));

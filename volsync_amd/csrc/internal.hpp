@@ -257,7 +257,10 @@ struct ShaSliceArgs {
     uint32_t quad_chains;    // the first (longest) chains of the order run in latency mode
     uint32_t tiles;          // kShaTilesAll / kShaTilesQuad / kShaTilesSplit: which tiles
                              // this launch takes (an isolated drain launches both kinds apart)
+    uint32_t *resident;      // isolated quad launch: host-visible count of resident workgroups
 };
+// an isolated quad tile's LDS: static 32 KiB + this = the CU's 160 KiB
+constexpr uint32_t kIsoPadBytes = 128 * 1024;
 enum { kShaTilesAll = 0, kShaTilesQuad = 1, kShaTilesSplit = 2 };
 
 // Host side of the engine: a double-buffered active list on the device, fed by
@@ -294,15 +297,15 @@ struct ShaEngine {
     static constexpr uint32_t kQuadAuto = 0xffffffffu;
     uint32_t quad_pct = kQuadAuto;
     uint32_t last_quad_chains = 0;  // chains the last drain ran in quad mode (stats)
-    // Isolated latency drain (VS_OPT_SHA_ISOLATE, default on): the quad tiles
-    // run on a stream masked to a reserved set of CUs, two per CU (one wave
-    // per SIMD), and the split tiles on a stream masked to the rest, so the
-    // drain's critical chains never share a SIMD with the bulk
-    bool isolate = true;
-    uint32_t iso_cus = 0;                     // CUs reserved by iso_q's mask
-    hipStream_t iso_q = nullptr, iso_b = nullptr;
-    hipEvent_t iso_ev[3] = {nullptr, nullptr, nullptr};   // fork, quad done, bulk done
-    int iso_streams(uint32_t r);
+    // Isolated latency drain (VS_OPT_SHA_ISOLATE, default on): every quad
+    // tile holds a CU alone (its LDS padded to the whole CU), resident before
+    // the split tiles are launched, so the drain's critical chains never
+    // share a CU with the bulk
+    uint32_t isolate = 1;
+    hipStream_t iso_q = nullptr;
+    hipEvent_t iso_ev[2] = {nullptr, nullptr};   // fork, quad tiles done
+    uint32_t *iso_res_h = nullptr, *iso_res_d = nullptr;   // residency counter (host / device view)
+    int iso_setup();
     // persistent-grid cap (VS_OPT_SHA_GRID_PER_CU): split mode workgroups per
     // CU (default 5, the LDS limit), throughput mode waves per SIMD (default 3)
     uint32_t grid_per_cu = 0;

@@ -28,7 +28,9 @@
 // v_bitop3_b32 does Ch / Maj / three-way XORs, v_alignbit_b32 the rotates and
 // v_perm_b32 the big-endian, byte-misaligned message words.
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
+#include <thread>
 
 #include "internal.hpp"
 
@@ -360,6 +362,33 @@ __device__ __forceinline__ void produce_tile(uint4 (&wk)[2][16 * 64], const ShaC
     }
 }
 
+// VS_SHA_TRACE builds (A/B diagnostics only): every tile of sha_slice_kernel
+// records {kind | tile, HW_ID, XCC_ID, start, end} (s_memrealtime, 100 MHz)
+// from its consumer wave, read back with vs_debug_sha_trace
+#ifndef VS_SHA_TRACE
+#define VS_SHA_TRACE 0
+#endif
+#if VS_SHA_TRACE
+constexpr uint32_t kTraceCap = 1u << 16;
+__device__ uint64_t g_sha_trace[kTraceCap * 4];
+__device__ uint32_t g_sha_trace_n;
+__device__ __forceinline__ void trace_tile(bool quad, uint32_t t, uint64_t t0, uint32_t lane) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+        const uint32_t k = atomicAdd(&g_sha_trace_n, 1u);
+        if (k < kTraceCap) {
+            g_sha_trace[4 * k + 0] = ((uint64_t)quad << 63) | t;
+            g_sha_trace[4 * k + 1] = ((uint64_t)xcc << 32) | hw;
+            g_sha_trace[4 * k + 2] = t0;
+            g_sha_trace[4 * k + 3] = t1;
+        }
+    }
+}
+#endif
+
 #ifndef VS_SHA_QUAD_PPRIO
 // latency tiles' producers at the consumers' priority: measured slower in a
 // mixed drain (C3 rank single pass 334-371 against 321-327 ms,
@@ -390,6 +419,8 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
     // tiles alone / the split tiles alone
     const uint32_t t_lo = a.tiles == kShaTilesSplit ? qt : 0u;
     const uint32_t ntiles = a.tiles == kShaTilesQuad ? qt : qt + (n - nq + 63) / 64;
+    if (a.resident && threadIdx.x == 0)   // isolated quad launch: this tile's CU is held
+        __hip_atomic_fetch_add(a.resident, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     if (qt && a.tiles != kShaTilesSplit) {
         for (uint32_t i = threadIdx.x; i < 16 * 16; i += blockDim.x) zero_kw[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
@@ -415,6 +446,9 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
         for (int o = 32; o > 0; o >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, o, 64));
         steps = __builtin_amdgcn_readfirstlane(steps);
         if (steps == 0) continue;
+#if VS_SHA_TRACE
+        const uint64_t t_tile = __builtin_amdgcn_s_memrealtime();
+#endif
         if (producer) {
             if (quad) {
                 // a latency tile's producer feeds the drain's critical path:
@@ -451,6 +485,9 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
                 st[4 + i] = x[i];
             }
             retire(a, ch0, st, valid && role == 0, mine, left, lane);
+#if VS_SHA_TRACE
+            trace_tile(true, t, t_tile, lane);
+#endif
             __builtin_amdgcn_s_setprio(2);
         } else {
             uint32_t st[8];
@@ -462,6 +499,9 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
                 __syncthreads();
             }
             retire(a, ch0, st, valid, mine, left, lane);
+#if VS_SHA_TRACE
+            trace_tile(false, t, t_tile, lane);
+#endif
         }
     }
 }
@@ -701,15 +741,15 @@ int ShaEngine::init(int dev) {
 }
 
 void ShaEngine::release() {
-    for (hipStream_t *q : {&iso_q, &iso_b})
-        if (*q) {
-            (void)hipStreamSynchronize(*q);
-            (void)hipStreamDestroy(*q);
-            *q = nullptr;
-        }
-    iso_cus = 0;
+    if (iso_q) {
+        (void)hipStreamSynchronize(iso_q);
+        (void)hipStreamDestroy(iso_q);
+        iso_q = nullptr;
+    }
     for (auto &e : iso_ev)
         if (e) (void)hipEventDestroy(e), e = nullptr;
+    if (iso_res_h) (void)hipHostFree(iso_res_h);
+    iso_res_h = iso_res_d = nullptr;
     for (DevBuf *b : {&list[0], &list[1], &order, &hist, &ctl}) b->release();
     groups.clear();
     ub = 0;
@@ -820,12 +860,22 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
         double blocks = 0;
         for (uint32_t k = first; k < kShaBuckets; ++k) blocks += (double)hist_h[k] * bucket_blocks(k);
         // Per-block costs of a chain: split mode beside a busy
-        // chip ~2.8 us (the producer crowded on its SIMD), quad mode ~1.6 us
-        // (11 issue slots per round); the backlog clears at split-mode
-        // throughput, ~1.45 TB/s = 22.7 G blocks/s.
-        constexpr double kSplitBlockS = 2.8e-6, kQuadBlockS = 1.6e-6, kBulkBlocksPerS = 22.7e9;
+        // chip ~2.8 us (the producer crowded on its SIMD); quad mode ~1.6 us
+        // beside split tiles, ~1.45 us on a CU of its own (isolated drain,
+        // profiles/r06_drain); the backlog clears at split-mode throughput,
+        // ~1.45 TB/s = 22.7 G blocks/s over the whole chip.
+        constexpr double kSplitBlockS = 2.8e-6, kBulkBlocksPerS = 22.7e9;
+        const double quad_s = isolate ? 1.45e-6 : 1.6e-6;
         const double lmax = first < kShaBuckets ? (double)bucket_blocks(first) : 0.0;
         const double t_bulk = blocks / kBulkBlocksPerS;
+        auto count_above = [&](double floor_s) {   // chains whose split-mode time passes floor_s
+            uint32_t c = 0;
+            for (uint32_t k = first; k < kShaBuckets; ++k) {
+                if ((double)bucket_blocks(k) * kSplitBlockS <= floor_s) break;
+                c += hist_h[k];
+            }
+            return c;
+        };
         // latency-bound only: the longest chain in split mode would outlast the
         // backlog; otherwise the quad tiles' idle producer lanes only cost
         // throughput
@@ -833,11 +883,18 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
             if (quad_pct == kQuadAuto) {
                 // the drain cannot end before max(longest chain in quad mode,
                 // backlog); every chain that would pass that floor in split
-                // mode runs in quad mode, started first (tile order)
-                const double floor_s = std::max(lmax * kQuadBlockS, t_bulk);
-                for (uint32_t k = first; k < kShaBuckets; ++k) {
-                    if ((double)bucket_blocks(k) * kSplitBlockS <= floor_s) break;
-                    quad_chains += hist_h[k];
+                // mode runs in quad mode, started first.  Isolated, each quad
+                // tile holds a CU, so the backlog clears on the others: raise
+                // the floor until it does
+                double floor_s = std::max(lmax * quad_s, t_bulk);
+                for (int it = 0; it < 6; ++it) {
+                    quad_chains = count_above(floor_s);
+                    if (!isolate) break;
+                    const double qtiles = (quad_chains + 15) / 16;
+                    const double free_cus = std::max((double)cus - qtiles, 1.0);
+                    const double tb = t_bulk * cus / free_cus;
+                    if (tb <= floor_s) break;
+                    floor_s = tb;
                 }
             } else {
                 for (uint32_t k = first; k < kShaBuckets; ++k) {
@@ -865,33 +922,41 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
     hipEvent_t ka = ev_get ? ev_get() : nullptr, kb = ka ? ev_get() : nullptr;
     if (kb) VS_HIP(hipEventRecord(ka, s));
     const uint64_t qt = (quad_chains + 15) / 16;
-    // reserved CUs: two quad tiles per CU, in steps of 16 CUs, at most half
-    const uint32_t r_cus = (uint32_t)std::min<uint64_t>(((qt + 1) / 2 + 15) / 16 * 16,
-                                                         (uint64_t)std::max(cus, 2) / 2);
-    if (mode == kShaQuad && qt && isolate && iso_streams(r_cus) == 0) {
-        // the quad tiles on the reserved CUs, padded to 64 KiB of LDS per
-        // workgroup so that at most two share a CU (their four waves one per
-        // SIMD); the split tiles on the other CUs; s resumes after both
+    if (mode == kShaQuad && qt && isolate && qt <= (uint64_t)cus * 3 / 4 && iso_setup() == 0) {
+        // Isolated drain: each quad tile takes a CU to itself -- its LDS padded
+        // to the CU's whole 160 KiB, so no split workgroup can join it -- and
+        // is resident before the split tiles are launched beside it; the
+        // split grid covers every CU and takes the quad tiles' CUs as they
+        // finish.  (CU-masked streams were tried first: the masks did not hold
+        // from one stream pair to the next on this runtime, split tiles ran
+        // on "reserved" CUs, profiles/r06_drain/trace_*.log.)
         VS_HIP(hipMemsetAsync(count(3), 0, 4, s));
         VS_HIP(hipEventRecord(iso_ev[0], s));
         VS_HIP(hipStreamWaitEvent(iso_q, iso_ev[0], 0));
-        VS_HIP(hipStreamWaitEvent(iso_b, iso_ev[0], 0));
         ShaSliceArgs aq = a, ab = a;
         aq.tiles = kShaTilesQuad;
+        aq.resident = iso_res_d;
         ab.tiles = kShaTilesSplit;
         ab.tile_ctr = count(3);
-        sha_slice_kernel<<<(uint32_t)std::min<uint64_t>(qt, 2ull * iso_cus), 128, 32 * 1024, iso_q>>>(aq);
+        __atomic_store_n(iso_res_h, 0u, __ATOMIC_RELAXED);
+        sha_slice_kernel<<<(uint32_t)qt, 128, kIsoPadBytes, iso_q>>>(aq);
         VS_HIP(hipGetLastError());
-        const uint64_t st = tiles - qt;
-        if (st) {
-            const uint64_t slots = (uint64_t)std::max<int>(cus - (int)iso_cus, 1) * (grid_per_cu ? grid_per_cu : 5);
-            sha_slice_kernel<<<(uint32_t)std::min<uint64_t>(st, slots), 128, 0, iso_b>>>(ab);
+        VS_HIP(hipEventRecord(iso_ev[1], iso_q));
+        // the quad tiles first: the host sees every one of them resident
+        // (each bumps a host-visible counter as it starts) before the split
+        // grid can take their CUs.  Bounded: after 10 s the split tiles go
+        // anyway (results do not depend on the placement).
+        const auto t0 = std::chrono::steady_clock::now();
+        while (__atomic_load_n(iso_res_h, __ATOMIC_ACQUIRE) < (uint32_t)qt &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10))
+            std::this_thread::yield();
+        if (tiles > qt) {
+            sha_slice_kernel<<<(uint32_t)std::min<uint64_t>(tiles - qt, (uint64_t)std::max(cus, 1) *
+                                                                           (grid_per_cu ? grid_per_cu : 5)),
+                               128, 0, s>>>(ab);
             VS_HIP(hipGetLastError());
         }
-        VS_HIP(hipEventRecord(iso_ev[1], iso_q));
-        VS_HIP(hipEventRecord(iso_ev[2], iso_b));
         VS_HIP(hipStreamWaitEvent(s, iso_ev[1], 0));
-        VS_HIP(hipStreamWaitEvent(s, iso_ev[2], 0));
     } else if (mode == kShaWide) {
         // persistent grid: 3 waves per SIMD (launch bounds: <= 168 VGPRs)
         const uint64_t slots =
@@ -924,42 +989,53 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
     return 0;
 }
 
-// the isolated drain's two CU-masked streams: r reserved CUs spread evenly
-// over the mask (every XCD and shader engine gets its share), the rest for
-// the bulk.  A masked stream owns its hardware queue.  0 = ready.
-int ShaEngine::iso_streams(uint32_t r) {
-    if (r == 0 || r >= (uint32_t)cus) return -1;
-    if (iso_q && iso_cus == r) return 0;
-    for (hipStream_t *q : {&iso_q, &iso_b})
-        if (*q) {
-            (void)hipStreamSynchronize(*q);
-            (void)hipStreamDestroy(*q);
-            *q = nullptr;
-        }
-    iso_cus = 0;
+// the isolated drain's second stream, its events and the host-visible
+// residency counter.  0 = ready.
+int ShaEngine::iso_setup() {
+    if (iso_q) return 0;
+    // the quad launch pads its LDS to the CU's whole 160 KiB
+    if (hipFuncSetAttribute((const void *)sha_slice_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kIsoPadBytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
     for (auto &e : iso_ev)
         if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
             (void)hipGetLastError();
             e = nullptr;
             return -1;
         }
-    const uint32_t words = ((uint32_t)cus + 31) / 32;
-    std::vector<uint32_t> mq(words, 0), mb(words, 0);
-    for (uint32_t i = 0; i < (uint32_t)cus; ++i) {
-        // CU i is reserved when floor(i r / cus) steps: r of them, evenly spaced
-        const bool res = (uint64_t)(i + 1) * r / (uint32_t)cus != (uint64_t)i * r / (uint32_t)cus;
-        (res ? mq : mb)[i / 32] |= 1u << (i % 32);
+    if (!iso_res_h) {
+        if (hipHostMalloc((void **)&iso_res_h, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&iso_res_d, iso_res_h, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            if (iso_res_h) (void)hipHostFree(iso_res_h);
+            iso_res_h = iso_res_d = nullptr;
+            return -1;
+        }
     }
-    if (hipExtStreamCreateWithCUMask(&iso_q, words, mq.data()) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&iso_b, words, mb.data()) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&iso_q, hipStreamNonBlocking) != hipSuccess) {
         (void)hipGetLastError();
-        for (hipStream_t *q : {&iso_q, &iso_b})
-            if (*q) (void)hipStreamDestroy(*q), *q = nullptr;
+        iso_q = nullptr;
         return -1;
     }
-    iso_cus = r;
     return 0;
 }
+
+#if VS_SHA_TRACE
+extern "C" __attribute__((visibility("default"))) int vs_debug_sha_trace(uint64_t *out, uint32_t cap,
+                                                                        uint32_t *n, int reset) {
+    uint32_t k = 0;
+    if (hipMemcpyFromSymbol(&k, HIP_SYMBOL(g_sha_trace_n), 4) != hipSuccess) return -1;
+    k = std::min(k, kTraceCap);
+    if (n) *n = k;
+    if (out && cap && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sha_trace), (size_t)std::min(k, cap) * 32) != hipSuccess)
+        return -1;
+    const uint32_t z = 0;
+    if (reset && hipMemcpyToSymbol(HIP_SYMBOL(g_sha_trace_n), &z, 4) != hipSuccess) return -1;
+    return 0;
+}
+#endif
 
 // ---- synthetic volume bytes -------------------------------------
 __device__ __forceinline__ uint64_t splitmix_word(uint64_t seed, uint64_t i) {
