@@ -186,14 +186,17 @@ def test_sha256_batch_vs_hashlib(gpu):
         assert g == hashlib.sha256(buf[o:o + n]).digest()
 
 
-@pytest.mark.parametrize("pct", [0, 1, 50, 100])
-def test_sha256_drain_modes_vs_hashlib(gpu, pct):
-    """The final drain's latency (quad, 4 lanes per chain) and split tiles in one
-    launch: VS_OPT_SHA_QUAD_PCT 0 is split only, 1 puts nearly every chain in
-    quad tiles, 50 / 100 mix the two; every length class from 0 to 1 MiB."""
+@pytest.mark.parametrize("iso", [1, 0])
+@pytest.mark.parametrize("pct", [0, 1, 50, 100, -1])
+def test_sha256_drain_modes_vs_hashlib(gpu, pct, iso):
+    """The final drain's latency (quad, 4 lanes per chain) and split tiles:
+    VS_OPT_SHA_QUAD_PCT 0 is split only, 1 puts nearly every chain in quad
+    tiles, 50 / 100 mix the two, -1 the automatic rule; VS_OPT_SHA_ISOLATE 1
+    runs the quad tiles as their own launch, a CU each, beside the split
+    launch, 0 as one launch; every length class from 0 to 1 MiB."""
     import torch
     from volsync_amd import DeviceSha256
-    from volsync_amd._lib import VS_OPT_SHA_QUAD_PCT
+    from volsync_amd._lib import VS_OPT_SHA_ISOLATE, VS_OPT_SHA_QUAD_PCT
     rng = np.random.default_rng(pct + 11)
     host = O.synth(71, 0, 4 << 20)
     buf = host.tobytes()
@@ -206,12 +209,43 @@ def test_sha256_drain_modes_vs_hashlib(gpu, pct):
     out = torch.zeros(len(lens) * 32, dtype=torch.uint8, device="cuda")
     sh = DeviceSha256(0)
     sh.set_option(VS_OPT_SHA_QUAD_PCT, pct)
+    sh.set_option(VS_OPT_SHA_ISOLATE, iso)
     sh.run(d.data_ptr(), do.data_ptr(), dl.data_ptr(), len(lens), out.data_ptr(), None)
     torch.cuda.synchronize()
     sh.close()
     got = out.cpu().numpy().reshape(-1, 32)
     for o, n, g in zip(offs, lens, got):
         assert g.tobytes() == hashlib.sha256(buf[o:o + n]).digest(), n
+
+
+def test_fence_distinct_volumes(gpu):
+    """bench.py --distinct: volumes of three seeds in rotation, step k fenced
+    on step k - 3 (vs_cdc_fence) with a short slice budget, so the fences
+    drain chains still queued; every batch's chunk list (Start, Length, Cut,
+    blob ID) equals the oracle's for its volume."""
+    import torch
+    from volsync_amd import DeviceChunker, TestPol
+    n = 48 << 20
+    seeds = (2, 7, 8)
+    host = [O.synth(sd, 0, n) for sd in seeds]
+    dev = [torch.from_numpy(h).cuda() for h in host]
+    want = [O.cdc_hash(h, TestPol, 512 << 10, 8 << 20, 20) for h in host]
+    torch.cuda.synchronize()
+    dc = DeviceChunker(TestPol, 512 << 10, 8 << 20, 20, device=0)
+    dc.set_hash_slice(64)
+    first, _ = dc.batches()
+    got_n = []
+    for j in range(9):
+        if j >= 3:
+            dc.fence(first + j - 3)
+        nch, _ = dc.process(dev[j % 3].data_ptr(), n, 0, True)
+        got_n.append(nch)
+    for j in range(6, 9):
+        got = [(c.Start, c.Length, c.Cut, c.ID.hex()) for c in dc.batch_chunks(first + j, 0, got_n[j])]
+        assert got == want[j % 3], (j, len(got), len(want[j % 3]))
+    with pytest.raises(Exception):
+        dc.fence(first + 9)      # not finished yet
+    dc.close()
 
 
 def test_small_files_device_sha(gpu):

@@ -23,7 +23,37 @@ hostinfo() {
     python3 -c "import os; print('affinity', len(os.sched_getaffinity(0)))"; } > gpurun_out/hostinfo.txt
   cat gpurun_out/hostinfo.txt
 }
+trace() {  # trace <tag> <bench args...>: kernel trace + stats only (no counters)
+  local tag=$1 out=$PWD/gpurun_out/trace_$1 repo=$PWD
+  shift
+  mkdir -p "$out"
+  (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/raw" \
+     -o run --output-format csv -- python3 "$repo/bench.py" "$@") > "$out/bench.log" 2>&1
+  local rc=$?
+  echo "=== trace_$tag rc=$rc"; tail -n 2 "$out/bench.log" | cut -c1-300
+  [ $rc -eq 0 ] || return $rc
+  find "$out/raw" -name '*kernel_stats.csv' -exec cp {} "$out/kernel_stats.csv" \;
+  find "$out/raw" -name '*kernel_trace.csv' -exec cp {} "$out/kernel_trace.csv" \;
+  rm -rf "$out/raw"
+}
 case $1 in
+  validate)   # the whole GPU suite, smoke, every bench line
+    bash tools/gpu.sh tests && bash tools/gpu.sh smoke && bash "$0" benches ;;
+  benches)
+    bash tools/gpu.sh bench c2 --gpus 1 --steps 20 --warmup 5 &&
+    bash tools/gpu.sh bench c3r3 --share 3/8 --steps 20 --warmup 5 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c5 --mode smallfiles --steps 5 --warmup 1 &&
+    bash tools/gpu.sh bench c4 --mode rsync --steps 20 --warmup 2 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c4share --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 &&
+    bash tools/gpu.sh bench c4share_nofs --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum &&
+    bash tools/gpu.sh bench seal --mode seal --steps 3 --warmup 1 &&
+    trace c2 --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 0 ;;
+  cdc)   # the CDC lines (C2 with its companions, C3 rank 3) and the C2 kernel trace
+    bash tools/gpu.sh bench c2 --gpus 1 --steps 20 --warmup 5 &&
+    bash tools/gpu.sh bench c3r3 --share 3/8 --steps 20 --warmup 5 --no-cpu-baseline &&
+    trace c2 --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 0 ;;
+  counters)  # C2 counter passes (traffic, VALU activity) -> gpurun_out/profile_c2
+    bash tools/gpu.sh prof c2 'fp_kernel|sha_slice_kernel' --gpus 1 --steps 5 --warmup 1 --distinct 0 ;;
   first)
     hostinfo &&
     bash tools/gpu.sh tests tests/test_gpu_cdc.py -x &&
@@ -43,5 +73,5 @@ case $1 in
     mv gpurun_out/py_sha_trace.log gpurun_out/trace_c3r3.log &&
     VSGPU_LIB=$PWD/$(var shatrace) bash tools/gpu.sh py tools/sha_trace.py --gib 64 --quad auto:1,auto:0 &&
     mv gpurun_out/py_sha_trace.log gpurun_out/trace_c2.log ;;
-  *) echo "usage: tools/r06_runs.sh first|iso|trace" >&2; exit 2 ;;
+  *) echo "usage: tools/r06_runs.sh validate|benches|first|iso|isotrace|trace" >&2; exit 2 ;;
 esac

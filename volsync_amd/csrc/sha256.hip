@@ -737,6 +737,9 @@ int ShaEngine::init(int dev) {
     VS_HIP(hipMemset(ctl.p, 0, 64));
     VS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     if (!live_h) VS_HIP(hipHostMalloc((void **)&live_h, 4, hipHostMallocDefault));
+    // the isolated drain's stream and counter now, not inside the first
+    // latency-bound drain (creating them took ~30 ms there: profiles/r06_val1)
+    if (isolate) (void)iso_setup();
     return 0;
 }
 
@@ -864,8 +867,12 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
         // beside split tiles, ~1.45 us on a CU of its own (isolated drain,
         // profiles/r06_drain); the backlog clears at split-mode throughput,
         // ~1.45 TB/s = 22.7 G blocks/s over the whole chip.
-        constexpr double kSplitBlockS = 2.8e-6, kBulkBlocksPerS = 22.7e9;
+        // (split chains beside a busy chip after a long run, the clock down:
+        // up to 3.3 us, profiles/r06_val1/trace_c2; the rule takes 3.0)
+        constexpr double kSplitBlockS = 3.0e-6, kBulkBlocksPerS = 22.7e9;
         const double quad_s = isolate ? 1.45e-6 : 1.6e-6;
+        // isolated, at most half the CUs hold quad tiles (16 chains each)
+        const uint32_t quad_cap = isolate ? (uint32_t)std::max(cus, 2) / 2 * 16 : 0xffffffffu;
         const double lmax = first < kShaBuckets ? (double)bucket_blocks(first) : 0.0;
         const double t_bulk = blocks / kBulkBlocksPerS;
         auto count_above = [&](double floor_s) {   // chains whose split-mode time passes floor_s
@@ -888,7 +895,7 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
                 // the floor until it does
                 double floor_s = std::max(lmax * quad_s, t_bulk);
                 for (int it = 0; it < 6; ++it) {
-                    quad_chains = count_above(floor_s);
+                    quad_chains = std::min(count_above(floor_s), quad_cap);
                     if (!isolate) break;
                     const double qtiles = (quad_chains + 15) / 16;
                     const double free_cus = std::max((double)cus - qtiles, 1.0);
@@ -922,7 +929,7 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
     hipEvent_t ka = ev_get ? ev_get() : nullptr, kb = ka ? ev_get() : nullptr;
     if (kb) VS_HIP(hipEventRecord(ka, s));
     const uint64_t qt = (quad_chains + 15) / 16;
-    if (mode == kShaQuad && qt && isolate && qt <= (uint64_t)cus * 3 / 4 && iso_setup() == 0) {
+    if (mode == kShaQuad && qt && isolate && qt <= (uint64_t)cus / 2 && iso_setup() == 0) {
         // Isolated drain: each quad tile takes a CU to itself -- its LDS padded
         // to the CU's whole 160 KiB, so no split workgroup can join it -- and
         // is resident before the split tiles are launched beside it; the
