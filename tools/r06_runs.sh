@@ -52,6 +52,11 @@ case $1 in
     bash tools/gpu.sh bench c2 --gpus 1 --steps 20 --warmup 5 &&
     bash tools/gpu.sh bench c3r3 --share 3/8 --steps 20 --warmup 5 --no-cpu-baseline &&
     trace c2 --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 0 ;;
+  r7check)   # the C4 shape with R7 again, and with the file-sum trace build
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py tests/test_gpu_rsync_stream.py -x -k "file_sum or stream or fifo" &&
+    bash tools/gpu.sh bench c4 --mode rsync --steps 10 --warmup 2 --no-cpu-baseline &&
+    bash tools/gpu.sh bench c4share --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 &&
+    VSGPU_LIB=$PWD/$(var fstrace) bash tools/gpu.sh bench c4_fstrace --mode rsync --steps 4 --warmup 1 --no-cpu-baseline ;;
   counters)  # C2 counter passes (traffic, VALU activity) -> gpurun_out/profile_c2
     bash tools/gpu.sh prof c2 'fp_kernel|sha_slice_kernel' --gpus 1 --steps 5 --warmup 1 --distinct 0 ;;
   first)

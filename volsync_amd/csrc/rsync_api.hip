@@ -75,9 +75,8 @@ struct RsRun {
 // pinned ring and are hashed on the host thread.
 struct FsJob {
     static constexpr uint64_t kRowsCap = 8ull << 30;   // rows of a 128 GiB file
-    // pinned row copies per handle, over its jobs: three 64 GiB
-    // files in flight fit; beyond it idle slots give theirs up, then the job
-    // takes the piece ring
+    // pinned row copies per handle: three 64 GiB files in
+    // flight fit; a job that would pass it takes the piece ring
     static constexpr uint64_t kPinnedRowsCap = 16ull << 30;
     DmaD2H dma;
     DevBuf rows;                          // rows-first: every block's row
@@ -211,6 +210,11 @@ struct vs_rsync {
     FsJob fs[kFsJobs];
     uint32_t fs_head = 0, fs_tail = 0;   // jobs [head, tail) are in flight
     FsJob fs_sync;                       // the blocking vs_rsync_file_sum's own job
+    // pinned row copies not held by a job (rows first): a job
+    // takes one at its start and returns it once waited for, so the pinned
+    // bytes follow the jobs in flight, at most FsJob::kPinnedRowsCap in all
+    std::vector<std::pair<uint8_t *, uint64_t>> fs_pool;
+    uint64_t fs_pinned = 0;              // bytes pinned for row copies (pool + jobs)
     double fs_dev_ms = 0, fs_host_ms = 0; // the last job waited for
     DevBuf rc_pieces;               // receiver reconstruction
     // scan
@@ -1558,7 +1562,7 @@ void fs_release(FsJob &j) {
     if (j.s) (void)hipStreamSynchronize(j.s);
     j.dma.release();
     j.rows.release();
-    pinned_free(j.hrows);
+    pinned_free(j.hrows);   // a copy still held by the job (the pool frees the rest)
     j.hrows = nullptr;
     j.hrows_cap = 0;
     for (auto &p : j.hC) pinned_free(p), p = nullptr;
@@ -1580,6 +1584,16 @@ void fs_account(vs_rsync *h, const FsJob &j) {
     h->kn[4] += 1;
     h->fs_dev_ms = j.dev_ms;
     h->fs_host_ms = j.host_ms;
+}
+
+// the job's pinned row copy back to the handle's pool (its thread has been
+// joined: every DMA into it has landed)
+void fs_rows_put(vs_rsync *h, FsJob &j) {
+    if (!j.hrows) return;
+    if (j.th.joinable()) j.th.join();
+    h->fs_pool.push_back({j.hrows, j.hrows_cap});
+    j.hrows = nullptr;
+    j.hrows_cap = 0;
 }
 
 // whole: the digest of the file p[0, len); else the accumulators after the
@@ -1619,45 +1633,43 @@ int fs_start(vs_rsync *h, const uint8_t *p, uint64_t len, int csum, bool whole,
         // kRowsCap, a failed pin and hosts without the DMA path take)
         j.rows_first = h->fs_piece == 0 && j.nb > 0 && j.nb * 64 <= FsJob::kRowsCap &&
                        j.dma.init(j.device);
-        if (j.rows_first && j.hrows_cap < j.nb * 64) {
-            // The pinned copy, kept across jobs and bounded per handle
-            // (kPinnedRowsCap over the FIFO's slots and the blocking job).
-            // Page-locking 4 GiB takes ~175 ms on the caller's thread, so idle
-            // slots are sized at once as far as the bound allows (the first
-            // file pays for all, not the first file of each slot:
-            // profiles/r05_r7/queued)
+        if (j.rows_first) {
+            // The pinned copy of the rows: the smallest pooled one that fits,
+            // else a new one within the handle's bound, else the piece ring.
+            // Page-locking 4 GiB takes ~175 ms on the caller's thread, so the
+            // first allocation also pools copies for the jobs that usually
+            // follow it in flight (profiles/r05_r7/queued), within the bound.
             const uint64_t need = j.nb * 64;
-            auto busy = [&](uint32_t k) {   // slot k holds a job in flight
-                return ((k - h->fs_head) % vs_rsync::kFsJobs) < h->fs_tail - h->fs_head;
-            };
-            auto total = [&] {
-                uint64_t t = h->fs_sync.hrows_cap;
-                for (auto &o : h->fs) t += o.hrows_cap;
-                return t;
-            };
-            auto drop = [&](FsJob &o) {
-                if (o.th.joinable()) o.th.join();
-                pinned_free(o.hrows);
-                o.hrows = nullptr;
-                o.hrows_cap = 0;
-            };
-            auto grow = [&](FsJob &o) {
-                drop(o);
-                o.hrows = (uint8_t *)pinned_alloc((size_t)need);
-                o.hrows_cap = o.hrows ? need : 0;
-            };
-            drop(j);
-            // over the bound: release idle slots' smaller copies first
-            for (uint32_t k = 0; k < vs_rsync::kFsJobs && total() + need > FsJob::kPinnedRowsCap; ++k)
-                if (&h->fs[k] != &j && !busy(k)) drop(h->fs[k]);
-            if (total() + need <= FsJob::kPinnedRowsCap) grow(j);
-            if (!sync)
-                for (uint32_t k = 0; k < vs_rsync::kFsJobs; ++k) {
-                    FsJob &o = h->fs[k];
-                    if (&o != &j && !busy(k) && o.hrows_cap < need &&
-                        total() - o.hrows_cap + need <= FsJob::kPinnedRowsCap)
-                        grow(o);
+            fs_rows_put(h, j);   // (a job that was never waited for)
+            size_t best = h->fs_pool.size();
+            for (size_t i = 0; i < h->fs_pool.size(); ++i)
+                if (h->fs_pool[i].second >= need &&
+                    (best == h->fs_pool.size() || h->fs_pool[i].second < h->fs_pool[best].second))
+                    best = i;
+            if (best == h->fs_pool.size()) {
+                // free pooled copies too small to serve, then pin within the bound
+                for (size_t i = h->fs_pool.size(); i-- > 0;)
+                    if (h->fs_pinned + need > FsJob::kPinnedRowsCap) {
+                        pinned_free(h->fs_pool[i].first);
+                        h->fs_pinned -= h->fs_pool[i].second;
+                        h->fs_pool.erase(h->fs_pool.begin() + (long)i);
+                    }
+                const bool first = h->fs_pinned == 0;
+                for (uint32_t k = 0; k < (first && !sync ? vs_rsync::kFsJobs - 1 : 1u); ++k) {
+                    if (h->fs_pinned + need > FsJob::kPinnedRowsCap) break;
+                    uint8_t *b = (uint8_t *)pinned_alloc((size_t)need);
+                    if (!b) break;
+                    h->fs_pinned += need;
+                    h->fs_pool.push_back({b, need});
                 }
+                best = h->fs_pool.empty() || h->fs_pool.back().second < need ? h->fs_pool.size()
+                                                                              : h->fs_pool.size() - 1;
+            }
+            if (best < h->fs_pool.size()) {
+                j.hrows = h->fs_pool[best].first;
+                j.hrows_cap = h->fs_pool[best].second;
+                h->fs_pool.erase(h->fs_pool.begin() + (long)best);
+            }
             j.rows_first = j.hrows != nullptr;   // else the bounded piece ring
         }
         if (j.rows_first) {
@@ -2195,6 +2207,9 @@ VS_API void vs_rsync_close(vs_rsync *h) {
     ss_release(h);
     for (FsJob &j : h->fs) fs_release(j);
     fs_release(h->fs_sync);
+    for (auto &b : h->fs_pool) pinned_free(b.first);
+    h->fs_pool.clear();
+    h->fs_pinned = 0;
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (DevBuf *b : {&h->d_sum1, &h->d_keys, &h->d_tkey, &h->d_dir, &h->d_filt, &h->d_tmp, &h->d_bkt, &h->px,
                       &h->pt, &h->pxs, &h->pts, &h->partials, &h->c_off, &h->c_sum, &h->c_off2,
@@ -2361,6 +2376,7 @@ VS_API int vs_rsync_file_sum_wait(vs_rsync *h, uint8_t out[16]) {
     VS_TRY(rs_dev(h));
     h->fs_head++;
     const int rc = fs_finish(j);   // joins the job's thread, syncs its stream
+    fs_rows_put(h, j);
     j.active = false;
     VS_TRY(rc);
     fs_account(h, j);
@@ -2382,6 +2398,7 @@ VS_API int vs_rsync_file_sum(vs_rsync *h, const void *dev_src, int64_t len, int 
     FsJob &j = h->fs_sync;
     VS_TRY(fs_start(h, (const uint8_t *)dev_src, (uint64_t)len, csum_type, true, nullptr, &j));
     const int rc = fs_finish(j);
+    fs_rows_put(h, j);
     j.active = false;
     VS_TRY(rc);
     fs_account(h, j);
@@ -2406,6 +2423,7 @@ VS_API int vs_rsync_file_sum_blocks_wait(vs_rsync *h, uint64_t acc_out[8]) {
     VS_TRY(rs_dev(h));
     h->fs_head++;
     const int rc = fs_finish(j);   // joins the job's thread, syncs its stream
+    fs_rows_put(h, j);
     j.active = false;
     VS_TRY(rc);
     fs_account(h, j);
