@@ -57,6 +57,11 @@ case $1 in
     bash tools/gpu.sh bench c4 --mode rsync --steps 10 --warmup 2 --no-cpu-baseline &&
     bash tools/gpu.sh bench c4share --mode rsync --share 3/8 --per-gpu-gib 32 --steps 10 --warmup 1 &&
     VSGPU_LIB=$PWD/$(var fstrace) bash tools/gpu.sh bench c4_fstrace --mode rsync --steps 4 --warmup 1 --no-cpu-baseline ;;
+  multirank)   # shared-GPU rehearsals of the N-rank paths (gloo collectives, one card)
+    export VSGPU_BENCH_SHARED_GPU=1
+    bash tools/gpu.sh bench cdc2 --gpus 2 --per-gpu-gib 4 --steps 3 --warmup 1 &&
+    bash tools/gpu.sh bench cdc4 --gpus 4 --per-gpu-gib 2 --steps 3 --warmup 1 &&
+    bash tools/gpu.sh bench c4relay4 --mode rsync --gpus 4 --per-gpu-gib 4 --steps 2 --warmup 1 ;;
   counters)  # C2 counter passes (traffic, VALU activity) -> gpurun_out/profile_c2
     bash tools/gpu.sh prof c2 'fp_kernel|sha_slice_kernel' --gpus 1 --steps 5 --warmup 1 --distinct 0 ;;
   first)
