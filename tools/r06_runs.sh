@@ -62,6 +62,9 @@ case $1 in
     bash tools/gpu.sh bench cdc2 --gpus 2 --per-gpu-gib 4 --steps 3 --warmup 1 &&
     bash tools/gpu.sh bench cdc4 --gpus 4 --per-gpu-gib 2 --steps 3 --warmup 1 &&
     bash tools/gpu.sh bench c4relay4 --mode rsync --gpus 4 --per-gpu-gib 4 --steps 2 --warmup 1 ;;
+  walkab)   # walk occupancy A/B at the real C4 rank (w12: 12 waves/CU, 168 VGPRs, no prefilter)
+    S="bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline"
+    ab ab_walk_share 2 "base=,w12=$(var w12),w12d8=$(var w12d8),w8nopf=$(var w8nopf)" $S ;;
   counters)  # C2 counter passes (traffic, VALU activity) -> gpurun_out/profile_c2
     bash tools/gpu.sh prof c2 'fp_kernel|sha_slice_kernel' --gpus 1 --steps 5 --warmup 1 --distinct 0 ;;
   first)

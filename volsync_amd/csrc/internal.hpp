@@ -495,6 +495,7 @@ struct RsWalkArgs {
     uint64_t *dbg;                   // debug builds: per-wave progress records (host-mapped)
     uint64_t *prof;                  // VS_WALK_PROF builds: per-wave phase cycles/counts [waves][16]
 };
+int rs_walk_waves_per_cu();   // the device walk's resident waves per CU (one workgroup)
 hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t s);
 // fill the membership buckets (zeroed by the caller) from the sorted keys:
 // each distinct sum1 of a full-length block once (the short final block,

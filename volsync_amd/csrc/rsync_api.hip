@@ -982,7 +982,7 @@ int walk_scan(vs_rsync *h) {
         // instead of 43 idle-heavy ones).  VS_OPT_WALK_SEGMENT_BLOCKS
         // overrides it.
         const int64_t range = std::max<int64_t>(a.hi - a.lo, 1);
-        const int64_t waves = (int64_t)std::max(h->cus, 1) * 8;
+        const int64_t waves = (int64_t)std::max(h->cus, 1) * rs_walk_waves_per_cu();
         int64_t sl = (int64_t)h->blength * (h->seg_blocks ? h->seg_blocks : 48);
         if (!h->seg_blocks && range / sl < 2 * waves)
             sl = std::max<int64_t>(range / (2 * waves), h->blength);
@@ -1014,7 +1014,7 @@ int walk_scan(vs_rsync *h) {
     // finish closer together: 20 % when the grid gets fewer than four
     // segments per wave, else 10 % (the real C4's rank: walk 44.6 -> 41.2 ms;
     // the 64 GiB shape: 42.0 -> 41.1)
-    const int64_t waves = (int64_t)std::max(h->cus, 1) * 8;
+    const int64_t waves = (int64_t)std::max(h->cus, 1) * rs_walk_waves_per_cu();
     const int32_t tailpct = h->opt_tailpct >= 0 ? h->opt_tailpct : ((int64_t)a.nseg < 4 * waves ? 20 : 10);
     if (tailpct > 0) {
 #ifndef VS_TAIL_DIV

@@ -47,7 +47,10 @@ using vsstrong::P32_1;
 #endif
 constexpr uint32_t kWalkThreads = VS_WALK_T;             // 8 waves (up to 256 VGPRs each); the 128 KiB prefilter admits one WG/CU
 constexpr uint32_t kWalkRing = VS_WALK_RRING;                  // window blocks in flight per lane in the wave walk
-constexpr uint32_t kLdsFiltWordsW = 1u << 15;      // 2^20-bit LDS prefilter
+#ifndef VS_WALK_LDSF
+#define VS_WALK_LDSF (1u << 15)
+#endif
+constexpr uint32_t kLdsFiltWordsW = VS_WALK_LDSF;  // 2^20-bit LDS prefilter
 constexpr uint64_t kBatch = 1024;                  // STEP offsets per wave batch (16 per lane)
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -1462,6 +1465,8 @@ __global__ void rs_pad_sum2_kernel(const uint8_t *sum2, uint32_t count, uint32_t
 
 }  // namespace
 
+int rs_walk_waves_per_cu() { return (int)(kWalkThreads / 64); }
+
 hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t s) {
     if (!a.nseg) return hipSuccess;
     if (a.lbits > 20) return hipErrorInvalidValue;
@@ -1473,10 +1478,14 @@ hipError_t launch_rs_walk(const RsWalkArgs &a, bool stitch, int cus, hipStream_t
     const uint64_t grid = std::min<uint64_t>((a.nseg + waves - 1) / waves, (uint64_t)std::max(cus, 1));
     hipError_t e = hipMemsetAsync(a.work, 0, 4, s);
     if (e != hipSuccess) return e;
+    // a build whose LDS prefilter array is smaller than the table's runs
+    // without it (the prefilter only rejects; results are the same)
+    RsWalkArgs b = a;
+    if (b.lbits && ((1u << b.lbits) / 32) > kLdsFiltWordsW) b.lbits = 0;
     if (stitch)
-        rs_walk_stitch_kernel<<<(uint32_t)grid, kWalkThreads, 0, s>>>(a);
+        rs_walk_stitch_kernel<<<(uint32_t)grid, kWalkThreads, 0, s>>>(b);
     else
-        rs_walk_spec_kernel<kWalkThreads, kWalkRing><<<(uint32_t)grid, kWalkThreads, 0, s>>>(a);
+        rs_walk_spec_kernel<kWalkThreads, kWalkRing><<<(uint32_t)grid, kWalkThreads, 0, s>>>(b);
     return hipGetLastError();
 }
 
