@@ -65,6 +65,10 @@ case $1 in
   walkab)   # walk occupancy A/B at the real C4 rank (w12: 12 waves/CU, 168 VGPRs, no prefilter)
     S="bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline"
     ab ab_walk_share 2 "base=,w12=$(var w12),w12d8=$(var w12d8),w8nopf=$(var w8nopf)" $S ;;
+  corun)   # fingerprint + SHA-256 co-residency A/B
+    bash tools/gpu.sh py tools/corun.py --sha-gb 4,8,16 --sha-grid 0 && mv gpurun_out/py_corun.log gpurun_out/corun_base_grid5.log &&
+    VSGPU_LIB=$PWD/$(var corun) bash tools/gpu.sh py tools/corun.py --sha-gb 4,8,16 --sha-grid 1 && mv gpurun_out/py_corun.log gpurun_out/corun_co_grid1.log &&
+    VSGPU_LIB=$PWD/$(var corun) bash tools/gpu.sh py tools/corun.py --sha-gb 4,8,16 --sha-grid 0 && mv gpurun_out/py_corun.log gpurun_out/corun_co_grid5.log ;;
   counters)  # C2 counter passes (traffic, VALU activity) -> gpurun_out/profile_c2
     bash tools/gpu.sh prof c2 'fp_kernel|sha_slice_kernel' --gpus 1 --steps 5 --warmup 1 --distinct 0 ;;
   first)

@@ -437,6 +437,14 @@ __global__ __launch_bounds__(THREADS) void fp_kernel(FpArgs a) {
     }
 }
 
+// the register budget the kernel is compiled for: its launch size, unless a
+// co-residency A/B build (VS_FP_LB 1024, VS_FP_THREADS 768) launches fewer
+// waves than it budgets for, leaving a SHA-256 workgroup room on every CU
+#ifndef VS_FP_LB
+#define VS_FP_LB VS_FP_THREADS
+#endif
+constexpr int kFpLaunchBound = VS_FP_LB;
+
 hipError_t launch_fingerprint(const FpArgs &a, bool wide, bool fast, int cus, hipStream_t s) {
     const bool deg53 = fast && a.idx_shift == 13;
     const uint64_t units = (a.k_hi - a.k_lo + kUnit - 1) / kUnit;
@@ -444,13 +452,13 @@ hipError_t launch_fingerprint(const FpArgs &a, bool wide, bool fast, int cus, hi
     const uint64_t grid =
         std::max<uint64_t>(1, std::min<uint64_t>(units, (uint64_t)std::max(cus, 1)));
     if (wide)
-        fp_kernel<kFpWide, kFpThreads><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
+        fp_kernel<kFpWide, kFpLaunchBound><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
     else if (deg53)
-        fp_kernel<kFpFast53, kFpThreads><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
+        fp_kernel<kFpFast53, kFpLaunchBound><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
     else if (fast)
-        fp_kernel<kFpFast, kFpThreads><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
+        fp_kernel<kFpFast, kFpLaunchBound><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
     else
-        fp_kernel<kFpNarrow, kFpThreads><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
+        fp_kernel<kFpNarrow, kFpLaunchBound><<<(uint32_t)grid, kFpThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 

@@ -398,7 +398,13 @@ __device__ __forceinline__ void trace_tile(bool quad, uint32_t t, uint64_t t0, u
 // Tiles [0, qt) hold the first (longest) a.quad_chains chains of the order, 16
 // per tile, consumed in latency mode (compress_quad; the producer's lanes
 // 16..63 idle); the later tiles hold 64 chains each in split mode.
+// VS_SHA_MINW (A/B builds): at least this many waves per SIMD, i.e. a
+// register budget that fits beside a co-resident fingerprint workgroup
+#ifdef VS_SHA_MINW
+__global__ __launch_bounds__(128, VS_SHA_MINW) void sha_slice_kernel(ShaSliceArgs a) {
+#else
 __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
+#endif
     __shared__ uint4 wk[2][16 * 64];  // 2 x 16 KiB: W of one block of 64 chains
     // the tile broadcast borrows W slot 1's first word: between tiles no block
     // is in flight, and the next tile's producer writes slot 1 only after the
