@@ -69,6 +69,12 @@ case $1 in
     bash tools/gpu.sh py tools/corun.py --sha-gb 4,8,16 --sha-grid 0 && mv gpurun_out/py_corun.log gpurun_out/corun_base_grid5.log &&
     VSGPU_LIB=$PWD/$(var corun) bash tools/gpu.sh py tools/corun.py --sha-gb 4,8,16 --sha-grid 1 && mv gpurun_out/py_corun.log gpurun_out/corun_co_grid1.log &&
     VSGPU_LIB=$PWD/$(var corun) bash tools/gpu.sh py tools/corun.py --sha-gb 4,8,16 --sha-grid 0 && mv gpurun_out/py_corun.log gpurun_out/corun_co_grid5.log ;;
+  wideab)   # C2 replay with the drain's bulk in throughput (wide) mode
+    for r in 1 2; do
+      bash tools/gpu.sh bench c2_split_$r --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 0 &&
+      bash tools/gpu.sh bench c2_wide98k_$r --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 0 --hash-wide 98304 &&
+      bash tools/gpu.sh bench c2_wide256k_$r --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 0 --hash-wide 262144 --wide-drain 16384 || exit 1
+    done ;;
   counters)  # C2 counter passes (traffic, VALU activity) -> gpurun_out/profile_c2
     bash tools/gpu.sh prof c2 'fp_kernel|sha_slice_kernel' --gpus 1 --steps 5 --warmup 1 --distinct 0 ;;
   first)

@@ -105,6 +105,7 @@ struct vs_cdc {
     uint64_t sorigin = 0, batch_bytes = 512ull << 20;
     bool streaming = false;          // the handle is in streaming mode (first feed .. reset)
     uint32_t pre_stream_budget = 0;  // hash_budget before streaming changed it
+    uint32_t pre_stream_isolate = 1; // the engine's isolated-drain setting before streaming
     std::deque<uint64_t> spend;      // batches whose chunks are not yet collected
     std::deque<vs_chunk> ready;
     bool final_fed = false;
@@ -768,6 +769,11 @@ static int stream_begin(vs_cdc *h) {
         if (h->own_hm) h->hstream = h->own_hm;
     }
     h->pre_stream_budget = h->hash_budget;
+    // no isolated drains while streaming: the fingerprint grid of the next
+    // batch may hold CUs a quad tile would wait to take whole, and the hash
+    // stream is masked to half the CUs
+    h->pre_stream_isolate = h->sha.isolate;
+    h->sha.isolate = 0;
     const uint64_t mb = sha_blocks(h->max_size);
     const uint64_t budget = (mb + vs_cdc::kStreamSlots - 3) / (vs_cdc::kStreamSlots - 2);
     h->hash_budget = (uint32_t)std::max<uint64_t>(budget, 1);
@@ -981,6 +987,7 @@ VS_API int vs_cdc_reset(vs_cdc *h, uint64_t pol, uint32_t min_size, uint32_t max
     VS_TRY(cdc_wait(h));
     if (h->streaming) {
         h->hash_budget = h->pre_stream_budget;   // the device API's budget again
+        h->sha.isolate = h->pre_stream_isolate;
         if (h->own_hm && h->hstream == h->own_hm) h->hstream = h->own_h;
     }
     VS_TRY(set_params(h, pol, min_size, max_size, avg_bits));
@@ -1483,6 +1490,13 @@ VS_API int vs_cdc_set_option(vs_cdc *h, int option, int64_t value) {
     VS_TRY(cdc_wait(h));
     if (option == VS_OPT_FP_GENERIC) {
         h->fp_generic = value != 0;
+        return 0;
+    }
+    if (option == VS_OPT_SHA_ISOLATE && h->streaming) {   // applies once the stream ends
+        const uint32_t cur = h->sha.isolate;
+        VS_TRY(sha_option(h->sha, option, value));
+        h->pre_stream_isolate = h->sha.isolate;
+        h->sha.isolate = cur;
         return 0;
     }
     return sha_option(h->sha, option, value);
