@@ -77,6 +77,14 @@ case $1 in
     done ;;
   counters)  # C2 counter passes (traffic, VALU activity) -> gpurun_out/profile_c2
     bash tools/gpu.sh prof c2 'fp_kernel|sha_slice_kernel' --gpus 1 --steps 5 --warmup 1 --distinct 0 ;;
+  quadtrace)   # the latency tiles' duration, clock and the longest chain (VS_SHA_TRACE build shatrace)
+    VSGPU_LIB=$PWD/$(var shatrace) bash tools/gpu.sh py tools/sha_trace.py --gib 64 --quad auto:1 &&
+    mv gpurun_out/py_sha_trace.log gpurun_out/trace_c2_quad.log ;;
+  quadfinal)   # the isolated latency form in the product: CDC tests, single pass and the C2 line against HEAD's build (var head)
+    bash tools/gpu.sh tests tests/test_gpu_cdc.py tests/test_gpu_c3.py -x && mv gpurun_out/gputests.log gpurun_out/gputests_cdc.log &&
+    ab ab_final_single_c2 2 "head=$(var head),new=" tools/single_pass.py --gib 64 --quad auto:1,auto:0 --rounds 2 &&
+    ab ab_final_single_c3r3 2 "head=$(var head),new=" tools/single_pass.py --share 3/8 --quad auto --rounds 2 &&
+    ab ab_final_c2 2 "head=$(var head),new=" bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 0 ;;
   first)
     hostinfo &&
     bash tools/gpu.sh tests tests/test_gpu_cdc.py -x &&
@@ -96,5 +104,5 @@ case $1 in
     mv gpurun_out/py_sha_trace.log gpurun_out/trace_c3r3.log &&
     VSGPU_LIB=$PWD/$(var shatrace) bash tools/gpu.sh py tools/sha_trace.py --gib 64 --quad auto:1,auto:0 &&
     mv gpurun_out/py_sha_trace.log gpurun_out/trace_c2.log ;;
-  *) echo "usage: tools/r06_runs.sh validate|benches|first|iso|isotrace|trace" >&2; exit 2 ;;
+  *) echo "usage: tools/r06_runs.sh validate|benches|cdc|quadfinal|quadtrace|..." >&2; exit 2 ;;
 esac

@@ -57,8 +57,12 @@ def one():
     return dc.process(buf.data_ptr(), dlen, 0, True)[0]
 
 
-one()
+n0 = one()
 dc.wait()
+from bench import _chunk_records  # noqa: E402
+rec = np.frombuffer(_chunk_records(dc, n0), dtype=np.uint64).reshape(n0, 7)
+lmax_blocks = int(rec[:, 1].max()) // 64 + 1   # the longest chunk's SHA-256 blocks
+print("longest chunk", int(rec[:, 1].max()), "bytes,", lmax_blocks, "blocks", flush=True)
 cap = 1 << 16
 arr = np.zeros((cap, 4), np.uint64)
 n = ctypes.c_uint32(0)
@@ -74,6 +78,7 @@ for q in a.quad.split(","):
     fn(arr.ctypes.data, cap, ctypes.byref(n), 1)
     t = arr[: n.value]
     quad = (t[:, 0] >> np.uint64(63)) == 1
+    cyc = ((t[:, 0] >> np.uint64(20)) & np.uint64((1 << 43) - 1)).astype(np.int64)
     hw = (t[:, 1] & np.uint64(0xffffffff)).astype(np.int64)
     xcc = (t[:, 1] >> np.uint64(32)).astype(np.int64)
     cu = xcc * 4096 + ((hw >> 13) & 7) * 512 + ((hw >> 12) & 1) * 256 + ((hw >> 8) & 15)
@@ -83,7 +88,7 @@ for q in a.quad.split(","):
     qi = np.nonzero(quad)[0]
     si = np.nonzero(~quad)[0]
     drain0 = int(t0[qi].min()) if len(qi) else base
-    res = {"tiles": int(n.value), "quad_tiles": int(len(qi))}
+    res = {"tiles": int(n.value), "quad_tiles": int(len(qi)), "longest_chain_blocks": lmax_blocks}
     if len(qi):
         qs = (t0[qi] - drain0) / 1e5
         qd = (t1[qi] - t0[qi]) / 1e5
@@ -91,6 +96,9 @@ for q in a.quad.split(","):
                                       round(float(qs.max()), 2)],
                     "quad_ms": [round(float(qd.min()), 1), round(float(np.median(qd)), 1),
                                 round(float(qd.max()), 1)],
+                    # shader clock over the tile (s_memtime cycles / s_memrealtime)
+                    "quad_clock_GHz": [round(float(x), 3) for x in
+                                       np.percentile(cyc[qi] / np.maximum(t1[qi] - t0[qi], 1) / 10.0, [0, 50, 100])],
                     "quad_distinct_cus": int(len(set(cu[qi].tolist()))),
                     "quad_distinct_simds": int(len(set(simd[qi].tolist())))})
         # split tiles overlapping a quad tile in time on its CU / SIMD
@@ -104,6 +112,8 @@ for q in a.quad.split(","):
         if len(late):
             res["split_after_drain_start_ms"] = round(float((t1[late].max() - drain0) / 1e5), 1)
     res["span_ms"] = round(float((t1.max() - base) / 1e5), 1)
+    if len(si):
+        res["split_clock_GHz_median"] = round(float(np.median(cyc[si] / np.maximum(t1[si] - t0[si], 1) / 10.0)), 3)
     out[q] = res
     print(q, json.dumps(res), flush=True)
 print(json.dumps({"volume": a.share or f"C2 {a.gib} GiB", "rules": out}))

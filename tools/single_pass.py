@@ -20,6 +20,7 @@ ap.add_argument("--gib", type=int, default=64)
 ap.add_argument("--share", default=None)
 ap.add_argument("--quad", default="auto:1,auto:0")
 ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--no-check", action="store_true", help="timing diagnostics (VS_SHA_DIAG builds): skip the golden check")
 a = ap.parse_args()
 
 import torch  # noqa: E402
@@ -78,12 +79,12 @@ for rd in range(a.rounds):
         res[q].append(dt)
         import hashlib
         d = hashlib.sha256(_chunk_records(dc, n)).hexdigest()
-        if gold is not None and (n, d) != (gold["chunks"], gold["digest"]):
+        if gold is not None and not a.no_check and (n, d) != (gold["chunks"], gold["digest"]):
             print(f"[{q} r{rd}] CHUNK LIST DIFFERS FROM THE GOLDEN", flush=True)
             sys.exit(1)
         print(f"[{q} r{rd}] {dt:.1f} ms  fp {ms[0]:.1f}  sha(outside fp) {det['sha_outside_fp_ms']:.1f}"
               f"  latency-mode chains {det['quad_chains']}  chunks {n}", flush=True)
-ok = gold is not None   # every pass's list was checked against it above
+ok = gold is not None and not a.no_check   # every pass's list was checked against it above
 print(json.dumps({"volume": a.share or f"C2 {a.gib} GiB", "bytes": spec.own_hi - spec.own_lo,
                   "golden_match_every_pass": ok,
                   "ms": {q: {"min": round(min(v), 1), "median": round(statistics.median(v), 1)}

@@ -140,12 +140,18 @@ __device__ __forceinline__ void message(uint32_t (&w)[16], const uint32_t (&d)[1
     }
 }
 
-// Producer: W[t] for t = 0..63 into the LDS slot (word group q of
-// lane l at uint4 index q*64 + l: conflict-free ds_write_b128 / ds_read_b128).
-// quad: the compact latency-mode layout (16 chains: q * 16 + lane) with K
-// added here, so a lane that reads a zero slot instead gets exactly 0
-__device__ __forceinline__ void schedule_to_lds(uint32_t (&w)[16], uint4 *slot, uint32_t lane,
-                                                bool quad = false) {
+// W slot layouts: split tiles (64 chains, word group q of lane l at uint4
+// q*64 + l: conflict-free ds_write_b128 / ds_read_b128); latency tiles (16
+// chains at q*16 + lane, K added here, so a lane that reads a zero slot gets
+// exactly 0); isolated latency tiles (the same, one word early: uint4 q holds
+// words 4q+1 .. 4q+4 and word 0 ends uint4 15, so an eight-round group of
+// compress_quad_iso reads exactly two uint4s).
+enum { kSlotSplit = 0, kSlotQuad = 1, kSlotQuadEarly = 2 };
+
+// Producer: W[t] (+ K[t]) for t = 0..63 into an LDS slot of layout L.
+template <int L>
+__device__ __forceinline__ void schedule_to_lds(uint32_t (&w)[16], uint4 *slot, uint32_t lane) {
+    uint32_t k0 = 0, c1 = 0, c2 = 0, c3 = 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
         uint32_t o[4];
@@ -161,10 +167,19 @@ __device__ __forceinline__ void schedule_to_lds(uint32_t (&w)[16], uint4 *slot, 
                 const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
                 wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
             }
-            o[i] = quad ? wt + kK256[t] : wt;
+            o[i] = L == kSlotSplit ? wt : wt + kK256[t];
         }
-        slot[q * (quad ? 16 : 64) + lane] = make_uint4(o[0], o[1], o[2], o[3]);
+        if constexpr (L == kSlotQuadEarly) {
+            if (q == 0) k0 = o[0];
+            else slot[(q - 1) * 16 + lane] = make_uint4(c1, c2, c3, o[0]);
+            c1 = o[1];
+            c2 = o[2];
+            c3 = o[3];
+        } else {
+            slot[q * (L == kSlotQuad ? 16 : 64) + lane] = make_uint4(o[0], o[1], o[2], o[3]);
+        }
     }
+    if constexpr (L == kSlotQuadEarly) slot[15 * 16 + lane] = make_uint4(c1, c2, c3, k0);
 }
 
 #define VS_SHA_ROUND(a, b, c, d, e, f, g, h, wk)                                   \
@@ -245,6 +260,84 @@ __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
         p3 = dpp_u32<0xB1>(a_) + t_;   /* quad_perm [1,0,3,2] */                            \
     }
 
+// Isolated latency tiles (a CU each) use a second form: one
+// DPP add per round and no select.  Lane 0 folds d into its sum (T = T1 + d =
+// e'), lane 1 carries -d (T = T2 - d), and the new value is T + the quad's
+// lane-2 zero (lane 0) / lane 0's T (lane 1):
+//   Z = h + (K + W) + d | -d | 0          (one round ahead: v_xad + DPP add)
+//   new = DPP[2,0,2,2](T) + T = e' | T1 + T2 | 0
+// Lane 1 reads a slot of ones for K + W, so (~c) + 1 = -c exactly.  Eight
+// rounds per asm statement (hipcc reassociates Z into T, 13 VALU, or pads
+// wait states, when it schedules the round itself): 10 VALU per round and no
+// s_nop.  Measured alone on a SIMD (tools/probe/quad_round.hip): 47.9 cycles
+// per round against the select form's 64.8.  The K + W slot is one word early
+// (kSlotQuadEarly) so a group reads exactly two uint4s.  Wait states inside:
+// the DPP read of T follows its v_add3 by two instructions; the DPP read of p2
+// is of a value written three rounds before (s_nop 1 opens a block's first
+// group, whose p2 comes from hipcc's code).
+#define VS_QA(cur, p1, p2, p3, k)                                                           \
+    "v_alignbit_b32 %[r1], %[" #cur "], %[" #cur "], %[s1]\n\t"                            \
+    "v_alignbit_b32 %[r2], %[" #cur "], %[" #cur "], %[s2]\n\t"                            \
+    "v_alignbit_b32 %[r3], %[" #cur "], %[" #cur "], %[s3]\n\t"                            \
+    "v_bitop3_b32 %[xx], %[" #cur "], %[" #p1 "], %[m] bitop3:0xd2\n\t"                    \
+    "v_bitop3_b32 %[r1], %[r1], %[r2], %[r3] bitop3:0x96\n\t"                              \
+    "v_bitop3_b32 %[xx], %[xx], %[" #p1 "], %[" #p2 "] bitop3:0xca\n\t"                    \
+    "v_add3_u32 %[tt], %[r1], %[xx], %[z]\n\t"                                             \
+    "v_xad_u32 %[yy], %[" #p2 "], %[m], %[" #k "]\n\t"                                      \
+    "v_add_u32_dpp %[z], %[" #p2 "], %[yy] quad_perm:[1,2,2,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t" \
+    "v_add_u32_dpp %[" #p3 "], %[tt], %[tt] quad_perm:[2,0,2,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+
+// extra arguments: unused inputs (they make hipcc issue those loads earlier)
+#define VS_QUAD8(pre, A, B, ...)                                                             \
+    {                                                                                        \
+        uint32_t r1, r2, r3, xx, tt, yy;                                                     \
+        asm(pre VS_QA(x0, x1, x2, x3, k0) VS_QA(x3, x0, x1, x2, k1) VS_QA(x2, x3, x0, x1, k2) \
+                VS_QA(x1, x2, x3, x0, k3) VS_QA(x0, x1, x2, x3, k4) VS_QA(x3, x0, x1, x2, k5) \
+                    VS_QA(x2, x3, x0, x1, k6) VS_QA(x1, x2, x3, x0, k7)                       \
+            : [x0] "+v"(x0), [x1] "+v"(x1), [x2] "+v"(x2), [x3] "+v"(x3), [z] "+v"(z),       \
+              [r1] "=&v"(r1), [r2] "=&v"(r2), [r3] "=&v"(r3), [xx] "=&v"(xx), [tt] "=&v"(tt), \
+              [yy] "=&v"(yy)                                                                 \
+            : [k0] "v"(A.x), [k1] "v"(A.y), [k2] "v"(A.z), [k3] "v"(A.w), [k4] "v"(B.x),      \
+              [k5] "v"(B.y), [k6] "v"(B.z), [k7] "v"(B.w), [m] "v"(ql.m), [s1] "v"(ql.s1),   \
+              [s2] "v"(ql.s2), [s3] "v"(ql.s3), ##__VA_ARGS__);                              \
+    }
+
+// One block in the isolated form, its first K + W words (kz = word 0, a, b =
+// words 1..8) already in registers; returns the next block's (from kwn).
+__device__ __forceinline__ void compress_quad_iso(uint32_t (&x)[4], const uint4 *kw, const uint4 *kwn,
+                                                  const QuadLane &ql, uint32_t &kz, uint4 &a, uint4 &b) {
+    uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3];
+    uint32_t z = dpp_u32<0xA9>(x3) + ((x3 ^ ql.m) + kz);
+    // the next block's first words ride as unused inputs of groups 6 and 7,
+    // so hipcc issues their loads a group ahead and they land while a group
+    // runs (left to itself it sinks them below the last group and waits)
+    const uint4 pa = kwn[0], pb = kwn[16];
+    const uint32_t pz = kwn[15 * 16].w;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        uint4 na = pa, nb = pb;
+        if (g < 7) {
+            na = kw[(2 * g + 2) * 16];
+            nb = kw[(2 * g + 3) * 16];
+        }
+        if (g == 0)
+            VS_QUAD8("s_nop 1\n\t", a, b)
+        else if (g == 6)
+            VS_QUAD8("", a, b, "v"(pa.x), "v"(pa.y), "v"(pa.z), "v"(pa.w), "v"(pz))
+        else if (g == 7)
+            VS_QUAD8("", a, b, "v"(pb.x), "v"(pb.y), "v"(pb.z), "v"(pb.w))
+        else
+            VS_QUAD8("", a, b)
+        a = na;
+        b = nb;
+    }
+    kz = pz;
+    x[0] += x0;
+    x[1] += x1;
+    x[2] += x2;
+    x[3] += x3;
+}
+
 __device__ __forceinline__ void compress_quad(uint32_t (&x)[4], const uint4 *kw, const QuadLane &ql) {
     uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3];
     uint4 v = kw[0];
@@ -264,6 +357,8 @@ __device__ __forceinline__ void compress_quad(uint32_t (&x)[4], const uint4 *kw,
     x[3] += x3;
 }
 #undef VS_QUAD_ROUND
+#undef VS_QA
+#undef VS_QUAD8
 
 // End of a chain's turn in a slice: write the digest of a finished chain, or
 // append the midstate of an unfinished one to the next active list
@@ -338,7 +433,7 @@ __device__ __forceinline__ void produce_tile(uint4 (&wk)[2][16 * 64], const ShaC
     c = S[3];
     if (mine > 0) {
         message(w, d, p, e, L);
-        schedule_to_lds(w, wk[0], lane, QUAD);
+        schedule_to_lds<QUAD ? kSlotQuad : kSlotSplit>(w, wk[0], lane);
     }
     __syncthreads();
     for (uint32_t j = 0; j < steps; ++j) {
@@ -356,9 +451,61 @@ __device__ __forceinline__ void produce_tile(uint4 (&wk)[2][16 * 64], const ShaC
         c = S[3];
         if (j + 1 < mine) {
             message(w, d, p + 64ull * (j + 1), e, L);
-            schedule_to_lds(w, slot, lane, QUAD);
+            schedule_to_lds<QUAD ? kSlotQuad : kSlotSplit>(w, slot, lane);
         }
         __syncthreads();
+    }
+}
+
+// An isolated latency tile's producer uses all 64 lanes -- lane
+// 4c + k builds block 4m + k of chain c -- so one pass over the message
+// schedule yields a batch of four blocks and the producer no longer paces the
+// rounds (it did: 16 lanes of work per block took as long as the consumer's
+// block).  The W ring lives in the launch's dynamic LDS (the isolation
+// padding): 16 slots, block j in slot j % 16 at a 4 KiB + 64 B stride (the
+// four blocks of a pass land in different banks).  One barrier per batch: the
+// consumer runs batch m while the producer builds batch m + 2 into the slots
+// of batch m - 2, so batch m + 1 is complete and the consumer reads each next
+// block's first K + W during the current one; a batch's segments are loaded
+// one batch ahead.
+constexpr uint32_t kRingStride = 16 * 16 + 4;  // uint4 per ring slot
+constexpr uint32_t kRingSlots = 16;
+static_assert(kRingSlots * kRingStride * sizeof(uint4) <= kIsoPadBytes, "W ring exceeds the isolation padding");
+
+__device__ __forceinline__ void produce_quad4(uint4 *ring, const ShaChain &ch0, uint32_t mine, uint32_t steps,
+                                              uint32_t lane) {
+    const uint64_t p = ch0.ptr, e = ch0.end, L = ch0.len;
+    const uint64_t A = p & ~15ull;
+    const uint64_t safe = L ? ((e - 1) & ~15ull) : ((uint64_t)(uintptr_t)ch0.out & ~15ull);
+    const uint32_t q = (uint32_t)(p & 15) >> 2, k = lane & 3, c = lane >> 2;
+    uint4 S0, S[4];
+    uint32_t d[17], w[16];
+    auto load = [&](uint32_t m) {  // batch m: this lane's block 4m + k
+        const uint64_t b = A + 64ull * (4 * m + k);
+        S0 = load_seg(b, e, safe);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) S[s] = load_seg(b + 16 * (s + 1), e, safe);
+    };
+    auto build = [&](uint32_t m) {
+        const uint32_t blk = 4 * m + k;
+        if (blk < mine) {
+            window_words(d, S0, S, q);
+            message(w, d, p + 64ull * blk, e, L);
+            schedule_to_lds<kSlotQuadEarly>(w, ring + (blk % kRingSlots) * kRingStride, c);
+        }
+    };
+    // build i happens before barrier i (none before barrier 0: batches 0 and
+    // 1 precede the consumer's first block), i.e. batch m + 2 while the
+    // consumer runs batch m.  One copy of the build code (VGPR budget);
+    // 1 + ceil(steps / 4) barriers, as the consumer.
+    const uint32_t nb = (steps + 3) / 4;
+    load(0);
+    for (uint32_t i = 0; i < nb + 2; ++i) {
+        if (i < nb) {
+            build(i);
+            load(i + 1);
+        }
+        if (i >= 1) __syncthreads();
     }
 }
 
@@ -372,15 +519,17 @@ __device__ __forceinline__ void produce_tile(uint4 (&wk)[2][16 * 64], const ShaC
 constexpr uint32_t kTraceCap = 1u << 16;
 __device__ uint64_t g_sha_trace[kTraceCap * 4];
 __device__ uint32_t g_sha_trace_n;
-__device__ __forceinline__ void trace_tile(bool quad, uint32_t t, uint64_t t0, uint32_t lane) {
+// word 0: quad << 63 | shader-clock cycles of the tile (s_memtime) << 20 | tile
+__device__ __forceinline__ void trace_tile(bool quad, uint32_t t, uint64_t t0, uint64_t c0, uint32_t lane) {
     uint32_t hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t cyc = (uint64_t)__builtin_amdgcn_s_memtime() - c0;
     if (lane == 0) {
         const uint32_t k = atomicAdd(&g_sha_trace_n, 1u);
         if (k < kTraceCap) {
-            g_sha_trace[4 * k + 0] = ((uint64_t)quad << 63) | t;
+            g_sha_trace[4 * k + 0] = ((uint64_t)quad << 63) | ((cyc < (1ull << 43) ? cyc : (1ull << 43) - 1) << 20) | (t & 0xfffffu);
             g_sha_trace[4 * k + 1] = ((uint64_t)xcc << 32) | hw;
             g_sha_trace[4 * k + 2] = t0;
             g_sha_trace[4 * k + 3] = t1;
@@ -396,8 +545,9 @@ __device__ __forceinline__ void trace_tile(bool quad, uint32_t t, uint64_t t0, u
 #define VS_SHA_QUAD_PPRIO 0
 #endif
 // Tiles [0, qt) hold the first (longest) a.quad_chains chains of the order, 16
-// per tile, consumed in latency mode (compress_quad; the producer's lanes
-// 16..63 idle); the later tiles hold 64 chains each in split mode.
+// per tile, consumed in latency mode (compress_quad, the producer's lanes
+// 16..63 idle; in an isolated launch compress_quad_iso fed by produce_quad4);
+// the later tiles hold 64 chains each in split mode.
 // VS_SHA_MINW (A/B builds): at least this many waves per SIMD, i.e. a
 // register budget that fits beside a co-resident fingerprint workgroup
 #ifdef VS_SHA_MINW
@@ -416,8 +566,12 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
     // segments 0..318); a workgroup's tiles come in tile-counter order, so it
     // runs every quad tile it gets before its first split tile
     uint4 *const zero_kw = &wk[0][512];
+    uint4 *const one_kw = &wk[0][768];  // isolated form: lane 1's K + W (-d = ~d + 1)
     const uint32_t lane = threadIdx.x & 63;
     const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;  // wave-uniform
+    // an isolated latency launch: the W ring in its dynamic LDS (produce_quad4)
+    extern __shared__ uint4 iso_ring[];
+    const bool iso = a.resident != nullptr;
     const uint32_t n = *a.n_cur;
     const uint32_t nq = min(a.quad_chains, n);
     const uint32_t qt = (nq + 15) / 16;
@@ -428,7 +582,10 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
     if (a.resident && threadIdx.x == 0)   // isolated quad launch: this tile's CU is held
         __hip_atomic_fetch_add(a.resident, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     if (qt && a.tiles != kShaTilesSplit) {
-        for (uint32_t i = threadIdx.x; i < 16 * 16; i += blockDim.x) zero_kw[i] = make_uint4(0, 0, 0, 0);
+        for (uint32_t i = threadIdx.x; i < 16 * 16; i += blockDim.x) {
+            zero_kw[i] = make_uint4(0, 0, 0, 0);
+            one_kw[i] = make_uint4(1, 1, 1, 1);
+        }
         __syncthreads();
     }
     if (!producer) __builtin_amdgcn_s_setprio(2);  // the rounds are the critical path
@@ -439,7 +596,7 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
         __syncthreads();
         if (t >= ntiles) break;
         const bool quad = t < qt;  // wave-uniform
-        const uint32_t my = quad ? (producer ? lane : lane >> 2) : lane;
+        const uint32_t my = quad ? (producer && !iso ? lane : lane >> 2) : lane;
         const uint32_t idx = quad ? t * 16 + my : nq + (t - qt) * 64 + my;
         const bool valid = quad ? (my < 16 && idx < nq) : idx < n;
         const uint32_t ci = valid ? (a.order ? a.order[idx] : idx) : 0u;
@@ -454,6 +611,7 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
         if (steps == 0) continue;
 #if VS_SHA_TRACE
         const uint64_t t_tile = __builtin_amdgcn_s_memrealtime();
+        const uint64_t c_tile = __builtin_amdgcn_s_memtime();
 #endif
         if (producer) {
             if (quad) {
@@ -461,7 +619,10 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
                 // beside busy split tiles it would otherwise need ~6000
                 // cycles per block against the quad consumer's ~3800
                 if (VS_SHA_QUAD_PPRIO) __builtin_amdgcn_s_setprio(3);
-                produce_tile<true>(wk, ch0, mine, steps, lane);
+                if (iso)
+                    produce_quad4(iso_ring, ch0, mine, steps, lane);
+                else
+                    produce_tile<true>(wk, ch0, mine, steps, lane);
                 if (VS_SHA_QUAD_PPRIO) __builtin_amdgcn_s_setprio(0);
             } else {
                 produce_tile<false>(wk, ch0, mine, steps, lane);
@@ -480,9 +641,33 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) x[i] = role == 0 ? ch0.st[4 + i] : role == 1 ? ch0.st[i] : 0u;
             __syncthreads();
-            for (uint32_t j = 0; j < steps; ++j) {
-                if (j < mine) compress_quad(x, role == 0 ? &wk[j & 1][c] : &zero_kw[c], ql);
-                __syncthreads();
+            if (iso) {
+                // a batch of four blocks per barrier (produce_quad4), straight-line:
+                // every lane runs all four and keeps the blocks it owns; each
+                // block's first K + W words are read during the block before.
+                // Per-lane base and slot stride (0 for lanes 1-3): no branch
+                const uint4 *kbase = role == 0 ? &iso_ring[c] : role == 1 ? &one_kw[c] : &zero_kw[c];
+                const uint32_t kstride = role == 0 ? kRingStride : 0u;
+                auto kwp = [&](uint32_t j) { return kbase + (j % kRingSlots) * kstride; };
+                uint32_t kz = kwp(0)[15 * 16].w;
+                uint4 qa = kwp(0)[0], qb = kwp(0)[16];
+                for (uint32_t j0 = 0; j0 < steps; j0 += 4) {
+#pragma unroll
+                    for (uint32_t kk = 0; kk < 4; ++kk) {
+                        const uint32_t j = j0 + kk;
+                        uint32_t y[4] = {x[0], x[1], x[2], x[3]};
+                        compress_quad_iso(y, kwp(j), kwp(j + 1), ql, kz, qa, qb);
+                        const bool on = j < mine;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) x[i] = on ? y[i] : x[i];
+                    }
+                    __syncthreads();
+                }
+            } else {
+                for (uint32_t j = 0; j < steps; ++j) {
+                    if (j < mine) compress_quad(x, role == 0 ? &wk[j & 1][c] : &zero_kw[c], ql);
+                    __syncthreads();
+                }
             }
             uint32_t st[8];
 #pragma unroll
@@ -492,7 +677,7 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
             }
             retire(a, ch0, st, valid && role == 0, mine, left, lane);
 #if VS_SHA_TRACE
-            trace_tile(true, t, t_tile, lane);
+            trace_tile(true, t, t_tile, c_tile, lane);
 #endif
             __builtin_amdgcn_s_setprio(2);
         } else {
@@ -506,7 +691,7 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
             }
             retire(a, ch0, st, valid, mine, left, lane);
 #if VS_SHA_TRACE
-            trace_tile(false, t, t_tile, lane);
+            trace_tile(false, t, t_tile, c_tile, lane);
 #endif
         }
     }
@@ -870,13 +1055,14 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
         for (uint32_t k = first; k < kShaBuckets; ++k) blocks += (double)hist_h[k] * bucket_blocks(k);
         // Per-block costs of a chain: split mode beside a busy
         // chip ~2.8 us (the producer crowded on its SIMD); quad mode ~1.6 us
-        // beside split tiles, ~1.45 us on a CU of its own (isolated drain,
-        // profiles/r06_drain); the backlog clears at split-mode throughput,
+        // beside split tiles, ~1.34 us on a CU of its own (isolated drain:
+        // compress_quad_iso fed by produce_quad4, profiles/r06_quad; 1.45 us
+        // with the shared-CU form, profiles/r06_drain); the backlog clears at split-mode throughput,
         // ~1.45 TB/s = 22.7 G blocks/s over the whole chip.
         // (split chains beside a busy chip after a long run, the clock down:
         // up to 3.3 us, profiles/r06_val1/trace_c2; the rule takes 3.0)
         constexpr double kSplitBlockS = 3.0e-6, kBulkBlocksPerS = 22.7e9;
-        const double quad_s = isolate ? 1.45e-6 : 1.6e-6;
+        const double quad_s = isolate ? 1.34e-6 : 1.6e-6;
         // isolated, at most half the CUs hold quad tiles (16 chains each)
         const uint32_t quad_cap = isolate ? (uint32_t)std::max(cus, 2) / 2 * 16 : 0xffffffffu;
         const double lmax = first < kShaBuckets ? (double)bucket_blocks(first) : 0.0;
