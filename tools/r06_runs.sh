@@ -77,6 +77,9 @@ case $1 in
     done ;;
   counters)  # C2 counter passes (traffic, VALU activity) -> gpurun_out/profile_c2
     bash tools/gpu.sh prof c2 'fp_kernel|sha_slice_kernel' --gpus 1 --steps 5 --warmup 1 --distinct 0 ;;
+  quadprobe)   # cycles per latency-mode round alone on a SIMD, per round form (tools/probe/quad_round.hip)
+    mkdir -p tools/probe/bin && /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/probe/bin/quad_round tools/probe/quad_round.hip &&
+    timeout -k 10 60 ./tools/probe/bin/quad_round > gpurun_out/quad_round.txt 2>&1; rc=$?; cat gpurun_out/quad_round.txt; exit $rc ;;
   quadtrace)   # the latency tiles' duration, clock and the longest chain (VS_SHA_TRACE build shatrace)
     VSGPU_LIB=$PWD/$(var shatrace) bash tools/gpu.sh py tools/sha_trace.py --gib 64 --quad auto:1 &&
     mv gpurun_out/py_sha_trace.log gpurun_out/trace_c2_quad.log ;;
