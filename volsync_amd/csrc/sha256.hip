@@ -222,7 +222,8 @@ __device__ __forceinline__ void compress_lds(uint32_t (&st)[8], const uint4 *slo
 #undef VS_SHA_ROUND
 
 // Latency (quad) consumer: four lanes per chain, so one wave's instruction
-// stream advances a chain with ~10 VALU per round instead of ~15.  Lane roles
+// stream advances a chain with 10 VALU and a select per round instead of the
+// split form's 14 (compress_quad_iso below drops the select).  Lane roles
 // in a quad: 0 runs the e-path (cur = e, history f, g, h), 1 the a-path
 // (cur = a, history b, c, d), 2 and 3 hold zeros.  Per round, with per-lane
 // rotation amounts and masks:
