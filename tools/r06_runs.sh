@@ -77,6 +77,16 @@ case $1 in
     done ;;
   counters)  # C2 counter passes (traffic, VALU activity) -> gpurun_out/profile_c2
     bash tools/gpu.sh prof c2 'fp_kernel|sha_slice_kernel' --gpus 1 --steps 5 --warmup 1 --distinct 0 ;;
+  pscanab)   # STEP probes batched a lane per survivor (product) against per-lane probes (pscan0): walk tests, real-C4 rank, C4 shape
+    bash tools/gpu.sh tests tests/test_gpu_rsync.py tests/test_gpu_rsync_stream.py -x && mv gpurun_out/gputests.log gpurun_out/gputests_rsync.log &&
+    ab ab_pscan_share 2 "pscan0=$(var pscan0),new=" bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline &&
+    ab ab_pscan_c4 2 "pscan0=$(var pscan0),new=" bench.py --mode rsync --steps 5 --warmup 1 --no-file-sum --no-cpu-baseline ;;
+  pscanprof)   # walk phase profiles at the real-C4 rank, batched probes (walkprof) and per-lane (walkprof0)
+    for v in walkprof walkprof0; do
+      VSGPU_LIB=$PWD/$(var $v) timeout -k 10 300 python bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 1 --warmup 1 \
+        --no-cpu-baseline --no-file-sum > gpurun_out/bench_$v.log 2>&1 || exit 1
+      echo "== $v"; grep "walk prof" gpurun_out/bench_$v.log | tail -1
+    done ;;
   quadprobe)   # cycles per latency-mode round alone on a SIMD, per round form (tools/probe/quad_round.hip)
     mkdir -p tools/probe/bin && /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/probe/bin/quad_round tools/probe/quad_round.hip &&
     timeout -k 10 60 ./tools/probe/bin/quad_round > gpurun_out/quad_round.txt 2>&1; rc=$?; cat gpurun_out/quad_round.txt; exit $rc ;;

@@ -45,6 +45,11 @@ using vsstrong::P32_1;
 #ifndef VS_WALK_FRING
 #define VS_WALK_FRING 2
 #endif
+// STEP probes: every survivor of a batch in one round trip, a lane each
+// (stage1 / stage2 in walk_segment); 0 = each lane probes its own in turn
+#ifndef VS_WALK_PSCAN
+#define VS_WALK_PSCAN 1
+#endif
 constexpr uint32_t kWalkThreads = VS_WALK_T;             // 8 waves (up to 256 VGPRs each); the 128 KiB prefilter admits one WG/CU
 constexpr uint32_t kWalkRing = VS_WALK_RRING;                  // window blocks in flight per lane in the wave walk
 #ifndef VS_WALK_LDSF
@@ -891,7 +896,7 @@ __device__ __forceinline__ int64_t by_row(int64_t v, uint32_t lane, uint32_t nv)
 // is dropped, so matches and false alarms are hash_search's.
 template <uint32_t RING>
 __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const uint32_t *lfilt,
-                                  uint8_t *wring,
+                                  uint8_t *wring, uint32_t *pscr,
                                   uint32_t lane, int64_t o, int32_t want, int64_t stop,
                                   int64_t *out_off, int32_t *out_idx, int64_t *out_fab,
                                   uint32_t cap, const SpecView *spec, WProf &wp,
@@ -1017,6 +1022,10 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
             uint32_t sums[16];   // (s1 & 0xffff) | (s2 << 16) per offset
             uint32_t t1, t2;     // the sums at the next batch's first offset (uniform)
             uint32_t pt;         // the probed offset of the lane (16: none)
+#if VS_WALK_PSCAN
+            uint32_t base;       // spread: the lane's first survivor's rank in the batch
+            uint32_t ns;         // spread: survivors in the batch (uniform; 0: each lane its own)
+#endif
             uint4 b0, b1;        // its membership bucket
         };
         uint4 nwo = cwo, nwi = cwi;
@@ -1098,6 +1107,31 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
             }
             st.hit = hit;
             st.pt = hit ? (uint32_t)__builtin_ctz(hit) : 16u;
+#if VS_WALK_PSCAN
+            // A lane with several survivors used to probe them one dependent
+            // load at a time, and the wave waited for its most crowded lane
+            // (≈ 2.5 loads per batch at the real C4 density, 7.3 K cycles:
+            // profiles/r05_walk/flushspan).  When some lane has more than one,
+            // the batch's survivors are spread a lane each instead: survivor
+            // r (offset order) goes to pscr[r], lane r loads its bucket, and
+            // every probe is one round trip in flight behind the next batch's
+            // stage 1.  pt then carries lane j's survivor sum.
+            st.ns = 0;
+            if (__ballot(hit & (hit - 1u))) {
+                const uint32_t pc = (uint32_t)__builtin_popcount(hit);
+                st.base = excl_scan(pc, lane);
+                st.ns = uni((uint32_t)__builtin_amdgcn_readlane((int)(st.base + pc), 63));
+                uint32_t r = st.base;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    if (((hit >> t) & 1u) && r < 64) pscr[r] = st.sums[t];
+                    r += (hit >> t) & 1u;
+                }
+                // (a wave's LDS accesses complete in issue order)
+                st.pt = lane < st.ns ? pscr[lane] : 0u;
+                if (lane < st.ns) bucket_load(a, st.pt, st.b0, st.b1);
+            } else
+#endif
             if (hit) {
                 uint32_t sv = st.sums[0];
 #pragma unroll
@@ -1121,6 +1155,28 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
             // the lane's first offset, the rest probed now -- rare)
             uint64_t tsub = wclock(wp);
             uint32_t hit = cur.hit;
+#if VS_WALK_PSCAN
+            if (cur.ns) {
+                const bool in = lane < cur.ns && bucket_has(a, cur.pt, cur.b0, cur.b1);
+                const uint64_t res = __ballot(in);   // bit r: survivor r's sum is in the table
+                uint32_t keep = 0, r = cur.base;
+                for (uint32_t mm = cur.hit; mm; ++r) {
+                    const int t = __builtin_ctz(mm);
+                    mm &= mm - 1;
+                    bool ok;
+                    if (r < 64) {
+                        ok = (res >> r) & 1u;
+                    } else {   // past the wave's 64 survivors (rare): probed here
+                        uint32_t st = cur.sums[0];
+#pragma unroll
+                        for (int k = 1; k < 16; ++k) st = (t == k) ? cur.sums[k] : st;
+                        ok = probe_bucket(a, st);
+                    }
+                    keep |= (uint32_t)ok << t;
+                }
+                hit = keep;
+            } else
+#endif
             if (hit) {
                 uint32_t sv = cur.sums[0];
 #pragma unroll
@@ -1289,6 +1345,7 @@ __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
     __shared__ uint32_t lfilt[kLdsFiltWordsW];
     __shared__ __attribute__((aligned(16))) uint64_t lsec[kSecWords];
     __shared__ __attribute__((aligned(16))) uint8_t wring[kWideRingBytes * (kWalkThreads / 64) + 16];
+    __shared__ uint32_t pscr[kWalkThreads / 64][64];   // per wave: a STEP batch's survivors' sums
     load_secret(lsec, a.seed);
     load_prefilter(a, lfilt);
     const uint32_t lane = threadIdx.x & 63;
@@ -1302,7 +1359,7 @@ __global__ __launch_bounds__(T) void rs_walk_spec_kernel(RsWalkArgs a) {
         const uint64_t base = (uint64_t)k * a.cap;
         FaRec rec{a.spec_fao + (uint64_t)k * a.facap, a.spec_fac + (uint64_t)k * a.facap,
                   a.facap, 0};
-        const SegResult r = walk_segment<RING>(a, rs, lfilt, wring, lane, e, w, seg_hi(a, k),
+        const SegResult r = walk_segment<RING>(a, rs, lfilt, wring, pscr[threadIdx.x >> 6], lane, e, w, seg_hi(a, k),
                                                a.spec_off + base, a.spec_idx + base,
                                                a.spec_fab + base, a.cap, nullptr, wp, &rec);
         wadd(wp, kPrSeg, ts);
@@ -1390,6 +1447,7 @@ __global__ __launch_bounds__(kWalkThreads) void rs_walk_stitch_kernel(RsWalkArgs
     __shared__ uint32_t lfilt[kLdsFiltWordsW];
     __shared__ __attribute__((aligned(16))) uint64_t lsec[kSecWords];
     __shared__ __attribute__((aligned(16))) uint8_t wring[kWideRingBytes * (kWalkThreads / 64) + 16];
+    __shared__ uint32_t pscr[kWalkThreads / 64][64];   // per wave: a STEP batch's survivors' sums
     load_secret(lsec, a.seed);
     load_prefilter(a, lfilt);
     const uint32_t lane = threadIdx.x & 63;
@@ -1426,7 +1484,7 @@ __global__ __launch_bounds__(kWalkThreads) void rs_walk_stitch_kernel(RsWalkArgs
             }
         }
         if (walk) {
-            r = walk_segment<kWalkRing>(a, rs, lfilt, wring, lane, ws, w, seg_hi(a, k), a.fin_off + base,
+            r = walk_segment<kWalkRing>(a, rs, lfilt, wring, pscr[threadIdx.x >> 6], lane, ws, w, seg_hi(a, k), a.fin_off + base,
                                     a.fin_idx + base, a.fin_fab + base, a.cap, &sv, wp);
             r.fa += fadj;
         }
