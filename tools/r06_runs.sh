@@ -87,6 +87,8 @@ case $1 in
         --no-cpu-baseline --no-file-sum > gpurun_out/bench_$v.log 2>&1 || exit 1
       echo "== $v"; grep "walk prof" gpurun_out/bench_$v.log | tail -1
     done ;;
+  walkcounters)   # counter passes of the real-C4 rank's walk (spread STEP probes) -> gpurun_out/profile_c4share
+    bash tools/gpu.sh prof c4share 'rs_walk_spec_kernel' --mode rsync --share 3/8 --per-gpu-gib 32 --steps 2 --warmup 1 --no-file-sum ;;
   quadprobe)   # cycles per latency-mode round alone on a SIMD, per round form (tools/probe/quad_round.hip)
     mkdir -p tools/probe/bin && /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/probe/bin/quad_round tools/probe/quad_round.hip &&
     timeout -k 10 60 ./tools/probe/bin/quad_round > gpurun_out/quad_round.txt 2>&1; rc=$?; cat gpurun_out/quad_round.txt; exit $rc ;;
