@@ -89,6 +89,13 @@ case $1 in
     done ;;
   walkcounters)   # counter passes of the real-C4 rank's walk (spread STEP probes) -> gpurun_out/profile_c4share
     bash tools/gpu.sh prof c4share 'rs_walk_spec_kernel' --mode rsync --share 3/8 --per-gpu-gib 32 --steps 2 --warmup 1 --no-file-sum ;;
+  isoab)   # isolated latency kernel: one consumer wave per CU (product) against two (iso2) and HEAD's build (head)
+    bash tools/gpu.sh tests tests/test_gpu_cdc.py tests/test_gpu_c3.py -x && mv gpurun_out/gputests.log gpurun_out/gputests_cdc.log &&
+    VSGPU_LIB=$PWD/$(var iso2) bash tools/gpu.sh tests tests/test_gpu_cdc.py -x -k "drain or sha256 or blob" && mv gpurun_out/gputests.log gpurun_out/gputests_iso2.log &&
+    ab ab_iso_single_c2 2 "head=$(var head),new=,iso2=$(var iso2)" tools/single_pass.py --gib 64 --quad auto --rounds 2 &&
+    ab ab_iso_single_c3r3 2 "head=$(var head),new=,iso2=$(var iso2)" tools/single_pass.py --share 3/8 --quad auto --rounds 2 &&
+    VSGPU_LIB=$PWD/$(var shatrace) bash tools/gpu.sh py tools/sha_trace.py --gib 64 --quad auto:1 && mv gpurun_out/py_sha_trace.log gpurun_out/trace_c2_iso1.log &&
+    VSGPU_LIB=$PWD/$(var iso2trace) bash tools/gpu.sh py tools/sha_trace.py --gib 64 --quad auto:1 && mv gpurun_out/py_sha_trace.log gpurun_out/trace_c2_iso2.log ;;
   quadprobe)   # cycles per latency-mode round alone on a SIMD, per round form (tools/probe/quad_round.hip)
     mkdir -p tools/probe/bin && /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/probe/bin/quad_round tools/probe/quad_round.hip &&
     timeout -k 10 60 ./tools/probe/bin/quad_round > gpurun_out/quad_round.txt 2>&1; rc=$?; cat gpurun_out/quad_round.txt; exit $rc ;;

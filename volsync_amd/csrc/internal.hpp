@@ -255,13 +255,11 @@ struct ShaSliceArgs {
     uint32_t *tile_ctr;
     uint32_t budget;         // max blocks per chain in this slice (0xffffffff: all)
     uint32_t quad_chains;    // the first (longest) chains of the order run in latency mode
-    uint32_t tiles;          // kShaTilesAll / kShaTilesQuad / kShaTilesSplit: which tiles
-                             // this launch takes (an isolated drain launches both kinds apart)
-    uint32_t *resident;      // isolated quad launch: host-visible count of resident workgroups
+    uint32_t tiles;          // sha_slice_kernel: kShaTilesAll, or kShaTilesSplit beside an
+                             // isolated drain's sha_iso_kernel (the latency tiles)
+    uint32_t *resident;      // sha_iso_kernel: host-visible count of resident workgroups
 };
-// an isolated quad tile's LDS: static 32 KiB + this = the CU's 160 KiB
-constexpr uint32_t kIsoPadBytes = 128 * 1024;
-enum { kShaTilesAll = 0, kShaTilesQuad = 1, kShaTilesSplit = 2 };
+enum { kShaTilesAll = 0, kShaTilesSplit = 2 };
 
 // Host side of the engine: a double-buffered active list on the device, fed by
 // append_*() and advanced by slice(); every call queues on the given stream
@@ -297,10 +295,11 @@ struct ShaEngine {
     static constexpr uint32_t kQuadAuto = 0xffffffffu;
     uint32_t quad_pct = kQuadAuto;
     uint32_t last_quad_chains = 0;  // chains the last drain ran in quad mode (stats)
-    // Isolated latency drain (VS_OPT_SHA_ISOLATE, default on): every quad
-    // tile holds a CU alone (its LDS padded to the whole CU), resident before
-    // the split tiles are launched, so the drain's critical chains never
-    // share a CU with the bulk
+    // Isolated latency drain (VS_OPT_SHA_ISOLATE, default on): the latency
+    // tiles run in sha_iso_kernel, 32 chains per workgroup, each holding a
+    // CU alone (it asks for the CU's whole LDS), resident before the split
+    // tiles are launched, so the drain's critical chains never share a CU
+    // with the bulk
     uint32_t isolate = 1;
     hipStream_t iso_q = nullptr;
     hipEvent_t iso_ev[2] = {nullptr, nullptr};   // fork, quad tiles done

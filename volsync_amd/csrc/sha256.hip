@@ -149,7 +149,7 @@ __device__ __forceinline__ void message(uint32_t (&w)[16], const uint32_t (&d)[1
 enum { kSlotSplit = 0, kSlotQuad = 1, kSlotQuadEarly = 2 };
 
 // Producer: W[t] (+ K[t]) for t = 0..63 into an LDS slot of layout L.
-template <int L>
+template <int L, int CS = 16>   // CS: chains per slot (latency layouts)
 __device__ __forceinline__ void schedule_to_lds(uint32_t (&w)[16], uint4 *slot, uint32_t lane) {
     uint32_t k0 = 0, c1 = 0, c2 = 0, c3 = 0;
 #pragma unroll
@@ -171,15 +171,15 @@ __device__ __forceinline__ void schedule_to_lds(uint32_t (&w)[16], uint4 *slot, 
         }
         if constexpr (L == kSlotQuadEarly) {
             if (q == 0) k0 = o[0];
-            else slot[(q - 1) * 16 + lane] = make_uint4(c1, c2, c3, o[0]);
+            else slot[(q - 1) * CS + lane] = make_uint4(c1, c2, c3, o[0]);
             c1 = o[1];
             c2 = o[2];
             c3 = o[3];
         } else {
-            slot[q * (L == kSlotQuad ? 16 : 64) + lane] = make_uint4(o[0], o[1], o[2], o[3]);
+            slot[q * (L == kSlotQuad ? CS : 64) + lane] = make_uint4(o[0], o[1], o[2], o[3]);
         }
     }
-    if constexpr (L == kSlotQuadEarly) slot[15 * 16 + lane] = make_uint4(c1, c2, c3, k0);
+    if constexpr (L == kSlotQuadEarly) slot[15 * CS + lane] = make_uint4(c1, c2, c3, k0);
 }
 
 #define VS_SHA_ROUND(a, b, c, d, e, f, g, h, wk)                                   \
@@ -305,6 +305,7 @@ __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
 
 // One block in the isolated form, its first K + W words (kz = word 0, a, b =
 // words 1..8) already in registers; returns the next block's (from kwn).
+template <int CS = 16>   // chains per K + W slot
 __device__ __forceinline__ void compress_quad_iso(uint32_t (&x)[4], const uint4 *kw, const uint4 *kwn,
                                                   const QuadLane &ql, uint32_t &kz, uint4 &a, uint4 &b) {
     uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3];
@@ -312,14 +313,14 @@ __device__ __forceinline__ void compress_quad_iso(uint32_t (&x)[4], const uint4 
     // the next block's first words ride as unused inputs of groups 6 and 7,
     // so hipcc issues their loads a group ahead and they land while a group
     // runs (left to itself it sinks them below the last group and waits)
-    const uint4 pa = kwn[0], pb = kwn[16];
-    const uint32_t pz = kwn[15 * 16].w;
+    const uint4 pa = kwn[0], pb = kwn[CS];
+    const uint32_t pz = kwn[15 * CS].w;
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
         uint4 na = pa, nb = pb;
         if (g < 7) {
-            na = kw[(2 * g + 2) * 16];
-            nb = kw[(2 * g + 3) * 16];
+            na = kw[(2 * g + 2) * CS];
+            nb = kw[(2 * g + 3) * CS];
         }
         if (g == 0)
             VS_QUAD8("s_nop 1\n\t", a, b)
@@ -458,53 +459,82 @@ __device__ __forceinline__ void produce_tile(uint4 (&wk)[2][16 * 64], const ShaC
     }
 }
 
-// An isolated latency tile's producer uses all 64 lanes -- lane
-// 4c + k builds block 4m + k of chain c -- so one pass over the message
-// schedule yields a batch of four blocks and the producer no longer paces the
-// rounds (it did: 16 lanes of work per block took as long as the consumer's
-// block).  The W ring lives in the launch's dynamic LDS (the isolation
-// padding): 16 slots, block j in slot j % 16 at a 4 KiB + 64 B stride (the
-// four blocks of a pass land in different banks).  One barrier per batch: the
-// consumer runs batch m while the producer builds batch m + 2 into the slots
-// of batch m - 2, so batch m + 1 is complete and the consumer reads each next
-// block's first K + W during the current one; a batch's segments are loaded
-// one batch ahead.
-constexpr uint32_t kRingStride = 16 * 16 + 4;  // uint4 per ring slot
+// Isolated latency tiles run in their own kernel,
+// sha_iso_kernel: a workgroup holds a CU alone (the launch asks for the CU's
+// whole 160 KiB of LDS) and kIsoChains chains.  Wave 0 produces, each other
+// wave consumes 16 chains in compress_quad_iso, on a SIMD of its own.  The
+// producer uses all 64 lanes: lane 4c + k builds block 4m + k of chain c (and
+// 16 + c), so one pass over the message schedule per chain yields a batch of
+// four blocks (16 lanes of work per block, as in a shared-CU tile, took as
+// long as the consumer's block).  The W ring: 16 slots of kIsoChains chains,
+// block j in slot j % 16 at a 64 B-padded stride (the four blocks of a pass land in
+// different banks).  One barrier per batch: the consumers run batch m while
+// the producer builds batch m + 2 into the slots of batch m - 2, so batch
+// m + 1 is complete and a consumer reads each next block's first K + W during
+// the current one; a batch's segments are loaded one batch ahead.
+// consumer waves per isolated tile: two (a SIMD each) put the tail on half
+// as many CUs and leave the rest to the bulk -- C2 alone 200.4-201.5 ->
+// 198.5-199.0 ms, a C3 rank 226.5-233.8 -> 223.1-227.9 against the round's
+// one-consumer form (profiles/r06_iso32)
+#ifndef VS_SHA_ISO_CONSUMERS
+#define VS_SHA_ISO_CONSUMERS 2
+#endif
+constexpr uint32_t kIsoWaves = 1 + VS_SHA_ISO_CONSUMERS;   // producer + consumers
+constexpr uint32_t kIsoChains = 16 * VS_SHA_ISO_CONSUMERS;  // chains per isolated tile
 constexpr uint32_t kRingSlots = 16;
-static_assert(kRingSlots * kRingStride * sizeof(uint4) <= kIsoPadBytes, "W ring exceeds the isolation padding");
+constexpr uint32_t kIsoRingStride = kIsoChains * 16 + 4;  // uint4 per ring slot
+constexpr uint32_t kIsoLdsBytes = 160 * 1024;             // the CU's whole LDS
+static_assert((kRingSlots * kIsoRingStride + 2 * 16 * kIsoChains + 1) * sizeof(uint4) <= kIsoLdsBytes,
+              "W ring exceeds the CU's LDS");
 
-__device__ __forceinline__ void produce_quad4(uint4 *ring, const ShaChain &ch0, uint32_t mine, uint32_t steps,
-                                              uint32_t lane) {
-    const uint64_t p = ch0.ptr, e = ch0.end, L = ch0.len;
-    const uint64_t A = p & ~15ull;
-    const uint64_t safe = L ? ((e - 1) & ~15ull) : ((uint64_t)(uintptr_t)ch0.out & ~15ull);
-    const uint32_t q = (uint32_t)(p & 15) >> 2, k = lane & 3, c = lane >> 2;
+struct IsoSrc {  // one chain's byte source in produce_iso
+    uint64_t p, e, L, A, safe;
+    uint32_t q, mine;
     uint4 S0, S[4];
-    uint32_t d[17], w[16];
-    auto load = [&](uint32_t m) {  // batch m: this lane's block 4m + k
-        const uint64_t b = A + 64ull * (4 * m + k);
+    __device__ __forceinline__ void init(const ShaChain &ch, uint32_t m) {
+        p = ch.ptr;
+        e = ch.end;
+        L = ch.len;
+        A = p & ~15ull;
+        safe = L ? ((e - 1) & ~15ull) : ((uint64_t)(uintptr_t)ch.out & ~15ull);
+        q = (uint32_t)(p & 15) >> 2;
+        mine = m;
+    }
+    __device__ __forceinline__ void load(uint32_t blk) {
+        const uint64_t b = A + 64ull * blk;
         S0 = load_seg(b, e, safe);
 #pragma unroll
         for (int s = 0; s < 4; ++s) S[s] = load_seg(b + 16 * (s + 1), e, safe);
-    };
-    auto build = [&](uint32_t m) {
+    }
+};
+
+__device__ __forceinline__ void produce_iso(uint4 *ring, const ShaChain &c0, uint32_t m0, const ShaChain &c1,
+                                            uint32_t m1, uint32_t steps, uint32_t lane) {
+    const uint32_t k = lane & 3, c = lane >> 2;
+    IsoSrc x0, x1;
+    x0.init(c0, m0);
+    x1.init(c1, m1);
+    uint32_t d[17], w[16];
+    auto build = [&](const IsoSrc &x, uint32_t m, uint32_t cc) {
         const uint32_t blk = 4 * m + k;
-        if (blk < mine) {
-            window_words(d, S0, S, q);
-            message(w, d, p + 64ull * blk, e, L);
-            schedule_to_lds<kSlotQuadEarly>(w, ring + (blk % kRingSlots) * kRingStride, c);
+        if (blk < x.mine) {
+            window_words(d, x.S0, x.S, x.q);
+            message(w, d, x.p + 64ull * blk, x.e, x.L);
+            schedule_to_lds<kSlotQuadEarly, kIsoChains>(w, ring + (blk % kRingSlots) * kIsoRingStride, cc);
         }
     };
     // build i happens before barrier i (none before barrier 0: batches 0 and
-    // 1 precede the consumer's first block), i.e. batch m + 2 while the
-    // consumer runs batch m.  One copy of the build code (VGPR budget);
-    // 1 + ceil(steps / 4) barriers, as the consumer.
+    // 1 precede the consumers' first block), i.e. batch m + 2 while the
+    // consumers run batch m; 1 + ceil(steps / 4) barriers, as the consumers
     const uint32_t nb = (steps + 3) / 4;
-    load(0);
+    x0.load(k);
+    if (kIsoChains > 16) x1.load(k);
     for (uint32_t i = 0; i < nb + 2; ++i) {
         if (i < nb) {
-            build(i);
-            load(i + 1);
+            build(x0, i, c);
+            if (kIsoChains > 16) build(x1, i, 16 + c);
+            x0.load(4 * (i + 1) + k);
+            if (kIsoChains > 16) x1.load(4 * (i + 1) + k);
         }
         if (i >= 1) __syncthreads();
     }
@@ -546,9 +576,9 @@ __device__ __forceinline__ void trace_tile(bool quad, uint32_t t, uint64_t t0, u
 #define VS_SHA_QUAD_PPRIO 0
 #endif
 // Tiles [0, qt) hold the first (longest) a.quad_chains chains of the order, 16
-// per tile, consumed in latency mode (compress_quad, the producer's lanes
-// 16..63 idle; in an isolated launch compress_quad_iso fed by produce_quad4);
-// the later tiles hold 64 chains each in split mode.
+// per tile, consumed in latency mode (compress_quad; the producer's lanes
+// 16..63 idle); the later tiles hold 64 chains each in split mode.  (An
+// isolated drain runs its latency tiles in sha_iso_kernel instead.)
 // VS_SHA_MINW (A/B builds): at least this many waves per SIMD, i.e. a
 // register budget that fits beside a co-resident fingerprint workgroup
 #ifdef VS_SHA_MINW
@@ -567,26 +597,17 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
     // segments 0..318); a workgroup's tiles come in tile-counter order, so it
     // runs every quad tile it gets before its first split tile
     uint4 *const zero_kw = &wk[0][512];
-    uint4 *const one_kw = &wk[0][768];  // isolated form: lane 1's K + W (-d = ~d + 1)
     const uint32_t lane = threadIdx.x & 63;
     const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;  // wave-uniform
-    // an isolated latency launch: the W ring in its dynamic LDS (produce_quad4)
-    extern __shared__ uint4 iso_ring[];
-    const bool iso = a.resident != nullptr;
     const uint32_t n = *a.n_cur;
     const uint32_t nq = min(a.quad_chains, n);
     const uint32_t qt = (nq + 15) / 16;
-    // the launch's tile range: every tile, or (an isolated drain) the quad
-    // tiles alone / the split tiles alone
+    // the launch's tile range: every tile, or (beside an isolated drain's
+    // sha_iso_kernel) the split tiles alone
     const uint32_t t_lo = a.tiles == kShaTilesSplit ? qt : 0u;
-    const uint32_t ntiles = a.tiles == kShaTilesQuad ? qt : qt + (n - nq + 63) / 64;
-    if (a.resident && threadIdx.x == 0)   // isolated quad launch: this tile's CU is held
-        __hip_atomic_fetch_add(a.resident, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t ntiles = qt + (n - nq + 63) / 64;
     if (qt && a.tiles != kShaTilesSplit) {
-        for (uint32_t i = threadIdx.x; i < 16 * 16; i += blockDim.x) {
-            zero_kw[i] = make_uint4(0, 0, 0, 0);
-            one_kw[i] = make_uint4(1, 1, 1, 1);
-        }
+        for (uint32_t i = threadIdx.x; i < 16 * 16; i += blockDim.x) zero_kw[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
     }
     if (!producer) __builtin_amdgcn_s_setprio(2);  // the rounds are the critical path
@@ -597,7 +618,7 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
         __syncthreads();
         if (t >= ntiles) break;
         const bool quad = t < qt;  // wave-uniform
-        const uint32_t my = quad ? (producer && !iso ? lane : lane >> 2) : lane;
+        const uint32_t my = quad ? (producer ? lane : lane >> 2) : lane;
         const uint32_t idx = quad ? t * 16 + my : nq + (t - qt) * 64 + my;
         const bool valid = quad ? (my < 16 && idx < nq) : idx < n;
         const uint32_t ci = valid ? (a.order ? a.order[idx] : idx) : 0u;
@@ -620,10 +641,7 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
                 // beside busy split tiles it would otherwise need ~6000
                 // cycles per block against the quad consumer's ~3800
                 if (VS_SHA_QUAD_PPRIO) __builtin_amdgcn_s_setprio(3);
-                if (iso)
-                    produce_quad4(iso_ring, ch0, mine, steps, lane);
-                else
-                    produce_tile<true>(wk, ch0, mine, steps, lane);
+                produce_tile<true>(wk, ch0, mine, steps, lane);
                 if (VS_SHA_QUAD_PPRIO) __builtin_amdgcn_s_setprio(0);
             } else {
                 produce_tile<false>(wk, ch0, mine, steps, lane);
@@ -642,33 +660,9 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) x[i] = role == 0 ? ch0.st[4 + i] : role == 1 ? ch0.st[i] : 0u;
             __syncthreads();
-            if (iso) {
-                // a batch of four blocks per barrier (produce_quad4), straight-line:
-                // every lane runs all four and keeps the blocks it owns; each
-                // block's first K + W words are read during the block before.
-                // Per-lane base and slot stride (0 for lanes 1-3): no branch
-                const uint4 *kbase = role == 0 ? &iso_ring[c] : role == 1 ? &one_kw[c] : &zero_kw[c];
-                const uint32_t kstride = role == 0 ? kRingStride : 0u;
-                auto kwp = [&](uint32_t j) { return kbase + (j % kRingSlots) * kstride; };
-                uint32_t kz = kwp(0)[15 * 16].w;
-                uint4 qa = kwp(0)[0], qb = kwp(0)[16];
-                for (uint32_t j0 = 0; j0 < steps; j0 += 4) {
-#pragma unroll
-                    for (uint32_t kk = 0; kk < 4; ++kk) {
-                        const uint32_t j = j0 + kk;
-                        uint32_t y[4] = {x[0], x[1], x[2], x[3]};
-                        compress_quad_iso(y, kwp(j), kwp(j + 1), ql, kz, qa, qb);
-                        const bool on = j < mine;
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) x[i] = on ? y[i] : x[i];
-                    }
-                    __syncthreads();
-                }
-            } else {
-                for (uint32_t j = 0; j < steps; ++j) {
-                    if (j < mine) compress_quad(x, role == 0 ? &wk[j & 1][c] : &zero_kw[c], ql);
-                    __syncthreads();
-                }
+            for (uint32_t j = 0; j < steps; ++j) {
+                if (j < mine) compress_quad(x, role == 0 ? &wk[j & 1][c] : &zero_kw[c], ql);
+                __syncthreads();
             }
             uint32_t st[8];
 #pragma unroll
@@ -695,6 +689,115 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
             trace_tile(false, t, t_tile, c_tile, lane);
 #endif
         }
+    }
+}
+
+// An isolated drain's latency tiles (see produce_iso): a.quad_chains chains
+// of the order, kIsoChains per workgroup of kIsoWaves waves, each launched
+// with the CU's whole LDS so it holds the CU alone; a.resident counts the
+// workgroups that have started (the host launches the split tiles only then).
+__global__ __launch_bounds__(64 * kIsoWaves) void sha_iso_kernel(ShaSliceArgs a) {
+    extern __shared__ uint4 iso_lds[];
+    uint4 *const ring = iso_lds;
+    uint4 *const zero_kw = ring + kRingSlots * kIsoRingStride;  // lanes 2-3's K + W
+    uint4 *const one_kw = zero_kw + 16 * kIsoChains;             // lane 1's (-d = ~d + 1)
+    uint32_t *const tile_w = (uint32_t *)(one_kw + 16 * kIsoChains);   // [0] tile, [1] steps
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t n = *a.n_cur;
+    const uint32_t nq = min(a.quad_chains, n);
+    const uint32_t ntiles = (nq + kIsoChains - 1) / kIsoChains;
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(a.resident, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (uint32_t i = threadIdx.x; i < 16 * kIsoChains; i += blockDim.x) {
+        zero_kw[i] = make_uint4(0, 0, 0, 0);
+        one_kw[i] = make_uint4(1, 1, 1, 1);
+    }
+    if (wave) __builtin_amdgcn_s_setprio(3);  // the drain's critical path
+    // chain cc of tile t (uniform per lane group of four)
+    auto chain = [&](uint32_t t, uint32_t cc, ShaChain &ch, uint32_t &left, bool &valid) {
+        const uint32_t idx = t * kIsoChains + cc;
+        valid = idx < nq;
+        ch = a.cur[valid ? (a.order ? a.order[idx] : idx) : 0u];
+        left = valid ? blocks_left(ch.ptr, ch.end) : 0u;
+    };
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) tile_w[0] = atomicAdd(a.tile_ctr, 1u);
+        __syncthreads();
+        const uint32_t t = tile_w[0];
+        if (t >= ntiles) break;
+        ShaChain c0, c1;
+        uint32_t l0, l1;
+        bool v0, v1;
+        const uint32_t c = lane >> 2;
+        if (wave == 0) {
+            // the producer holds all the tile's chains: chain c (and 16 + c) per lane
+            chain(t, c, c0, l0, v0);
+            c1 = c0;
+            l1 = 0;
+            if (kIsoChains > 16) chain(t, 16 + c, c1, l1, v1);
+            uint32_t m = max(min(l0, a.budget), min(l1, a.budget));
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+            if (threadIdx.x == 0) tile_w[1] = m;
+        } else {
+            chain(t, 16 * (wave - 1) + c, c0, l0, v0);
+        }
+        __syncthreads();
+        const uint32_t steps = __builtin_amdgcn_readfirstlane(tile_w[1]);
+        if (steps == 0) continue;
+#if VS_SHA_TRACE
+        const uint64_t t_tile = __builtin_amdgcn_s_memrealtime();
+        const uint64_t c_tile = __builtin_amdgcn_s_memtime();
+#endif
+        if (wave == 0) {
+            produce_iso(ring, c0, min(l0, a.budget), c1, min(l1, a.budget), steps, lane);
+            continue;
+        }
+        const uint32_t mine = min(l0, a.budget);
+        const uint32_t role = lane & 3, cc = 16 * (wave - 1) + c;
+        QuadLane ql;
+        ql.s1 = role == 0 ? 6 : role == 1 ? 2 : 0;
+        ql.s2 = role == 0 ? 11 : role == 1 ? 13 : 0;
+        ql.s3 = role == 0 ? 25 : role == 1 ? 22 : 0;
+        ql.m = role == 1 ? 0xffffffffu : 0u;
+        ql.l1 = role == 1;
+        // lane 0: e f g h, lane 1: a b c d, lanes 2-3: zeros
+        uint32_t x[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = role == 0 ? c0.st[4 + i] : role == 1 ? c0.st[i] : 0u;
+        __syncthreads();
+        // a batch of four blocks per barrier, straight-line: every lane runs
+        // all four and keeps the blocks it owns; each block's first K + W words
+        // are read during the block before.  Per-lane base and slot stride (0
+        // for lanes 1-3): no branch
+        const uint4 *kbase = role == 0 ? &ring[cc] : role == 1 ? &one_kw[cc] : &zero_kw[cc];
+        const uint32_t kstride = role == 0 ? kIsoRingStride : 0u;
+        auto kwp = [&](uint32_t j) { return kbase + (j % kRingSlots) * kstride; };
+        uint32_t kz = kwp(0)[15 * kIsoChains].w;
+        uint4 qa = kwp(0)[0], qb = kwp(0)[kIsoChains];
+        for (uint32_t j0 = 0; j0 < steps; j0 += 4) {
+#pragma unroll
+            for (uint32_t kk = 0; kk < 4; ++kk) {
+                const uint32_t j = j0 + kk;
+                uint32_t y[4] = {x[0], x[1], x[2], x[3]};
+                compress_quad_iso<kIsoChains>(y, kwp(j), kwp(j + 1), ql, kz, qa, qb);
+                const bool on = j < mine;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[i] = on ? y[i] : x[i];
+            }
+            __syncthreads();
+        }
+        uint32_t st[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            st[i] = (uint32_t)__shfl((int)x[i], (int)(lane | 1), 64);
+            st[4 + i] = x[i];
+        }
+        retire(a, c0, st, v0 && role == 0, mine, l0, lane);
+#if VS_SHA_TRACE
+        trace_tile(true, 2 * t + wave - 1, t_tile, c_tile, lane);
+#endif
     }
 }
 
@@ -1057,14 +1160,16 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
         // Per-block costs of a chain: split mode beside a busy
         // chip ~2.8 us (the producer crowded on its SIMD); quad mode ~1.6 us
         // beside split tiles, ~1.34 us on a CU of its own (isolated drain:
-        // compress_quad_iso fed by produce_quad4, profiles/r06_quad; 1.45 us
-        // with the shared-CU form, profiles/r06_drain); the backlog clears at split-mode throughput,
+        // sha_iso_kernel, profiles/r06_quad; 1.45 us with the shared-CU form,
+        // profiles/r06_drain); the backlog clears at split-mode throughput,
         // ~1.45 TB/s = 22.7 G blocks/s over the whole chip.
         // (split chains beside a busy chip after a long run, the clock down:
         // up to 3.3 us, profiles/r06_val1/trace_c2; the rule takes 3.0)
         constexpr double kSplitBlockS = 3.0e-6, kBulkBlocksPerS = 22.7e9;
         const double quad_s = isolate ? 1.34e-6 : 1.6e-6;
-        // isolated, at most half the CUs hold quad tiles (16 chains each)
+        // isolated, at most 16 chains per two CUs run in latency mode (with
+        // two consumer waves per tile, 3 638 chains for a C3 rank on half the
+        // CUs took its single pass 225 -> 237-256 ms, profiles/r06_iso32)
         const uint32_t quad_cap = isolate ? (uint32_t)std::max(cus, 2) / 2 * 16 : 0xffffffffu;
         const double lmax = first < kShaBuckets ? (double)bucket_blocks(first) : 0.0;
         const double t_bulk = blocks / kBulkBlocksPerS;
@@ -1090,7 +1195,7 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
                 for (int it = 0; it < 6; ++it) {
                     quad_chains = std::min(count_above(floor_s), quad_cap);
                     if (!isolate) break;
-                    const double qtiles = (quad_chains + 15) / 16;
+                    const double qtiles = (quad_chains + kIsoChains - 1) / kIsoChains;
                     const double free_cus = std::max((double)cus - qtiles, 1.0);
                     const double tb = t_bulk * cus / free_cus;
                     if (tb <= floor_s) break;
@@ -1121,25 +1226,26 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
     const uint64_t tiles = (ub + 63) / 64 + (quad_chains + 15) / 16;
     hipEvent_t ka = ev_get ? ev_get() : nullptr, kb = ka ? ev_get() : nullptr;
     if (kb) VS_HIP(hipEventRecord(ka, s));
-    const uint64_t qt = (quad_chains + 15) / 16;
-    if (mode == kShaQuad && qt && isolate && qt <= (uint64_t)cus / 2 && iso_setup() == 0) {
-        // Isolated drain: each quad tile takes a CU to itself -- its LDS padded
-        // to the CU's whole 160 KiB, so no split workgroup can join it -- and
-        // is resident before the split tiles are launched beside it; the
-        // split grid covers every CU and takes the quad tiles' CUs as they
-        // finish.  (CU-masked streams were tried first: the masks did not hold
-        // from one stream pair to the next on this runtime, split tiles ran
-        // on "reserved" CUs, profiles/r06_drain/trace_*.log.)
+    const uint64_t qt = (quad_chains + 15) / 16;              // shared-CU latency tiles
+    const uint64_t qi = (quad_chains + kIsoChains - 1) / kIsoChains;   // isolated ones
+    if (mode == kShaQuad && qi && isolate && qi <= (uint64_t)cus / 2 && iso_setup() == 0) {
+        // Isolated drain: each latency tile (sha_iso_kernel, kIsoChains) takes
+        // a CU to itself -- it asks for the CU's whole 160 KiB of LDS, so no
+        // split workgroup can join it -- and is resident before the split
+        // tiles are launched beside it; the split grid covers every CU and
+        // takes the latency tiles' CUs as they finish.  (CU-masked streams were
+        // tried first: the masks did not hold from one stream pair to the
+        // next on this runtime, split tiles ran on "reserved" CUs,
+        // profiles/r06_drain/trace_*.log.)
         VS_HIP(hipMemsetAsync(count(3), 0, 4, s));
         VS_HIP(hipEventRecord(iso_ev[0], s));
         VS_HIP(hipStreamWaitEvent(iso_q, iso_ev[0], 0));
         ShaSliceArgs aq = a, ab = a;
-        aq.tiles = kShaTilesQuad;
         aq.resident = iso_res_d;
         ab.tiles = kShaTilesSplit;
         ab.tile_ctr = count(3);
         __atomic_store_n(iso_res_h, 0u, __ATOMIC_RELAXED);
-        sha_slice_kernel<<<(uint32_t)qt, 128, kIsoPadBytes, iso_q>>>(aq);
+        sha_iso_kernel<<<(uint32_t)qi, 64 * kIsoWaves, kIsoLdsBytes, iso_q>>>(aq);
         VS_HIP(hipGetLastError());
         VS_HIP(hipEventRecord(iso_ev[1], iso_q));
         // the quad tiles first: the host sees every one of them resident
@@ -1147,7 +1253,7 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
         // grid can take their CUs.  Bounded: after 10 s the split tiles go
         // anyway (results do not depend on the placement).
         const auto t0 = std::chrono::steady_clock::now();
-        while (__atomic_load_n(iso_res_h, __ATOMIC_ACQUIRE) < (uint32_t)qt &&
+        while (__atomic_load_n(iso_res_h, __ATOMIC_ACQUIRE) < (uint32_t)qi &&
                std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10))
             std::this_thread::yield();
         if (tiles > qt) {
@@ -1193,9 +1299,9 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
 // residency counter.  0 = ready.
 int ShaEngine::iso_setup() {
     if (iso_q) return 0;
-    // the quad launch pads its LDS to the CU's whole 160 KiB
-    if (hipFuncSetAttribute((const void *)sha_slice_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            kIsoPadBytes) != hipSuccess) {
+    // an isolated latency tile asks for the CU's whole 160 KiB of LDS
+    if (hipFuncSetAttribute((const void *)sha_iso_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kIsoLdsBytes) != hipSuccess) {
         (void)hipGetLastError();
         return -1;
     }
