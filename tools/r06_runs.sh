@@ -96,6 +96,8 @@ case $1 in
     ab ab_iso_single_c3r3 2 "head=$(var head),new=,iso2=$(var iso2)" tools/single_pass.py --share 3/8 --quad auto --rounds 2 &&
     VSGPU_LIB=$PWD/$(var shatrace) bash tools/gpu.sh py tools/sha_trace.py --gib 64 --quad auto:1 && mv gpurun_out/py_sha_trace.log gpurun_out/trace_c2_iso1.log &&
     VSGPU_LIB=$PWD/$(var iso2trace) bash tools/gpu.sh py tools/sha_trace.py --gib 64 --quad auto:1 && mv gpurun_out/py_sha_trace.log gpurun_out/trace_c2_iso2.log ;;
+  distinctab)   # the distinct-volume line, two latency consumers per CU (product) against one (iso1)
+    ab ab_distinct 2 "iso1=$(var iso1),new=" bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 3 ;;
   quadprobe)   # cycles per latency-mode round alone on a SIMD, per round form (tools/probe/quad_round.hip)
     mkdir -p tools/probe/bin && /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/probe/bin/quad_round tools/probe/quad_round.hip &&
     timeout -k 10 60 ./tools/probe/bin/quad_round > gpurun_out/quad_round.txt 2>&1; rc=$?; cat gpurun_out/quad_round.txt; exit $rc ;;
