@@ -98,6 +98,12 @@ case $1 in
     VSGPU_LIB=$PWD/$(var iso2trace) bash tools/gpu.sh py tools/sha_trace.py --gib 64 --quad auto:1 && mv gpurun_out/py_sha_trace.log gpurun_out/trace_c2_iso2.log ;;
   distinctab)   # the distinct-volume line, two latency consumers per CU (product) against one (iso1)
     ab ab_distinct 2 "iso1=$(var iso1),new=" bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 3 ;;
+  iso3ab)   # three latency consumers per CU (iso3, ring lead 1) against two (product)
+    VSGPU_LIB=$PWD/$(var iso3) bash tools/gpu.sh tests tests/test_gpu_cdc.py tests/test_gpu_c3.py -x && mv gpurun_out/gputests.log gpurun_out/gputests_iso3.log &&
+    bash tools/gpu.sh tests tests/test_gpu_cdc.py -x -k "drain or sha256 or blob" && mv gpurun_out/gputests.log gpurun_out/gputests_iso2.log &&
+    ab ab_iso3_single_c2 2 "new=,iso3=$(var iso3)" tools/single_pass.py --gib 64 --quad auto --rounds 2 &&
+    ab ab_iso3_single_c3r3 2 "new=,iso3=$(var iso3)" tools/single_pass.py --share 3/8 --quad auto --rounds 2 &&
+    ab ab_iso3_distinct 2 "new=,iso3=$(var iso3)" bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 3 ;;
   quadprobe)   # cycles per latency-mode round alone on a SIMD, per round form (tools/probe/quad_round.hip)
     mkdir -p tools/probe/bin && /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/probe/bin/quad_round tools/probe/quad_round.hip &&
     timeout -k 10 60 ./tools/probe/bin/quad_round > gpurun_out/quad_round.txt 2>&1; rc=$?; cat gpurun_out/quad_round.txt; exit $rc ;;

@@ -481,7 +481,12 @@ __device__ __forceinline__ void produce_tile(uint4 (&wk)[2][16 * 64], const ShaC
 #endif
 constexpr uint32_t kIsoWaves = 1 + VS_SHA_ISO_CONSUMERS;   // producer + consumers
 constexpr uint32_t kIsoChains = 16 * VS_SHA_ISO_CONSUMERS;  // chains per isolated tile
-constexpr uint32_t kRingSlots = 16;
+// the producer builds batch m + kIsoLead while the consumers run batch m; with
+// a lead of 2 batch m + 1 is complete, so a consumer reads each next block's
+// first K + W during the current one (three consumers' ring fits only a lead
+// of 1: the first block of a batch then waits for its words after the barrier)
+constexpr uint32_t kIsoLead = VS_SHA_ISO_CONSUMERS > 2 ? 1 : 2;
+constexpr uint32_t kRingSlots = 8 * kIsoLead;
 constexpr uint32_t kIsoRingStride = kIsoChains * 16 + 4;  // uint4 per ring slot
 constexpr uint32_t kIsoLdsBytes = 160 * 1024;             // the CU's whole LDS
 static_assert((kRingSlots * kIsoRingStride + 2 * 16 * kIsoChains + 1) * sizeof(uint4) <= kIsoLdsBytes,
@@ -508,35 +513,37 @@ struct IsoSrc {  // one chain's byte source in produce_iso
     }
 };
 
-__device__ __forceinline__ void produce_iso(uint4 *ring, const ShaChain &c0, uint32_t m0, const ShaChain &c1,
-                                            uint32_t m1, uint32_t steps, uint32_t lane) {
+__device__ __forceinline__ void produce_iso(uint4 *ring, const ShaChain (&ch)[VS_SHA_ISO_CONSUMERS],
+                                            const uint32_t (&mine)[VS_SHA_ISO_CONSUMERS], uint32_t steps,
+                                            uint32_t lane) {
+    constexpr int NC = VS_SHA_ISO_CONSUMERS;
     const uint32_t k = lane & 3, c = lane >> 2;
-    IsoSrc x0, x1;
-    x0.init(c0, m0);
-    x1.init(c1, m1);
+    IsoSrc x[NC];
+#pragma unroll
+    for (int i = 0; i < NC; ++i) x[i].init(ch[i], mine[i]);
     uint32_t d[17], w[16];
-    auto build = [&](const IsoSrc &x, uint32_t m, uint32_t cc) {
+    auto build = [&](const IsoSrc &xs, uint32_t m, uint32_t cc) {
         const uint32_t blk = 4 * m + k;
-        if (blk < x.mine) {
-            window_words(d, x.S0, x.S, x.q);
-            message(w, d, x.p + 64ull * blk, x.e, x.L);
+        if (blk < xs.mine) {
+            window_words(d, xs.S0, xs.S, xs.q);
+            message(w, d, xs.p + 64ull * blk, xs.e, xs.L);
             schedule_to_lds<kSlotQuadEarly, kIsoChains>(w, ring + (blk % kRingSlots) * kIsoRingStride, cc);
         }
     };
-    // build i happens before barrier i (none before barrier 0: batches 0 and
-    // 1 precede the consumers' first block), i.e. batch m + 2 while the
-    // consumers run batch m; 1 + ceil(steps / 4) barriers, as the consumers
+    // build i happens before barrier i - (kIsoLead - 1): batches 0 .. lead-1
+    // precede the consumers' first block, then batch m + lead while they run
+    // batch m; 1 + ceil(steps / 4) barriers, as the consumers
     const uint32_t nb = (steps + 3) / 4;
-    x0.load(k);
-    if (kIsoChains > 16) x1.load(k);
-    for (uint32_t i = 0; i < nb + 2; ++i) {
+#pragma unroll
+    for (int i = 0; i < NC; ++i) x[i].load(k);
+    for (uint32_t i = 0; i < nb + kIsoLead; ++i) {
         if (i < nb) {
-            build(x0, i, c);
-            if (kIsoChains > 16) build(x1, i, 16 + c);
-            x0.load(4 * (i + 1) + k);
-            if (kIsoChains > 16) x1.load(4 * (i + 1) + k);
+#pragma unroll
+            for (int j = 0; j < NC; ++j) build(x[j], i, 16 * j + c);
+#pragma unroll
+            for (int j = 0; j < NC; ++j) x[j].load(4 * (i + 1) + k);
         }
-        if (i >= 1) __syncthreads();
+        if (i + 1 >= kIsoLead) __syncthreads();
     }
 }
 
@@ -726,17 +733,21 @@ __global__ __launch_bounds__(64 * kIsoWaves) void sha_iso_kernel(ShaSliceArgs a)
         __syncthreads();
         const uint32_t t = tile_w[0];
         if (t >= ntiles) break;
-        ShaChain c0, c1;
-        uint32_t l0, l1;
-        bool v0, v1;
+        constexpr int NC = VS_SHA_ISO_CONSUMERS;
+        ShaChain pc[NC];      // the producer's chains (lane: c, 16 + c, ...)
+        uint32_t pm[NC];
+        ShaChain c0;
+        uint32_t l0;
+        bool v0;
         const uint32_t c = lane >> 2;
         if (wave == 0) {
-            // the producer holds all the tile's chains: chain c (and 16 + c) per lane
-            chain(t, c, c0, l0, v0);
-            c1 = c0;
-            l1 = 0;
-            if (kIsoChains > 16) chain(t, 16 + c, c1, l1, v1);
-            uint32_t m = max(min(l0, a.budget), min(l1, a.budget));
+            uint32_t m = 0;
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+                chain(t, 16 * i + c, pc[i], l0, v0);
+                pm[i] = min(l0, a.budget);
+                m = max(m, pm[i]);
+            }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
             if (threadIdx.x == 0) tile_w[1] = m;
@@ -751,7 +762,7 @@ __global__ __launch_bounds__(64 * kIsoWaves) void sha_iso_kernel(ShaSliceArgs a)
         const uint64_t c_tile = __builtin_amdgcn_s_memtime();
 #endif
         if (wave == 0) {
-            produce_iso(ring, c0, min(l0, a.budget), c1, min(l1, a.budget), steps, lane);
+            produce_iso(ring, pc, pm, steps, lane);
             continue;
         }
         const uint32_t mine = min(l0, a.budget);
@@ -781,12 +792,19 @@ __global__ __launch_bounds__(64 * kIsoWaves) void sha_iso_kernel(ShaSliceArgs a)
             for (uint32_t kk = 0; kk < 4; ++kk) {
                 const uint32_t j = j0 + kk;
                 uint32_t y[4] = {x[0], x[1], x[2], x[3]};
-                compress_quad_iso<kIsoChains>(y, kwp(j), kwp(j + 1), ql, kz, qa, qb);
+                // (lead 1: the next batch is being written, so the last block
+                // re-reads its own words and the next batch's come after the barrier)
+                compress_quad_iso<kIsoChains>(y, kwp(j), kwp(kIsoLead > 1 || kk < 3 ? j + 1 : j), ql, kz, qa, qb);
                 const bool on = j < mine;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) x[i] = on ? y[i] : x[i];
             }
             __syncthreads();
+            if (kIsoLead == 1) {
+                kz = kwp(j0 + 4)[15 * kIsoChains].w;
+                qa = kwp(j0 + 4)[0];
+                qb = kwp(j0 + 4)[kIsoChains];
+            }
         }
         uint32_t st[8];
 #pragma unroll
