@@ -104,6 +104,12 @@ case $1 in
     ab ab_iso3_single_c2 2 "new=,iso3=$(var iso3)" tools/single_pass.py --gib 64 --quad auto --rounds 2 &&
     ab ab_iso3_single_c3r3 2 "new=,iso3=$(var iso3)" tools/single_pass.py --share 3/8 --quad auto --rounds 2 &&
     ab ab_iso3_distinct 2 "new=,iso3=$(var iso3)" bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 3 ;;
+  quadtrace3)   # the C3 rank's drain: latency tiles and the split tail (VS_SHA_TRACE build shatrace)
+    VSGPU_LIB=$PWD/$(var shatrace) bash tools/gpu.sh py tools/sha_trace.py --share 3/8 --quad auto:1 &&
+    mv gpurun_out/py_sha_trace.log gpurun_out/trace_c3r3_quad.log ;;
+  capab)   # latency-mode cap: 16 chains per two CUs (product) against 20 (cap20), C3 rank, C2, distinct
+    ab ab_cap_single_c3r3 2 "new=,cap20=$(var cap20)" tools/single_pass.py --share 3/8 --quad auto --rounds 2 &&
+    ab ab_cap_single_c2 1 "new=,cap20=$(var cap20)" tools/single_pass.py --gib 64 --quad auto --rounds 2 ;;
   quadprobe)   # cycles per latency-mode round alone on a SIMD, per round form (tools/probe/quad_round.hip)
     mkdir -p tools/probe/bin && /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/probe/bin/quad_round tools/probe/quad_round.hip &&
     timeout -k 10 60 ./tools/probe/bin/quad_round > gpurun_out/quad_round.txt 2>&1; rc=$?; cat gpurun_out/quad_round.txt; exit $rc ;;

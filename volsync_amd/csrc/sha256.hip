@@ -1184,11 +1184,14 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
         // (split chains beside a busy chip after a long run, the clock down:
         // up to 3.3 us, profiles/r06_val1/trace_c2; the rule takes 3.0)
         constexpr double kSplitBlockS = 3.0e-6, kBulkBlocksPerS = 22.7e9;
+#ifndef VS_SHA_QUAD_CAP2
+#define VS_SHA_QUAD_CAP2 16   // isolated: latency-mode chains per two CUs
+#endif
         const double quad_s = isolate ? 1.34e-6 : 1.6e-6;
         // isolated, at most 16 chains per two CUs run in latency mode (with
         // two consumer waves per tile, 3 638 chains for a C3 rank on half the
         // CUs took its single pass 225 -> 237-256 ms, profiles/r06_iso32)
-        const uint32_t quad_cap = isolate ? (uint32_t)std::max(cus, 2) / 2 * 16 : 0xffffffffu;
+        const uint32_t quad_cap = isolate ? (uint32_t)std::max(cus, 2) / 2 * VS_SHA_QUAD_CAP2 : 0xffffffffu;
         const double lmax = first < kShaBuckets ? (double)bucket_blocks(first) : 0.0;
         const double t_bulk = blocks / kBulkBlocksPerS;
         auto count_above = [&](double floor_s) {   // chains whose split-mode time passes floor_s
