@@ -110,6 +110,8 @@ case $1 in
   capab)   # latency-mode cap: 16 chains per two CUs (product) against 20 (cap20), C3 rank, C2, distinct
     ab ab_cap_single_c3r3 2 "new=,cap20=$(var cap20)" tools/single_pass.py --share 3/8 --quad auto --rounds 2 &&
     ab ab_cap_single_c2 1 "new=,cap20=$(var cap20)" tools/single_pass.py --gib 64 --quad auto --rounds 2 ;;
+  tracec3)   # kernel trace + stats of the C3 rank-3 line (rocprofv3, no counters)
+    trace c3r3 --share 3/8 --steps 20 --warmup 5 --no-cpu-baseline ;;
   quadprobe)   # cycles per latency-mode round alone on a SIMD, per round form (tools/probe/quad_round.hip)
     mkdir -p tools/probe/bin && /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/probe/bin/quad_round tools/probe/quad_round.hip &&
     timeout -k 10 60 ./tools/probe/bin/quad_round > gpurun_out/quad_round.txt 2>&1; rc=$?; cat gpurun_out/quad_round.txt; exit $rc ;;
