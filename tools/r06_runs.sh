@@ -112,6 +112,18 @@ case $1 in
     ab ab_cap_single_c2 1 "new=,cap20=$(var cap20)" tools/single_pass.py --gib 64 --quad auto --rounds 2 ;;
   tracec3)   # kernel trace + stats of the C3 rank-3 line (rocprofv3, no counters)
     trace c3r3 --share 3/8 --steps 20 --warmup 5 --no-cpu-baseline ;;
+  sharedab)   # chains past the isolated cap in shared-CU latency tiles (product) against split mode (noshared)
+    bash tools/gpu.sh tests tests/test_gpu_cdc.py tests/test_gpu_c3.py -x && mv gpurun_out/gputests.log gpurun_out/gputests_cdc.log &&
+    ab ab_shared_single_c3r3 2 "noshared=$(var noshared),new=" tools/single_pass.py --share 3/8 --quad auto --rounds 2 &&
+    ab ab_shared_single_c2 1 "noshared=$(var noshared),new=" tools/single_pass.py --gib 64 --quad auto --rounds 2 &&
+    ab ab_shared_distinct 1 "noshared=$(var noshared),new=" bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 3 ;;
+  shareddist)   # the distinct-volume line again, shared tail (product) against noshared, two rounds
+    ab ab_shared_distinct2 2 "noshared=$(var noshared),new=" bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 3 ;;
+  sharedab2)   # shared tail only in tail-bound drains (product) against noshared: C3 rank, distinct
+    ab ab_shared2_single_c3r3 2 "noshared=$(var noshared),new=" tools/single_pass.py --share 3/8 --quad auto --rounds 2 &&
+    ab ab_shared2_distinct 2 "noshared=$(var noshared),new=" bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 3 ;;
+  sharedreplay)   # the replayed C2 line, shared tail (product) against noshared, three rounds
+    ab ab_shared_replay 3 "noshared=$(var noshared),new=" bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --distinct 0 ;;
   quadprobe)   # cycles per latency-mode round alone on a SIMD, per round form (tools/probe/quad_round.hip)
     mkdir -p tools/probe/bin && /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/probe/bin/quad_round tools/probe/quad_round.hip &&
     timeout -k 10 60 ./tools/probe/bin/quad_round > gpurun_out/quad_round.txt 2>&1; rc=$?; cat gpurun_out/quad_round.txt; exit $rc ;;

@@ -255,11 +255,10 @@ struct ShaSliceArgs {
     uint32_t *tile_ctr;
     uint32_t budget;         // max blocks per chain in this slice (0xffffffff: all)
     uint32_t quad_chains;    // the first (longest) chains of the order run in latency mode
-    uint32_t tiles;          // sha_slice_kernel: kShaTilesAll, or kShaTilesSplit beside an
-                             // isolated drain's sha_iso_kernel (the latency tiles)
+    uint32_t quad_lo;        // sha_slice_kernel: of those, the first quad_lo run in an isolated
+                             // drain's sha_iso_kernel; its own latency tiles take the rest
     uint32_t *resident;      // sha_iso_kernel: host-visible count of resident workgroups
 };
-enum { kShaTilesAll = 0, kShaTilesSplit = 2 };
 
 // Host side of the engine: a double-buffered active list on the device, fed by
 // append_*() and advanced by slice(); every call queues on the given stream

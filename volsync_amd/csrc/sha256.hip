@@ -582,10 +582,10 @@ __device__ __forceinline__ void trace_tile(bool quad, uint32_t t, uint64_t t0, u
 // profiles/r06_first/ab_single_c3r3.log), so off
 #define VS_SHA_QUAD_PPRIO 0
 #endif
-// Tiles [0, qt) hold the first (longest) a.quad_chains chains of the order, 16
+// Tiles [0, qt) hold chains [a.quad_lo, a.quad_chains) of the order (the
+// longest; an isolated drain's sha_iso_kernel takes the first a.quad_lo), 16
 // per tile, consumed in latency mode (compress_quad; the producer's lanes
-// 16..63 idle); the later tiles hold 64 chains each in split mode.  (An
-// isolated drain runs its latency tiles in sha_iso_kernel instead.)
+// 16..63 idle); the later tiles hold 64 chains each in split mode.
 // VS_SHA_MINW (A/B builds): at least this many waves per SIMD, i.e. a
 // register budget that fits beside a co-resident fingerprint workgroup
 #ifdef VS_SHA_MINW
@@ -608,25 +608,23 @@ __global__ __launch_bounds__(128) void sha_slice_kernel(ShaSliceArgs a) {
     const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;  // wave-uniform
     const uint32_t n = *a.n_cur;
     const uint32_t nq = min(a.quad_chains, n);
-    const uint32_t qt = (nq + 15) / 16;
-    // the launch's tile range: every tile, or (beside an isolated drain's
-    // sha_iso_kernel) the split tiles alone
-    const uint32_t t_lo = a.tiles == kShaTilesSplit ? qt : 0u;
+    const uint32_t q0 = min(a.quad_lo, nq);
+    const uint32_t qt = (nq - q0 + 15) / 16;
     const uint32_t ntiles = qt + (n - nq + 63) / 64;
-    if (qt && a.tiles != kShaTilesSplit) {
+    if (qt) {
         for (uint32_t i = threadIdx.x; i < 16 * 16; i += blockDim.x) zero_kw[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
     }
     if (!producer) __builtin_amdgcn_s_setprio(2);  // the rounds are the critical path
     for (;;) {
-        if (threadIdx.x == 0) tile_sh = t_lo + atomicAdd(a.tile_ctr, 1u);
+        if (threadIdx.x == 0) tile_sh = atomicAdd(a.tile_ctr, 1u);
         __syncthreads();
         const uint32_t t = tile_sh;
         __syncthreads();
         if (t >= ntiles) break;
         const bool quad = t < qt;  // wave-uniform
         const uint32_t my = quad ? (producer ? lane : lane >> 2) : lane;
-        const uint32_t idx = quad ? t * 16 + my : nq + (t - qt) * 64 + my;
+        const uint32_t idx = quad ? q0 + t * 16 + my : nq + (t - qt) * 64 + my;
         const bool valid = quad ? (my < 16 && idx < nq) : idx < n;
         const uint32_t ci = valid ? (a.order ? a.order[idx] : idx) : 0u;
         const ShaChain ch0 = a.cur[ci];
@@ -1167,7 +1165,8 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
     sha_scatter_kernel<<<sb, 256, 0, s>>>(list[cur].as<ShaChain>(), count(cur), budget, cursor,
                                           order.as<uint32_t>());
     // quad drain (bucket histogram read back: one synchronisation per drain)
-    uint32_t quad_chains = 0;
+    uint32_t quad_chains = 0, iso_chains = 0;   // latency-mode chains; of those, isolated
+    bool shared_tail = false;                    // iso_chains < quad_chains
     if (mode == kShaQuad) {
         VS_HIP(hipMemcpyAsync(hist_h, hist.p, kShaBuckets * 4, hipMemcpyDeviceToHost, s));
         VS_HIP(hipStreamSynchronize(s));
@@ -1184,6 +1183,9 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
         // (split chains beside a busy chip after a long run, the clock down:
         // up to 3.3 us, profiles/r06_val1/trace_c2; the rule takes 3.0)
         constexpr double kSplitBlockS = 3.0e-6, kBulkBlocksPerS = 22.7e9;
+#ifndef VS_SHA_SHARED_TAIL
+#define VS_SHA_SHARED_TAIL 1   // isolated drain: chains past the cap in shared-CU latency tiles
+#endif
 #ifndef VS_SHA_QUAD_CAP2
 #define VS_SHA_QUAD_CAP2 16   // isolated: latency-mode chains per two CUs
 #endif
@@ -1222,6 +1224,19 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
                     if (tb <= floor_s) break;
                     floor_s = tb;
                 }
+                // isolated: the chains above the floor past the cap run in
+                // shared-CU latency tiles of the split launch (1.6 us per block
+                // beside split tiles, not ~3 in a split tile; a C3 rank's split
+                // tail otherwise outlasted its isolated tail, profiles/r06_iso32)
+                // Only when the drain is tail-bound (the floor is the longest
+                // chain, not the backlog): a fence drain's large backlog lost
+                // 3 % to the shared tiles' idle producer lanes
+                // (profiles/r06_iso32/ab_shared_distinct2_always.log)
+                if (isolate && VS_SHA_SHARED_TAIL && floor_s <= lmax * quad_s) {
+                    iso_chains = quad_chains;
+                    quad_chains = std::max(quad_chains, count_above(floor_s));
+                    shared_tail = true;
+                }
             } else {
                 for (uint32_t k = first; k < kShaBuckets; ++k) {
                     if ((double)bucket_blocks(k) * 100 < lmax * quad_pct) break;
@@ -1243,12 +1258,11 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
     a.tile_ctr = count(2);
     a.budget = budget;
     a.quad_chains = quad_chains;
-    a.tiles = kShaTilesAll;
     const uint64_t tiles = (ub + 63) / 64 + (quad_chains + 15) / 16;
     hipEvent_t ka = ev_get ? ev_get() : nullptr, kb = ka ? ev_get() : nullptr;
     if (kb) VS_HIP(hipEventRecord(ka, s));
-    const uint64_t qt = (quad_chains + 15) / 16;              // shared-CU latency tiles
-    const uint64_t qi = (quad_chains + kIsoChains - 1) / kIsoChains;   // isolated ones
+    if (!shared_tail) iso_chains = quad_chains;
+    const uint64_t qi = (iso_chains + kIsoChains - 1) / kIsoChains;   // isolated latency tiles
     if (mode == kShaQuad && qi && isolate && qi <= (uint64_t)cus / 2 && iso_setup() == 0) {
         // Isolated drain: each latency tile (sha_iso_kernel, kIsoChains) takes
         // a CU to itself -- it asks for the CU's whole 160 KiB of LDS, so no
@@ -1262,8 +1276,9 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
         VS_HIP(hipEventRecord(iso_ev[0], s));
         VS_HIP(hipStreamWaitEvent(iso_q, iso_ev[0], 0));
         ShaSliceArgs aq = a, ab = a;
+        aq.quad_chains = iso_chains;
         aq.resident = iso_res_d;
-        ab.tiles = kShaTilesSplit;
+        ab.quad_lo = iso_chains;   // the split launch: its own latency tiles take the rest
         ab.tile_ctr = count(3);
         __atomic_store_n(iso_res_h, 0u, __ATOMIC_RELAXED);
         sha_iso_kernel<<<(uint32_t)qi, 64 * kIsoWaves, kIsoLdsBytes, iso_q>>>(aq);
@@ -1277,6 +1292,7 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
         while (__atomic_load_n(iso_res_h, __ATOMIC_ACQUIRE) < (uint32_t)qi &&
                std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10))
             std::this_thread::yield();
+        const uint64_t qt = (iso_chains + 15) / 16;   // tiles' worth of chains the iso launch took
         if (tiles > qt) {
             sha_slice_kernel<<<(uint32_t)std::min<uint64_t>(tiles - qt, (uint64_t)std::max(cus, 1) *
                                                                            (grid_per_cu ? grid_per_cu : 5)),
