@@ -87,6 +87,10 @@ case $1 in
         --no-cpu-baseline --no-file-sum > gpurun_out/bench_$v.log 2>&1 || exit 1
       echo "== $v"; grep "walk prof" gpurun_out/bench_$v.log | tail -1
     done ;;
+  latefwab)   # STEP filter words tested after the previous batch's probe results (latefw = -DVS_WALK_LATEFW=1): walk tests, real-C4 rank, C4 shape
+    VSGPU_LIB=$PWD/$(var latefw) bash tools/gpu.sh tests tests/test_gpu_rsync.py -x && mv gpurun_out/gputests.log gpurun_out/gputests_rsync_latefw.log &&
+    ab ab_latefw_share 2 "latefw=$(var latefw),base=" bench.py --mode rsync --share 3/8 --per-gpu-gib 32 --steps 3 --warmup 1 --no-file-sum --no-cpu-baseline &&
+    ab ab_latefw_c4 2 "latefw=$(var latefw),base=" bench.py --mode rsync --steps 5 --warmup 1 --no-file-sum --no-cpu-baseline ;;
   walkcounters)   # counter passes of the real-C4 rank's walk (spread STEP probes) -> gpurun_out/profile_c4share
     bash tools/gpu.sh prof c4share 'rs_walk_spec_kernel' --mode rsync --share 3/8 --per-gpu-gib 32 --steps 2 --warmup 1 --no-file-sum ;;
   isoab)   # isolated latency kernel: one consumer wave per CU (product) against two (iso2) and HEAD's build (head)

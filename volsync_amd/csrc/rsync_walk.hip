@@ -47,6 +47,9 @@ using vsstrong::P32_1;
 #endif
 // STEP probes: every survivor of a batch in one round trip, a lane each
 // (stage1 / stage2 in walk_segment); 0 = each lane probes its own in turn
+#ifndef VS_WALK_LATEFW
+#define VS_WALK_LATEFW 0
+#endif
 #ifndef VS_WALK_PSCAN
 #define VS_WALK_PSCAN 1
 #endif
@@ -1029,7 +1032,8 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
             uint4 b0, b1;        // its membership bucket
         };
         uint4 nwo = cwo, nwi = cwi;
-        auto stage1 = [&](uint64_t Ab, const uint4 &bo, const uint4 &bi, uint32_t t1, uint32_t t2,
+        uint64_t fw[16];
+        auto stage1a = [&](uint64_t Ab, const uint4 &bo, const uint4 &bi, uint32_t t1, uint32_t t2,
                           int64_t fromb, Stage &st) {
             uint64_t tb = wclock(wp);
             const uint64_t c = Ab + 16 * (uint64_t)lane;
@@ -1090,13 +1094,19 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
             }
             wadd(wp, kPrStepLds, tsub);
             tsub = wclock(wp);
-            {
-                uint64_t fw[16];
 #pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    const bool on = (hit >> t) & 1u;
-                    fw[t] = a.filt_b[on ? rs_bloom_word(st.sums[t], a.fbits) : 0u];
-                }
+            for (int t = 0; t < 16; ++t) {
+                const bool on = (hit >> t) & 1u;
+                fw[t] = a.filt_b[on ? rs_bloom_word(st.sums[t], a.fbits) : 0u];
+            }
+            st.hit = hit;
+            wadd(wp, kPrStepGather, tsub);
+        };
+        // the blocked filter's words (issued by stage1a, tested by stage1b)
+        auto stage1b = [&](Stage &st) {
+            uint64_t tsub = wclock(wp);
+            uint32_t hit = st.hit;
+            {
                 uint32_t pass = 0;
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
@@ -1141,7 +1151,8 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
             wadd(wp, kPrStepGather, tsub);
         };
         Stage cur, nxt;
-        stage1(A, cwo, cwi, T1, T2, o, cur);
+        stage1a(A, cwo, cwi, T1, T2, o, cur);
+        stage1b(cur);
         for (;;) {
             uint64_t tb = wclock(wp);
             const uint64_t nx = A + kBatch;
@@ -1149,7 +1160,10 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
             if (!last) {
                 cwo = nwo;
                 cwi = nwi;
-                stage1(nx, cwo, cwi, cur.t1, cur.t2, (int64_t)nx, nxt);
+                stage1a(nx, cwo, cwi, cur.t1, cur.t2, (int64_t)nx, nxt);
+#if !VS_WALK_LATEFW
+                stage1b(nxt);
+#endif
             }
             // stage 2 of batch A: the probe results (the preloaded bucket for
             // the lane's first offset, the rest probed now -- rare)
@@ -1192,6 +1206,10 @@ __device__ SegResult walk_segment(const RsWalkArgs &a, const RowSec &rs, const u
                 }
             }
             wadd(wp, kPrStepProbe, tsub);
+#if VS_WALK_LATEFW
+            // batch A + 1024's filter words land behind batch A's probe results
+            if (!last) stage1b(nxt);
+#endif
             // queue the hits in offset order (lane order, then bit order);
             // a full queue is flushed and queueing goes on with the batch's
             // remaining hits (all past the last visited one)
