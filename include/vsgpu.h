@@ -195,6 +195,11 @@ typedef struct vs_sha vs_sha;
 int vs_sha256_open(int device, vs_sha **h);
 int vs_sha256_run_device(vs_sha *h, const void *dev_buf, const uint64_t *dev_off,
                          const uint32_t *dev_len, size_t n, uint8_t *dev_out, void *hip_stream);
+/* The last drain of vs_sha256_run_device: out[0] = chains it ran in latency
+ * mode (4 lanes per chain), out[1] = those of them in isolated tiles (a CU
+ * each); the rest ran as latency tiles beside the split tiles.  Diagnostics
+ * for tests and benches; the digests never depend on the split. */
+int vs_sha256_drain_stats(vs_sha *h, uint64_t out[2]);
 /* Same knob as vs_cdc_set_hash_wide for a vs_sha handle. */
 int vs_sha256_set_wide(vs_sha *h, uint32_t min_chains, uint32_t drain_blocks);
 void vs_sha256_close(vs_sha *h);

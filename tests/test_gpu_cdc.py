@@ -218,6 +218,42 @@ def test_sha256_drain_modes_vs_hashlib(gpu, pct, iso):
         assert g.tobytes() == hashlib.sha256(buf[o:o + n]).digest(), n
 
 
+def test_sha256_drain_shared_tail_vs_hashlib(gpu):
+    """A tail-bound drain with more long chains than the isolated tiles take
+    (16 per two CUs): the first cap chains run in sha_iso_kernel, a CU per
+    tile, and the rest as latency tiles of the split launch beside the split
+    tiles (ShaSliceArgs.quad_lo; the C3 rank's drain, profiles/r06_iso32).
+    vs_sha256_drain_stats shows both parts ran; every digest = hashlib's."""
+    import torch
+    from volsync_amd import DeviceSha256
+    from volsync_amd._lib import VS_OPT_SHA_ISOLATE, VS_OPT_SHA_QUAD_PCT
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    cap = cus // 2 * 16
+    n_long = cap + cap // 2
+    rng = np.random.default_rng(29)
+    host = O.synth(73, 0, 16 << 20)
+    buf = host.tobytes()
+    lens = [int(x) for x in rng.integers(192 << 10, 320 << 10, n_long)] + \
+        [int(x) for x in rng.integers(0, 4096, 500)]
+    offs = [int(rng.integers(0, len(buf) - n)) for n in lens]
+    d = torch.from_numpy(host).cuda()
+    do = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    dl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    out = torch.zeros(len(lens) * 32, dtype=torch.uint8, device="cuda")
+    sh = DeviceSha256(0)
+    sh.set_option(VS_OPT_SHA_QUAD_PCT, -1)
+    sh.set_option(VS_OPT_SHA_ISOLATE, 1)
+    sh.run(d.data_ptr(), do.data_ptr(), dl.data_ptr(), len(lens), out.data_ptr(), None)
+    torch.cuda.synchronize()
+    latency, isolated = sh.drain_stats()
+    sh.close()
+    assert isolated == cap, (latency, isolated, cap)
+    assert cap < latency <= n_long, (latency, isolated, n_long)
+    got = out.cpu().numpy().reshape(-1, 32)
+    for o, n, g in zip(offs, lens, got):
+        assert g.tobytes() == hashlib.sha256(buf[o:o + n]).digest(), n
+
+
 def test_fence_distinct_volumes(gpu):
     """bench.py --distinct: volumes of three seeds in rotation, step k fenced
     on step k - 3 (vs_cdc_fence) with a short slice budget, so the fences

@@ -213,6 +213,7 @@ def _load() -> ctypes.CDLL:
         "vs_rsync_set_option": (c_int, [vp, c_int, i64]),
         "vs_cdc_set_option": (c_int, [vp, c_int, i64]),
         "vs_sha256_set_option": (c_int, [vp, c_int, i64]),
+        "vs_sha256_drain_stats": (c_int, [vp, vp]),
         "vs_seal_set_option": (c_int, [vp, c_int, i64]),
         "vs_rsync_signatures": (c_int, [c_int, vp, i64, i32, i32, c_int, c_u32, vp, vp]),
         "vs_rsync_match": (c_int, [c_int, vp, i64, ctypes.POINTER(VsSigTable), c_int, c_u32,

@@ -351,6 +351,12 @@ class DeviceSha256:
                                        ctypes.c_void_p(dev_len), n, ctypes.c_void_p(dev_out),
                                        ctypes.c_void_p(stream or None)))
 
+    def drain_stats(self) -> tuple:
+        """(latency-mode chains, of those isolated) of the last run's drain."""
+        out = (ctypes.c_uint64 * 2)()
+        check(lib.vs_sha256_drain_stats(self._h, out))
+        return int(out[0]), int(out[1])
+
     def set_wide(self, min_chains: int = 0, drain_blocks: int = 0) -> None:
         """Throughput mode from min_chains active blobs (0 = default, 0xffffffff = never)."""
         check(lib.vs_sha256_set_wide(self._h, int(min_chains), int(drain_blocks)))

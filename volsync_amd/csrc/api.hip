@@ -1508,6 +1508,14 @@ VS_API int vs_sha256_set_option(vs_sha *h, int option, int64_t value) {
     return sha_option(h->eng, option, value);
 }
 
+VS_API int vs_sha256_drain_stats(vs_sha *h, uint64_t out[2]) {
+    if (!h || !out) return fail(VS_ERR_ARG, "null argument");
+    if (h->ran) VS_HIP(hipEventSynchronize(h->done));
+    out[0] = h->eng.last_quad_chains;
+    out[1] = h->eng.last_iso_chains;
+    return 0;
+}
+
 VS_API int vs_sha256_set_wide(vs_sha *h, uint32_t min_chains, uint32_t drain_blocks) {
     if (!h) return fail(VS_ERR_ARG, "null handle");
     if (h->ran) VS_HIP(hipEventSynchronize(h->done));

@@ -294,6 +294,7 @@ struct ShaEngine {
     static constexpr uint32_t kQuadAuto = 0xffffffffu;
     uint32_t quad_pct = kQuadAuto;
     uint32_t last_quad_chains = 0;  // chains the last drain ran in quad mode (stats)
+    uint32_t last_iso_chains = 0;   // of those, in isolated tiles (sha_iso_kernel)
     // Isolated latency drain (VS_OPT_SHA_ISOLATE, default on): the latency
     // tiles run in sha_iso_kernel, 32 chains per workgroup, each holding a
     // CU alone (it asks for the CU's whole LDS), resident before the split

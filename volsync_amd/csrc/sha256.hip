@@ -1263,7 +1263,9 @@ int ShaEngine::launch(uint32_t budget, int mode, hipStream_t s) {
     if (kb) VS_HIP(hipEventRecord(ka, s));
     if (!shared_tail) iso_chains = quad_chains;
     const uint64_t qi = (iso_chains + kIsoChains - 1) / kIsoChains;   // isolated latency tiles
+    last_iso_chains = 0;
     if (mode == kShaQuad && qi && isolate && qi <= (uint64_t)cus / 2 && iso_setup() == 0) {
+        last_iso_chains = iso_chains;
         // Isolated drain: each latency tile (sha_iso_kernel, kIsoChains) takes
         // a CU to itself -- it asks for the CU's whole 160 KiB of LDS, so no
         // split workgroup can join it -- and is resident before the split
